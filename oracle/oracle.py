@@ -1,0 +1,276 @@
+"""ctypes front-end of the CPU oracle (oracle/smore_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py -- never by the smore_amd product package.
+
+Also holds a tiny pure-Python edge-list reader that restates the reference
+loader's id assignment (src/proNet.cpp:115-236: vertex ids in first-appearance
+order, directed edge slots pushed per line as v1->v2 then v2->v1 when
+undirected), used to build test graphs for the oracle.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+
+VM = {"out_degrees": 0, "no_degrees": 1, "degrees": 2}
+NM = {"degrees": 0, "in_degrees": 1, "no_degrees": 2}
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = C.CDLL(LIB_PATH)
+        _declare(_lib)
+    return _lib
+
+
+P = C.c_void_p
+i64, u64, i32, u32, dbl = C.c_int64, C.c_uint64, C.c_int32, C.c_uint32, C.c_double
+
+
+def _declare(L):
+    L.orc_philox4x32_10.argtypes = [P, P, P]
+    L.orc_word.restype = u32
+    L.orc_word.argtypes = [u64, u32, u64, u32]
+    L.orc_words.argtypes = [u64, u32, u64, u32, P]
+    L.orc_glibc_rand_fill.argtypes = [u32, P, i64]
+    L.orc_alias_cpp.argtypes = [P, i64, P, P]
+    L.orc_alias_go.argtypes = [P, i64, dbl, P, P]
+    L.orc_alias_encode.argtypes = [P, P, i64, P, P, P]
+    L.orc_build_graph.restype = C.c_int
+    L.orc_build_graph.argtypes = [i64, i64, P, P, P, C.c_int, C.c_int] + [P] * 10
+    L.orc_sample_line.argtypes = [P, u64, u64, u64, C.c_int, P]
+    L.orc_sample_bpr.argtypes = [P, u64, u64, u64, P]
+    L.orc_sigmoid_table.argtypes = [P]
+    L.orc_fast_sigmoid.restype = dbl
+    L.orc_fast_sigmoid.argtypes = [dbl]
+    L.orc_alpha_line.restype = dbl
+    L.orc_alpha_line.argtypes = [u64, dbl, u64]
+    L.orc_alpha_walk.restype = dbl
+    L.orc_alpha_walk.argtypes = [u64, dbl, u64]
+    L.orc_train_edge_f64.restype = C.c_int
+    L.orc_train_edge_f64.argtypes = [P, C.c_int, P, P, C.c_int, C.c_int, dbl, dbl, u64, u64, u64, u64]
+    L.orc_train_bpr_f64.restype = C.c_int
+    L.orc_train_bpr_f64.argtypes = [P, P, C.c_int, dbl, u64, u64, u64, u64]
+    L.orc_train_deepwalk_f64.restype = C.c_int
+    L.orc_train_deepwalk_f64.argtypes = [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, dbl, u64, P]
+    L.orc_train_edge_f32.restype = C.c_int
+    L.orc_train_edge_f32.argtypes = [P, C.c_int, P, P, C.c_int, C.c_int, C.c_int, dbl, dbl, u64, u64, u64, u64, C.c_int]
+    L.orc_train_bpr_f32.restype = C.c_int
+    L.orc_train_bpr_f32.argtypes = [P, P, C.c_int, C.c_int, dbl, u64, u64, u64, u64, C.c_int]
+    L.orc_train_deepwalk_f32.restype = C.c_int
+    L.orc_train_deepwalk_f32.argtypes = [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, dbl, u64, P, u64, u64]
+    L.orc_lane_width.restype = C.c_int
+    L.orc_lane_width.argtypes = [C.c_int]
+
+
+def ptr(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+# --------------------------------------------------------------------- RNG
+def philox(ctr, key):
+    c = np.asarray(ctr, dtype=np.uint32)
+    k = np.asarray(key, dtype=np.uint32)
+    o = np.zeros(4, np.uint32)
+    lib().orc_philox4x32_10(ptr(c), ptr(k), ptr(o))
+    return o
+
+
+def words(seed, stream, unit, nslots):
+    o = np.zeros(nslots, np.uint32)
+    lib().orc_words(seed, stream, unit, nslots, ptr(o))
+    return o
+
+
+def glibc_rand(n, seed=1):
+    o = np.zeros(n, np.int32)
+    lib().orc_glibc_rand_fill(seed, ptr(o), n)
+    return o
+
+
+# --------------------------------------------------------------------- alias
+def alias_cpp(dist):
+    d = np.ascontiguousarray(dist, dtype=np.float64)
+    p = np.zeros(len(d))
+    a = np.zeros(len(d), np.int64)
+    lib().orc_alias_cpp(ptr(d), len(d), ptr(p), ptr(a))
+    return p, a
+
+
+def alias_go(dist, power):
+    d = np.ascontiguousarray(dist, dtype=np.float64)
+    p = np.zeros(len(d))
+    a = np.zeros(len(d), np.int64)
+    lib().orc_alias_go(ptr(d), len(d), power, ptr(p), ptr(a))
+    return p, a
+
+
+def alias_encode(prob, alias, self_ids=None):
+    prob = np.ascontiguousarray(prob, np.float64)
+    alias = np.ascontiguousarray(alias, np.int64)
+    t = np.zeros(len(prob), np.uint32)
+    a = np.zeros(len(prob), np.int32)
+    s = None if self_ids is None else np.ascontiguousarray(self_ids, np.int32)
+    lib().orc_alias_encode(ptr(prob), ptr(alias), len(prob), ptr(s), ptr(t), ptr(a))
+    return t, a
+
+
+# --------------------------------------------------------------------- graph
+def read_edgelist(path, undirected):
+    """Reference id assignment and edge push order (src/proNet.cpp:165-216)."""
+    ids, names = {}, []
+    src, dst, w = [], [], []
+    with open(path, "rb") as f:
+        for line in f:
+            parts = line.split()
+            if len(parts) < 3:
+                continue
+            a, b = parts[0].decode(), parts[1].decode()
+            x = float(parts[2])
+            for n in (a, b):
+                if n not in ids:
+                    ids[n] = len(names)
+                    names.append(n)
+            src.append(ids[a]); dst.append(ids[b]); w.append(x)
+            if undirected:
+                src.append(ids[b]); dst.append(ids[a]); w.append(x)
+    return names, np.array(src, np.int32), np.array(dst, np.int32), np.array(w, np.float64)
+
+
+class Graph:
+    """CSR + alias tables built by the oracle, encoded like the HIP path."""
+
+    def __init__(self, V, src, dst, w, vertex_method="out_degrees", negative_method="degrees", names=None):
+        self.V, self.E = V, len(src)
+        self.names = names
+        V, E = self.V, self.E
+        self.offsets = np.zeros(V + 1, np.int64)
+        self.targets = np.zeros(max(E, 1), np.int32)
+        self.out_deg = np.zeros(V); self.in_deg = np.zeros(V)
+        self.vprob = np.zeros(V); self.valias = np.zeros(V, np.int64)
+        self.nprob = np.zeros(V); self.nalias = np.zeros(V, np.int64)
+        self.cprob = np.zeros(max(E, 1)); self.calias = np.zeros(max(E, 1), np.int64)
+        src = np.ascontiguousarray(src, np.int32); dst = np.ascontiguousarray(dst, np.int32)
+        w = np.ascontiguousarray(w, np.float64)
+        rc = lib().orc_build_graph(V, E, ptr(src), ptr(dst), ptr(w), VM[vertex_method], NM[negative_method],
+                                   ptr(self.offsets), ptr(self.targets), ptr(self.out_deg), ptr(self.in_deg),
+                                   ptr(self.vprob), ptr(self.valias), ptr(self.nprob), ptr(self.nalias),
+                                   ptr(self.cprob), ptr(self.calias))
+        if rc != 0:
+            raise ValueError("bad edge list")
+        self.vthr, self.valias_enc = alias_encode(self.vprob, self.valias)
+        self.nthr, self.nalias_enc = alias_encode(self.nprob, self.nalias)
+        self.cthr, self.calias_enc = alias_encode(self.cprob, self.calias, self.targets)
+        self._struct = _OrcGraph(V, E, ptr(self.offsets), ptr(self.targets), ptr(self.vthr), ptr(self.valias_enc),
+                                 ptr(self.nthr), ptr(self.nalias_enc), ptr(self.cthr), ptr(self.calias_enc))
+
+    @classmethod
+    def from_file(cls, path, undirected, vertex_method="out_degrees", negative_method="degrees"):
+        names, s, d, w = read_edgelist(path, undirected)
+        return cls(len(names), s, d, w, vertex_method, negative_method, names)
+
+    @property
+    def ref(self):
+        return C.byref(self._struct)
+
+
+class _OrcGraph(C.Structure):
+    _fields_ = [("V", i64), ("E", i64), ("offsets", P), ("targets", P), ("vthr", P), ("valias", P),
+                ("nthr", P), ("nalias", P), ("cthr", P), ("calias", P)]
+
+
+def sample_line(g, seed, begin, count, K):
+    o = np.zeros((count, 2 + K), np.int32)
+    lib().orc_sample_line(g.ref, seed, begin, count, K, ptr(o))
+    return o
+
+
+def sample_bpr(g, seed, begin, count):
+    o = np.zeros((count, 7), np.int32)
+    lib().orc_sample_bpr(g.ref, seed, begin, count, ptr(o))
+    return o
+
+
+def sigmoid_table():
+    t = np.zeros(1001)
+    lib().orc_sigmoid_table(ptr(t))
+    return t
+
+
+def fast_sigmoid(x):
+    return lib().orc_fast_sigmoid(float(x))
+
+
+def alpha_line(c, alpha0, total):
+    return lib().orc_alpha_line(c, alpha0, total)
+
+
+def lane_width(dpad):
+    return lib().orc_lane_width(dpad)
+
+
+MODEL = {"line2": 0, "line1": 1, "mf": 2}
+
+
+def train_edge_f64(g, model, W, C_, K, alpha0, reg, total, begin, end, seed):
+    dim = W.shape[1]
+    return lib().orc_train_edge_f64(g.ref, MODEL[model], ptr(W), ptr(C_), dim, K, alpha0, reg, total, begin, end, seed)
+
+
+def train_edge_f32(g, model, W, C_, dim, K, alpha0, reg, total, begin, end, seed, threads=1):
+    dpad = W.shape[1]
+    return lib().orc_train_edge_f32(g.ref, MODEL[model], ptr(W), ptr(C_), dim, dpad, K, alpha0, reg, total,
+                                    begin, end, seed, threads)
+
+
+def train_bpr_f64(g, W, alpha0, total, begin, end, seed):
+    return lib().orc_train_bpr_f64(g.ref, ptr(W), W.shape[1], alpha0, total, begin, end, seed)
+
+
+def train_bpr_f32(g, W, dim, alpha0, total, begin, end, seed, threads=1):
+    return lib().orc_train_bpr_f32(g.ref, ptr(W), dim, W.shape[1], alpha0, total, begin, end, seed, threads)
+
+
+def deepwalk_order(V, walk_times, rand_calls_before):
+    """Walk start order of DeepWalk::Train (src/model/DeepWalk.cpp:122-131):
+    per walk_time a Fisher-Yates pass with glibc rand(), continuing the rand()
+    stream after Init consumed `rand_calls_before` values."""
+    r = glibc_rand(rand_calls_before + walk_times * V)[rand_calls_before:]
+    order = np.zeros(walk_times * V, np.int64)
+    k = 0
+    for t in range(walk_times):
+        keys = np.arange(V, dtype=np.int64)
+        for vid in range(V):
+            rdx = vid + int(r[k]) % (V - vid)
+            k += 1
+            keys[vid], keys[rdx] = keys[rdx], keys[vid]
+        order[t * V:(t + 1) * V] = keys
+    return order
+
+
+def train_deepwalk_f64(g, W, C_, walk_times, walk_steps, window, K, alpha0, seed, order):
+    order = np.ascontiguousarray(order, np.int64)
+    return lib().orc_train_deepwalk_f64(g.ref, ptr(W), ptr(C_), W.shape[1], walk_times, walk_steps, window, K,
+                                        alpha0, seed, ptr(order))
+
+
+def train_deepwalk_f32(g, W, C_, dim, walk_times, walk_steps, window, K, alpha0, seed, order, begin=0, end=None):
+    order = np.ascontiguousarray(order, np.int64)
+    if end is None:
+        end = walk_times * g.V
+    return lib().orc_train_deepwalk_f32(g.ref, ptr(W), ptr(C_), dim, W.shape[1], walk_times, walk_steps, window,
+                                        K, alpha0, seed, ptr(order), begin, end)

@@ -1,0 +1,778 @@
+/*
+ * smore_oracle.c -- CPU restatement of SMORe's sampled negative-sampling SGD hot
+ * path (proNet alias samplers + Opt_SigmoidSGD / Opt_SGD / Opt_BPRSGD updates).
+ *
+ * TEST INFRASTRUCTURE ONLY (see smore_oracle.h).  Not shipped, not measured
+ * except as bench.py's cpu_baseline ("port").
+ *
+ * Reference citations are to RainBoltz/smore (C++ proNet-core, src/...).
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off -fopenmp).  No fast-math:
+ * the fp64 paths must reproduce the reference's sequential operation order.
+ */
+#include "smore_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ========================================================================== */
+/* RNG spec.  Philox4x32-10 (Salmon et al., SC'11; Random123 constants).       */
+/* word(seed, stream, unit, slot) = philox(ctr = {lo(unit), hi(unit),          */
+/*   slot/4, stream}, key = {lo(seed), hi(seed)})[slot % 4].                   */
+/* It replaces src/random.cpp:5-13 (thread_local mt19937 seeded by            */
+/* random_device), which is non-reproducible by construction.                 */
+/* ========================================================================== */
+#define PHILOX_M0 0xD2511F53u
+#define PHILOX_M1 0xCD9E8D57u
+#define PHILOX_W0 0x9E3779B9u
+#define PHILOX_W1 0xBB67AE85u
+
+void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+    uint32_t k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; ++r) {
+        if (r) { k0 += PHILOX_W0; k1 += PHILOX_W1; }
+        uint64_t p0 = (uint64_t)PHILOX_M0 * c0;
+        uint64_t p1 = (uint64_t)PHILOX_M1 * c2;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        c0 = hi1 ^ c1 ^ k0;
+        c1 = lo1;
+        c2 = hi0 ^ c3 ^ k1;
+        c3 = lo0;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+uint32_t orc_word(uint64_t seed, uint32_t stream, uint64_t unit, uint32_t slot) {
+    uint32_t ctr[4] = {(uint32_t)unit, (uint32_t)(unit >> 32), slot >> 2, stream};
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t o[4];
+    orc_philox4x32_10(ctr, key, o);
+    return o[slot & 3];
+}
+
+void orc_words(uint64_t seed, uint32_t stream, uint64_t unit, uint32_t nslots, uint32_t* out) {
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    for (uint32_t b = 0; b * 4 < nslots; ++b) {
+        uint32_t ctr[4] = {(uint32_t)unit, (uint32_t)(unit >> 32), b, stream};
+        uint32_t o[4];
+        orc_philox4x32_10(ctr, key, o);
+        for (uint32_t j = 0; j < 4 && b * 4 + j < nslots; ++j) out[b * 4 + j] = o[j];
+    }
+}
+
+/* index draw: floor(k * n / 2^32) -- the value the interposed random_gen(0, n)
+ * returns and the reference truncates to long (src/proNet.cpp:638,650,676). */
+static inline uint32_t draw_index(uint32_t k, uint64_t n) {
+    return (uint32_t)(((uint64_t)k * n) >> 32);
+}
+/* uniform draw u = k * 2^-32, exact in fp64 (random_gen(0,1)). */
+static inline double draw_unit(uint32_t k) { return ldexp((double)k, -32); }
+
+/* ========================================================================== */
+/* glibc rand(): TYPE_3 additive feedback generator, srand(1) default state.   */
+/* The reference initialises embeddings with rand() (src/model/LINE.cpp:83,    */
+/* src/model/BPR.cpp:49, src/model/MF.cpp:50, src/model/DeepWalk.cpp:47,54)    */
+/* and shuffles DeepWalk starts with it (src/model/DeepWalk.cpp:124-131).      */
+/* ========================================================================== */
+void orc_glibc_srand(orc_glibc_rand* st, uint32_t seed) {
+    int32_t r[344];
+    if (seed == 0) seed = 1;
+    r[0] = (int32_t)seed;
+    for (int i = 1; i < 31; ++i) {
+        /* Schrage: 16807 * r mod (2^31 - 1), as glibc srandom_r */
+        int32_t hi = r[i - 1] / 127773, lo = r[i - 1] % 127773;
+        int32_t word = 16807 * lo - 2836 * hi;
+        if (word < 0) word += 2147483647;
+        r[i] = word;
+    }
+    for (int i = 31; i < 34; ++i) r[i] = r[i - 31];
+    for (int i = 34; i < 344; ++i) r[i] = (int32_t)((uint32_t)r[i - 31] + (uint32_t)r[i - 3]);
+    for (int i = 0; i < 34; ++i) st->tbl[i] = (uint32_t)r[310 + i];
+    st->fptr = 0;
+}
+
+int32_t orc_glibc_rand_next(orc_glibc_rand* st) {
+    /* ring of the last 34 outputs: x[n] = x[n-31] + x[n-3] */
+    int n = st->fptr;                      /* position to write (mod 34) */
+    uint32_t v = st->tbl[(n + 34 - 31) % 34] + st->tbl[(n + 34 - 3) % 34];
+    st->tbl[n] = v;
+    st->fptr = (n + 1) % 34;
+    return (int32_t)(v >> 1);
+}
+
+void orc_glibc_rand_fill(uint32_t seed, int32_t* out, int64_t n) {
+    orc_glibc_rand st;
+    orc_glibc_srand(&st, seed);
+    for (int64_t i = 0; i < n; ++i) out[i] = orc_glibc_rand_next(&st);
+}
+
+/* ========================================================================== */
+/* Alias method.                                                               */
+/* ========================================================================== */
+
+/* C++ rule, src/proNet.cpp:544-620: q_i = d_i^0.75 * n / sum (the `power`
+ * argument is ignored, :558,564); LIFO small/large stacks (:570-603);
+ * leftovers get prob 1.0 and keep alias -1 (:605-617). */
+void orc_alias_cpp(const double* dist, int64_t n, double* prob, int64_t* alias) {
+    double sum = 0.0;
+    for (int64_t i = 0; i < n; ++i) sum += pow(dist[i], 0.75);
+    double norm = (double)n / sum;
+    double* q = (double*)malloc(sizeof(double) * (n ? n : 1));
+    int64_t* small = (int64_t*)malloc(sizeof(int64_t) * (n ? n : 1));
+    int64_t* large = (int64_t*)malloc(sizeof(int64_t) * (n ? n : 1));
+    int64_t ns = 0, nl = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        q[i] = pow(dist[i], 0.75) * norm;
+        alias[i] = -1;
+        prob[i] = 0.0;
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        if (q[i] < 1) small[ns++] = i; else large[nl++] = i;
+    }
+    while (ns && nl) {
+        int64_t s = small[--ns];
+        int64_t l = large[--nl];
+        alias[s] = l;
+        prob[s] = q[s];
+        q[l] = q[l] + q[s] - 1;
+        if (q[l] < 1) small[ns++] = l; else large[nl++] = l;
+    }
+    while (nl) prob[large[--nl]] = 1.0;
+    while (ns) prob[small[--ns]] = 1.0;
+    free(q); free(small); free(large);
+}
+
+/* Go rule, pkg/pronet/alias.go:10-90: q_i = d_i^power (0 for d_i <= 0),
+ * sum == 0 -> uniform; leftovers alias = self. */
+void orc_alias_go(const double* dist, int64_t n, double power, double* prob, int64_t* alias) {
+    double* q = (double*)malloc(sizeof(double) * (n ? n : 1));
+    int64_t* small = (int64_t*)malloc(sizeof(int64_t) * (n ? n : 1));
+    int64_t* large = (int64_t*)malloc(sizeof(int64_t) * (n ? n : 1));
+    int64_t ns = 0, nl = 0;
+    double sum = 0.0;
+    for (int64_t i = 0; i < n; ++i) {
+        q[i] = dist[i] > 0 ? pow(dist[i], power) : 0.0;
+        sum += q[i];
+        prob[i] = 0.0; alias[i] = 0;
+    }
+    if (sum == 0) {
+        for (int64_t i = 0; i < n; ++i) { prob[i] = 1.0; alias[i] = i; }
+        free(q); free(small); free(large);
+        return;
+    }
+    for (int64_t i = 0; i < n; ++i) q[i] = q[i] * (double)n / sum;
+    for (int64_t i = 0; i < n; ++i) { if (q[i] < 1.0) small[ns++] = i; else large[nl++] = i; }
+    while (ns && nl) {
+        int64_t l = small[--ns];
+        int64_t g = large[--nl];
+        prob[l] = q[l]; alias[l] = g;
+        q[g] = q[g] + q[l] - 1.0;
+        if (q[g] < 1.0) small[ns++] = g; else large[nl++] = g;
+    }
+    while (nl) { int64_t g = large[--nl]; prob[g] = 1.0; alias[g] = g; }
+    while (ns) { int64_t l = small[--ns]; prob[l] = 1.0; alias[l] = l; }
+    free(q); free(small); free(large);
+}
+
+/* Encode {prob, alias} as {accept threshold, alias id}: u < prob with
+ * u = k * 2^-32  <=>  k < ceil(prob * 2^32).  T >= 2^32 (always accept) is
+ * stored as {0xFFFFFFFF, self} so the draw never needs a 33-bit compare.
+ * self_ids == NULL: self = entry index; else self = self_ids[i] (context
+ * table: the entry's target vid).  alias -1 (C++ leftovers, prob 1) -> self. */
+void orc_alias_encode(const double* prob, const int64_t* alias, int64_t n,
+                      const int32_t* self_ids, uint32_t* thresh, int32_t* alias_out) {
+    for (int64_t i = 0; i < n; ++i) {
+        int32_t self = self_ids ? self_ids[i] : (int32_t)i;
+        double t = ceil(ldexp(prob[i], 32));
+        if (!(t >= 0)) t = 0;                      /* NaN guard: never accept */
+        if (t >= 4294967296.0) {
+            thresh[i] = 0xFFFFFFFFu;
+            alias_out[i] = self;
+        } else {
+            thresh[i] = (uint32_t)t;
+            alias_out[i] = alias[i] < 0 ? self : (int32_t)alias[i];
+        }
+    }
+}
+
+/* ========================================================================== */
+/* Graph build, src/proNet.cpp:410-542 (BuildAliasMethod).                    */
+/* Input: directed edge slots in the reference's push order (per input line:   */
+/* v1->v2, then v2->v1 if undirected, src/proNet.cpp:208-215).                 */
+/* CSR: vertex[v].offset/branch with targets in push order (:417-446).         */
+/* ========================================================================== */
+int orc_build_graph(int64_t V, int64_t E, const int32_t* src, const int32_t* dst,
+                    const double* w, int vertex_method, int negative_method,
+                    int64_t* offsets, int32_t* targets, double* out_deg, double* in_deg,
+                    double* vprob, int64_t* valias, double* nprob, int64_t* nalias,
+                    double* cprob, int64_t* calias) {
+    int64_t* cnt = (int64_t*)calloc((size_t)V + 1, sizeof(int64_t));
+    double* ew = (double*)malloc(sizeof(double) * (E ? E : 1));
+    for (int64_t e = 0; e < E; ++e) {
+        if (src[e] < 0 || src[e] >= V || dst[e] < 0 || dst[e] >= V) { free(cnt); free(ew); return -1; }
+        cnt[src[e] + 1]++;
+    }
+    offsets[0] = 0;
+    for (int64_t v = 0; v < V; ++v) offsets[v + 1] = offsets[v] + cnt[v + 1];
+    for (int64_t v = 0; v <= V; ++v) cnt[v] = offsets[v < V ? v : V];
+    for (int64_t e = 0; e < E; ++e) {           /* stable: keeps push order per source */
+        int64_t p = cnt[src[e]]++;
+        targets[p] = dst[e];
+        ew[p] = w[e];
+    }
+    /* degrees: out_degree summed in adjacency order (:431-436), in_degree by a
+     * pass over the context array in CSR order (:439-443) */
+    for (int64_t v = 0; v < V; ++v) { out_deg[v] = 0.0; in_deg[v] = 0.0; }
+    for (int64_t v = 0; v < V; ++v)
+        for (int64_t p = offsets[v]; p < offsets[v + 1]; ++p) out_deg[v] += ew[p];
+    for (int64_t p = 0; p < E; ++p) in_deg[targets[p]] += ew[p];
+
+    double* dist = (double*)malloc(sizeof(double) * (V ? V : 1));
+    /* vertex table (:457-482) */
+    for (int64_t v = 0; v < V; ++v) {
+        if (vertex_method == ORC_VM_OUT_DEGREES) dist[v] = out_deg[v];
+        else if (vertex_method == ORC_VM_NO_DEGREES) dist[v] = out_deg[v] == 0 ? 0 : 1;
+        else dist[v] = in_deg[v] + out_deg[v];
+    }
+    orc_alias_cpp(dist, V, vprob, valias);
+    /* negative table (:485-510) */
+    for (int64_t v = 0; v < V; ++v) {
+        if (negative_method == ORC_NM_DEGREES) dist[v] = in_deg[v] + out_deg[v];
+        else if (negative_method == ORC_NM_IN_DEGREES) dist[v] = in_deg[v];
+        else dist[v] = in_deg[v] == 0 ? 0 : 1;
+    }
+    orc_alias_cpp(dist, V, nprob, nalias);
+    free(dist);
+    /* per-vertex context tables, alias remapped to the target vid (:517-537) */
+    for (int64_t v = 0; v < V; ++v) {
+        int64_t off = offsets[v], br = offsets[v + 1] - offsets[v];
+        if (br == 0) continue;
+        orc_alias_cpp(ew + off, br, cprob + off, calias + off);
+        for (int64_t i = 0; i < br; ++i)
+            if (calias[off + i] != -1) calias[off + i] = targets[off + calias[off + i]];
+    }
+    free(cnt); free(ew);
+    return 0;
+}
+
+/* ========================================================================== */
+/* Samplers.                                                                   */
+/* ========================================================================== */
+/* SourceSample src/proNet.cpp:647-657: p first, then index. */
+static inline int32_t source_sample(const orc_graph* g, uint32_t kp, uint32_t ki) {
+    uint32_t i = draw_index(ki, (uint64_t)g->V);
+    return kp < g->vthr[i] ? (int32_t)i : g->valias[i];
+}
+/* TargetSample(vid) src/proNet.cpp:671-683: branch 0 -> -1; p first. */
+static inline int32_t target_sample(const orc_graph* g, int32_t v, uint32_t kp, uint32_t ki) {
+    int64_t off = g->offsets[v], br = g->offsets[v + 1] - off;
+    if (br == 0) return -1;
+    int64_t i = off + draw_index(ki, (uint64_t)br);
+    return kp < g->cthr[i] ? g->targets[i] : g->calias[i];
+}
+/* NegativeSample src/proNet.cpp:623-633: index FIRST, then p. */
+static inline int32_t negative_sample(const orc_graph* g, uint32_t ki, uint32_t kp) {
+    uint32_t i = draw_index(ki, (uint64_t)g->V);
+    return kp < g->nthr[i] ? (int32_t)i : g->nalias[i];
+}
+
+#define MAX_SLOTS 256
+/* LINE/MF sample slot layout: 0 src p, 1 src i, 2 tgt p, 3 tgt i,
+ * 4+2j neg_j i, 5+2j neg_j p. */
+void orc_sample_line(const orc_graph* g, uint64_t seed, uint64_t begin, uint64_t count,
+                     int K, int32_t* out) {
+    uint32_t w[MAX_SLOTS];
+    for (uint64_t t = 0; t < count; ++t) {
+        uint64_t s = begin + t;
+        orc_words(seed, 0, s, 4 + 2 * K, w);
+        int32_t* o = out + t * (2 + K);
+        int32_t v = source_sample(g, w[0], w[1]);
+        o[0] = v;
+        o[1] = target_sample(g, v, w[2], w[3]);
+        for (int j = 0; j < K; ++j) o[2 + j] = negative_sample(g, w[4 + 2 * j], w[5 + 2 * j]);
+    }
+}
+
+/* BPR slot layout: 0-3 as LINE, 4-5 neg j0 (i,p), 6+2r/7+2r round r+1 neg. */
+void orc_sample_bpr(const orc_graph* g, uint64_t seed, uint64_t begin, uint64_t count,
+                    int32_t* out) {
+    uint32_t w[16];
+    for (uint64_t t = 0; t < count; ++t) {
+        uint64_t s = begin + t;
+        orc_words(seed, 0, s, 14, w);
+        int32_t* o = out + t * 7;
+        int32_t u = source_sample(g, w[0], w[1]);
+        o[0] = u;
+        o[1] = target_sample(g, u, w[2], w[3]);
+        for (int j = 0; j < 5; ++j) o[2 + j] = negative_sample(g, w[4 + 2 * j], w[5 + 2 * j]);
+    }
+}
+
+/* ========================================================================== */
+/* fastSigmoid, src/proNet.cpp:52-71 (table of 1001 entries; the reference     */
+/* allocates 1000, :54, and writes/reads index 1000 -- the Go port sizes 1001, */
+/* pkg/pronet/pronet.go:81).                                                   */
+/* ========================================================================== */
+void orc_sigmoid_table(double* tab) {
+    for (int i = 0; i != 1000 + 1; i++) {
+        double x = i * 2.0 * 8.0 / 1000 - 8.0;
+        tab[i] = 1.0 / (1.0 + exp(-x));
+    }
+}
+
+static double g_sig64[1001];
+static float g_sig32[1001];
+static int g_sig_init = 0;
+static void sig_init(void) {
+    if (g_sig_init) return;
+    orc_sigmoid_table(g_sig64);
+    for (int i = 0; i < 1001; ++i) g_sig32[i] = (float)g_sig64[i];
+    g_sig_init = 1;
+}
+
+static inline int sig_index(double x) { return (int)((x + 8.0) * 1000 / 8.0 / 2); }
+
+double orc_fast_sigmoid(double x) {
+    sig_init();
+    if (x < -8.0) return 0.0;
+    if (x > 8.0) return 1.0;
+    return g_sig64[sig_index(x)];
+}
+
+/* fp32 spec: f is an fp32 dot; the bucket index is evaluated in fp64 exactly
+ * as the reference expression. */
+static inline float fast_sigmoid_f32(float f) {
+    double x = (double)f;
+    if (x < -8.0) return 0.0f;
+    if (x > 8.0) return 1.0f;
+    return g_sig32[sig_index(x)];
+}
+
+/* ========================================================================== */
+/* Learning-rate schedules.                                                    */
+/* LINE/MF/BPR (src/model/LINE.cpp:166-187, MF.cpp:85-101, BPR.cpp:84-101):    */
+/* the sample run with counter value c uses alpha0 while c < 10^4, then        */
+/* alpha0 * (1 - cs/total) with cs = (floor(c/10^4) - 1) * 10^4, floored at    */
+/* alpha0 * 1e-4.  LINE's counter starts at 1, MF/BPR's at 0.                  */
+/* DeepWalk (src/model/DeepWalk.cpp:137-147): walk w uses                       */
+/* alpha0 * (1 - floor(w/10^4)*10^4 / total).                                  */
+/* ========================================================================== */
+double orc_alpha_line(uint64_t c, double alpha0, uint64_t total) {
+    uint64_t u = c / 10000;
+    if (u == 0) return alpha0;
+    uint64_t cs = (u - 1) * 10000;
+    double a = alpha0 * (1.0 - (double)cs / total);
+    double amin = alpha0 * 0.0001;
+    if (a < amin) a = amin;
+    return a;
+}
+
+double orc_alpha_walk(uint64_t w, double alpha0, uint64_t total) {
+    uint64_t u = w / 10000;
+    if (u == 0) return alpha0;
+    double a = alpha0 * (1.0 - (double)(u * 10000) / total);
+    double amin = alpha0 * 0.0001;
+    if (a < amin) a = amin;
+    return a;
+}
+
+/* ========================================================================== */
+/* fp64 training: the reference's arithmetic.                                   */
+/* ========================================================================== */
+
+/* Opt_SigmoidSGD, src/proNet.cpp:1312-1330 (loss_context aliases w_context). */
+static void opt_sigmoid_sgd_f64(const double* wv, double* wc, double label, int dim,
+                                double alpha, double* err) {
+    double f = 0, g;
+    for (int d = 0; d < dim; ++d) f += wv[d] * wc[d];
+    f = orc_fast_sigmoid(f);
+    g = (label - f) * alpha;
+    for (int d = 0; d < dim; ++d) err[d] += g * wc[d];
+    for (int d = 0; d < dim; ++d) wc[d] += g * wv[d];
+}
+
+/* Opt_SGD, src/proNet.cpp:991-1012 (linear, L2 reg). */
+static void opt_sgd_f64(const double* wv, double* wc, double label, double alpha, double reg,
+                        int dim, double* err) {
+    double f = 0, g;
+    for (int d = 0; d < dim; ++d) f += wv[d] * wc[d];
+    g = (label - f);
+    for (int d = 0; d < dim; ++d) err[d] += alpha * (g * wc[d] - reg * wv[d]);
+    for (int d = 0; d < dim; ++d) wc[d] += alpha * (g * wv[d] - reg * wc[d]);
+}
+
+/* One LINE-2 / LINE-1 / MF sample with the reference's arithmetic:
+ * UpdatePair src/proNet.cpp:1784-1809, UpdateFactorizedPair :2591-2614. */
+static void update_edge_f64(int model, double* W, double* C, int dim, int32_t v, int32_t c,
+                            const int32_t* negs, int K, double alpha, double reg, double* err) {
+    double* wv = W + (int64_t)v * dim;
+    double* T = (model == 0) ? C : W;             /* context table */
+    for (int d = 0; d < dim; ++d) err[d] = 0.0;
+    if (model == 2) {
+        opt_sgd_f64(wv, T + (int64_t)c * dim, 1.0, alpha, reg, dim, err);
+        for (int j = 0; j < K; ++j) opt_sgd_f64(wv, T + (int64_t)negs[j] * dim, -1.0, alpha, reg, dim, err);
+    } else {
+        opt_sigmoid_sgd_f64(wv, T + (int64_t)c * dim, 1.0, dim, alpha, err);
+        for (int j = 0; j < K; ++j) opt_sigmoid_sgd_f64(wv, T + (int64_t)negs[j] * dim, 0.0, dim, alpha, err);
+    }
+    for (int d = 0; d < dim; ++d) wv[d] += err[d];
+}
+
+/* Driver loops: LINE::Train src/model/LINE.cpp:160-191 (count from 1),
+ * MF::Train src/model/MF.cpp:78-101 (count from 0).  Samples [begin, end) of
+ * the global sample index s; counter value c = s + (LINE ? 1 : 0). */
+int orc_train_edge_f64(const orc_graph* g, int model, double* W, double* C, int dim,
+                       int K, double alpha0, double reg, uint64_t total, uint64_t begin,
+                       uint64_t end, uint64_t seed) {
+    sig_init();
+    double* err = (double*)malloc(sizeof(double) * dim);
+    uint32_t w[MAX_SLOTS];
+    int32_t negs[MAX_SLOTS];
+    int skipped = 0;
+    uint64_t base = (model == 2) ? 0 : 1;
+    for (uint64_t s = begin; s < end; ++s) {
+        orc_words(seed, 0, s, 4 + 2 * K, w);
+        int32_t v = source_sample(g, w[0], w[1]);
+        int32_t c = target_sample(g, v, w[2], w[3]);
+        if (c < 0) { skipped++; continue; }       /* reference: UB (index -1) */
+        for (int j = 0; j < K; ++j) negs[j] = negative_sample(g, w[4 + 2 * j], w[5 + 2 * j]);
+        double alpha = orc_alpha_line(s + base, alpha0, total);
+        update_edge_f64(model, W, C, dim, v, c, negs, K, alpha, reg, err);
+    }
+    free(err);
+    return skipped;
+}
+
+/* UpdateBPRPair src/proNet.cpp:1406-1455 with Opt_BPRSGD :1053-1068; one
+ * shared table (BPR::Train passes w_vertex twice, src/model/BPR.cpp:91). */
+static void update_bpr_f64(double* W, int dim, int32_t u, int32_t i, const int32_t* js,
+                           double alpha, double* verr, double* cerr, double* x) {
+    for (int d = 0; d < dim; ++d) verr[d] = 0.0;
+    double* wu = W + (int64_t)u * dim;
+    double* wi = W + (int64_t)i * dim;
+    for (int n = 0; n < 5; ++n) {
+        double* wj = W + (int64_t)js[n] * dim;
+        for (int d = 0; d < dim; ++d) { cerr[d] = 0.0; x[d] = wi[d] - wj[d]; }
+        double f = 0, g;
+        for (int d = 0; d < dim; ++d) f += wu[d] * x[d];
+        g = orc_fast_sigmoid(0.0 - f) * alpha;
+        for (int d = 0; d < dim; ++d) verr[d] += g * x[d];
+        for (int d = 0; d < dim; ++d) cerr[d] += g * wu[d];
+        for (int d = 0; d < dim; ++d) {
+            wi[d] -= alpha * 0.0025 * wi[d];
+            wj[d] -= alpha * 0.0025 * wj[d];
+            wi[d] += cerr[d];
+            wj[d] -= cerr[d];
+        }
+    }
+    for (int d = 0; d < dim; ++d) {
+        wu[d] -= alpha * 0.025 * wu[d];
+        wu[d] += verr[d];
+    }
+}
+
+/* BPR::Train src/model/BPR.cpp:77-101 (count from 0). */
+int orc_train_bpr_f64(const orc_graph* g, double* W, int dim, double alpha0, uint64_t total,
+                      uint64_t begin, uint64_t end, uint64_t seed) {
+    sig_init();
+    double* buf = (double*)malloc(sizeof(double) * dim * 3);
+    uint32_t w[16];
+    int32_t js[5];
+    int skipped = 0;
+    for (uint64_t s = begin; s < end; ++s) {
+        orc_words(seed, 0, s, 14, w);
+        int32_t u = source_sample(g, w[0], w[1]);
+        int32_t i = target_sample(g, u, w[2], w[3]);
+        if (i < 0) { skipped++; continue; }
+        for (int j = 0; j < 5; ++j) js[j] = negative_sample(g, w[4 + 2 * j], w[5 + 2 * j]);
+        double alpha = orc_alpha_line(s, alpha0, total);
+        update_bpr_f64(W, dim, u, i, js, alpha, buf, buf + dim, buf + 2 * dim);
+    }
+    free(buf);
+    return skipped;
+}
+
+/* ---- DeepWalk ---------------------------------------------------------------
+ * Walk w (global index t*V + i over walk_times t and shuffled position i)
+ * draws from stream 1, unit w, consecutive slots:
+ *   RandomWalk  src/proNet.cpp:704-724: 2 per step taken (p, i);
+ *   SkipGrams   src/proNet.cpp:769-809: 1 per walk position (window shrink);
+ *   UpdatePairs src/proNet.cpp:2741-2753 -> UpdatePair: 2 per negative (i, p).
+ */
+typedef struct { uint64_t seed, unit; uint32_t slot; uint32_t buf[4]; uint32_t bufblk; } walk_rng;
+static inline uint32_t walk_next(walk_rng* r) {
+    uint32_t blk = r->slot >> 2;
+    if (blk != r->bufblk) {
+        uint32_t ctr[4] = {(uint32_t)r->unit, (uint32_t)(r->unit >> 32), blk, 1u};
+        uint32_t key[2] = {(uint32_t)r->seed, (uint32_t)(r->seed >> 32)};
+        orc_philox4x32_10(ctr, key, r->buf);
+        r->bufblk = blk;
+    }
+    return r->buf[r->slot++ & 3];
+}
+
+static int random_walk(const orc_graph* g, walk_rng* r, int32_t start, int steps, int32_t* walk) {
+    int L = 0;
+    int32_t next = start;
+    walk[L++] = next;
+    for (int s = 0; s < steps; ++s) {
+        if (g->offsets[next + 1] - g->offsets[next] == 0) {
+            if (next == start) return L;
+            next = start;
+        }
+        uint32_t kp = walk_next(r), ki = walk_next(r);
+        next = target_sample(g, next, kp, ki);
+        walk[L++] = next;
+    }
+    return L;
+}
+
+/* pairs of SkipGrams(walk, window, 0); returns count */
+static int skip_grams(walk_rng* r, const int32_t* walk, int L, int window, int32_t* pv, int32_t* pc) {
+    int n = 0;
+    for (int i = 0; i < L; ++i) {
+        int reduce = (int)draw_index(walk_next(r), (uint64_t)window) + 1;
+        int left = i - reduce; if (left < 0) left = 0;
+        int right = i + reduce; if (right >= L) right = L - 1;
+        for (int j = left; j <= right; ++j) {
+            if (i == j) continue;
+            pv[n] = walk[i]; pc[n] = walk[j]; n++;
+        }
+    }
+    return n;
+}
+
+int orc_train_deepwalk_f64(const orc_graph* g, double* W, double* C, int dim,
+                           int walk_times, int walk_steps, int window, int K,
+                           double alpha0, uint64_t seed, const int64_t* order) {
+    sig_init();
+    int64_t V = g->V;
+    uint64_t total = (uint64_t)walk_times * (uint64_t)V;
+    int32_t* walk = (int32_t*)malloc(sizeof(int32_t) * (walk_steps + 1));
+    int maxp = 2 * window * (walk_steps + 1) + 1;
+    int32_t* pv = (int32_t*)malloc(sizeof(int32_t) * maxp);
+    int32_t* pc = (int32_t*)malloc(sizeof(int32_t) * maxp);
+    int32_t negs[MAX_SLOTS];
+    double* err = (double*)malloc(sizeof(double) * dim);
+    for (uint64_t w = 0; w < total; ++w) {
+        walk_rng r = {seed, w, 0, {0, 0, 0, 0}, 0xFFFFFFFFu};
+        double alpha = orc_alpha_walk(w, alpha0, total);
+        int L = random_walk(g, &r, (int32_t)order[w], walk_steps, walk);
+        int np = skip_grams(&r, walk, L, window, pv, pc);
+        for (int p = 0; p < np; ++p) {
+            for (int j = 0; j < K; ++j) {
+                uint32_t ki = walk_next(&r), kp = walk_next(&r);
+                negs[j] = negative_sample(g, ki, kp);
+            }
+            update_edge_f64(0, W, C, dim, pv[p], pc[p], negs, K, alpha, 0.0, err);
+        }
+    }
+    free(walk); free(pv); free(pc); free(err);
+    return 0;
+}
+
+/* ========================================================================== */
+/* fp32 spec (DESIGN.md "Arithmetic spec"), what the HIP kernels compute.      */
+/* Rows are padded to dpad (multiple of 4) floats.  A sample is owned by G      */
+/* lanes (G = min(64, pow2ceil(dpad/4))); lane l owns 4-float chunks q with     */
+/* q % G == l.  dot = pairwise tree over the G lane partials, each an fmaf     */
+/* chain over its chunks in increasing element order starting from +0.0f.      */
+/* ========================================================================== */
+int orc_lane_width(int dpad) {
+    int nq = dpad / 4, G = 1;
+    while (G < nq && G < 64) G <<= 1;
+    return G;
+}
+
+static float dot_spec(const float* a, const float* b, int dpad) {
+    float part[64];
+    int G = orc_lane_width(dpad), nq = dpad / 4;
+    for (int l = 0; l < G; ++l) part[l] = 0.0f;
+    for (int q = 0; q < nq; ++q) {
+        int l = q % G;
+        for (int e = 4 * q; e < 4 * q + 4; ++e) part[l] = fmaf(a[e], b[e], part[l]);
+    }
+    for (int w = 1; w < G; w <<= 1)
+        for (int l = 0; l < G; l += 2 * w) part[l] = part[l] + part[l + w];
+    return part[0];
+}
+
+/* fp32 LINE-2 / LINE-1 / MF sample.  Per element, in this order:
+ *   sigmoid rule (UpdatePair):  g = (label - sig(f)) * alpha
+ *                               e = fmaf(g, c, e);  c = fmaf(g, wv, c)
+ *   MF rule (Opt_SGD):          g = label - f
+ *                               e = fmaf(alpha, g*c - reg*wv, e)
+ *                               c = fmaf(alpha, g*wv - reg*c, c)
+ *   end:                        wv = wv + e
+ * Rows are updated in place, so a repeated id (negative == positive, or
+ * v == c in a shared table) sees the earlier update exactly as the
+ * reference's in-place vector<double> update does. */
+static void update_edge_f32(int model, float* W, float* C, int dpad, int32_t v, int32_t c,
+                            const int32_t* negs, int K, float alpha, float reg, float* e) {
+    float* wv = W + (int64_t)v * dpad;
+    float* T = (model == 0) ? C : W;
+    for (int d = 0; d < dpad; ++d) e[d] = 0.0f;
+    for (int j = -1; j < K; ++j) {
+        int32_t id = j < 0 ? c : negs[j];
+        float* cr = T + (int64_t)id * dpad;
+        float f = dot_spec(wv, cr, dpad);
+        if (model == 2) {
+            float label = j < 0 ? 1.0f : -1.0f;
+            float gg = label - f;
+            for (int d = 0; d < dpad; ++d) {
+                float ce = cr[d], we = wv[d];
+                float t1 = gg * ce - reg * we;
+                float t2 = gg * we - reg * ce;
+                e[d] = fmaf(alpha, t1, e[d]);
+                cr[d] = fmaf(alpha, t2, ce);
+            }
+        } else {
+            float label = j < 0 ? 1.0f : 0.0f;
+            float gg = (label - fast_sigmoid_f32(f)) * alpha;
+            for (int d = 0; d < dpad; ++d) {
+                float ce = cr[d], we = wv[d];
+                e[d] = fmaf(gg, ce, e[d]);
+                cr[d] = fmaf(gg, we, ce);
+            }
+        }
+    }
+    for (int d = 0; d < dpad; ++d) wv[d] = wv[d] + e[d];
+}
+
+int orc_train_edge_f32(const orc_graph* g, int model, float* W, float* C, int dim,
+                       int dpad, int K, double alpha0, double reg, uint64_t total,
+                       uint64_t begin, uint64_t end, uint64_t seed, int threads) {
+    (void)dim;
+    sig_init();
+    uint64_t base = (model == 2) ? 0 : 1;
+    int skipped = 0;
+    if (threads <= 1) {
+        float* e = (float*)malloc(sizeof(float) * dpad);
+        uint32_t w[MAX_SLOTS];
+        int32_t negs[MAX_SLOTS];
+        for (uint64_t s = begin; s < end; ++s) {
+            orc_words(seed, 0, s, 4 + 2 * K, w);
+            int32_t v = source_sample(g, w[0], w[1]);
+            int32_t c = target_sample(g, v, w[2], w[3]);
+            if (c < 0) { skipped++; continue; }
+            for (int j = 0; j < K; ++j) negs[j] = negative_sample(g, w[4 + 2 * j], w[5 + 2 * j]);
+            float alpha = (float)orc_alpha_line(s + base, alpha0, total);
+            update_edge_f32(model, W, C, dpad, v, c, negs, K, alpha, (float)reg, e);
+        }
+        free(e);
+        return skipped;
+    }
+#ifdef _OPENMP
+    /* Hogwild CPU baseline: the reference's OpenMP structure
+     * (src/model/LINE.cpp:162, racy shared rows), contiguous sample blocks. */
+    #pragma omp parallel num_threads(threads) reduction(+:skipped)
+    {
+        float* e = (float*)malloc(sizeof(float) * dpad);
+        uint32_t w[MAX_SLOTS];
+        int32_t negs[MAX_SLOTS];
+        #pragma omp for schedule(static)
+        for (int64_t si = (int64_t)begin; si < (int64_t)end; ++si) {
+            uint64_t s = (uint64_t)si;
+            orc_words(seed, 0, s, 4 + 2 * K, w);
+            int32_t v = source_sample(g, w[0], w[1]);
+            int32_t c = target_sample(g, v, w[2], w[3]);
+            if (c < 0) { skipped++; continue; }
+            for (int j = 0; j < K; ++j) negs[j] = negative_sample(g, w[4 + 2 * j], w[5 + 2 * j]);
+            float alpha = (float)orc_alpha_line(s + base, alpha0, total);
+            update_edge_f32(model, W, C, dpad, v, c, negs, K, alpha, (float)reg, e);
+        }
+        free(e);
+    }
+#endif
+    return skipped;
+}
+
+/* fp32 BPR (UpdateBPRPair, src/proNet.cpp:1406-1455).  Per round n, element
+ * order as the reference's d-loop:
+ *   x = wi - wj;  f = dot(wu, x);  g = sig(0 - f) * alpha   (0-f in fp64 == -f)
+ *   ve = fmaf(g, x, ve);  ce = g * wu
+ *   wi = fmaf(-r1, wi, wi); wj = fmaf(-r1, wj, wj); wi = wi + ce; wj = wj - ce
+ * with r1 = alpha * 0.0025f; end: wu = fmaf(-r2, wu, wu) + ve, r2 = alpha*0.025f. */
+static void update_bpr_f32(float* W, int dpad, int32_t u, int32_t i, const int32_t* js,
+                           float alpha, float* ve, float* x, float* ce) {
+    float* wu = W + (int64_t)u * dpad;
+    float* wi = W + (int64_t)i * dpad;
+    float r1 = alpha * 0.0025f, r2 = alpha * 0.025f;
+    for (int d = 0; d < dpad; ++d) ve[d] = 0.0f;
+    for (int n = 0; n < 5; ++n) {
+        float* wj = W + (int64_t)js[n] * dpad;
+        for (int d = 0; d < dpad; ++d) x[d] = wi[d] - wj[d];
+        float f = dot_spec(wu, x, dpad);
+        float gg = fast_sigmoid_f32(-f) * alpha;
+        for (int d = 0; d < dpad; ++d) { ve[d] = fmaf(gg, x[d], ve[d]); ce[d] = gg * wu[d]; }
+        for (int d = 0; d < dpad; ++d) {
+            wi[d] = fmaf(-r1, wi[d], wi[d]);
+            wj[d] = fmaf(-r1, wj[d], wj[d]);
+            wi[d] = wi[d] + ce[d];
+            wj[d] = wj[d] - ce[d];
+        }
+    }
+    for (int d = 0; d < dpad; ++d) wu[d] = fmaf(-r2, wu[d], wu[d]) + ve[d];
+}
+
+int orc_train_bpr_f32(const orc_graph* g, float* W, int dim, int dpad, double alpha0,
+                      uint64_t total, uint64_t begin, uint64_t end, uint64_t seed, int threads) {
+    (void)dim;
+    sig_init();
+    int skipped = 0;
+    #pragma omp parallel num_threads(threads > 1 ? threads : 1) reduction(+:skipped)
+    {
+        float* buf = (float*)malloc(sizeof(float) * dpad * 3);
+        uint32_t w[16];
+        int32_t js[5];
+        #pragma omp for schedule(static)
+        for (int64_t si = (int64_t)begin; si < (int64_t)end; ++si) {
+            uint64_t s = (uint64_t)si;
+            orc_words(seed, 0, s, 14, w);
+            int32_t u = source_sample(g, w[0], w[1]);
+            int32_t i = target_sample(g, u, w[2], w[3]);
+            if (i < 0) { skipped++; continue; }
+            for (int j = 0; j < 5; ++j) js[j] = negative_sample(g, w[4 + 2 * j], w[5 + 2 * j]);
+            float alpha = (float)orc_alpha_line(s, alpha0, total);
+            update_bpr_f32(W, dpad, u, i, js, alpha, buf, buf + dpad, buf + 2 * dpad);
+        }
+        free(buf);
+    }
+    return skipped;
+}
+
+int orc_train_deepwalk_f32(const orc_graph* g, float* W, float* C, int dim, int dpad,
+                           int walk_times, int walk_steps, int window, int K,
+                           double alpha0, uint64_t seed, const int64_t* order,
+                           uint64_t walk_begin, uint64_t walk_end) {
+    (void)dim;
+    sig_init();
+    uint64_t total = (uint64_t)walk_times * (uint64_t)g->V;
+    if (walk_end > total) walk_end = total;
+    int32_t* walk = (int32_t*)malloc(sizeof(int32_t) * (walk_steps + 1));
+    int maxp = 2 * window * (walk_steps + 1) + 1;
+    int32_t* pv = (int32_t*)malloc(sizeof(int32_t) * maxp);
+    int32_t* pc = (int32_t*)malloc(sizeof(int32_t) * maxp);
+    int32_t negs[MAX_SLOTS];
+    float* e = (float*)malloc(sizeof(float) * dpad);
+    for (uint64_t w = walk_begin; w < walk_end; ++w) {
+        walk_rng r = {seed, w, 0, {0, 0, 0, 0}, 0xFFFFFFFFu};
+        float alpha = (float)orc_alpha_walk(w, alpha0, total);
+        int L = random_walk(g, &r, (int32_t)order[w], walk_steps, walk);
+        int np = skip_grams(&r, walk, L, window, pv, pc);
+        for (int p = 0; p < np; ++p) {
+            for (int j = 0; j < K; ++j) {
+                uint32_t ki = walk_next(&r), kp = walk_next(&r);
+                negs[j] = negative_sample(g, ki, kp);
+            }
+            update_edge_f32(0, W, C, dpad, pv[p], pc[p], negs, K, alpha, 0.0f, e);
+        }
+    }
+    free(walk); free(pv); free(pc); free(e);
+    return 0;
+}
