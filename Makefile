@@ -1,0 +1,59 @@
+# Build of the MI355X (gfx950) hot path.  No cmake: plain make + hipcc.
+#   make            -> smore_amd/lib/libsmore_hip.so + smore_amd/bin/{line,bpr,mf,deepwalk}
+#   make oracle     -> oracle/build/liboracle.so (test infrastructure)
+#   make ref        -> oracle/_ref/ref_harness (needs /root/reference)
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+CXXFLAGS := -std=c++17 -O3 -fPIC -ffp-contract=off -Wall -Wno-unused-function
+HIPFLAGS := $(CXXFLAGS) --offload-arch=$(ARCH) -Wno-pass-failed
+SRC      := smore_amd/csrc
+OBJ      := build/obj
+LIB      := smore_amd/lib/libsmore_hip.so
+BIN      := smore_amd/bin
+HDRS     := $(wildcard $(SRC)/*.h) include/smore_hip.h
+
+.PHONY: all lib cli oracle ref clean
+all: lib cli
+
+lib: $(LIB)
+
+$(OBJ)/host_graph.o: $(SRC)/host_graph.cpp $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(CXXFLAGS) -c -o $@ $<
+
+$(OBJ)/capi.o: $(SRC)/capi.cpp $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(CXXFLAGS) -c -o $@ $<
+
+$(OBJ)/train_kernels.o: $(SRC)/train_kernels.hip $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(OBJ)/walk_kernels.o: $(SRC)/walk_kernels.hip $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+LIB_OBJS := $(OBJ)/host_graph.o $(OBJ)/capi.o $(OBJ)/train_kernels.o $(wildcard $(SRC)/walk_kernels.hip:%=)
+ifneq ($(wildcard $(SRC)/walk_kernels.hip),)
+LIB_OBJS += $(OBJ)/walk_kernels.o
+endif
+
+$(LIB): $(LIB_OBJS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread
+
+CLIS := $(patsubst $(SRC)/cli/%.cpp,$(BIN)/%,$(wildcard $(SRC)/cli/*.cpp))
+cli: $(CLIS)
+
+$(BIN)/%: $(SRC)/cli/%.cpp $(SRC)/cli/cli_common.h $(LIB)
+	@mkdir -p $(BIN)
+	g++ -std=c++17 -O2 -Wall -Iinclude -o $@ $< -L$(dir $(LIB)) -lsmore_hip -Wl,-rpath,'$$ORIGIN/../lib'
+
+oracle:
+	$(MAKE) -C oracle
+
+ref:
+	$(MAKE) -C oracle ref
+
+clean:
+	rm -rf build smore_amd/lib smore_amd/bin

@@ -1,0 +1,187 @@
+#!/usr/bin/env python3
+"""Benchmark: LINE order-2 edge-updates/s on MI355X (BASELINE.json metric).
+
+A "step" is one launch of the fused sample->gather->update kernel over
+`--samples` edge samples (default 2^27) of the synthetic power-law graph of
+config c2 (1M vertices / 20M undirected lines = 40M directed slots, d=64,
+K=5), inputs resident in HBM.  One process per GPU; with N > 1
+each rank runs its own disjoint global-sample range on a replicated graph and
+replicated tables, and the tables' deltas are all-reduced over RCCL every
+`--sync-every` steps (weak scaling).  Rank 0 prints one JSON line.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def algorithmic_bytes(dim, K):
+    """R = (2+K)*d*4 + 8 (vertex alias) + 16 (offset pair)
+    + 8 (context alias) + 4 (target vid) + 8K (negative alias); W = (2+K)*d*4."""
+    rows = (2 + K) * dim * 4
+    return rows + 36 + 8 * K, rows
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--negative", type=int, default=5)
+    ap.add_argument("--samples", type=int, default=1 << 27, help="edge samples per step per GPU")
+    ap.add_argument("--mode", default="hogwild", choices=["hogwild", "atomic"])
+    ap.add_argument("--sync-every", type=int, default=1)
+    ap.add_argument("--sync", default="sum", choices=["sum", "mean"])
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--seed", type=int, default=20251015)
+    return ap.parse_args()
+
+
+def cpu_baseline(V, src, dst, w, dim, K, seconds):
+    """The oracle's fp32 spec with OpenMP Hogwild threads on this host (the
+    reference sources do not travel to the GPU box), bounded in time."""
+    from oracle import oracle as orc
+    threads = min(16, os.cpu_count() or 1)
+    g = orc.Graph(V, src, dst, w)
+    dpad = (dim + 3) // 4 * 4
+    W = ((np.random.default_rng(1).random((V, dpad), dtype=np.float32) - 0.5) / dim).astype(np.float32)
+    W[:, dim:] = 0
+    C = np.zeros_like(W)
+    total = 1 << 40
+    chunk, done, t0 = 2_000_000, 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        orc.train_edge_f32(g, "line2", W, C, dim, K, 0.025, 0.0, total, done, done + chunk, 7, threads)
+        done += chunk
+    el = time.perf_counter() - t0
+    return {"value": round(done / el / 1e6, 4), "unit": "M edge-updates/s", "cores": threads, "kind": "port",
+            "sample": "%d LINE-2 samples (d=%d, K=%d) on the same c2 graph, %d OpenMP Hogwild threads, %.1f s"
+                      % (done, dim, K, threads, el)}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+
+    import smore_amd
+    from smore_amd import graphgen
+    from smore_amd.dist import ReplicaSync
+
+    V, (src, dst, w) = graphgen.config_edges(args.config)
+    pn = smore_amd.ProNet(local)
+    pn.set_graph_edges(V, src, dst, w)
+    E = pn.MAX_line
+    pn.alloc_tables(args.dim, 2)
+    pn.init_table_uniform(0, args.seed)     # W ~ (u-0.5)/d, as the reference Init law
+    pn.zero_table(1)                        # C = 0 (src/model/LINE.cpp:92)
+    stream = torch.cuda.current_stream()
+    pn.set_stream(stream.cuda_stream)
+    sync = ReplicaSync(pn, mean=(args.sync == "mean")) if world > 1 else None
+
+    S, K = args.samples, args.negative
+    total = (args.warmup + args.steps) * S * world     # alpha schedule over the whole job
+
+    def step(k):
+        begin = (k * world + rank) * S
+        pn.train_edges("line2", begin, S, total, K, 0.025, 0.0, args.seed, args.mode, sync=False)
+        if sync is not None and (k + 1) % args.sync_every == 0:
+            sync.allreduce()
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for k in range(args.warmup, args.warmup + args.steps):
+        step(k)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+    if dist:
+        t = torch.tensor([el], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    skipped = pn.skipped()
+
+    updates = S * args.steps * world
+    R, Wb = algorithmic_bytes(args.dim, K)
+    launch_s = gpu_ms / 1e3 / args.steps            # avg per-launch time on the launch stream
+    achieved = R * S / launch_s / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        p = json.load(open(pmc))
+        if p.get("config") == args.config and p.get("samples") == S and p.get("mode") == args.mode:
+            traffic = p.get("hbm_bytes_per_launch")
+    Wt = pn.get_table(0)
+    assert np.isfinite(Wt).all(), "non-finite embeddings"
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline and args.cpu_baseline_seconds > 0:
+            cpu = cpu_baseline(V, src, dst, w, args.dim, K, args.cpu_baseline_seconds)
+        out = {
+            "metric": "M edge-updates/sec (d=64, neg=5)",
+            "value": round(updates / el / 1e6, 3),
+            "unit": "M edge-updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el * 1e3 / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic power-law (Zipf 0.8 endpoints, seeded), random-init tables",
+            "config": {"workload": "LINE order-2 sampled negative-sampling SGD, config %s" % args.config,
+                       "vertices": V, "edge_slots": E, "dim": args.dim, "negative": K,
+                       "samples_per_step_per_gpu": S, "scatter": args.mode,
+                       "sync": ("%s every %d steps" % (args.sync, args.sync_every)) if world > 1 else "none",
+                       "parallelism": "replicas%d" % world},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "bytes_per_update_read": R, "bytes_per_update_write": Wb,
+                         "achieved_rw": round((R + Wb) * S / launch_s / 1e9, 1),
+                         "kernel_ms_per_launch": round(launch_s * 1e3, 3)},
+            "cpu_baseline": cpu,
+            "skipped_samples": int(skipped),
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,174 @@
+/*
+ * smore_hip.h -- C ABI of the MI355X-native SMORe hot path (libsmore_hip.so).
+ *
+ * The drop-in boundary: plain pointers and sizes, int status codes, no torch
+ * and no HIP types in the signatures.  A context owns device memory on ONE GPU
+ * (one process per GPU; multi-GPU replication is driven from above, see
+ * smore_amd/dist.py).  Calls are synchronous unless named *_async; a context is
+ * not thread-safe.  Host buffers are owned by the caller and copied in/out.
+ *
+ * Each entry point names the reference interface it replaces
+ * (RainBoltz/smore paths; C++ proNet-core unless marked Go).
+ * The cgo / ctypes bindings a maintainer adds are shown in INTEGRATION.md.
+ */
+#ifndef SMORE_HIP_H
+#define SMORE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct smore_ctx smore_ctx;
+
+/* status codes */
+#define SMORE_OK 0
+#define SMORE_EINVAL 1   /* bad argument (ids out of range, sizes, state)   */
+#define SMORE_EHIP 2     /* HIP runtime / kernel launch failure              */
+#define SMORE_ENOMEM 3   /* device or host allocation failure                */
+#define SMORE_ESTATE 4   /* call out of order (no graph, no tables, ...)     */
+#define SMORE_EIO 5      /* file open / parse / write failure                */
+
+/* sampling distributions (proNet::SetVertexMethod / SetNegativeMethod,
+ * src/proNet.cpp:20-25; distributions built at src/proNet.cpp:457-510) */
+#define SMORE_VM_OUT_DEGREES 0
+#define SMORE_VM_NO_DEGREES 1
+#define SMORE_VM_DEGREES 2
+#define SMORE_NM_DEGREES 0
+#define SMORE_NM_IN_DEGREES 1
+#define SMORE_NM_NO_DEGREES 2
+
+/* alias tables (proNet::vertex_AT / negative_AT / context_AT, src/proNet.h:143-145) */
+#define SMORE_AT_VERTEX 0
+#define SMORE_AT_NEGATIVE 1
+#define SMORE_AT_CONTEXT 2
+
+/* embedding tables: W = w_vertex, C = w_context (src/model/LINE.h:22-24) */
+#define SMORE_W 0
+#define SMORE_C 1
+
+/* update rules */
+#define SMORE_LINE2 0   /* UpdatePair(W, C, ...)  src/proNet.cpp:1784-1809 (LINE 2nd, DeepWalk pairs) */
+#define SMORE_LINE1 1   /* UpdatePair(W, W, ...)  src/model/LINE.cpp:126-157 */
+#define SMORE_MF 2      /* UpdateFactorizedPair(W, W, ...) src/proNet.cpp:2591-2614 */
+#define SMORE_BPR 3     /* UpdateBPRPair(W, W, ...) src/proNet.cpp:1406-1455 */
+
+/* scatter modes for the row updates */
+#define SMORE_HOGWILD 0  /* lock-free read-modify-write stores (the reference's Hogwild) */
+#define SMORE_ATOMIC 1   /* read, then float atomic add of each row's delta            */
+#define SMORE_SERIAL 2   /* one lane group, samples strictly in order (parity mode)    */
+
+/* ---- context --------------------------------------------------------------- */
+/* replaces: construction of proNet / LINE / BPR / MF / DeepWalk
+ * (src/proNet.cpp:3-15, Go pronet.NewProNet pkg/pronet/pronet.go:77) */
+int smore_create(int device, smore_ctx** out);
+void smore_destroy(smore_ctx* ctx);
+/* last error message of this context (empty string if none) */
+const char* smore_last_error(const smore_ctx* ctx);
+/* run on an external HIP stream (hipStream_t passed as void*); NULL = own stream */
+int smore_set_stream(smore_ctx* ctx, void* hip_stream);
+int smore_synchronize(smore_ctx* ctx);
+/* library version string */
+const char* smore_version(void);
+
+/* ---- graph ------------------------------------------------------------------ */
+/* replaces: proNet::LoadEdgeList (src/proNet.cpp:115-236; Go LoadEdgeList
+ * pkg/pronet/pronet.go:112-174).  Text edge list "v1 v2 w" per line (a file
+ * or a directory of files); ids in first-appearance order; undirected lines
+ * add both directions.  Builds CSR + alias tables and uploads them. */
+int smore_load_edgelist(smore_ctx* ctx, const char* path, int undirected,
+                        int vertex_method, int negative_method);
+/* replaces: the graph half of LoadEdgeList + BuildAliasMethod
+ * (src/proNet.cpp:410-542) for callers that already hold ids: E directed
+ * edge slots (src[e] -> dst[e], weight w[e]) in push order. */
+int smore_set_graph_edges(smore_ctx* ctx, int64_t V, int64_t E, const int32_t* src,
+                          const int32_t* dst, const double* w, int vertex_method,
+                          int negative_method);
+/* graph sizes (MAX_vid, MAX_line) */
+int smore_graph_info(const smore_ctx* ctx, int64_t* V, int64_t* E);
+/* vertex name of id (proNet::vertex_hash.keys / Go GetVertexName
+ * pkg/pronet/pronet.go:336); NULL when the graph was given by ids */
+const char* smore_vertex_name(const smore_ctx* ctx, int64_t vid);
+/* host copies of the CSR (offsets: V+1, targets: E) */
+int smore_get_csr(const smore_ctx* ctx, int64_t* offsets, int32_t* targets);
+/* replaces: direct assignment of proNet::*_AT / Go ProNet.NegativeAT
+ * (internal/models/ctdne/ctdne.go:109-122).  prob/alias in the reference's
+ * representation (alias -1 = none); for SMORE_AT_CONTEXT, n == E and alias
+ * holds target vids.  Re-encodes and re-uploads the table. */
+int smore_set_alias(smore_ctx* ctx, int which, const double* prob, const int64_t* alias,
+                    int64_t n);
+/* reference-representation copy of an alias table (prob, alias; n entries) */
+int smore_get_alias(const smore_ctx* ctx, int which, double* prob, int64_t* alias, int64_t n);
+/* device-encoded copy: accept threshold (u32) + alias id (i32) per entry */
+int smore_get_alias_encoded(const smore_ctx* ctx, int which, uint32_t* thresh, int32_t* alias,
+                            int64_t n);
+
+/* ---- embedding tables ---------------------------------------------------------- */
+/* allocate W (and C when ntables == 2) as [V][dpad] fp32, dpad = dim rounded up
+ * to a multiple of 4 (rows 16-byte aligned).  Tables start zeroed. */
+int smore_alloc_tables(smore_ctx* ctx, int dim, int ntables);
+/* replaces: the rand() initialisation in LINE/MF/BPR/DeepWalk::Init
+ * (src/model/LINE.cpp:83, MF.cpp:50, BPR.cpp:49, DeepWalk.cpp:47,54):
+ * table[v][d] = (rand()/RAND_MAX - 0.5)/dim with glibc rand() seeded by srand(1),
+ * skipping the first `skip` draws (so W then C reproduce the reference order). */
+int smore_init_table_glibc(smore_ctx* ctx, int which, uint64_t skip);
+/* on-device init (Philox stream 2): (u - 0.5)/dim, u uniform in [0,1) */
+int smore_init_table_uniform(smore_ctx* ctx, int which, uint64_t seed);
+int smore_zero_table(smore_ctx* ctx, int which);
+/* host <-> device copies, host rows unpadded [rows][dim] */
+int smore_set_table(smore_ctx* ctx, int which, const float* host, int64_t rows, int dim);
+int smore_get_table(const smore_ctx* ctx, int which, float* host, int64_t rows, int dim);
+/* device pointer + padded row stride (floats) of a table, for collectives */
+int smore_table_device(smore_ctx* ctx, int which, void** dptr, int64_t* stride);
+
+/* ---- training -------------------------------------------------------------------- */
+/* replaces: the hot loops of LINE::Train (src/model/LINE.cpp:160-191),
+ * MF::Train (src/model/MF.cpp:78-101), BPR::Train (src/model/BPR.cpp:77-101);
+ * Go (*LINE).Train internal/models/line/line.go:73-150.
+ * Runs global samples [begin, begin+count) of a run of `total` samples
+ * (learning-rate schedule of the reference from the global sample index).
+ * model: SMORE_LINE2 | SMORE_LINE1 | SMORE_MF | SMORE_BPR; K negatives
+ * (BPR: fixed 5 rounds, K ignored as in the reference); reg: MF only.
+ * mode: SMORE_HOGWILD | SMORE_ATOMIC | SMORE_SERIAL.  Asynchronous on the
+ * context stream; *_sync waits and reports launch errors. */
+int smore_train_edges_async(smore_ctx* ctx, int model, uint64_t begin, uint64_t count,
+                            uint64_t total, int K, double alpha0, double reg, uint64_t seed,
+                            int mode);
+int smore_train_edges(smore_ctx* ctx, int model, uint64_t begin, uint64_t count,
+                      uint64_t total, int K, double alpha0, double reg, uint64_t seed,
+                      int mode);
+/* samples whose source had no out-edge (reference: TargetSample -> -1) */
+int smore_skipped(smore_ctx* ctx, uint64_t* skipped);
+/* milliseconds of the last training launch (HIP events on the launch stream) */
+float smore_last_kernel_ms(const smore_ctx* ctx);
+
+/* replaces: DeepWalk::Train (src/model/DeepWalk.cpp:98-155): walks
+ * [walk_begin, walk_end) of walk_times*V, start vertices order[] (host,
+ * walk_times*V entries, see smore_deepwalk_order), RandomWalk + SkipGrams +
+ * UpdatePairs per walk on the GPU. */
+int smore_train_deepwalk(smore_ctx* ctx, uint64_t walk_begin, uint64_t walk_end,
+                         int walk_times, int walk_steps, int window, int K, double alpha0,
+                         uint64_t seed, const int64_t* order, int mode);
+/* the reference's walk start order: per walk_time a Fisher-Yates shuffle with
+ * glibc rand() after `skip` Init draws (src/model/DeepWalk.cpp:122-131) */
+int smore_deepwalk_order(int64_t V, int walk_times, uint64_t skip, int64_t* order);
+
+/* ---- samplers (parity tests) -------------------------------------------------------- */
+/* replaces: SourceSample/TargetSample/NegativeSample (src/proNet.cpp:623-683):
+ * draws of samples [begin, begin+count) as the training kernels draw them.
+ * out: count x (2+K) int32 {v, c, n1..nK} (model != BPR) or count x 7 {u,i,j0..j4}. */
+int smore_sample_edges(smore_ctx* ctx, int model, uint64_t begin, uint64_t count, int K,
+                       uint64_t seed, int32_t* out);
+
+/* ---- output ---------------------------------------------------------------------------- */
+/* replaces: SaveWeights (src/model/LINE.cpp:13-47; Go line.go:209-233):
+ * "V dim" header then "name v1 ... vdim" per vertex.  fmt 0 = C++ ostream
+ * default (%g, 6 significant digits), fmt 1 = Go "%.6f". */
+int smore_save_weights(const smore_ctx* ctx, int which, const char* path, int fmt);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

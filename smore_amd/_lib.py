@@ -1,0 +1,79 @@
+"""ctypes binding of libsmore_hip.so (include/smore_hip.h).
+
+The HIP library is the product: there is no Python or CPU fallback.  If the
+shared object is missing or fails to load, importing smore_amd raises.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libsmore_hip.so")
+
+OK, EINVAL, EHIP, ENOMEM, ESTATE, EIO = range(6)
+VM = {"out_degrees": 0, "no_degrees": 1, "degrees": 2}
+NM = {"degrees": 0, "in_degrees": 1, "no_degrees": 2}
+AT_VERTEX, AT_NEGATIVE, AT_CONTEXT = 0, 1, 2
+W, CTX = 0, 1
+MODEL = {"line2": 0, "line1": 1, "mf": 2, "bpr": 3}
+MODE = {"hogwild": 0, "atomic": 1, "serial": 2}
+
+
+class SmoreError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libsmore_hip.so not built (%s); run `make` or __graft_entry__.build()" % LIB_PATH)
+    L = C.CDLL(LIB_PATH)
+    P, i32, i64, u64, dbl = C.c_void_p, C.c_int, C.c_int64, C.c_uint64, C.c_double
+    sig = {
+        "smore_create": (i32, [i32, C.POINTER(P)]),
+        "smore_destroy": (None, [P]),
+        "smore_last_error": (C.c_char_p, [P]),
+        "smore_set_stream": (i32, [P, P]),
+        "smore_synchronize": (i32, [P]),
+        "smore_version": (C.c_char_p, []),
+        "smore_load_edgelist": (i32, [P, C.c_char_p, i32, i32, i32]),
+        "smore_set_graph_edges": (i32, [P, i64, i64, P, P, P, i32, i32]),
+        "smore_graph_info": (i32, [P, C.POINTER(i64), C.POINTER(i64)]),
+        "smore_vertex_name": (C.c_char_p, [P, i64]),
+        "smore_get_csr": (i32, [P, P, P]),
+        "smore_set_alias": (i32, [P, i32, P, P, i64]),
+        "smore_get_alias": (i32, [P, i32, P, P, i64]),
+        "smore_get_alias_encoded": (i32, [P, i32, P, P, i64]),
+        "smore_alloc_tables": (i32, [P, i32, i32]),
+        "smore_init_table_glibc": (i32, [P, i32, u64]),
+        "smore_init_table_uniform": (i32, [P, i32, u64]),
+        "smore_zero_table": (i32, [P, i32]),
+        "smore_set_table": (i32, [P, i32, P, i64, i32]),
+        "smore_get_table": (i32, [P, i32, P, i64, i32]),
+        "smore_table_device": (i32, [P, i32, C.POINTER(P), C.POINTER(i64)]),
+        "smore_train_edges_async": (i32, [P, i32, u64, u64, u64, i32, dbl, dbl, u64, i32]),
+        "smore_train_edges": (i32, [P, i32, u64, u64, u64, i32, dbl, dbl, u64, i32]),
+        "smore_skipped": (i32, [P, C.POINTER(u64)]),
+        "smore_last_kernel_ms": (C.c_float, [P]),
+        "smore_train_deepwalk": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, u64, P, i32]),
+        "smore_deepwalk_order": (i32, [i64, i32, u64, P]),
+        "smore_sample_edges": (i32, [P, i32, u64, u64, i32, u64, P]),
+        "smore_save_weights": (i32, [P, i32, C.c_char_p, i32]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    L._signatures = sig
+    return L
+
+
+lib = _load()
+
+
+def check(ctx, rc, what=""):
+    if rc != OK:
+        msg = lib.smore_last_error(ctx).decode() if ctx else ""
+        raise SmoreError("%s failed (status %d): %s" % (what, rc, msg))
+
+
+def ptr(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)

@@ -1,0 +1,487 @@
+// capi.cpp -- the C ABI (include/smore_hip.h) over the gfx950 kernels.
+//
+// A context owns one GPU's copy of the graph (CSR, encoded alias tables, the
+// fastSigmoid table) and the embedding tables.  Everything on the device is
+// uploaded once; training calls only launch kernels on the context stream.
+#include "../../include/smore_hip.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "host_graph.h"
+#include "train_kernels.h"
+
+using namespace smore;
+
+struct smore_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipStream_t own_stream = nullptr;
+    std::string err;
+    HostGraph g;
+    bool has_graph = false;
+    // device graph
+    int64_t* d_offsets = nullptr;
+    int32_t* d_targets = nullptr;
+    AliasEntry* d_vtab = nullptr;
+    AliasEntry* d_ntab = nullptr;
+    AliasEntry* d_ctab = nullptr;
+    float* d_sig = nullptr;
+    unsigned long long* d_skipped = nullptr;
+    // tables
+    float* d_table[2] = {nullptr, nullptr};
+    int dim = 0, dpad = 0, ntables = 0;
+    // timing
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    int cus = 0;
+};
+
+namespace {
+
+int fail(smore_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+#define HIPCHK(c, expr)                                                                     \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return fail((c), SMORE_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+template <class T>
+void dfree(T*& p) {
+    if (p) (void)hipFree((void*)p);
+    p = nullptr;
+}
+
+template <class T>
+int upload(smore_ctx* c, T*& d, const T* h, size_t n) {
+    dfree(d);
+    if (n == 0) n = 1;
+    HIPCHK(c, hipMalloc((void**)&d, n * sizeof(T)));
+    if (h) HIPCHK(c, hipMemcpy(d, h, n * sizeof(T), hipMemcpyHostToDevice));
+    return SMORE_OK;
+}
+
+int set_device(smore_ctx* c) {
+    if (c->device < 0) return fail(c, SMORE_ESTATE, "host-only context (device < 0) has no GPU state");
+    HIPCHK(c, hipSetDevice(c->device));
+    return SMORE_OK;
+}
+
+int upload_graph(smore_ctx* c) {
+    int rc;
+    if (c->device < 0) {
+        c->has_graph = true;
+        return SMORE_OK;
+    }
+    if ((rc = set_device(c))) return rc;
+    HostGraph& g = c->g;
+    if ((rc = upload(c, c->d_offsets, g.offsets.data(), g.offsets.size()))) return rc;
+    if ((rc = upload(c, c->d_targets, g.targets.data(), g.targets.size()))) return rc;
+    if ((rc = upload(c, c->d_vtab, g.vtab.data(), g.vtab.size()))) return rc;
+    if ((rc = upload(c, c->d_ntab, g.ntab.data(), g.ntab.size()))) return rc;
+    if ((rc = upload(c, c->d_ctab, g.ctab.data(), g.ctab.size()))) return rc;
+    // fastSigmoid table, 1001 entries (src/proNet.cpp:52-60; the reference
+    // sizes it 1000 and writes 1001 -- the build keeps all 1001)
+    std::vector<float> sig(1001);
+    for (int i = 0; i != 1000 + 1; i++) {
+        double x = i * 2.0 * 8.0 / 1000 - 8.0;
+        sig[i] = (float)(1.0 / (1.0 + std::exp(-x)));
+    }
+    if ((rc = upload(c, c->d_sig, sig.data(), sig.size()))) return rc;
+    c->has_graph = true;
+    return SMORE_OK;
+}
+
+DevGraph dev_graph(const smore_ctx* c) {
+    DevGraph d;
+    d.offsets = c->d_offsets;
+    d.targets = c->d_targets;
+    d.vtab = reinterpret_cast<const uint2*>(c->d_vtab);
+    d.ntab = reinterpret_cast<const uint2*>(c->d_ntab);
+    d.ctab = reinterpret_cast<const uint2*>(c->d_ctab);
+    d.V = (uint32_t)c->g.V;
+    return d;
+}
+
+float* table_ptr(smore_ctx* c, int which) {
+    if (which < 0 || which > 1) return nullptr;
+    return c->d_table[which];
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* smore_version(void) { return "smore_hip 0.1 (gfx950)"; }
+
+int smore_create(int device, smore_ctx** out) {
+    if (!out) return SMORE_EINVAL;
+    *out = nullptr;
+    smore_ctx* c = new smore_ctx();
+    c->device = device;
+    if (device < 0) {  // host-only context: graph/alias building, no device state
+        *out = c;
+        return SMORE_OK;
+    }
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+    if (e == hipSuccess) e = hipMalloc((void**)&c->d_skipped, sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(c->d_skipped, 0, sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device);
+    if (e != hipSuccess) {
+        delete c;
+        return SMORE_EHIP;
+    }
+    c->stream = c->own_stream;
+    *out = c;
+    return SMORE_OK;
+}
+
+void smore_destroy(smore_ctx* c) {
+    if (!c) return;
+    if (c->device >= 0) {
+        (void)hipSetDevice(c->device);
+        (void)hipStreamSynchronize(c->stream);
+    }
+    dfree(c->d_offsets); dfree(c->d_targets); dfree(c->d_vtab); dfree(c->d_ntab); dfree(c->d_ctab);
+    dfree(c->d_sig); dfree(c->d_skipped); dfree(c->d_table[0]); dfree(c->d_table[1]);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+const char* smore_last_error(const smore_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int smore_set_stream(smore_ctx* c, void* s) {
+    if (!c) return SMORE_EINVAL;
+    c->stream = s ? (hipStream_t)s : c->own_stream;
+    return SMORE_OK;
+}
+
+int smore_synchronize(smore_ctx* c) {
+    if (!c) return SMORE_EINVAL;
+    if (c->device < 0) return SMORE_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return SMORE_OK;
+}
+
+// ---------------------------------------------------------------- graph
+int smore_set_graph_edges(smore_ctx* c, int64_t V, int64_t E, const int32_t* src, const int32_t* dst,
+                          const double* w, int vm, int nm) {
+    if (!c) return SMORE_EINVAL;
+    if ((E > 0 && (!src || !dst || !w)) || vm < 0 || vm > 2 || nm < 0 || nm > 2)
+        return fail(c, SMORE_EINVAL, "bad arguments");
+    c->g = HostGraph();
+    if (!build_graph(V, E, src, dst, w, vm, nm, c->g, c->err)) return SMORE_EINVAL;
+    return upload_graph(c);
+}
+
+int smore_load_edgelist(smore_ctx* c, const char* path, int undirected, int vm, int nm) {
+    if (!c || !path) return SMORE_EINVAL;
+    std::vector<std::string> names;
+    std::vector<int32_t> src, dst;
+    std::vector<double> w;
+    if (!read_edgelist(path, undirected != 0, names, src, dst, w, c->err)) return SMORE_EIO;
+    if (names.empty()) return fail(c, SMORE_EIO, std::string("no edges in ") + path);
+    int rc = smore_set_graph_edges(c, (int64_t)names.size(), (int64_t)src.size(), src.data(), dst.data(),
+                                   w.data(), vm, nm);
+    if (rc == SMORE_OK) c->g.names = std::move(names);
+    return rc;
+}
+
+int smore_graph_info(const smore_ctx* c, int64_t* V, int64_t* E) {
+    if (!c) return SMORE_EINVAL;
+    if (V) *V = c->g.V;
+    if (E) *E = c->g.E;
+    return c->has_graph ? SMORE_OK : SMORE_ESTATE;
+}
+
+const char* smore_vertex_name(const smore_ctx* c, int64_t vid) {
+    if (!c || vid < 0 || vid >= (int64_t)c->g.names.size()) return nullptr;
+    return c->g.names[vid].c_str();
+}
+
+int smore_get_csr(const smore_ctx* c, int64_t* offsets, int32_t* targets) {
+    if (!c || !c->has_graph) return SMORE_ESTATE;
+    if (offsets) memcpy(offsets, c->g.offsets.data(), c->g.offsets.size() * sizeof(int64_t));
+    if (targets) memcpy(targets, c->g.targets.data(), c->g.targets.size() * sizeof(int32_t));
+    return SMORE_OK;
+}
+
+int smore_set_alias(smore_ctx* c, int which, const double* prob, const int64_t* alias, int64_t n) {
+    if (!c || !prob || !alias) return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    HostGraph& g = c->g;
+    int64_t want = which == SMORE_AT_CONTEXT ? g.E : g.V;
+    if (which < 0 || which > 2 || n != want) return fail(c, SMORE_EINVAL, "alias table size mismatch");
+    int64_t lim = g.V;
+    for (int64_t i = 0; i < n; ++i) {
+        if (alias[i] >= lim || alias[i] < -1 || !(prob[i] >= 0)) return fail(c, SMORE_EINVAL, "alias entry out of range");
+        if (which != SMORE_AT_CONTEXT && alias[i] >= g.V) return fail(c, SMORE_EINVAL, "alias out of range");
+    }
+    std::vector<double>& P = which == 0 ? g.vprob : which == 1 ? g.nprob : g.cprob;
+    std::vector<int64_t>& A = which == 0 ? g.valias : which == 1 ? g.nalias : g.calias;
+    std::vector<AliasEntry>& T = which == 0 ? g.vtab : which == 1 ? g.ntab : g.ctab;
+    P.assign(prob, prob + n);
+    A.assign(alias, alias + n);
+    T.resize((size_t)n);
+    alias_encode(P.data(), A.data(), n, which == SMORE_AT_CONTEXT ? g.targets.data() : nullptr, T.data());
+    if (c->device < 0) return SMORE_OK;
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    AliasEntry*& d = which == 0 ? c->d_vtab : which == 1 ? c->d_ntab : c->d_ctab;
+    return upload(c, d, T.data(), T.size());
+}
+
+int smore_get_alias(const smore_ctx* c, int which, double* prob, int64_t* alias, int64_t n) {
+    if (!c || !c->has_graph || which < 0 || which > 2) return SMORE_EINVAL;
+    const HostGraph& g = c->g;
+    const std::vector<double>& P = which == 0 ? g.vprob : which == 1 ? g.nprob : g.cprob;
+    const std::vector<int64_t>& A = which == 0 ? g.valias : which == 1 ? g.nalias : g.calias;
+    if (n != (int64_t)P.size()) return SMORE_EINVAL;
+    if (prob) memcpy(prob, P.data(), n * sizeof(double));
+    if (alias) memcpy(alias, A.data(), n * sizeof(int64_t));
+    return SMORE_OK;
+}
+
+int smore_get_alias_encoded(const smore_ctx* c, int which, uint32_t* thresh, int32_t* alias, int64_t n) {
+    if (!c || !c->has_graph || which < 0 || which > 2) return SMORE_EINVAL;
+    const HostGraph& g = c->g;
+    const std::vector<AliasEntry>& T = which == 0 ? g.vtab : which == 1 ? g.ntab : g.ctab;
+    if (n != (int64_t)T.size()) return SMORE_EINVAL;
+    for (int64_t i = 0; i < n; ++i) {
+        if (thresh) thresh[i] = T[i].thresh;
+        if (alias) alias[i] = T[i].alias;
+    }
+    return SMORE_OK;
+}
+
+// ---------------------------------------------------------------- tables
+int smore_alloc_tables(smore_ctx* c, int dim, int ntables) {
+    if (!c) return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    if (dim <= 0 || dim > 1024 || ntables < 1 || ntables > 2) return fail(c, SMORE_EINVAL, "bad dim/ntables");
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    dfree(c->d_table[0]);
+    dfree(c->d_table[1]);
+    c->dim = dim;
+    c->dpad = (dim + 3) / 4 * 4;
+    c->ntables = ntables;
+    size_t bytes = (size_t)c->g.V * c->dpad * sizeof(float);
+    for (int t = 0; t < ntables; ++t) {
+        HIPCHK(c, hipMalloc((void**)&c->d_table[t], bytes));
+        HIPCHK(c, hipMemset(c->d_table[t], 0, bytes));
+    }
+    return SMORE_OK;
+}
+
+static int check_table(smore_ctx* c, int which) {
+    if (!c) return SMORE_EINVAL;
+    if (which < 0 || which >= c->ntables || !c->d_table[which]) return fail(c, SMORE_ESTATE, "table not allocated");
+    return SMORE_OK;
+}
+
+int smore_init_table_glibc(smore_ctx* c, int which, uint64_t skip) {
+    int rc;
+    if ((rc = check_table(c, which))) return rc;
+    GlibcRand r;
+    r.discard(skip);
+    std::vector<float> h((size_t)c->g.V * c->dpad, 0.0f);
+    for (int64_t v = 0; v < c->g.V; ++v)
+        for (int d = 0; d < c->dim; ++d)
+            h[(size_t)v * c->dpad + d] = (float)((r.next() / (double)2147483647 - 0.5) / c->dim);
+    if ((rc = set_device(c))) return rc;
+    HIPCHK(c, hipMemcpy(c->d_table[which], h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
+    return SMORE_OK;
+}
+
+int smore_init_table_uniform(smore_ctx* c, int which, uint64_t seed) {
+    int rc;
+    if ((rc = check_table(c, which))) return rc;
+    if ((rc = set_device(c))) return rc;
+    HIPCHK(c, launch_init_uniform(c->d_table[which], c->g.V, c->dim, c->dpad, seed, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return SMORE_OK;
+}
+
+int smore_zero_table(smore_ctx* c, int which) {
+    int rc;
+    if ((rc = check_table(c, which))) return rc;
+    if ((rc = set_device(c))) return rc;
+    HIPCHK(c, hipMemsetAsync(c->d_table[which], 0, (size_t)c->g.V * c->dpad * sizeof(float), c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return SMORE_OK;
+}
+
+int smore_set_table(smore_ctx* c, int which, const float* host, int64_t rows, int dim) {
+    int rc;
+    if ((rc = check_table(c, which))) return rc;
+    if (!host || rows != c->g.V || dim != c->dim) return fail(c, SMORE_EINVAL, "table shape mismatch");
+    if ((rc = set_device(c))) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy2D(c->d_table[which], c->dpad * sizeof(float), host, dim * sizeof(float),
+                          dim * sizeof(float), rows, hipMemcpyHostToDevice));
+    return SMORE_OK;
+}
+
+int smore_get_table(const smore_ctx* cc, int which, float* host, int64_t rows, int dim) {
+    smore_ctx* c = const_cast<smore_ctx*>(cc);
+    int rc;
+    if ((rc = check_table(c, which))) return rc;
+    if (!host || rows != c->g.V || dim != c->dim) return fail(c, SMORE_EINVAL, "table shape mismatch");
+    if ((rc = set_device(c))) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy2D(host, dim * sizeof(float), c->d_table[which], c->dpad * sizeof(float),
+                          dim * sizeof(float), rows, hipMemcpyDeviceToHost));
+    return SMORE_OK;
+}
+
+int smore_table_device(smore_ctx* c, int which, void** dptr, int64_t* stride) {
+    int rc;
+    if ((rc = check_table(c, which))) return rc;
+    if (dptr) *dptr = c->d_table[which];
+    if (stride) *stride = c->dpad;
+    return SMORE_OK;
+}
+
+// ---------------------------------------------------------------- training
+static int edge_grid(smore_ctx* c, const EdgeArgs& a) {
+    if (a.mode == SMORE_SERIAL) return 1;
+    int per_cu = 0;
+    const void* sym = edge_kernel_symbol(a);
+    if (!sym || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sym, 256, 0) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    int64_t grid = (int64_t)c->cus * per_cu;
+    const int G = lanes_of(a.dpad);
+    const int64_t groups_per_block = 256 / G;
+    const int64_t need = ((int64_t)a.count + groups_per_block - 1) / groups_per_block;
+    if (need < grid) grid = need;
+    return (int)(grid < 1 ? 1 : grid);
+}
+
+int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t count, uint64_t total, int K,
+                            double alpha0, double reg, uint64_t seed, int mode) {
+    if (!c) return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    if (model < 0 || model > 3 || mode < 0 || mode > 2 || K < 0 || K > 20)
+        return fail(c, SMORE_EINVAL, "bad model/mode/K");
+    const int need_tables = model == SMORE_LINE2 ? 2 : 1;
+    if (c->ntables < need_tables) return fail(c, SMORE_ESTATE, "tables not allocated");
+    if (total == 0) return fail(c, SMORE_EINVAL, "total == 0");
+    if (count == 0) return SMORE_OK;
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    EdgeArgs a;
+    a.g = dev_graph(c);
+    a.sig = c->d_sig;
+    a.W = c->d_table[0];
+    a.C = model == SMORE_LINE2 ? c->d_table[1] : c->d_table[0];
+    a.skipped = c->d_skipped;
+    a.begin = begin;
+    a.count = count;
+    a.total = total;
+    a.seed = seed;
+    a.alpha0 = alpha0;
+    a.reg = (float)reg;
+    a.dpad = c->dpad;
+    a.K = model == SMORE_BPR ? 5 : K;
+    a.model = model;
+    a.mode = mode;
+    const int grid = edge_grid(c, a);
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    HIPCHK(c, launch_edge_train(a, grid, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
+    return SMORE_OK;
+}
+
+int smore_train_edges(smore_ctx* c, int model, uint64_t begin, uint64_t count, uint64_t total, int K,
+                      double alpha0, double reg, uint64_t seed, int mode) {
+    int rc = smore_train_edges_async(c, model, begin, count, total, K, alpha0, reg, seed, mode);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipGetLastError());
+    return SMORE_OK;
+}
+
+int smore_skipped(smore_ctx* c, uint64_t* skipped) {
+    if (!c || !skipped) return SMORE_EINVAL;
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    unsigned long long h = 0;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(&h, c->d_skipped, sizeof(h), hipMemcpyDeviceToHost));
+    *skipped = h;
+    return SMORE_OK;
+}
+
+float smore_last_kernel_ms(const smore_ctx* c) {
+    if (!c || !c->timed) return -1.0f;
+    float ms = -1.0f;
+    if (hipEventSynchronize(c->ev1) != hipSuccess) return -1.0f;
+    if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) return -1.0f;
+    return ms;
+}
+
+int smore_deepwalk_order(int64_t V, int walk_times, uint64_t skip, int64_t* order) {
+    if (V <= 0 || walk_times < 0 || !order) return SMORE_EINVAL;
+    deepwalk_order(V, walk_times, skip, order);
+    return SMORE_OK;
+}
+
+int smore_sample_edges(smore_ctx* c, int model, uint64_t begin, uint64_t count, int K, uint64_t seed,
+                       int32_t* out) {
+    if (!c || !out) return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    if (K < 0 || K > 20) return fail(c, SMORE_EINVAL, "bad K");
+    if (count == 0) return SMORE_OK;
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    const int bpr = model == SMORE_BPR;
+    const size_t width = bpr ? 7 : 2 + K;
+    int32_t* d = nullptr;
+    HIPCHK(c, hipMalloc((void**)&d, count * width * sizeof(int32_t)));
+    hipError_t e = launch_sample(dev_graph(c), seed, begin, count, K, bpr, d, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(out, d, count * width * sizeof(int32_t), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(c, SMORE_EHIP, std::string("sample: ") + hipGetErrorString(e));
+    return SMORE_OK;
+}
+
+int smore_save_weights(const smore_ctx* cc, int which, const char* path, int fmt) {
+    smore_ctx* c = const_cast<smore_ctx*>(cc);
+    int rc;
+    if ((rc = check_table(c, which))) return rc;
+    if (!path) return SMORE_EINVAL;
+    std::vector<float> h((size_t)c->g.V * c->dpad);
+    if ((rc = set_device(c))) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(h.data(), c->d_table[which], h.size() * sizeof(float), hipMemcpyDeviceToHost));
+    if (!save_weights(path, c->g, h.data(), c->g.V, c->dim, c->dpad, fmt, c->err)) return SMORE_EIO;
+    return SMORE_OK;
+}
+
+int smore_train_deepwalk(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
+                         int window, int K, double alpha0, uint64_t seed, const int64_t* order, int mode) {
+    (void)walk_begin; (void)walk_end; (void)walk_times; (void)walk_steps; (void)window; (void)K;
+    (void)alpha0; (void)seed; (void)order; (void)mode;
+    return fail(c, SMORE_ESTATE, "deepwalk: not built yet");
+}
+
+}  // extern "C"

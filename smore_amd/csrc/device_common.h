@@ -1,0 +1,144 @@
+// device_common.h -- gfx950 device helpers shared by the hot-path kernels:
+// the Philox RNG spec, the alias samplers, the fastSigmoid table lookup and
+// the lane-group reductions.  Arithmetic follows DESIGN.md "Arithmetic spec"
+// (mirrored bit for bit by oracle/smore_oracle.c *_f32).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace smore {
+
+// ---- RNG spec: Philox4x32-10, ctr = {lo(unit), hi(unit), slot/4, stream},
+// key = {lo(seed), hi(seed)}; replaces src/random.cpp:5-13.
+__device__ __forceinline__ uint4 philox_block(uint64_t seed, uint32_t stream, uint64_t unit,
+                                              uint32_t blk) {
+    uint32_t c0 = (uint32_t)unit, c1 = (uint32_t)(unit >> 32), c2 = blk, c3 = stream;
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        c0 = hi1 ^ c1 ^ k0;
+        c1 = lo1;
+        c2 = hi0 ^ c3 ^ k1;
+        c3 = lo0;
+    }
+    return make_uint4(c0, c1, c2, c3);
+}
+
+__device__ __forceinline__ uint32_t comp(const uint4& b, int c) {
+    return c == 0 ? b.x : c == 1 ? b.y : c == 2 ? b.z : b.w;
+}
+
+// Encoded graph in HBM (DESIGN.md "Data layout").
+struct DevGraph {
+    const int64_t* offsets;   // V+1
+    const int32_t* targets;   // E
+    const uint2* vtab;        // V   {accept threshold, alias}
+    const uint2* ntab;        // V
+    const uint2* ctab;        // E   alias already a target vid
+    uint32_t V;
+};
+
+// index draw floor(k*n/2^32) == interposed random_gen(0, n) truncated.
+__device__ __forceinline__ uint32_t draw_index(uint32_t k, uint32_t n) { return __umulhi(k, n); }
+
+// SourceSample src/proNet.cpp:647-657 (p, then index)
+__device__ __forceinline__ int32_t source_sample(const DevGraph& g, uint32_t kp, uint32_t ki) {
+    const uint32_t i = draw_index(ki, g.V);
+    const uint2 e = g.vtab[i];
+    return kp < e.x ? (int32_t)i : (int32_t)e.y;
+}
+
+// TargetSample(vid) src/proNet.cpp:671-683 (branch 0 -> -1; p, then index)
+__device__ __forceinline__ int32_t target_sample(const DevGraph& g, int32_t v, uint32_t kp,
+                                                 uint32_t ki) {
+    const int64_t off = g.offsets[v];
+    const int64_t br = g.offsets[v + 1] - off;
+    if (br == 0) return -1;
+    const int64_t i = off + draw_index(ki, (uint32_t)br);
+    const uint2 e = g.ctab[i];
+    const int32_t t = g.targets[i];
+    return kp < e.x ? t : (int32_t)e.y;
+}
+
+// NegativeSample src/proNet.cpp:623-633 (index FIRST, then p)
+__device__ __forceinline__ int32_t negative_sample(const DevGraph& g, uint32_t ki, uint32_t kp) {
+    const uint32_t i = draw_index(ki, g.V);
+    const uint2 e = g.ntab[i];
+    return kp < e.x ? (int32_t)i : (int32_t)e.y;
+}
+
+// fastSigmoid src/proNet.cpp:62-71 on an fp32 dot: bucket index in fp64.
+__device__ __forceinline__ float fast_sigmoid(float f, const float* tab) {
+    const double x = (double)f;
+    if (x < -8.0) return 0.0f;
+    if (x > 8.0) return 1.0f;
+    return tab[(int)((x + 8.0) * 1000 / 8.0 / 2)];
+}
+
+// learning rate of the sample run with counter value c
+// (src/model/LINE.cpp:180-184, MF.cpp:95-99, BPR.cpp:95-99)
+__device__ __forceinline__ float alpha_at(uint64_t c, double alpha0, uint64_t total) {
+    const uint64_t u = c / 10000;
+    double a = alpha0;
+    if (u != 0) {
+        a = alpha0 * (1.0 - (double)((u - 1) * 10000) / (double)total);
+        const double amin = alpha0 * 0.0001;
+        if (a < amin) a = amin;
+    }
+    return (float)a;
+}
+
+// DeepWalk walk w (src/model/DeepWalk.cpp:141-147)
+__device__ __forceinline__ float alpha_walk(uint64_t w, double alpha0, uint64_t total) {
+    const uint64_t u = w / 10000;
+    double a = alpha0;
+    if (u != 0) {
+        a = alpha0 * (1.0 - (double)(u * 10000) / (double)total);
+        const double amin = alpha0 * 0.0001;
+        if (a < amin) a = amin;
+    }
+    return (float)a;
+}
+
+// pairwise-tree sum over the G lanes of a sample group; every lane of the
+// group ends with the bit-identical total (IEEE add is commutative).
+template <int G>
+__device__ __forceinline__ float group_sum(float p) {
+#pragma unroll
+    for (int m = 1; m < G; m <<= 1) p += __shfl_xor(p, m, G);
+    return p;
+}
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, const float4& v) { *reinterpret_cast<float4*>(p) = v; }
+
+__device__ __forceinline__ void atomic_add4(float* p, const float4& d) {
+    unsafeAtomicAdd(p + 0, d.x);
+    unsafeAtomicAdd(p + 1, d.y);
+    unsafeAtomicAdd(p + 2, d.z);
+    unsafeAtomicAdd(p + 3, d.w);
+}
+
+__device__ __forceinline__ float4 sub4(const float4& a, const float4& b) {
+    return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
+}
+__device__ __forceinline__ float4 add4(const float4& a, const float4& b) {
+    return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ float4 fma4(float s, const float4& a, const float4& b) {
+    return make_float4(__builtin_fmaf(s, a.x, b.x), __builtin_fmaf(s, a.y, b.y),
+                       __builtin_fmaf(s, a.z, b.z), __builtin_fmaf(s, a.w, b.w));
+}
+// partial dot: fmaf chain in element order starting from p
+__device__ __forceinline__ float dot4(const float4& a, const float4& b, float p) {
+    p = __builtin_fmaf(a.x, b.x, p);
+    p = __builtin_fmaf(a.y, b.y, p);
+    p = __builtin_fmaf(a.z, b.z, p);
+    p = __builtin_fmaf(a.w, b.w, p);
+    return p;
+}
+
+}  // namespace smore

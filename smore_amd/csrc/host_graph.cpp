@@ -1,0 +1,291 @@
+// host_graph.cpp -- see host_graph.h.
+#include "host_graph.h"
+
+#include <dirent.h>
+#include <sys/stat.h>
+
+#include <algorithm>
+#include <functional>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <thread>
+#include <unordered_map>
+
+namespace smore {
+
+void alias_cpp(const double* dist, int64_t n, double* prob, int64_t* alias) {
+    // sequential sum in index order, as src/proNet.cpp:556-559
+    double sum = 0.0;
+    for (int64_t i = 0; i < n; ++i) sum += std::pow(dist[i], 0.75);
+    const double norm = (double)n / sum;
+    std::vector<double> q((size_t)n);
+    std::vector<int64_t> small, large;
+    small.reserve((size_t)n);
+    large.reserve((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        q[i] = std::pow(dist[i], 0.75) * norm;
+        prob[i] = 0.0;
+        alias[i] = -1;
+    }
+    for (int64_t i = 0; i < n; ++i) (q[i] < 1 ? small : large).push_back(i);
+    while (!small.empty() && !large.empty()) {
+        int64_t s = small.back(); small.pop_back();
+        int64_t l = large.back(); large.pop_back();
+        alias[s] = l;
+        prob[s] = q[s];
+        q[l] = q[l] + q[s] - 1;
+        (q[l] < 1 ? small : large).push_back(l);
+    }
+    while (!large.empty()) { prob[large.back()] = 1.0; large.pop_back(); }
+    while (!small.empty()) { prob[small.back()] = 1.0; small.pop_back(); }
+}
+
+void alias_encode(const double* prob, const int64_t* alias, int64_t n, const int32_t* self_ids,
+                  AliasEntry* out) {
+    for (int64_t i = 0; i < n; ++i) {
+        const int32_t self = self_ids ? self_ids[i] : (int32_t)i;
+        double t = std::ceil(std::ldexp(prob[i], 32));
+        if (!(t >= 0)) t = 0;  // NaN: never accept
+        if (t >= 4294967296.0) {
+            out[i].thresh = 0xFFFFFFFFu;
+            out[i].alias = self;
+        } else {
+            out[i].thresh = (uint32_t)t;
+            out[i].alias = alias[i] < 0 ? self : (int32_t)alias[i];
+        }
+    }
+}
+
+static void parallel_for(int64_t n, int64_t grain, const std::function<void(int64_t, int64_t)>& fn) {
+    unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    unsigned nt = (unsigned)std::min<int64_t>(std::min<unsigned>(hw, 16u), (n + grain - 1) / grain);
+    if (nt <= 1) { fn(0, n); return; }
+    std::vector<std::thread> th;
+    int64_t chunk = (n + nt - 1) / nt;
+    for (unsigned t = 0; t < nt; ++t) {
+        int64_t b = t * chunk, e = std::min(n, b + chunk);
+        if (b < e) th.emplace_back(fn, b, e);
+    }
+    for (auto& x : th) x.join();
+}
+
+bool build_graph(int64_t V, int64_t E, const int32_t* src, const int32_t* dst, const double* w,
+                 int vertex_method, int negative_method, HostGraph& g, std::string& err) {
+    if (V <= 0 || V >= (int64_t)1 << 31 || E < 0) { err = "bad graph size"; return false; }
+    for (int64_t e = 0; e < E; ++e)
+        if (src[e] < 0 || src[e] >= V || dst[e] < 0 || dst[e] >= V) {
+            err = "edge " + std::to_string(e) + " has a vertex id out of range";
+            return false;
+        }
+    g.V = V;
+    g.E = E;
+    g.offsets.assign((size_t)V + 1, 0);
+    g.targets.resize((size_t)E);
+    g.weights.resize((size_t)E);
+    // CSR by a stable counting sort: per source, targets keep push order
+    // (graph[vid1].push_back(vid2), src/proNet.cpp:208-215 and :427-437)
+    for (int64_t e = 0; e < E; ++e) g.offsets[src[e] + 1]++;
+    for (int64_t v = 0; v < V; ++v) g.offsets[v + 1] += g.offsets[v];
+    {
+        std::vector<int64_t> cur(g.offsets.begin(), g.offsets.end() - 1);
+        for (int64_t e = 0; e < E; ++e) {
+            int64_t p = cur[src[e]]++;
+            g.targets[p] = dst[e];
+            g.weights[p] = w[e];
+        }
+    }
+    // degrees (src/proNet.cpp:431-443): out in adjacency order, in over the CSR
+    g.out_deg.assign((size_t)V, 0.0);
+    g.in_deg.assign((size_t)V, 0.0);
+    for (int64_t v = 0; v < V; ++v)
+        for (int64_t p = g.offsets[v]; p < g.offsets[v + 1]; ++p) g.out_deg[v] += g.weights[p];
+    for (int64_t p = 0; p < E; ++p) g.in_deg[g.targets[p]] += g.weights[p];
+
+    std::vector<double> dist((size_t)V);
+    // vertex table (src/proNet.cpp:457-482)
+    for (int64_t v = 0; v < V; ++v) {
+        if (vertex_method == 0) dist[v] = g.out_deg[v];
+        else if (vertex_method == 1) dist[v] = g.out_deg[v] == 0 ? 0 : 1;
+        else dist[v] = g.in_deg[v] + g.out_deg[v];
+    }
+    g.vprob.resize((size_t)V); g.valias.resize((size_t)V);
+    alias_cpp(dist.data(), V, g.vprob.data(), g.valias.data());
+    // negative table (src/proNet.cpp:485-510)
+    for (int64_t v = 0; v < V; ++v) {
+        if (negative_method == 0) dist[v] = g.in_deg[v] + g.out_deg[v];
+        else if (negative_method == 1) dist[v] = g.in_deg[v];
+        else dist[v] = g.in_deg[v] == 0 ? 0 : 1;
+    }
+    g.nprob.resize((size_t)V); g.nalias.resize((size_t)V);
+    alias_cpp(dist.data(), V, g.nprob.data(), g.nalias.data());
+    // per-vertex context tables, alias remapped to the target vid
+    // (src/proNet.cpp:517-537); vertices are independent -> threads
+    g.cprob.resize((size_t)E); g.calias.resize((size_t)E);
+    g.vtab.resize((size_t)V); g.ntab.resize((size_t)V); g.ctab.resize((size_t)E);
+    parallel_for(V, 1 << 14, [&](int64_t b, int64_t e) {
+        for (int64_t v = b; v < e; ++v) {
+            int64_t off = g.offsets[v], br = g.offsets[v + 1] - off;
+            if (br == 0) continue;
+            alias_cpp(g.weights.data() + off, br, g.cprob.data() + off, g.calias.data() + off);
+            for (int64_t i = 0; i < br; ++i)
+                if (g.calias[off + i] != -1) g.calias[off + i] = g.targets[off + g.calias[off + i]];
+            alias_encode(g.cprob.data() + off, g.calias.data() + off, br, g.targets.data() + off,
+                         g.ctab.data() + off);
+        }
+    });
+    alias_encode(g.vprob.data(), g.valias.data(), V, nullptr, g.vtab.data());
+    alias_encode(g.nprob.data(), g.nalias.data(), V, nullptr, g.ntab.data());
+    return true;
+}
+
+// ---------------------------------------------------------------- loader
+static bool is_dir(const std::string& p) {
+    struct stat st;
+    return stat(p.c_str(), &st) == 0 && S_ISDIR(st.st_mode);
+}
+
+bool read_edgelist(const std::string& path, bool undirected, std::vector<std::string>& names,
+                   std::vector<int32_t>& src, std::vector<int32_t>& dst, std::vector<double>& w,
+                   std::string& err) {
+    std::vector<std::string> files;
+    if (is_dir(path)) {  // directory input (src/proNet.cpp:124-134), readdir order
+        DIR* d = opendir(path.c_str());
+        if (!d) { err = "cannot open directory " + path; return false; }
+        while (struct dirent* ent = readdir(d)) {
+            std::string f = path + "/" + ent->d_name;
+            if (!is_dir(f)) files.push_back(f);
+        }
+        closedir(d);
+    } else {
+        files.push_back(path);
+    }
+    std::unordered_map<std::string, int32_t> ids;
+    auto intern = [&](const char* b, size_t n) -> int32_t {
+        std::string key(b, n);
+        auto it = ids.find(key);
+        if (it != ids.end()) return it->second;
+        int32_t id = (int32_t)names.size();
+        ids.emplace(std::move(key), id);
+        names.emplace_back(b, n);
+        return id;
+    };
+    std::vector<char> buf(1 << 22);
+    for (const auto& fn : files) {
+        FILE* f = fopen(fn.c_str(), "rb");
+        if (!f) { err = "cannot open " + fn; return false; }
+        std::string carry;
+        size_t got;
+        auto handle_line = [&](const char* s, const char* e) {
+            // first three whitespace-separated fields "v1 v2 w" (lines with
+            // fewer are skipped, as pkg/pronet/pronet.go:132-134)
+            const char* tok[3]; size_t len[3]; int nt = 0;
+            const char* p = s;
+            while (p < e && nt < 3) {
+                while (p < e && (*p == ' ' || *p == '\t' || *p == '\r')) ++p;
+                if (p >= e) break;
+                const char* q = p;
+                while (q < e && !(*q == ' ' || *q == '\t' || *q == '\r')) ++q;
+                tok[nt] = p; len[nt] = (size_t)(q - p); ++nt;
+                p = q;
+            }
+            if (nt < 3) return;
+            char wb[64];
+            size_t wl = std::min<size_t>(len[2], 63);
+            memcpy(wb, tok[2], wl); wb[wl] = 0;
+            char* endp;
+            double x = strtod(wb, &endp);
+            if (endp == wb) return;
+            int32_t a = intern(tok[0], len[0]);
+            int32_t b = intern(tok[1], len[1]);
+            src.push_back(a); dst.push_back(b); w.push_back(x);
+            if (undirected) { src.push_back(b); dst.push_back(a); w.push_back(x); }
+        };
+        while ((got = fread(buf.data(), 1, buf.size(), f)) > 0) {
+            const char* s = buf.data();
+            const char* end = s + got;
+            const char* nl;
+            while ((nl = (const char*)memchr(s, '\n', (size_t)(end - s)))) {
+                if (!carry.empty()) {
+                    carry.append(s, nl);
+                    handle_line(carry.data(), carry.data() + carry.size());
+                    carry.clear();
+                } else {
+                    handle_line(s, nl);
+                }
+                s = nl + 1;
+            }
+            carry.append(s, end);
+        }
+        if (!carry.empty()) handle_line(carry.data(), carry.data() + carry.size());
+        fclose(f);
+        if (names.size() >= ((size_t)1 << 31) - 1) { err = "too many vertices"; return false; }
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------- glibc rand
+GlibcRand::GlibcRand(uint32_t seed) {
+    int32_t r[344];
+    if (seed == 0) seed = 1;
+    r[0] = (int32_t)seed;
+    for (int i = 1; i < 31; ++i) {
+        int32_t hi = r[i - 1] / 127773, lo = r[i - 1] % 127773;
+        int32_t word = 16807 * lo - 2836 * hi;
+        if (word < 0) word += 2147483647;
+        r[i] = word;
+    }
+    for (int i = 31; i < 34; ++i) r[i] = r[i - 31];
+    for (int i = 34; i < 344; ++i) r[i] = (int32_t)((uint32_t)r[i - 31] + (uint32_t)r[i - 3]);
+    for (int i = 0; i < 34; ++i) tbl_[i] = (uint32_t)r[310 + i];
+    pos_ = 0;
+}
+
+int32_t GlibcRand::next() {
+    uint32_t v = tbl_[(pos_ + 3) % 34] + tbl_[(pos_ + 31) % 34];
+    tbl_[pos_] = v;
+    pos_ = (pos_ + 1) % 34;
+    return (int32_t)(v >> 1);
+}
+
+void GlibcRand::discard(uint64_t n) {
+    for (uint64_t i = 0; i < n; ++i) next();
+}
+
+void deepwalk_order(int64_t V, int walk_times, uint64_t skip, int64_t* order) {
+    GlibcRand r;
+    r.discard(skip);
+    for (int t = 0; t < walk_times; ++t) {
+        int64_t* keys = order + (int64_t)t * V;
+        for (int64_t v = 0; v < V; ++v) keys[v] = v;
+        for (int64_t v = 0; v < V; ++v) {
+            int rdx = (int)(v + r.next() % (V - v));
+            std::swap(keys[v], keys[rdx]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- saver
+bool save_weights(const std::string& path, const HostGraph& g, const float* table, int64_t rows,
+                  int dim, int stride, int fmt, std::string& err) {
+    FILE* f = fopen(path.c_str(), "wb");
+    if (!f) { err = "cannot open " + path; return false; }
+    std::vector<char> obuf(1 << 22);
+    setvbuf(f, obuf.data(), _IOFBF, obuf.size());
+    fprintf(f, "%lld %d\n", (long long)rows, dim);
+    for (int64_t v = 0; v < rows; ++v) {
+        if (!g.names.empty()) fputs(g.names[v].c_str(), f);
+        else fprintf(f, "%lld", (long long)v);
+        const float* r = table + v * stride;
+        for (int d = 0; d < dim; ++d) {
+            if (fmt == 1) fprintf(f, " %.6f", (double)r[d]);
+            else fprintf(f, " %g", (double)r[d]);
+        }
+        fputc('\n', f);
+    }
+    bool ok = fclose(f) == 0;
+    if (!ok) err = "write failed: " + path;
+    return ok;
+}
+
+}  // namespace smore

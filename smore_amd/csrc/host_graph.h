@@ -1,0 +1,71 @@
+// host_graph.h -- host-side graph construction for the MI355X hot path.
+//
+// Everything here runs once per run on the host (not in the metric): edge-list
+// loading, CSR build, Vose alias tables and their device encoding, glibc
+// rand() initialisation and the text saver.  Each function cites the
+// reference code it replaces (RainBoltz/smore, C++ proNet-core).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace smore {
+
+struct AliasEntry {          // device encoding of one alias-table entry (8 B)
+    uint32_t thresh;         // accept iff k < thresh (k = 32-bit uniform word)
+    int32_t alias;           // id returned otherwise (self when always accepted)
+};
+
+struct HostGraph {
+    int64_t V = 0, E = 0;
+    std::vector<std::string> names;          // empty when built from ids
+    std::vector<int64_t> offsets;            // V+1
+    std::vector<int32_t> targets;            // E, push order per source
+    std::vector<double> weights;             // E
+    std::vector<double> out_deg, in_deg;     // V
+    // reference representation (prob, alias with -1 = none)
+    std::vector<double> vprob, nprob, cprob;
+    std::vector<int64_t> valias, nalias, calias;
+    // device encoding
+    std::vector<AliasEntry> vtab, ntab, ctab;
+};
+
+// Vose alias method, C++ rule (src/proNet.cpp:544-620): q = d^0.75 * n / sum
+// (power argument ignored, :558,564), LIFO stacks, leftovers prob 1 alias -1.
+void alias_cpp(const double* dist, int64_t n, double* prob, int64_t* alias);
+
+// {prob, alias} -> {ceil(prob * 2^32), alias}; always-accept entries store
+// {0xFFFFFFFF, self}; alias -1 -> self.  self_ids == nullptr: self = index.
+void alias_encode(const double* prob, const int64_t* alias, int64_t n, const int32_t* self_ids,
+                  AliasEntry* out);
+
+// CSR + degrees + all three alias tables from directed edge slots in the
+// reference's push order (src/proNet.cpp:208-215, 410-542).  Returns false on
+// an id out of range.
+bool build_graph(int64_t V, int64_t E, const int32_t* src, const int32_t* dst, const double* w,
+                 int vertex_method, int negative_method, HostGraph& g, std::string& err);
+
+// Text edge list(s) -> names + directed slots (src/proNet.cpp:115-236).
+bool read_edgelist(const std::string& path, bool undirected, std::vector<std::string>& names,
+                   std::vector<int32_t>& src, std::vector<int32_t>& dst, std::vector<double>& w,
+                   std::string& err);
+
+// glibc TYPE_3 rand() stream after srand(1) (the reference's Init).
+class GlibcRand {
+  public:
+    explicit GlibcRand(uint32_t seed = 1);
+    int32_t next();
+    void discard(uint64_t n);
+  private:
+    uint32_t tbl_[34];
+    int pos_ = 0;
+};
+
+// DeepWalk walk-start order (src/model/DeepWalk.cpp:122-131).
+void deepwalk_order(int64_t V, int walk_times, uint64_t skip, int64_t* order);
+
+// SaveWeights text format (src/model/LINE.cpp:13-47 / Go line.go:209-233).
+bool save_weights(const std::string& path, const HostGraph& g, const float* table, int64_t rows,
+                  int dim, int stride, int fmt, std::string& err);
+
+}  // namespace smore

@@ -1,0 +1,29 @@
+// train_kernels.h -- launch interface of the gfx950 hot-path kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "device_common.h"
+
+namespace smore {
+
+struct EdgeArgs {
+    DevGraph g;
+    const float* sig;              // 1001-entry fastSigmoid table
+    float* W;                      // [V][dpad]
+    float* C;                      // [V][dpad] (== W for shared-table models)
+    unsigned long long* skipped;   // samples whose source had no out-edge
+    uint64_t begin, count, total, seed;
+    double alpha0;
+    float reg;
+    int dpad, K, model, mode;
+};
+
+int lanes_of(int dpad);
+hipError_t launch_edge_train(const EdgeArgs& a, int grid, hipStream_t st);
+const void* edge_kernel_symbol(const EdgeArgs& a);
+hipError_t launch_sample(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K,
+                         int bpr, int32_t* out, hipStream_t st);
+hipError_t launch_init_uniform(float* T, int64_t rows, int dim, int dpad, uint64_t seed,
+                               hipStream_t st);
+
+}  // namespace smore

@@ -1,0 +1,200 @@
+"""ProNet: host-side mirror of the reference proNet core (src/proNet.h:109-269,
+Go pkg/pronet/pronet.go:47-74) backed by one libsmore_hip context (one GPU).
+
+Method names follow the reference (SetNegativeMethod, LoadEdgeList,
+SourceSample/TargetSample/NegativeSample as batch samplers, ...).  All work
+happens in the C ABI; this module only marshals numpy buffers.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib, ptr
+
+
+class ProNet:
+    """Graph + alias tables + embedding tables on one GPU.
+
+    device=-1 gives a host-only context (graph and alias building, no GPU)."""
+
+    def __init__(self, device=0):
+        self.ctx = C.c_void_p()
+        rc = lib.smore_create(int(device), C.byref(self.ctx))
+        if rc != _lib.OK:
+            raise _lib.SmoreError("smore_create(device=%d) failed with status %d" % (device, rc))
+        self.device = device
+        self.vertex_method = "out_degrees"    # src/proNet.cpp:9
+        self.negative_method = "degrees"      # src/proNet.cpp:11
+        self.dim = 0
+
+    # ---------------------------------------------------------------- lifecycle
+    def close(self):
+        if self.ctx:
+            lib.smore_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc, what):
+        check(self.ctx, rc, what)
+
+    # ---------------------------------------------------------------- methods
+    def SetNegativeMethod(self, method):
+        if method not in _lib.NM:
+            raise ValueError(method)
+        self.negative_method = method
+
+    def SetVertexMethod(self, method):
+        if method not in _lib.VM:
+            raise ValueError(method)
+        self.vertex_method = method
+
+    # ---------------------------------------------------------------- graph
+    def LoadEdgeList(self, filename, undirect):
+        """proNet::LoadEdgeList (src/proNet.cpp:115-236)."""
+        self._chk(lib.smore_load_edgelist(self.ctx, filename.encode(), int(bool(undirect)),
+                                          _lib.VM[self.vertex_method], _lib.NM[self.negative_method]),
+                  "LoadEdgeList(%s)" % filename)
+
+    def set_graph_edges(self, V, src, dst, w):
+        """Graph from ids: directed edge slots src->dst (weight w) in push order."""
+        src = np.ascontiguousarray(src, np.int32)
+        dst = np.ascontiguousarray(dst, np.int32)
+        w = np.ascontiguousarray(w, np.float64)
+        self._chk(lib.smore_set_graph_edges(self.ctx, int(V), len(src), ptr(src), ptr(dst), ptr(w),
+                                            _lib.VM[self.vertex_method], _lib.NM[self.negative_method]),
+                  "set_graph_edges")
+
+    def _info(self):
+        V, E = C.c_int64(), C.c_int64()
+        self._chk(lib.smore_graph_info(self.ctx, C.byref(V), C.byref(E)), "graph_info")
+        return V.value, E.value
+
+    @property
+    def MAX_vid(self):
+        return self._info()[0]
+
+    @property
+    def MAX_line(self):
+        return self._info()[1]
+
+    def vertex_name(self, vid):
+        n = lib.smore_vertex_name(self.ctx, int(vid))
+        return None if n is None else n.decode()
+
+    @property
+    def names(self):
+        return [self.vertex_name(v) for v in range(self.MAX_vid)]
+
+    def csr(self):
+        V, E = self._info()
+        off = np.zeros(V + 1, np.int64)
+        tgt = np.zeros(max(E, 1), np.int32)
+        self._chk(lib.smore_get_csr(self.ctx, ptr(off), ptr(tgt)), "get_csr")
+        return off, tgt[:E]
+
+    def alias(self, which):
+        """(prob, alias) of vertex_AT / negative_AT / context_AT."""
+        V, E = self._info()
+        n = E if which == _lib.AT_CONTEXT else V
+        p = np.zeros(n)
+        a = np.zeros(n, np.int64)
+        self._chk(lib.smore_get_alias(self.ctx, which, ptr(p), ptr(a), n), "get_alias")
+        return p, a
+
+    def alias_encoded(self, which):
+        V, E = self._info()
+        n = E if which == _lib.AT_CONTEXT else V
+        t = np.zeros(n, np.uint32)
+        a = np.zeros(n, np.int32)
+        self._chk(lib.smore_get_alias_encoded(self.ctx, which, ptr(t), ptr(a), n), "get_alias_encoded")
+        return t, a
+
+    def set_alias(self, which, prob, alias):
+        """Inject an alias table (Go CTDNE assigns ProNet.NegativeAT directly)."""
+        prob = np.ascontiguousarray(prob, np.float64)
+        alias = np.ascontiguousarray(alias, np.int64)
+        self._chk(lib.smore_set_alias(self.ctx, which, ptr(prob), ptr(alias), len(prob)), "set_alias")
+
+    # ---------------------------------------------------------------- samplers
+    def sample_edges(self, model, begin, count, K, seed):
+        """Draws of samples [begin, begin+count): rows {v, c, n1..nK} (BPR: {u, i, j0..j4})."""
+        width = 7 if model == "bpr" else 2 + K
+        out = np.zeros((count, width), np.int32)
+        self._chk(lib.smore_sample_edges(self.ctx, _lib.MODEL[model], begin, count, K, seed, ptr(out)),
+                  "sample_edges")
+        return out
+
+    # ---------------------------------------------------------------- tables
+    def alloc_tables(self, dim, ntables):
+        self._chk(lib.smore_alloc_tables(self.ctx, int(dim), int(ntables)), "alloc_tables")
+        self.dim = dim
+
+    def init_table_glibc(self, which, skip=0):
+        self._chk(lib.smore_init_table_glibc(self.ctx, which, int(skip)), "init_table_glibc")
+
+    def init_table_uniform(self, which, seed):
+        self._chk(lib.smore_init_table_uniform(self.ctx, which, int(seed)), "init_table_uniform")
+
+    def zero_table(self, which):
+        self._chk(lib.smore_zero_table(self.ctx, which), "zero_table")
+
+    def set_table(self, which, host):
+        host = np.ascontiguousarray(host, np.float32)
+        self._chk(lib.smore_set_table(self.ctx, which, ptr(host), host.shape[0], host.shape[1]), "set_table")
+
+    def get_table(self, which):
+        V = self.MAX_vid
+        out = np.zeros((V, self.dim), np.float32)
+        self._chk(lib.smore_get_table(self.ctx, which, ptr(out), V, self.dim), "get_table")
+        return out
+
+    def table_device(self, which):
+        p, s = C.c_void_p(), C.c_int64()
+        self._chk(lib.smore_table_device(self.ctx, which, C.byref(p), C.byref(s)), "table_device")
+        return p.value, s.value
+
+    # ---------------------------------------------------------------- training
+    def set_stream(self, stream_handle):
+        self._chk(lib.smore_set_stream(self.ctx, C.c_void_p(stream_handle) if stream_handle else None),
+                  "set_stream")
+
+    def train_edges(self, model, begin, count, total, K, alpha0, reg=0.0, seed=1, mode="hogwild", sync=True):
+        fn = lib.smore_train_edges if sync else lib.smore_train_edges_async
+        self._chk(fn(self.ctx, _lib.MODEL[model], int(begin), int(count), int(total), int(K), float(alpha0),
+                     float(reg), int(seed), _lib.MODE[mode]), "train_edges")
+
+    def train_deepwalk(self, walk_begin, walk_end, walk_times, walk_steps, window, K, alpha0, seed, order,
+                       mode="hogwild"):
+        order = np.ascontiguousarray(order, np.int64)
+        self._chk(lib.smore_train_deepwalk(self.ctx, int(walk_begin), int(walk_end), int(walk_times),
+                                           int(walk_steps), int(window), int(K), float(alpha0), int(seed),
+                                           ptr(order), _lib.MODE[mode]), "train_deepwalk")
+
+    def synchronize(self):
+        self._chk(lib.smore_synchronize(self.ctx), "synchronize")
+
+    def skipped(self):
+        s = C.c_uint64()
+        self._chk(lib.smore_skipped(self.ctx, C.byref(s)), "skipped")
+        return s.value
+
+    def last_kernel_ms(self):
+        return float(lib.smore_last_kernel_ms(self.ctx))
+
+    def save_weights(self, which, path, fmt=0):
+        self._chk(lib.smore_save_weights(self.ctx, which, path.encode(), int(fmt)), "save_weights")
+
+
+def deepwalk_order(V, walk_times, skip):
+    """Walk start order of DeepWalk::Train (src/model/DeepWalk.cpp:122-131)."""
+    out = np.zeros(int(V) * int(walk_times), np.int64)
+    rc = lib.smore_deepwalk_order(int(V), int(walk_times), int(skip), ptr(out))
+    if rc != _lib.OK:
+        raise _lib.SmoreError("deepwalk_order failed")
+    return out
