@@ -25,18 +25,11 @@ $(OBJ)/capi.o: $(SRC)/capi.cpp $(HDRS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(CXXFLAGS) -c -o $@ $<
 
-$(OBJ)/train_kernels.o: $(SRC)/train_kernels.hip $(HDRS)
+$(OBJ)/%.o: $(SRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-$(OBJ)/walk_kernels.o: $(SRC)/walk_kernels.hip $(HDRS)
-	@mkdir -p $(OBJ)
-	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
-
-LIB_OBJS := $(OBJ)/host_graph.o $(OBJ)/capi.o $(OBJ)/train_kernels.o $(wildcard $(SRC)/walk_kernels.hip:%=)
-ifneq ($(wildcard $(SRC)/walk_kernels.hip),)
-LIB_OBJS += $(OBJ)/walk_kernels.o
-endif
+LIB_OBJS := $(OBJ)/host_graph.o $(OBJ)/capi.o $(patsubst $(SRC)/%.hip,$(OBJ)/%.o,$(wildcard $(SRC)/*.hip))
 
 $(LIB): $(LIB_OBJS)
 	@mkdir -p $(dir $@)

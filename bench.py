@@ -97,7 +97,8 @@ def main():
     pn.alloc_tables(args.dim, 2)
     pn.init_table_uniform(0, args.seed)     # W ~ (u-0.5)/d, as the reference Init law
     pn.zero_table(1)                        # C = 0 (src/model/LINE.cpp:92)
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream()             # a real stream: the default one is the null stream
+    torch.cuda.set_stream(stream)
     pn.set_stream(stream.cuda_stream)
     sync = ReplicaSync(pn, mean=(args.sync == "mean")) if world > 1 else None
 

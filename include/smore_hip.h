@@ -107,7 +107,7 @@ int smore_get_alias_encoded(const smore_ctx* ctx, int which, uint32_t* thresh, i
 
 /* ---- embedding tables ---------------------------------------------------------- */
 /* allocate W (and C when ntables == 2) as [V][dpad] fp32, dpad = dim rounded up
- * to a multiple of 4 (rows 16-byte aligned).  Tables start zeroed. */
+ * to a multiple of 4 (rows 16-byte aligned); 1 <= dim <= 512.  Tables start zeroed. */
 int smore_alloc_tables(smore_ctx* ctx, int dim, int ntables);
 /* replaces: the rand() initialisation in LINE/MF/BPR/DeepWalk::Init
  * (src/model/LINE.cpp:83, MF.cpp:50, BPR.cpp:49, DeepWalk.cpp:47,54):

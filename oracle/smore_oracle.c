@@ -579,9 +579,11 @@ int orc_train_deepwalk_f64(const orc_graph* g, double* W, double* C, int dim,
 /* ========================================================================== */
 /* fp32 spec (DESIGN.md "Arithmetic spec"), what the HIP kernels compute.      */
 /* Rows are padded to dpad (multiple of 4) floats.  A sample is owned by G      */
-/* lanes (G = min(64, pow2ceil(dpad/4))); lane l owns 4-float chunks q with     */
-/* q % G == l.  dot = pairwise tree over the G lane partials, each an fmaf     */
-/* chain over its chunks in increasing element order starting from +0.0f.      */
+/* lanes (G = min(64, pow2ceil(dpad/4))); lane l owns the elements l, l+G,      */
+/* l+2G, ... below dpad (interleaved, so one wave instruction touches a         */
+/* contiguous 4G-byte row segment).  dot = pairwise tree over the G lane        */
+/* partials, each an fmaf chain over its elements in increasing order from     */
+/* +0.0f.                                                                      */
 /* ========================================================================== */
 int orc_lane_width(int dpad) {
     int nq = dpad / 4, G = 1;
@@ -591,11 +593,11 @@ int orc_lane_width(int dpad) {
 
 static float dot_spec(const float* a, const float* b, int dpad) {
     float part[64];
-    int G = orc_lane_width(dpad), nq = dpad / 4;
-    for (int l = 0; l < G; ++l) part[l] = 0.0f;
-    for (int q = 0; q < nq; ++q) {
-        int l = q % G;
-        for (int e = 4 * q; e < 4 * q + 4; ++e) part[l] = fmaf(a[e], b[e], part[l]);
+    int G = orc_lane_width(dpad);
+    for (int l = 0; l < G; ++l) {
+        float p = 0.0f;
+        for (int e = l; e < dpad; e += G) p = fmaf(a[e], b[e], p);
+        part[l] = p;
     }
     for (int w = 1; w < G; w <<= 1)
         for (int l = 0; l < G; l += 2 * w) part[l] = part[l] + part[l + w];

@@ -274,7 +274,7 @@ int smore_get_alias_encoded(const smore_ctx* c, int which, uint32_t* thresh, int
 int smore_alloc_tables(smore_ctx* c, int dim, int ntables) {
     if (!c) return SMORE_EINVAL;
     if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
-    if (dim <= 0 || dim > 1024 || ntables < 1 || ntables > 2) return fail(c, SMORE_EINVAL, "bad dim/ntables");
+    if (dim <= 0 || dim > 512 || ntables < 1 || ntables > 2) return fail(c, SMORE_EINVAL, "bad dim/ntables");
     int rc;
     if ((rc = set_device(c))) return rc;
     dfree(c->d_table[0]);

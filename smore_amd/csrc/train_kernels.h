@@ -19,6 +19,12 @@ struct EdgeArgs {
 };
 
 int lanes_of(int dpad);
+hipError_t launch_edge_store(const EdgeArgs& a, int grid, hipStream_t st);
+hipError_t launch_edge_atomic(const EdgeArgs& a, int grid, hipStream_t st);
+hipError_t launch_bpr(const EdgeArgs& a, int grid, hipStream_t st);
+const void* edge_symbol_store(const EdgeArgs& a);
+const void* edge_symbol_atomic(const EdgeArgs& a);
+const void* bpr_symbol(const EdgeArgs& a);
 hipError_t launch_edge_train(const EdgeArgs& a, int grid, hipStream_t st);
 const void* edge_kernel_symbol(const EdgeArgs& a);
 hipError_t launch_sample(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K,
