@@ -59,6 +59,7 @@ typedef struct smore_ctx smore_ctx;
 #define SMORE_HOGWILD 0  /* lock-free read-modify-write stores (the reference's Hogwild) */
 #define SMORE_ATOMIC 1   /* read, then float atomic add of each row's delta            */
 #define SMORE_SERIAL 2   /* one lane group, samples strictly in order (parity mode)    */
+#define SMORE_HYBRID 3   /* atomic adds for rows hot enough to collide, stores elsewhere */
 
 /* ---- context --------------------------------------------------------------- */
 /* replaces: construction of proNet / LINE / BPR / MF / DeepWalk
@@ -131,7 +132,7 @@ int smore_table_device(smore_ctx* ctx, int which, void** dptr, int64_t* stride);
  * (learning-rate schedule of the reference from the global sample index).
  * model: SMORE_LINE2 | SMORE_LINE1 | SMORE_MF | SMORE_BPR; K negatives
  * (BPR: fixed 5 rounds, K ignored as in the reference); reg: MF only.
- * mode: SMORE_HOGWILD | SMORE_ATOMIC | SMORE_SERIAL.  Asynchronous on the
+ * mode: SMORE_HOGWILD | SMORE_ATOMIC | SMORE_HYBRID | SMORE_SERIAL.  Asynchronous on the
  * context stream; *_sync waits and reports launch errors. */
 int smore_train_edges_async(smore_ctx* ctx, int model, uint64_t begin, uint64_t count,
                             uint64_t total, int K, double alpha0, double reg, uint64_t seed,
@@ -139,6 +140,11 @@ int smore_train_edges_async(smore_ctx* ctx, int model, uint64_t begin, uint64_t 
 int smore_train_edges(smore_ctx* ctx, int model, uint64_t begin, uint64_t count,
                       uint64_t total, int K, double alpha0, double reg, uint64_t seed,
                       int mode);
+/* SMORE_HYBRID: a row takes float atomics when (resident sample groups) x
+ * (its per-sample touch probability) > tau (default 0.1); see DESIGN.md */
+int smore_set_hot_threshold(smore_ctx* ctx, double tau);
+/* rows marked hot in W and C by the last hybrid launch */
+int smore_hot_rows(const smore_ctx* ctx, int64_t* hot_w, int64_t* hot_c);
 /* samples whose source had no out-edge (reference: TargetSample -> -1) */
 int smore_skipped(smore_ctx* ctx, uint64_t* skipped);
 /* milliseconds of the last training launch (HIP events on the launch stream) */

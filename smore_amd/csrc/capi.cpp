@@ -7,6 +7,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -36,6 +37,19 @@ struct smore_ctx {
     // tables
     float* d_table[2] = {nullptr, nullptr};
     int dim = 0, dpad = 0, ntables = 0;
+    // hybrid scatter: hot-row bitmaps (1 bit per row), keyed by what built them
+    uint32_t* d_hotW = nullptr;
+    uint32_t* d_hotC = nullptr;
+    double hot_tau = 0.1;
+    std::string hot_key;
+    int64_t hot_rows[2] = {0, 0};
+    // DeepWalk buffers
+    int64_t* d_order = nullptr;
+    uint64_t walk_order_n = 0;
+    const int64_t* walk_order_host = nullptr;
+    int32_t* d_walks = nullptr;
+    int32_t* d_lens = nullptr;
+    size_t walk_buf_n = 0;
     // timing
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
@@ -157,6 +171,8 @@ void smore_destroy(smore_ctx* c) {
     }
     dfree(c->d_offsets); dfree(c->d_targets); dfree(c->d_vtab); dfree(c->d_ntab); dfree(c->d_ctab);
     dfree(c->d_sig); dfree(c->d_skipped); dfree(c->d_table[0]); dfree(c->d_table[1]);
+    dfree(c->d_hotW); dfree(c->d_hotC);
+    dfree(c->d_order); dfree(c->d_walks); dfree(c->d_lens);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -186,6 +202,7 @@ int smore_set_graph_edges(smore_ctx* c, int64_t V, int64_t E, const int32_t* src
     if ((E > 0 && (!src || !dst || !w)) || vm < 0 || vm > 2 || nm < 0 || nm > 2)
         return fail(c, SMORE_EINVAL, "bad arguments");
     c->g = HostGraph();
+    c->hot_key.clear();
     if (!build_graph(V, E, src, dst, w, vm, nm, c->g, c->err)) return SMORE_EINVAL;
     return upload_graph(c);
 }
@@ -238,6 +255,7 @@ int smore_set_alias(smore_ctx* c, int which, const double* prob, const int64_t* 
     std::vector<AliasEntry>& T = which == 0 ? g.vtab : which == 1 ? g.ntab : g.ctab;
     P.assign(prob, prob + n);
     A.assign(alias, alias + n);
+    c->hot_key.clear();
     T.resize((size_t)n);
     alias_encode(P.data(), A.data(), n, which == SMORE_AT_CONTEXT ? g.targets.data() : nullptr, T.data());
     if (c->device < 0) return SMORE_OK;
@@ -359,6 +377,34 @@ int smore_table_device(smore_ctx* c, int which, void** dptr, int64_t* stride) {
     return SMORE_OK;
 }
 
+// ---------------------------------------------------------------- hybrid scatter
+// A row is "hot" when the expected number of resident sample groups touching
+// it at once, M * p(row), exceeds tau; hot rows take float atomics, the rest
+// plain stores (DESIGN.md "Scatter modes").
+static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
+    char key[128];
+    snprintf(key, sizeof key, "%d/%d/%lld/%.9g", model, K, (long long)M, c->hot_tau);
+    if (c->hot_key == key) return SMORE_OK;
+    std::vector<double> ps, pn, pc;
+    draw_probabilities(c->g, ps, pn, pc);
+    const int64_t V = c->g.V, words = (V + 31) / 32;
+    std::vector<uint32_t> bw((size_t)words, 0), bc((size_t)words, 0);
+    const int negs = model == SMORE_BPR ? 5 : K;
+    c->hot_rows[0] = c->hot_rows[1] = 0;
+    for (int64_t v = 0; v < V; ++v) {
+        double pw, pcx;
+        if (model == SMORE_LINE2) { pw = ps[v]; pcx = pc[v] + negs * pn[v]; }
+        else { pw = pcx = ps[v] + pc[v] + negs * pn[v]; }
+        if ((double)M * pw > c->hot_tau) { bw[v >> 5] |= 1u << (v & 31); c->hot_rows[0]++; }
+        if ((double)M * pcx > c->hot_tau) { bc[v >> 5] |= 1u << (v & 31); c->hot_rows[1]++; }
+    }
+    int rc;
+    if ((rc = upload(c, c->d_hotW, bw.data(), bw.size()))) return rc;
+    if ((rc = upload(c, c->d_hotC, bc.data(), bc.size()))) return rc;
+    c->hot_key = key;
+    return SMORE_OK;
+}
+
 // ---------------------------------------------------------------- training
 static int edge_grid(smore_ctx* c, const EdgeArgs& a) {
     if (a.mode == SMORE_SERIAL) return 1;
@@ -378,7 +424,7 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
                             double alpha0, double reg, uint64_t seed, int mode) {
     if (!c) return SMORE_EINVAL;
     if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
-    if (model < 0 || model > 3 || mode < 0 || mode > 2 || K < 0 || K > 20)
+    if (model < 0 || model > 3 || mode < 0 || mode > 3 || K < 0 || K > 20)
         return fail(c, SMORE_EINVAL, "bad model/mode/K");
     const int need_tables = model == SMORE_LINE2 ? 2 : 1;
     if (c->ntables < need_tables) return fail(c, SMORE_ESTATE, "tables not allocated");
@@ -402,7 +448,14 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
     a.K = model == SMORE_BPR ? 5 : K;
     a.model = model;
     a.mode = mode;
+    a.hotW = a.hotC = nullptr;
     const int grid = edge_grid(c, a);
+    if (mode == SMORE_HYBRID) {
+        const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
+        if ((rc = build_hot_maps(c, model, a.K, M))) return rc;
+        a.hotW = c->d_hotW;
+        a.hotC = model == SMORE_LINE2 ? c->d_hotC : c->d_hotW;
+    }
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     HIPCHK(c, launch_edge_train(a, grid, c->stream));
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
@@ -416,6 +469,19 @@ int smore_train_edges(smore_ctx* c, int model, uint64_t begin, uint64_t count, u
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipGetLastError());
+    return SMORE_OK;
+}
+
+int smore_set_hot_threshold(smore_ctx* c, double tau) {
+    if (!c || !(tau >= 0)) return SMORE_EINVAL;
+    c->hot_tau = tau;
+    return SMORE_OK;
+}
+
+int smore_hot_rows(const smore_ctx* c, int64_t* hot_w, int64_t* hot_c) {
+    if (!c) return SMORE_EINVAL;
+    if (hot_w) *hot_w = c->hot_rows[0];
+    if (hot_c) *hot_c = c->hot_rows[1];
     return SMORE_OK;
 }
 
@@ -479,9 +545,79 @@ int smore_save_weights(const smore_ctx* cc, int which, const char* path, int fmt
 
 int smore_train_deepwalk(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
                          int window, int K, double alpha0, uint64_t seed, const int64_t* order, int mode) {
-    (void)walk_begin; (void)walk_end; (void)walk_times; (void)walk_steps; (void)window; (void)K;
-    (void)alpha0; (void)seed; (void)order; (void)mode;
-    return fail(c, SMORE_ESTATE, "deepwalk: not built yet");
+    if (!c) return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    if (c->ntables < 2) return fail(c, SMORE_ESTATE, "DeepWalk needs W and C tables");
+    if (!order || walk_times <= 0 || walk_steps < 0 || window <= 0 || K < 0 || K > 10 || mode < 0 || mode > 3)
+        return fail(c, SMORE_EINVAL, "bad DeepWalk arguments");
+    const uint64_t total = (uint64_t)walk_times * (uint64_t)c->g.V;
+    if (walk_end > total) walk_end = total;
+    if (walk_begin >= walk_end) return SMORE_OK;
+    for (uint64_t i = 0; i < total; ++i)
+        if (order[i] < 0 || order[i] >= c->g.V) return fail(c, SMORE_EINVAL, "walk start out of range");
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    // device copy of the start order; re-uploaded when the caller passes a
+    // different array (the caller must not mutate one it has passed)
+    if (c->walk_order_n != total || c->walk_order_host != order) {
+        if ((rc = upload(c, c->d_order, order, total))) return rc;
+        c->walk_order_n = total;
+        c->walk_order_host = order;
+    }
+    const uint64_t chunk = std::min<uint64_t>(walk_end - walk_begin, (uint64_t)1 << 20);
+    const size_t need = chunk * (size_t)(walk_steps + 1);
+    if (c->walk_buf_n < need) {
+        dfree(c->d_walks);
+        dfree(c->d_lens);
+        HIPCHK(c, hipMalloc((void**)&c->d_walks, need * sizeof(int32_t)));
+        HIPCHK(c, hipMalloc((void**)&c->d_lens, chunk * sizeof(int32_t)));
+        c->walk_buf_n = need;
+    }
+    EdgeArgs a;
+    a.g = dev_graph(c);
+    a.sig = c->d_sig;
+    a.W = c->d_table[0];
+    a.C = c->d_table[1];
+    a.skipped = c->d_skipped;
+    a.begin = 0; a.count = 0; a.total = total; a.seed = seed; a.alpha0 = alpha0; a.reg = 0.0f;
+    a.dpad = c->dpad; a.K = K; a.model = SMORE_LINE2; a.mode = mode;
+    a.hotW = a.hotC = nullptr;
+    int grid = 1;
+    if (mode != SMORE_SERIAL) {
+        int per_cu = 0;
+        const void* sym = walk_pairs_symbol(a);
+        if (!sym || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sym, 256, 0) != hipSuccess || per_cu < 1)
+            per_cu = 1;
+        grid = c->cus * per_cu;
+    }
+    if (mode == SMORE_HYBRID) {
+        const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
+        if ((rc = build_hot_maps(c, SMORE_LINE2, K, M))) return rc;
+        a.hotW = c->d_hotW;
+        a.hotC = c->d_hotC;
+    }
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    for (uint64_t b = walk_begin; b < walk_end; b += chunk) {
+        WalkArgs w;
+        w.order = c->d_order;
+        w.walks = c->d_walks;
+        w.lens = c->d_lens;
+        w.walk_begin = b;
+        w.nwalks = std::min<uint64_t>(chunk, walk_end - b);
+        w.total_walks = total;
+        w.steps = walk_steps;
+        w.window = window;
+        HIPCHK(c, launch_walk_gen(a.g, w, seed, c->stream));
+        const int64_t groups_per_block = 256 / lanes_of(c->dpad);
+        int g2 = grid;
+        if ((int64_t)g2 * groups_per_block > (int64_t)w.nwalks && mode != SMORE_SERIAL)
+            g2 = (int)std::max<int64_t>(1, ((int64_t)w.nwalks + groups_per_block - 1) / groups_per_block);
+        HIPCHK(c, launch_walk_pairs(a, w, g2, c->stream));
+    }
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return SMORE_OK;
 }
 
 }  // extern "C"

@@ -23,7 +23,11 @@
 
 namespace smore {
 
-enum { MODE_STORE = 0, MODE_ATOMIC = 1 };
+enum { MODE_STORE = 0, MODE_ATOMIC = 1, MODE_HYBRID = 3 };
+
+__device__ __forceinline__ bool hot_row(const uint32_t* bits, int32_t id) {
+    return (bits[id >> 5] >> (id & 31)) & 1u;
+}
 
 // The 4+2K (or 14 for BPR) words of a sample: lane l of the group computes
 // Philox block (l % NBLK) of unit s; word j is broadcast from lane j/4.
@@ -48,6 +52,185 @@ struct SampleWords {
     }
 };
 
+// NW consecutive words of one unit starting at an arbitrary slot0 (the
+// DeepWalk draw sequence): lane l computes block slot0/4 + l % NB, word j is
+// broadcast from the lane holding slot0 + j.
+template <int G, int NW>
+struct SlotWords {
+    static constexpr int NB = (NW + 3) / 4 + 1;
+    uint32_t w[NW];
+    __device__ __forceinline__ void draw(uint64_t seed, uint32_t stream, uint64_t unit, uint32_t slot0,
+                                         int lane) {
+        const uint32_t b0 = slot0 >> 2, off = slot0 & 3;
+        if constexpr (G >= NB) {
+            const uint4 b = philox_block(seed, stream, unit, b0 + (uint32_t)(lane % NB));
+#pragma unroll
+            for (int j = 0; j < NW; ++j) {
+                const uint32_t x = off + (uint32_t)j;
+                w[j] = __shfl(comp(b, (int)(x & 3)), (int)(x >> 2), G);
+            }
+        } else {
+            uint4 b[NB];
+#pragma unroll
+            for (int k = 0; k < NB; ++k) b[k] = philox_block(seed, stream, unit, b0 + (uint32_t)k);
+#pragma unroll
+            for (int j = 0; j < NW; ++j) {
+                const uint32_t x = off + (uint32_t)j;
+                uint32_t r = 0;
+#pragma unroll
+                for (int k = 0; k < NB; ++k)
+                    if ((x >> 2) == (uint32_t)k) r = comp(b[k], (int)(x & 3));
+                w[j] = r;
+            }
+        }
+    }
+};
+
+// ------------------------------------------------------------------ update core
+// One UpdatePair / UpdateFactorizedPair on rows W_v and the K+1 context refs
+// id[0] (positive) and id[1..K] (negatives), done by the G lanes of a group.
+//
+// Scatter bookkeeping without a copy of the original rows: after reference k
+// is processed its new value is propagated to the LATER references with the
+// same id (the in-place semantics), then rows[k] is turned into this step's
+// delta if the row is scattered by atomic add (every occurrence adds its own
+// delta), or kept as the value if it is stored (only the last occurrence of an
+// id stores, and it holds the final value).  A reference to W_v's own row in
+// a shared table is never scattered itself: W_v's scatter carries it.
+template <int G, int M, int KMAX, int MODE>
+__device__ __forceinline__ void sgd_update(const EdgeArgs& a, const float* s_sig, int lane,
+                                           const bool (&ev)[M], int32_t v, const int32_t (&id)[KMAX + 1],
+                                           float alpha, bool shared, bool mf) {
+    constexpr bool DELTA = MODE == MODE_ATOMIC || MODE == MODE_HYBRID;
+    const int dpad = a.dpad;
+    float* const Tw = a.W;
+    float* const Tc = shared ? a.W : a.C;
+    const int32_t vs = shared ? v : -2;   // id of W_v inside the context table
+
+    // ---- gather
+    float wv[M], rows[KMAX + 1][M];
+    {
+        const float* wp = Tw + (int64_t)v * dpad + lane;
+#pragma unroll
+        for (int m = 0; m < M; ++m) wv[m] = ev[m] ? wp[m * G] : 0.0f;
+    }
+#pragma unroll
+    for (int k = 0; k <= KMAX; ++k) {
+        const float* cp = Tc + (int64_t)(id[k] < 0 ? 0 : id[k]) * dpad + lane;
+#pragma unroll
+        for (int m = 0; m < M; ++m) rows[k][m] = (ev[m] && id[k] >= 0) ? cp[m * G] : 0.0f;
+    }
+    bool hot[KMAX + 1];
+    bool hotw = MODE == MODE_ATOMIC;
+#pragma unroll
+    for (int k = 0; k <= KMAX; ++k) hot[k] = MODE == MODE_ATOMIC;
+    if constexpr (MODE == MODE_HYBRID) {
+        hotw = hot_row(a.hotW, v);
+#pragma unroll
+        for (int k = 0; k <= KMAX; ++k) hot[k] = id[k] >= 0 && hot_row(a.hotC, id[k]);
+    }
+    // canonicalise repeated ids onto their first occurrence
+#pragma unroll
+    for (int k = 1; k <= KMAX; ++k)
+#pragma unroll
+        for (int k2 = 0; k2 < k; ++k2)
+            if (id[k2] == id[k]) {
+#pragma unroll
+                for (int m = 0; m < M; ++m) rows[k][m] = rows[k2][m];
+            }
+#pragma unroll
+    for (int k = 0; k <= KMAX; ++k)
+        if (id[k] == vs) {
+#pragma unroll
+            for (int m = 0; m < M; ++m) rows[k][m] = wv[m];
+        }
+    float wv0[DELTA ? M : 1];
+    if constexpr (DELTA) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) wv0[m] = wv[m];
+    }
+    float e[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) e[m] = 0.0f;
+
+    // ---- K+1 sequential Opt_SigmoidSGD / Opt_SGD steps
+#pragma unroll
+    for (int k = 0; k <= KMAX; ++k) {
+        if (id[k] >= 0) {
+            float p = 0.0f;
+#pragma unroll
+            for (int m = 0; m < M; ++m) p = __builtin_fmaf(wv[m], rows[k][m], p);
+            const float f = group_sum<G>(p);
+            float nk[M];
+            if (mf) {
+                const float gg = (k == 0 ? 1.0f : -1.0f) - f;
+#pragma unroll
+                for (int m = 0; m < M; ++m) {
+                    const float ce = rows[k][m], we = wv[m];
+                    const float t1 = gg * ce - a.reg * we;
+                    const float t2 = gg * we - a.reg * ce;
+                    e[m] = __builtin_fmaf(alpha, t1, e[m]);
+                    nk[m] = __builtin_fmaf(alpha, t2, ce);
+                }
+            } else {
+                const float gg = ((k == 0 ? 1.0f : 0.0f) - fast_sigmoid(f, s_sig)) * alpha;
+#pragma unroll
+                for (int m = 0; m < M; ++m) {
+                    const float ce = rows[k][m];
+                    e[m] = __builtin_fmaf(gg, ce, e[m]);
+                    nk[m] = __builtin_fmaf(gg, wv[m], ce);
+                }
+            }
+            // in-place semantics: later references to this row see it
+#pragma unroll
+            for (int k2 = k + 1; k2 <= KMAX; ++k2)
+                if (id[k2] == id[k]) {
+#pragma unroll
+                    for (int m = 0; m < M; ++m) rows[k2][m] = nk[m];
+                }
+            if (id[k] == vs) {
+#pragma unroll
+                for (int m = 0; m < M; ++m) wv[m] = nk[m];
+            }
+#pragma unroll
+            for (int m = 0; m < M; ++m) rows[k][m] = (DELTA && hot[k]) ? nk[m] - rows[k][m] : nk[m];
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) wv[m] = wv[m] + e[m];
+
+    // ---- scatter
+    {
+        float* wq = Tw + (int64_t)v * dpad + lane;
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            if (!ev[m]) continue;
+            if (DELTA && hotw) unsafeAtomicAdd(wq + m * G, shared ? wv[m] - wv0[m] : e[m]);
+            else wq[m * G] = wv[m];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k <= KMAX; ++k) {
+        if (id[k] < 0 || id[k] == vs) continue;
+        if (DELTA && hot[k]) {
+            float* cq = Tc + (int64_t)id[k] * dpad + lane;
+#pragma unroll
+            for (int m = 0; m < M; ++m)
+                if (ev[m]) unsafeAtomicAdd(cq + m * G, rows[k][m]);
+        } else {
+            bool last = true;
+#pragma unroll
+            for (int k2 = k + 1; k2 <= KMAX; ++k2) last = last && (id[k2] != id[k]);
+            if (last) {
+                float* cq = Tc + (int64_t)id[k] * dpad + lane;
+#pragma unroll
+                for (int m = 0; m < M; ++m)
+                    if (ev[m]) cq[m * G] = rows[k][m];
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------ edge kernel
 // LINE-2 (W,C), LINE-1 (W,W), MF (W,W, Opt_SGD): the model is a wave-uniform
 // runtime switch; the scatter MODE is compile-time.
@@ -67,12 +250,9 @@ __global__ void __launch_bounds__(256) edge_train_kernel(EdgeArgs a) {
     }
     const bool shared = a.model != 0;
     const bool mf = a.model == 2;
-    const int dpad = a.dpad;
     bool ev[M];                      // element lane + G*m exists
 #pragma unroll
-    for (int m = 0; m < M; ++m) ev[m] = lane + G * m < dpad;
-    float* const Tw = a.W;
-    float* const Tc = shared ? a.W : a.C;
+    for (int m = 0; m < M; ++m) ev[m] = lane + G * m < a.dpad;
     const uint64_t base = mf ? 0 : 1;   // LINE counts from 1, MF from 0
 
     for (uint64_t t = group; t < a.count; t += ngroups) {
@@ -91,117 +271,60 @@ __global__ void __launch_bounds__(256) edge_train_kernel(EdgeArgs a) {
 #pragma unroll
         for (int j = 0; j < KMAX; ++j)
             id[j + 1] = (j < a.K) ? negative_sample(a.g, wd.w[4 + 2 * j], wd.w[5 + 2 * j]) : -1;
-        const int32_t vs = shared ? v : -2;   // id of W_v inside the context table
-
-        // ---- gather
-        float wv[M], rows[KMAX + 1][M];
-        {
-            const float* wp = Tw + (int64_t)v * dpad + lane;
-#pragma unroll
-            for (int m = 0; m < M; ++m) wv[m] = ev[m] ? wp[m * G] : 0.0f;
-        }
-#pragma unroll
-        for (int k = 0; k <= KMAX; ++k) {
-            const float* cp = Tc + (int64_t)(id[k] < 0 ? 0 : id[k]) * dpad + lane;
-#pragma unroll
-            for (int m = 0; m < M; ++m) rows[k][m] = (ev[m] && id[k] >= 0) ? cp[m * G] : 0.0f;
-        }
-        // canonicalise repeated ids onto their first occurrence
-#pragma unroll
-        for (int k = 1; k <= KMAX; ++k)
-#pragma unroll
-            for (int k2 = 0; k2 < k; ++k2)
-                if (id[k2] == id[k]) {
-#pragma unroll
-                    for (int m = 0; m < M; ++m) rows[k][m] = rows[k2][m];
-                }
-#pragma unroll
-        for (int k = 0; k <= KMAX; ++k)
-            if (id[k] == vs) {
-#pragma unroll
-                for (int m = 0; m < M; ++m) rows[k][m] = wv[m];
-            }
-        float orig[MODE == MODE_ATOMIC ? KMAX + 1 : 1][M], wv0[M];
-        if constexpr (MODE == MODE_ATOMIC) {
-#pragma unroll
-            for (int m = 0; m < M; ++m) {
-                wv0[m] = wv[m];
-#pragma unroll
-                for (int k = 0; k <= KMAX; ++k) orig[k][m] = rows[k][m];
-            }
-        }
-
         const float alpha = alpha_at(s + base, a.alpha0, a.total);
-        float e[M];
-#pragma unroll
-        for (int m = 0; m < M; ++m) e[m] = 0.0f;
+        sgd_update<G, M, KMAX, MODE>(a, s_sig, lane, ev, v, id, alpha, shared, mf);
+    }
+}
 
-        // ---- K+1 sequential Opt_SigmoidSGD / Opt_SGD steps
-#pragma unroll
-        for (int k = 0; k <= KMAX; ++k) {
-            if (k <= a.K) {
-                float p = 0.0f;
-#pragma unroll
-                for (int m = 0; m < M; ++m) p = __builtin_fmaf(wv[m], rows[k][m], p);
-                const float f = group_sum<G>(p);
-                if (mf) {
-                    const float gg = (k == 0 ? 1.0f : -1.0f) - f;
-#pragma unroll
-                    for (int m = 0; m < M; ++m) {
-                        const float ce = rows[k][m], we = wv[m];
-                        const float t1 = gg * ce - a.reg * we;
-                        const float t2 = gg * we - a.reg * ce;
-                        e[m] = __builtin_fmaf(alpha, t1, e[m]);
-                        rows[k][m] = __builtin_fmaf(alpha, t2, ce);
-                    }
-                } else {
-                    const float gg = ((k == 0 ? 1.0f : 0.0f) - fast_sigmoid(f, s_sig)) * alpha;
-#pragma unroll
-                    for (int m = 0; m < M; ++m) {
-                        const float ce = rows[k][m];
-                        e[m] = __builtin_fmaf(gg, ce, e[m]);
-                        rows[k][m] = __builtin_fmaf(gg, wv[m], ce);
-                    }
-                }
-                // in-place semantics: every other reference to this row sees it
-#pragma unroll
-                for (int k2 = 0; k2 <= KMAX; ++k2)
-                    if (k2 != k && id[k2] == id[k]) {
-#pragma unroll
-                        for (int m = 0; m < M; ++m) rows[k2][m] = rows[k][m];
-                    }
-                if (id[k] == vs) {
-#pragma unroll
-                    for (int m = 0; m < M; ++m) wv[m] = rows[k][m];
-                }
-            }
-        }
-#pragma unroll
-        for (int m = 0; m < M; ++m) wv[m] = wv[m] + e[m];
+// ------------------------------------------------------------------ DeepWalk pairs
+// DeepWalk::Train's per-walk body after RandomWalk (src/model/DeepWalk.cpp:
+// 133-139): SkipGrams with the random window shrink (src/proNet.cpp:769-809)
+// and UpdatePairs -> UpdatePair per pair (src/proNet.cpp:2741-2753), one
+// group per walk, pairs in the reference's order.  Draw slots of walk w
+// (stream 1): after the 2(L-1) walk draws, L window draws, then 2K per pair.
+template <int G, int M, int KMAX, int MODE>
+__global__ void __launch_bounds__(256) walk_pairs_kernel(EdgeArgs a, WalkArgs w) {
+    __shared__ float s_sig[1001];
+    for (int i = threadIdx.x; i < 1001; i += blockDim.x) s_sig[i] = a.sig[i];
+    __syncthreads();
 
-        // ---- scatter
-        {
-            float* wq = Tw + (int64_t)v * dpad + lane;
+    const int lane = threadIdx.x & (G - 1);
+    uint64_t group = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+    uint64_t ngroups = ((uint64_t)gridDim.x * blockDim.x) / G;
+    if (a.mode == 2) {
+        if (group != 0) return;
+        ngroups = 1;
+    }
+    bool ev[M];
 #pragma unroll
-            for (int m = 0; m < M; ++m) {
-                if (!ev[m]) continue;
-                if constexpr (MODE == MODE_ATOMIC) unsafeAtomicAdd(wq + m * G, shared ? wv[m] - wv0[m] : e[m]);
-                else wq[m * G] = wv[m];
-            }
-        }
+    for (int m = 0; m < M; ++m) ev[m] = lane + G * m < a.dpad;
+    const int stride = w.steps + 1;
+
+    for (uint64_t t = group; t < w.nwalks; t += ngroups) {
+        const uint64_t unit = w.walk_begin + t;
+        const int32_t* walk = w.walks + t * stride;
+        const int L = w.lens[t];
+        const float alpha = alpha_walk(unit, a.alpha0, w.total_walks);
+        const uint32_t win_base = 2u * (uint32_t)(L - 1);
+        uint32_t slot = win_base + (uint32_t)L;          // first negative slot
+        for (int i = 0; i < L; ++i) {
+            const uint32_t sw = win_base + (uint32_t)i;
+            const uint32_t kw = comp(philox_block(a.seed, 1, unit, sw >> 2), (int)(sw & 3));
+            const int reduce = (int)draw_index(kw, (uint32_t)w.window) + 1;
+            const int left = i - reduce < 0 ? 0 : i - reduce;
+            const int right = i + reduce >= L ? L - 1 : i + reduce;
+            const int32_t vi = walk[i];
+            for (int j = left; j <= right; ++j) {
+                if (j == i) continue;
+                int32_t id[KMAX + 1];
+                id[0] = walk[j];
+                SlotWords<G, 2 * KMAX> nw;
+                nw.draw(a.seed, 1, unit, slot, lane);
 #pragma unroll
-        for (int k = 0; k <= KMAX; ++k) {
-            bool last = id[k] >= 0 && id[k] != vs;
-#pragma unroll
-            for (int k2 = k + 1; k2 <= KMAX; ++k2) last = last && (id[k2] != id[k]);
-            if (last) {
-                float* cq = Tc + (int64_t)id[k] * dpad + lane;
-#pragma unroll
-                for (int m = 0; m < M; ++m) {
-                    if (!ev[m]) continue;
-                    if constexpr (MODE == MODE_ATOMIC) unsafeAtomicAdd(cq + m * G, rows[k][m] - orig[k][m]);
-                    else cq[m * G] = rows[k][m];
-                }
+                for (int n = 0; n < KMAX; ++n)
+                    id[n + 1] = n < a.K ? negative_sample(a.g, nw.w[2 * n], nw.w[2 * n + 1]) : -1;
+                slot += 2 * a.K;
+                sgd_update<G, M, KMAX, MODE>(a, s_sig, lane, ev, vi, id, alpha, false, false);
             }
         }
     }
@@ -259,8 +382,9 @@ __global__ void __launch_bounds__(256) bpr_train_kernel(EdgeArgs a) {
 #pragma unroll
                     for (int m = 0; m < M; ++m) row[k][m] = row[k2][m];
                 }
-        float orig[MODE == MODE_ATOMIC ? NS : 1][M];
-        if constexpr (MODE == MODE_ATOMIC) {
+        constexpr bool DELTA = MODE == MODE_ATOMIC || MODE == MODE_HYBRID;
+        float orig[DELTA ? NS : 1][M];
+        if constexpr (DELTA) {
 #pragma unroll
             for (int k = 0; k < NS; ++k)
 #pragma unroll
@@ -319,11 +443,17 @@ __global__ void __launch_bounds__(256) bpr_train_kernel(EdgeArgs a) {
             for (int k2 = k + 1; k2 < NS; ++k2) last = last && (id[k2] != id[k]);
             if (last) {
                 float* q = T + (int64_t)id[k] * dpad + lane;
+                bool atom = MODE == MODE_ATOMIC;
+                if constexpr (MODE == MODE_HYBRID) atom = hot_row(a.hotC, id[k]);
 #pragma unroll
                 for (int m = 0; m < M; ++m) {
                     if (!ev[m]) continue;
-                    if constexpr (MODE == MODE_ATOMIC) unsafeAtomicAdd(q + m * G, row[k][m] - orig[k][m]);
-                    else q[m * G] = row[k][m];
+                    if constexpr (DELTA) {
+                        if (atom) unsafeAtomicAdd(q + m * G, row[k][m] - orig[k][m]);
+                        else q[m * G] = row[k][m];
+                    } else {
+                        q[m * G] = row[k][m];
+                    }
                 }
             }
         }

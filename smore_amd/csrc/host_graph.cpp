@@ -139,6 +139,30 @@ bool build_graph(int64_t V, int64_t E, const int32_t* src, const int32_t* dst, c
     return true;
 }
 
+static void alias_marginal(const std::vector<double>& prob, const std::vector<int64_t>& alias, int64_t off,
+                           int64_t n, const int32_t* self_ids, double scale, std::vector<double>& p) {
+    for (int64_t i = 0; i < n; ++i) {
+        const double pr = prob[off + i];
+        const int64_t self = self_ids ? self_ids[off + i] : i;
+        p[self] += scale * pr;
+        if (alias[off + i] >= 0 && pr < 1.0) p[alias[off + i]] += scale * (1.0 - pr);
+    }
+}
+
+void draw_probabilities(const HostGraph& g, std::vector<double>& p_src, std::vector<double>& p_neg,
+                        std::vector<double>& p_ctx) {
+    p_src.assign((size_t)g.V, 0.0);
+    p_neg.assign((size_t)g.V, 0.0);
+    p_ctx.assign((size_t)g.V, 0.0);
+    alias_marginal(g.vprob, g.valias, 0, g.V, nullptr, 1.0 / g.V, p_src);
+    alias_marginal(g.nprob, g.nalias, 0, g.V, nullptr, 1.0 / g.V, p_neg);
+    for (int64_t v = 0; v < g.V; ++v) {
+        const int64_t off = g.offsets[v], br = g.offsets[v + 1] - off;
+        if (br == 0 || p_src[v] == 0) continue;
+        alias_marginal(g.cprob, g.calias, off, br, g.targets.data(), p_src[v] / br, p_ctx);
+    }
+}
+
 // ---------------------------------------------------------------- loader
 static bool is_dir(const std::string& p) {
     struct stat st;

@@ -61,6 +61,12 @@ class GlibcRand {
     int pos_ = 0;
 };
 
+// Exact per-draw probabilities encoded by the alias tables: source
+// (vertex_AT), negative (negative_AT) and the marginal context-target
+// probability sum_v p_src(v) * P(target | v).
+void draw_probabilities(const HostGraph& g, std::vector<double>& p_src, std::vector<double>& p_neg,
+                        std::vector<double>& p_ctx);
+
 // DeepWalk walk-start order (src/model/DeepWalk.cpp:122-131).
 void deepwalk_order(int64_t V, int walk_times, uint64_t skip, int64_t* order);
 

@@ -8,6 +8,7 @@ hipError_t launch_bpr(const EdgeArgs& a, int grid, hipStream_t st) {
 #define X(g, m)                                                                                        \
     if (G == g && M == m) {                                                                            \
         if (a.mode == 1) hipLaunchKernelGGL((bpr_train_kernel<g, m, MODE_ATOMIC>), dim3(grid), dim3(256), 0, st, a); \
+        else if (a.mode == 3) hipLaunchKernelGGL((bpr_train_kernel<g, m, MODE_HYBRID>), dim3(grid), dim3(256), 0, st, a); \
         else hipLaunchKernelGGL((bpr_train_kernel<g, m, MODE_STORE>), dim3(grid), dim3(256), 0, st, a);  \
         return hipGetLastError();                                                                      \
     }
@@ -21,6 +22,7 @@ const void* bpr_symbol(const EdgeArgs& a) {
 #define X(g, m)                                                                            \
     if (G == g && M == m)                                                                  \
         return a.mode == 1 ? (const void*)bpr_train_kernel<g, m, MODE_ATOMIC>              \
+             : a.mode == 3 ? (const void*)bpr_train_kernel<g, m, MODE_HYBRID>              \
                            : (const void*)bpr_train_kernel<g, m, MODE_STORE>;
     SMORE_FOR_EACH_GM(X)
 #undef X

@@ -12,15 +12,31 @@ struct EdgeArgs {
     float* W;                      // [V][dpad]
     float* C;                      // [V][dpad] (== W for shared-table models)
     unsigned long long* skipped;   // samples whose source had no out-edge
+    const uint32_t* hotW;          // hybrid mode: 1 bit per row, atomic scatter if set
+    const uint32_t* hotC;          //   (hotC == hotW for shared-table models)
     uint64_t begin, count, total, seed;
     double alpha0;
     float reg;
     int dpad, K, model, mode;
 };
 
+// DeepWalk: a chunk of walks [walk_begin, walk_begin + nwalks)
+struct WalkArgs {
+    const int64_t* order;          // walk start vertices, all walk_times * V
+    int32_t* walks;                // nwalks x (steps + 1)
+    int32_t* lens;                 // nwalks
+    uint64_t walk_begin, nwalks, total_walks;
+    int steps, window;
+};
+
 int lanes_of(int dpad);
+hipError_t launch_walk_gen(const DevGraph& g, const WalkArgs& w, uint64_t seed, hipStream_t st);
+hipError_t launch_walk_pairs(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st);
+const void* walk_pairs_symbol(const EdgeArgs& a);
 hipError_t launch_edge_store(const EdgeArgs& a, int grid, hipStream_t st);
 hipError_t launch_edge_atomic(const EdgeArgs& a, int grid, hipStream_t st);
+hipError_t launch_edge_hybrid(const EdgeArgs& a, int grid, hipStream_t st);
+const void* edge_symbol_hybrid(const EdgeArgs& a);
 hipError_t launch_bpr(const EdgeArgs& a, int grid, hipStream_t st);
 const void* edge_symbol_store(const EdgeArgs& a);
 const void* edge_symbol_atomic(const EdgeArgs& a);

@@ -61,12 +61,16 @@ int lanes_of(int dpad) {
 
 hipError_t launch_edge_train(const EdgeArgs& a, int grid, hipStream_t st) {
     if (a.model == 3) return launch_bpr(a, grid, st);
-    return a.mode == 1 ? launch_edge_atomic(a, grid, st) : launch_edge_store(a, grid, st);
+    if (a.mode == 1) return launch_edge_atomic(a, grid, st);
+    if (a.mode == 3) return launch_edge_hybrid(a, grid, st);
+    return launch_edge_store(a, grid, st);
 }
 
 const void* edge_kernel_symbol(const EdgeArgs& a) {
     if (a.model == 3) return bpr_symbol(a);
-    return a.mode == 1 ? edge_symbol_atomic(a) : edge_symbol_store(a);
+    if (a.mode == 1) return edge_symbol_atomic(a);
+    if (a.mode == 3) return edge_symbol_hybrid(a);
+    return edge_symbol_store(a);
 }
 
 hipError_t launch_sample(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K,

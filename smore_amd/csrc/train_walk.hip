@@ -1,0 +1,82 @@
+// train_walk.hip -- DeepWalk on the GPU: walk generation (RandomWalk,
+// src/proNet.cpp:704-724) and the skip-gram pair updates (walk_pairs_kernel).
+#include "edge_kernels.h"
+
+namespace smore {
+
+// One thread per walk; dependent CSR / context-alias loads per step.
+// Draw slots 2s, 2s+1 of walk unit (stream 1) for step s (p, then index).
+__global__ void walk_gen_kernel(DevGraph g, WalkArgs w, uint64_t seed) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= w.nwalks) return;
+    const uint64_t unit = w.walk_begin + t;
+    const int32_t start = (int32_t)w.order[unit];
+    int32_t* out = w.walks + t * (uint64_t)(w.steps + 1);
+    int L = 0;
+    int32_t next = start;
+    out[L++] = next;
+    uint4 b = make_uint4(0, 0, 0, 0);
+    for (int s = 0; s < w.steps; ++s) {
+        if (g.offsets[next + 1] - g.offsets[next] == 0) {
+            if (next == start) break;
+            next = start;
+        }
+        const uint32_t s0 = 2u * (uint32_t)s;
+        if ((s0 & 3) == 0) b = philox_block(seed, 1, unit, s0 >> 2);
+        const uint32_t kp = comp(b, (int)(s0 & 3)), ki = comp(b, (int)((s0 + 1) & 3));
+        next = target_sample(g, next, kp, ki);
+        out[L++] = next;
+    }
+    w.lens[t] = L;
+}
+
+hipError_t launch_walk_gen(const DevGraph& g, const WalkArgs& w, uint64_t seed, hipStream_t st) {
+    const int block = 256;
+    hipLaunchKernelGGL(walk_gen_kernel, dim3((unsigned)((w.nwalks + block - 1) / block)), dim3(block), 0, st, g,
+                       w, seed);
+    return hipGetLastError();
+}
+
+template <int G, int M, int KMAX>
+static hipError_t go(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st) {
+    if (a.mode == 1)
+        hipLaunchKernelGGL((walk_pairs_kernel<G, M, KMAX, MODE_ATOMIC>), dim3(grid), dim3(256), 0, st, a, w);
+    else if (a.mode == 3)
+        hipLaunchKernelGGL((walk_pairs_kernel<G, M, KMAX, MODE_HYBRID>), dim3(grid), dim3(256), 0, st, a, w);
+    else
+        hipLaunchKernelGGL((walk_pairs_kernel<G, M, KMAX, MODE_STORE>), dim3(grid), dim3(256), 0, st, a, w);
+    return hipGetLastError();
+}
+
+template <int G, int M, int KMAX>
+static const void* sym(const EdgeArgs& a) {
+    if (a.mode == 1) return (const void*)walk_pairs_kernel<G, M, KMAX, MODE_ATOMIC>;
+    if (a.mode == 3) return (const void*)walk_pairs_kernel<G, M, KMAX, MODE_HYBRID>;
+    return (const void*)walk_pairs_kernel<G, M, KMAX, MODE_STORE>;
+}
+
+hipError_t launch_walk_pairs(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st) {
+    const int G = lanes_of(a.dpad), M = (a.dpad + G - 1) / G;
+#define X(g, m)                                          \
+    if (G == g && M == m) {                              \
+        if (a.K <= 5) return go<g, m, 5>(a, w, grid, st); \
+        return go<g, m, 10>(a, w, grid, st);              \
+    }
+    SMORE_FOR_EACH_GM(X)
+#undef X
+    return hipErrorInvalidValue;
+}
+
+const void* walk_pairs_symbol(const EdgeArgs& a) {
+    const int G = lanes_of(a.dpad), M = (a.dpad + G - 1) / G;
+#define X(g, m)                                   \
+    if (G == g && M == m) {                       \
+        if (a.K <= 5) return sym<g, m, 5>(a);     \
+        return sym<g, m, 10>(a);                  \
+    }
+    SMORE_FOR_EACH_GM(X)
+#undef X
+    return nullptr;
+}
+
+}  // namespace smore

@@ -176,6 +176,14 @@ class ProNet:
                                            int(walk_steps), int(window), int(K), float(alpha0), int(seed),
                                            ptr(order), _lib.MODE[mode]), "train_deepwalk")
 
+    def set_hot_threshold(self, tau):
+        self._chk(lib.smore_set_hot_threshold(self.ctx, float(tau)), "set_hot_threshold")
+
+    def hot_rows(self):
+        w, c = C.c_int64(), C.c_int64()
+        self._chk(lib.smore_hot_rows(self.ctx, C.byref(w), C.byref(c)), "hot_rows")
+        return w.value, c.value
+
     def synchronize(self):
         self._chk(lib.smore_synchronize(self.ctx), "synchronize")
 

@@ -201,6 +201,49 @@ def test_end_to_end_vs_reference(smore, name, fname, und, nm, model, K, reg, n_o
         assert d.max() < 2e-3 and np.median(d) < 2e-4, (key, d.max(), np.median(d))
 
 
+# ---------------------------------------------------------------- DeepWalk
+@pytest.mark.parametrize("dim,K,window,steps", [(8, 2, 3, 10), (64, 5, 5, 40), (20, 1, 2, 7)])
+def test_deepwalk_serial_bit_exact_vs_oracle(smore, dim, K, window, steps):
+    g, pn = make_pair(smore, "pl100w.txt", 1)
+    V = g.V
+    W0, C0 = rand_tables(V, dim, 2, dim + K)
+    pn.alloc_tables(dim, 2)
+    pn.set_table(0, W0)
+    pn.set_table(1, C0)
+    order = orc.deepwalk_order(V, 2, 77)
+    pn.train_deepwalk(0, 2 * V, 2, steps, window, K, 0.025, SEED, order, "serial")
+    W, C = padded(W0, dim), padded(C0, dim)
+    orc.train_deepwalk_f32(g, W, C, dim, 2, steps, window, K, 0.025, SEED, order)
+    np.testing.assert_array_equal(pn.get_table(0), W[:, :dim])
+    np.testing.assert_array_equal(pn.get_table(1), C[:, :dim])
+
+
+def test_deepwalk_end_to_end_vs_reference(smore):
+    z = gold("e2e_deepwalk_pl100w")
+    _, pn = make_pair(smore, "pl100w.txt", 1)
+    V, dim = z["W0"].shape
+    pn.alloc_tables(dim, 2)
+    pn.init_table_glibc(0, 0)
+    pn.init_table_glibc(1, V * dim)
+    np.testing.assert_array_equal(pn.get_table(1), z["C0"].astype(np.float32))
+    order = smore.deepwalk_order(V, 2, 2 * V * dim)
+    pn.train_deepwalk(0, 2 * V, 2, 10, 3, 2, 0.025, SEED, order, "serial")
+    for t, key in ((0, "W"), (1, "C")):
+        d = np.abs(pn.get_table(t) - z[key])
+        assert d.max() < 2e-3 and np.median(d) < 2e-4, (key, d.max(), np.median(d))
+
+
+@pytest.mark.parametrize("mode", ["atomic", "hogwild"])
+def test_deepwalk_parallel_runs(smore, mode):
+    g, pn = make_pair(smore, "pl1k.txt", 1)
+    pn.alloc_tables(32, 2)
+    pn.init_table_glibc(0, 0)
+    pn.init_table_glibc(1, g.V * 32)
+    order = smore.deepwalk_order(g.V, 3, 2 * g.V * 32)
+    pn.train_deepwalk(0, 3 * g.V, 3, 20, 5, 5, 0.025, SEED, order, mode)
+    assert np.isfinite(pn.get_table(0)).all() and np.isfinite(pn.get_table(1)).all()
+
+
 # ---------------------------------------------------------------- Hogwild quality
 def _auc(W, C, g, rng, n=20000):
     src = np.repeat(np.arange(g.V), np.diff(g.offsets))

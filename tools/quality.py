@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
 """Embedding-quality check of the GPU scatter modes against the CPU Hogwild
-oracle on a benchmark graph (the reference has no quality metric; this uses
-the LINE-2 edge score W_v . C_c).
-
-AUC = P(score(positive edge) > score(random pair)) over 20k x 2k pairs.
+oracle on a benchmark graph.  The reference has no quality metric; this uses
+its own training objective on held-out draws (seed != training seed):
+  loss  = mean over samples of -log s(W_v.C_c) - sum_k log s(-W_v.C_nk)
+  auc   = P(W_v.C_c > W_v.C_n) for the sample's positive c vs its negatives n
+with (v, c, n1..n5) drawn by the reference samplers (source alias, per-vertex
+context alias, negative alias).
 
     python tools/quality.py --config c2 --samples 40000000 --modes hogwild atomic
 """
@@ -19,14 +21,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def auc(W, C, offsets, targets, rng, n=20000, m=2000):
-    V = len(offsets) - 1
-    E = len(targets)
-    src = np.repeat(np.arange(V, dtype=np.int64), np.diff(offsets))
-    pick = rng.integers(0, E, n)
-    pos = np.einsum("ij,ij->i", W[src[pick]], C[targets[pick]])
-    neg = np.einsum("ij,ij->i", W[rng.integers(0, V, m)], C[rng.integers(0, V, m)])
-    return float((pos[:, None] > neg[None, :]).mean())
+def objective(W, C, draws):
+    v, c, n = draws[:, 0], draws[:, 1], draws[:, 2:]
+    ok = c >= 0
+    v, c, n = v[ok], c[ok], n[ok]
+    pos = np.einsum("ij,ij->i", W[v], C[c])
+    neg = np.einsum("ij,ikj->ik", W[v], C[n])
+    ls = lambda x: -np.logaddexp(0.0, -x)  # log sigmoid
+    loss = float(np.mean(-ls(pos) - ls(-neg).sum(1)))
+    auc = float(np.mean(pos[:, None] > neg))
+    return {"loss": round(loss, 5), "auc": round(auc, 5)}
 
 
 def main():
@@ -44,9 +48,12 @@ def main():
     res = {"config": args.config, "samples": args.samples, "dim": args.dim}
     pn = smore_amd.ProNet(0)
     pn.set_graph_edges(V, src, dst, w)
-    off, tgt = pn.csr()
+    draws = pn.sample_edges("line2", 1 << 40, 200000, 5, 99991)   # held-out draws
     total = args.samples + 1
-    for mode in args.modes:
+    for spec in args.modes:
+        mode, _, tau = spec.partition(":")
+        if tau:
+            pn.set_hot_threshold(float(tau))
         pn.alloc_tables(args.dim, 2)
         pn.init_table_uniform(0, 3)
         pn.zero_table(1)
@@ -54,9 +61,11 @@ def main():
         pn.train_edges("line2", 0, args.samples, total, 5, 0.025, 0.0, 11, mode)
         el = time.perf_counter() - t
         W, C = pn.get_table(0), pn.get_table(1)
-        res[mode] = {"auc": auc(W, C, off, tgt, np.random.default_rng(0)), "seconds": el,
-                     "Mups": args.samples / el / 1e6, "finite": bool(np.isfinite(W).all())}
-        print(mode, res[mode], flush=True)
+        res[spec] = dict(objective(W, C, draws), seconds=round(el, 4), Mups=round(args.samples / el / 1e6, 2),
+                         finite=bool(np.isfinite(W).all()))
+        if mode == "hybrid":
+            res[spec]["hot_rows_w_c"] = pn.hot_rows()
+        print(spec, res[spec], flush=True)
     if args.cpu:
         from oracle import oracle as orc
         g = orc.Graph(V, src, dst, w)
@@ -68,8 +77,8 @@ def main():
         t = time.perf_counter()
         orc.train_edge_f32(g, "line2", W, C, args.dim, 5, 0.025, 0.0, total, 0, args.samples, 11, threads)
         el = time.perf_counter() - t
-        res["cpu"] = {"auc": auc(W, C, off, tgt, np.random.default_rng(0)), "seconds": el, "threads": threads,
-                      "Mups": args.samples / el / 1e6}
+        res["cpu"] = dict(objective(W, C, draws), seconds=round(el, 2), threads=threads,
+                          Mups=round(args.samples / el / 1e6, 3))
         print("cpu", res["cpu"], flush=True)
     if args.out:
         json.dump(res, open(args.out, "w"), indent=1)
