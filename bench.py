@@ -42,7 +42,10 @@ def parse():
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--negative", type=int, default=5)
     ap.add_argument("--samples", type=int, default=1 << 27, help="edge samples per step per GPU")
-    ap.add_argument("--mode", default="hogwild", choices=["hogwild", "atomic"])
+    ap.add_argument("--mode", default="atomic", choices=["hogwild", "atomic", "hybrid"],
+                    help="scatter: atomic (default; lock-free, no lost updates), hybrid, hogwild (plain stores)")
+    ap.add_argument("--hot-tau", type=float, default=0.1, help="hybrid: hot-row threshold")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
     ap.add_argument("--sync-every", type=int, default=1)
     ap.add_argument("--sync", default="sum", choices=["sum", "mean"])
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
@@ -79,12 +82,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
+    local = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
 
     import smore_amd
     from smore_amd import graphgen
@@ -94,6 +99,7 @@ def main():
     pn = smore_amd.ProNet(local)
     pn.set_graph_edges(V, src, dst, w)
     E = pn.MAX_line
+    pn.set_hot_threshold(args.hot_tau)
     pn.alloc_tables(args.dim, 2)
     pn.init_table_uniform(0, args.seed)     # W ~ (u-0.5)/d, as the reference Init law
     pn.zero_table(1)                        # C = 0 (src/model/LINE.cpp:92)

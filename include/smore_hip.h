@@ -168,7 +168,12 @@ int smore_deepwalk_order(int64_t V, int walk_times, uint64_t skip, int64_t* orde
 int smore_sample_edges(smore_ctx* ctx, int model, uint64_t begin, uint64_t count, int K,
                        uint64_t seed, int32_t* out);
 
-/* ---- output ---------------------------------------------------------------------------- */
+/* ---- warm start / output --------------------------------------------------------------- */
+/* replaces: proNet::LoadPreTrain (src/proNet.cpp:238-286), DeepWalk -load_v /
+ * -load_c (cli/deepwalk.cpp:61-62): rows of a SaveWeights-format file whose
+ * names are vertices of the loaded graph overwrite those rows of the table;
+ * a file whose dimension differs is skipped, as in the reference. */
+int smore_load_pretrain(smore_ctx* ctx, int which, const char* path);
 /* replaces: SaveWeights (src/model/LINE.cpp:13-47; Go line.go:209-233):
  * "V dim" header then "name v1 ... vdim" per vertex.  fmt 0 = C++ ostream
  * default (%g, 6 significant digits), fmt 1 = Go "%.6f". */

@@ -59,6 +59,7 @@ def _load():
         "smore_deepwalk_order": (i32, [i64, i32, u64, P]),
         "smore_sample_edges": (i32, [P, i32, u64, u64, i32, u64, P]),
         "smore_save_weights": (i32, [P, i32, C.c_char_p, i32]),
+        "smore_load_pretrain": (i32, [P, i32, C.c_char_p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

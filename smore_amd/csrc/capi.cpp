@@ -54,6 +54,7 @@ struct smore_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     int cus = 0;
+    int64_t last_loaded = 0;
 };
 
 namespace {
@@ -527,6 +528,22 @@ int smore_sample_edges(smore_ctx* c, int model, uint64_t begin, uint64_t count, 
     if (e == hipSuccess) e = hipMemcpy(out, d, count * width * sizeof(int32_t), hipMemcpyDeviceToHost);
     (void)hipFree(d);
     if (e != hipSuccess) return fail(c, SMORE_EHIP, std::string("sample: ") + hipGetErrorString(e));
+    return SMORE_OK;
+}
+
+int smore_load_pretrain(smore_ctx* c, int which, const char* path) {
+    int rc;
+    if ((rc = check_table(c, which))) return rc;
+    if (!path) return SMORE_EINVAL;
+    if (c->g.names.empty()) return fail(c, SMORE_ESTATE, "warm start needs vertex names (load an edge list)");
+    std::vector<float> h((size_t)c->g.V * c->dpad);
+    if ((rc = set_device(c))) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(h.data(), c->d_table[which], h.size() * sizeof(float), hipMemcpyDeviceToHost));
+    int64_t loaded = 0;
+    if (!load_pretrain(path, c->g, h.data(), c->dim, c->dpad, &loaded, c->err)) return SMORE_EIO;
+    c->last_loaded = loaded;
+    HIPCHK(c, hipMemcpy(c->d_table[which], h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
     return SMORE_OK;
 }
 

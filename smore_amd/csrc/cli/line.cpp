@@ -1,15 +1,9 @@
 // line -- flag-compatible replacement of cli/line.cpp (LINE 1st/2nd order) on
-// one MI355X.  Extra flags: -device <int>, -mode hogwild|atomic|serial,
+// one MI355X.  Extra flags: -device <int>, -mode hogwild|atomic|hybrid|serial,
 // -seed <int>, -format cpp|go (SaveWeights number format).
 #include <string>
 
 #include "cli_common.h"
-
-static int mode_of(const char* s) {
-    if (!strcmp(s, "atomic")) return SMORE_ATOMIC;
-    if (!strcmp(s, "serial")) return SMORE_SERIAL;
-    return SMORE_HOGWILD;
-}
 
 int main(int argc, char** argv) {
     int i;
@@ -25,14 +19,14 @@ int main(int argc, char** argv) {
         printf("\t-sample_times <int>\n\t\tNumber of training samples *Million; default is 10\n");
         printf("\t-threads <int>\n\t\tAccepted for compatibility (the GPU runs one Hogwild stream)\n");
         printf("\t-alpha <float>\n\t\tInit learning rate; default is 0.025\n");
-        printf("\t-device <int> -mode hogwild|atomic|serial -seed <int> -format cpp|go\n");
+        printf("\t-device <int> -mode hogwild|atomic|hybrid|serial -seed <int> -format cpp|go\n");
         printf("Usage:\n./line -train net.txt -save rep.txt -undirected 1 -order 2 -dimensions 64 "
                "-sample_times 10 -negative_samples 5 -alpha 0.025 -threads 1\n");
         return 0;
     }
     char network_file[4096] = "", rep_file[4096] = "";
     int dimensions = 64, undirected = 1, negative_samples = 5, sample_times = 10, threads = 1, order = 2;
-    int device = 0, mode = SMORE_HOGWILD, fmt = 0;
+    int device = 0, mode = SMORE_ATOMIC, fmt = 0;
     unsigned long long seed = 1;
     double init_alpha = 0.025;
     if ((i = ArgPos("-train", argc, argv)) > 0) snprintf(network_file, sizeof network_file, "%s", argv[i + 1]);
@@ -50,15 +44,9 @@ int main(int argc, char** argv) {
     if ((i = ArgPos("-format", argc, argv)) > 0) fmt = !strcmp(argv[i + 1], "go");
     order = order == 1 ? 1 : 2;
 
-    smore_ctx* ctx = nullptr;
-    if (smore_create(device, &ctx) != SMORE_OK) {
-        fprintf(stderr, "cannot create a context on device %d\n", device);
-        return 2;
-    }
+    smore_ctx* ctx = open_context(device);
     SMORE_CLI_CHECK(ctx, smore_load_edgelist(ctx, network_file, undirected, SMORE_VM_OUT_DEGREES, SMORE_NM_DEGREES));
-    int64_t V = 0, E = 0;
-    smore_graph_info(ctx, &V, &E);
-    printf("Connections:\n\t# of connection:\t%lld\n\t# of vertex:\t\t%lld\n", (long long)E, (long long)V);
+    print_graph(ctx);
     printf("Model Setting:\n\tdimension:\t\t%d\n", dimensions);
     SMORE_CLI_CHECK(ctx, smore_alloc_tables(ctx, dimensions, order == 1 ? 1 : 2));
     SMORE_CLI_CHECK(ctx, smore_init_table_glibc(ctx, SMORE_W, 0));
@@ -67,20 +55,10 @@ int main(int argc, char** argv) {
            negative_samples, init_alpha, threads);
     printf("Start Training:\n");
     const unsigned long long total = (unsigned long long)sample_times * 1000000ull;
-    const unsigned long long n = total ? total - 1 : 0;  // counts 1..total-1 (src/model/LINE.cpp:166-170)
-    const unsigned long long chunk = 1ull << 26;
-    for (unsigned long long done = 0; done < n;) {
-        unsigned long long c = n - done < chunk ? n - done : chunk;
-        SMORE_CLI_CHECK(ctx, smore_train_edges(ctx, order == 1 ? SMORE_LINE1 : SMORE_LINE2, done, c, total,
-                                               negative_samples, init_alpha, 0.0, seed, mode));
-        done += c;
-        printf("\tProgress: %.3f %%%c", (double)done / total * 100, 13);
-        fflush(stdout);
-    }
-    printf("\tProgress: 100.00 %%\n");
-    printf("Save Model:\n");
-    SMORE_CLI_CHECK(ctx, smore_save_weights(ctx, SMORE_W, rep_file, fmt));
-    printf("\tSave to <%s>\n", rep_file);
+    // one worker runs counts 1 .. total-1 (src/model/LINE.cpp:166-170)
+    train_chunks(ctx, order == 1 ? SMORE_LINE1 : SMORE_LINE2, total, total ? total - 1 : 0, negative_samples,
+                 init_alpha, 0.0, seed, mode);
+    save(ctx, rep_file, fmt);
     smore_destroy(ctx);
     return 0;
 }

@@ -289,6 +289,59 @@ void deepwalk_order(int64_t V, int walk_times, uint64_t skip, int64_t* order) {
     }
 }
 
+// ---------------------------------------------------------------- warm start
+bool load_pretrain(const std::string& path, const HostGraph& g, float* table, int dim, int stride,
+                   int64_t* loaded, std::string& err) {
+    *loaded = 0;
+    FILE* f = fopen(path.c_str(), "rb");
+    if (!f) { err = "cannot open " + path; return false; }
+    std::string line;
+    auto getline = [&](std::string& out) -> bool {
+        out.clear();
+        int ch;
+        while ((ch = fgetc(f)) != EOF) {
+            if (ch == '\n') return true;
+            out.push_back((char)ch);
+        }
+        return !out.empty();
+    };
+    if (!getline(line)) { fclose(f); return true; }
+    long long n = 0;
+    int d = 0;
+    if (sscanf(line.c_str(), "%lld %d", &n, &d) != 2 || d != dim) {
+        fclose(f);
+        *loaded = -1;   // "Dimension not matched, Skip Loading Pre-train model." (:259-262)
+        return true;
+    }
+    std::unordered_map<std::string, int32_t> ids;
+    ids.reserve(g.names.size());
+    for (size_t i = 0; i < g.names.size(); ++i) ids.emplace(g.names[i], (int32_t)i);
+    std::vector<float> row((size_t)dim);
+    while (getline(line)) {
+        const char* p = line.c_str();
+        while (*p == ' ' || *p == '\t') ++p;
+        const char* q = p;
+        while (*q && *q != ' ' && *q != '\t' && *q != '\r') ++q;
+        std::string name(p, q);
+        auto it = ids.find(name);
+        if (it == ids.end()) continue;
+        int got = 0;
+        char* endp = nullptr;
+        const char* cur = q;
+        for (; got < dim; ++got) {
+            double x = strtod(cur, &endp);
+            if (endp == cur) break;
+            row[got] = (float)x;
+            cur = endp;
+        }
+        if (got != dim) continue;   // malformed row: skipped (the reference would index past it)
+        std::copy(row.begin(), row.end(), table + (int64_t)it->second * stride);
+        ++*loaded;
+    }
+    fclose(f);
+    return true;
+}
+
 // ---------------------------------------------------------------- saver
 bool save_weights(const std::string& path, const HostGraph& g, const float* table, int64_t rows,
                   int dim, int stride, int fmt, std::string& err) {

@@ -70,6 +70,12 @@ void draw_probabilities(const HostGraph& g, std::vector<double>& p_src, std::vec
 // DeepWalk walk-start order (src/model/DeepWalk.cpp:122-131).
 void deepwalk_order(int64_t V, int walk_times, uint64_t skip, int64_t* order);
 
+// LoadPreTrain (src/proNet.cpp:238-286): "N dim" header, then "name v1..vdim"
+// rows; rows whose name is a vertex of g overwrite table[vid] (stride floats
+// per row); a dim mismatch skips the file (returns true, *loaded = -1).
+bool load_pretrain(const std::string& path, const HostGraph& g, float* table, int dim, int stride,
+                   int64_t* loaded, std::string& err);
+
 // SaveWeights text format (src/model/LINE.cpp:13-47 / Go line.go:209-233).
 bool save_weights(const std::string& path, const HostGraph& g, const float* table, int64_t rows,
                   int dim, int stride, int fmt, std::string& err);

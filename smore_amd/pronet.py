@@ -195,6 +195,10 @@ class ProNet:
     def last_kernel_ms(self):
         return float(lib.smore_last_kernel_ms(self.ctx))
 
+    def load_pretrain(self, which, path):
+        """proNet::LoadPreTrain (src/proNet.cpp:238-286)."""
+        self._chk(lib.smore_load_pretrain(self.ctx, which, path.encode()), "load_pretrain")
+
     def save_weights(self, which, path, fmt=0):
         self._chk(lib.smore_save_weights(self.ctx, which, path.encode(), int(fmt)), "save_weights")
 

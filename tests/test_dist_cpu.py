@@ -1,0 +1,62 @@
+"""Multi-process replica exchange (smore_amd/dist.py) on CPU with gloo,
+world_size 2: the snapshot-delta all-reduce applies every rank's updates
+exactly once (sum) or averages them (mean)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, mean, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from smore_amd.dist import DeltaAllReduce
+    torch.manual_seed(0)
+    base = [torch.randn(50, 8), torch.randn(50, 8)]
+    tabs = [b.clone() for b in base]
+    sync = DeltaAllReduce(tabs, mean=mean)
+    expect = [b.clone() for b in base]
+    for step in range(3):
+        # each rank updates disjoint and overlapping rows with its own deltas
+        deltas = []
+        for r in range(world):
+            g = torch.Generator().manual_seed(100 * step + r)
+            deltas.append([torch.randn(50, 8, generator=g) * 0.01 for _ in tabs])
+        for t, d in zip(tabs, deltas[rank]):
+            t.add_(d)
+        sync.allreduce()
+        for i in range(len(tabs)):
+            tot = sum(deltas[r][i] for r in range(world))
+            expect[i] += tot / world if mean else tot
+    ok = all(torch.allclose(t, e, atol=1e-5) for t, e in zip(tabs, expect))
+    same = [torch.empty_like(tabs[0]) for _ in range(world)]
+    dist.all_gather(same, tabs[0])
+    ok = ok and all(torch.equal(same[0], x) for x in same)
+    out[rank] = int(ok)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mean", [False, True])
+def test_delta_allreduce_gloo_world2(mean):
+    ctx = mp.get_context("spawn")
+    out = ctx.Array("i", [0, 0])
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, mean, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert list(out) == [1, 1]

@@ -291,3 +291,36 @@ def test_save_weights_format(smore, tmp_path):
     assert lines[1].split()[0] == "userA" and len(lines[1].split()) == 6
     W = pn.get_table(0)
     np.testing.assert_allclose([float(x) for x in lines[1].split()[1:]], W[0], rtol=1e-5)
+
+
+def test_replica_sync_rccl_single_rank(smore):
+    """RCCL all-reduce path of smore_amd/dist.py on the context's own device
+    tables (zero-copy views), world size 1: W_snap + sum(delta) == W."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+    from smore_amd.dist import ReplicaSync, table_tensor
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        _, pn = make_pair(smore, "pl1k.txt", 1)
+        pn.alloc_tables(64, 2)
+        pn.init_table_glibc(0, 0)
+        pn.zero_table(1)
+        sync = ReplicaSync(pn)
+        t = table_tensor(pn, 0)
+        assert t.data_ptr() == pn.table_device(0)[0]
+        pn.train_edges("line2", 0, 100000, 10 ** 6, 5, 0.025, 0.0, SEED, "atomic")
+        before = [pn.get_table(0), pn.get_table(1)]
+        sync.allreduce()
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(pn.get_table(0), before[0], atol=1e-6)
+        np.testing.assert_allclose(pn.get_table(1), before[1], atol=1e-6)
+        assert torch.equal(sync.snaps[0][:, :64].cpu(), torch.from_numpy(pn.get_table(0)))
+    finally:
+        dist.destroy_process_group()
