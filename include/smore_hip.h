@@ -124,6 +124,18 @@ int smore_get_table(const smore_ctx* ctx, int which, float* host, int64_t rows, 
 /* device pointer + padded row stride (floats) of a table, for collectives */
 int smore_table_device(smore_ctx* ctx, int which, void** dptr, int64_t* stride);
 
+/* semantics of the sampling and update rules (SURVEY.md 8a "C++ vs Go"):
+ * SMORE_SEM_CPP (default) = src/proNet.cpp; SMORE_SEM_GO = pkg/pronet +
+ * internal/models: source alias out_degree^1, negatives (in+out)^0.75 with the Go
+ * alias rule, CDF target draws, Go UpdatePair (skip duplicate negatives,
+ * deferred positive context), Go updateFirstOrder (LINE1), Go UpdateBPRPair
+ * (BPR: W users, C items, 1 negative, reg = lambda), Go DeepWalk (dead-end
+ * stop, fixed window).  Rebuilds the vertex/negative tables in place.
+ * (replaces the choice of binary: cli/ C++ vs cmd/ Go) */
+#define SMORE_SEM_CPP 0
+#define SMORE_SEM_GO 1
+int smore_set_semantics(smore_ctx* ctx, int semantics);
+
 /* ---- training -------------------------------------------------------------------- */
 /* replaces: the hot loops of LINE::Train (src/model/LINE.cpp:160-191),
  * MF::Train (src/model/MF.cpp:78-101), BPR::Train (src/model/BPR.cpp:77-101);
@@ -164,7 +176,8 @@ int smore_deepwalk_order(int64_t V, int walk_times, uint64_t skip, int64_t* orde
 /* ---- samplers (parity tests) -------------------------------------------------------- */
 /* replaces: SourceSample/TargetSample/NegativeSample (src/proNet.cpp:623-683):
  * draws of samples [begin, begin+count) as the training kernels draw them.
- * out: count x (2+K) int32 {v, c, n1..nK} (model != BPR) or count x 7 {u,i,j0..j4}. */
+ * out: count x (2+K) int32 {v, c, n1..nK} (model != BPR) or count x 7 {u,i,j0..j4};
+ * Go semantics: count x (2+K), BPR count x 3 {u, i, j}. */
 int smore_sample_edges(smore_ctx* ctx, int model, uint64_t begin, uint64_t count, int K,
                        uint64_t seed, int32_t* out);
 

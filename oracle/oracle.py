@@ -274,3 +274,97 @@ def train_deepwalk_f32(g, W, C_, dim, walk_times, walk_steps, window, K, alpha0,
         end = walk_times * g.V
     return lib().orc_train_deepwalk_f32(g.ref, ptr(W), ptr(C_), dim, W.shape[1], walk_times, walk_steps, window,
                                         K, alpha0, seed, ptr(order), begin, end)
+
+
+# --------------------------------------------------------------------- Go semantics
+class _OrcGoGraph(C.Structure):
+    _fields_ = [("base", _OrcGraph), ("tcum", P)]
+
+
+class GoGraph:
+    """Graph with the Go rules (pkg/pronet/pronet.go:191-249): VertexAT power 1,
+    NegativeAT power 0.75 (Go alias rule), CDF target sampling."""
+
+    def __init__(self, V, src, dst, w, names=None):
+        self.V, self.E, self.names = V, len(src), names
+        base = Graph(V, src, dst, w)               # CSR + degrees (same as C++)
+        self.offsets, self.targets = base.offsets, base.targets
+        self.out_deg, self.in_deg = base.out_deg, base.in_deg
+        self.weights = np.zeros(max(self.E, 1))
+        # CSR weights in push order
+        order = np.argsort(np.asarray(src), kind="stable")
+        self.weights[:self.E] = np.asarray(w, np.float64)[order]
+        self.vprob, self.valias = alias_go(self.out_deg, 1.0)
+        self.nprob, self.nalias = alias_go(self.in_deg + self.out_deg, 0.75)
+        self.vthr, self.valias_enc = alias_encode(self.vprob, self.valias)
+        self.nthr, self.nalias_enc = alias_encode(self.nprob, self.nalias)
+        self.tcum = np.zeros(max(self.E, 1))
+        lib().orc_go_cumsum(ptr(self.offsets), V, ptr(self.weights), ptr(self.tcum))
+        b = _OrcGraph(V, self.E, ptr(self.offsets), ptr(self.targets), ptr(self.vthr), ptr(self.valias_enc),
+                      ptr(self.nthr), ptr(self.nalias_enc), None, None)
+        self._struct = _OrcGoGraph(b, ptr(self.tcum))
+        self._keep = base
+
+    @classmethod
+    def from_file(cls, path, undirected):
+        names, s, d, w = read_edgelist(path, undirected)
+        return cls(len(names), s, d, w, names)
+
+    @property
+    def ref(self):
+        return C.byref(self._struct)
+
+
+GO_MODEL = {"line2": 0, "line1": 1, "bpr": 3}
+
+
+def _declare_go(L):
+    L.orc_go_cumsum.argtypes = [P, i64, P, P]
+    L.orc_go_sample.argtypes = [P, u64, u64, u64, C.c_int, P]
+    L.orc_go_train_f64.restype = C.c_int
+    L.orc_go_train_f64.argtypes = [P, C.c_int, P, P, C.c_int, C.c_int, dbl, dbl, u64, u64, u64, u64]
+    L.orc_go_train_f32.restype = C.c_int
+    L.orc_go_train_f32.argtypes = [P, C.c_int, P, P, C.c_int, C.c_int, C.c_int, dbl, dbl, u64, u64, u64, u64]
+    L.orc_go_deepwalk_f32.restype = C.c_int
+    L.orc_go_deepwalk_f32.argtypes = [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, dbl, u64, P,
+                                      u64, u64]
+    L.orc_go_deepwalk_f64.restype = C.c_int
+    L.orc_go_deepwalk_f64.argtypes = [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, dbl, u64, P]
+
+
+_orig_declare = _declare
+
+
+def _declare(L):  # noqa: F811
+    _orig_declare(L)
+    _declare_go(L)
+
+
+def go_sample(g, seed, begin, count, K):
+    o = np.zeros((count, 2 + K), np.int32)
+    lib().orc_go_sample(g.ref, seed, begin, count, K, ptr(o))
+    return o
+
+
+def go_train_f64(g, model, W, C_, K, alpha0, lam, total, begin, end, seed):
+    return lib().orc_go_train_f64(g.ref, GO_MODEL[model], ptr(W), ptr(C_), W.shape[1], K, alpha0, lam, total,
+                                  begin, end, seed)
+
+
+def go_train_f32(g, model, W, C_, dim, K, alpha0, lam, total, begin, end, seed):
+    return lib().orc_go_train_f32(g.ref, GO_MODEL[model], ptr(W), ptr(C_), dim, W.shape[1], K, alpha0, lam, total,
+                                  begin, end, seed)
+
+
+def go_deepwalk_f32(g, W, C_, dim, walk_times, walk_steps, window, K, alpha0, seed, order, begin=0, end=None):
+    order = np.ascontiguousarray(order, np.int64)
+    if end is None:
+        end = walk_times * g.V
+    return lib().orc_go_deepwalk_f32(g.ref, ptr(W), ptr(C_), dim, W.shape[1], walk_times, walk_steps, window, K,
+                                     alpha0, seed, ptr(order), begin, end)
+
+
+def go_deepwalk_f64(g, W, C_, walk_times, walk_steps, window, K, alpha0, seed, order):
+    order = np.ascontiguousarray(order, np.int64)
+    return lib().orc_go_deepwalk_f64(g.ref, ptr(W), ptr(C_), W.shape[1], walk_times, walk_steps, window, K, alpha0,
+                                     seed, ptr(order))

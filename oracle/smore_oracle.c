@@ -778,3 +778,290 @@ int orc_train_deepwalk_f32(const orc_graph* g, float* W, float* C, int dim, int 
     free(walk); free(pv); free(pc); free(e);
     return 0;
 }
+
+/* ========================================================================== */
+/* Go semantics (pkg/pronet, internal/models/{line,bpr,deepwalk}).             */
+/* No Go toolchain exists here: these restate the Go source and are            */
+/* cross-checked against an independent pure-Python restatement               */
+/* (tests/go_semantics_ref.py).                                                */
+/* ========================================================================== */
+
+/* prefix sums in the Go loop's order: cumWeight += w (pronet.go:275-279) */
+void orc_go_cumsum(const int64_t* offsets, int64_t V, const double* w, double* tcum) {
+    for (int64_t v = 0; v < V; ++v) {
+        double acc = 0.0;
+        for (int64_t e = offsets[v]; e < offsets[v + 1]; ++e) { acc += w[e]; tcum[e] = acc; }
+    }
+}
+
+/* aliasSample (alias.go:93-106): i = Intn(n) first, then r = Float64() */
+static inline int32_t go_alias(const uint32_t* thr, const int32_t* alias, int64_t n, uint32_t ki, uint32_t kp) {
+    uint32_t i = draw_index(ki, (uint64_t)n);
+    return kp < thr[i] ? (int32_t)i : alias[i];
+}
+
+/* TargetSample (pronet.go:257-284): r = Float64()*sum(w); first i with r <= cum_i */
+static inline int32_t go_target(const orc_go_graph* g, int32_t v, uint32_t kr) {
+    int64_t off = g->base.offsets[v], br = g->base.offsets[v + 1] - off;
+    if (br == 0) return -1;
+    double r = draw_unit(kr) * g->tcum[off + br - 1];
+    int64_t lo = 0, hi = br - 1;
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (r <= g->tcum[off + mid]) hi = mid; else lo = mid + 1;
+    }
+    return g->base.targets[off + lo];
+}
+
+void orc_go_sample(const orc_go_graph* g, uint64_t seed, uint64_t begin, uint64_t count, int K, int32_t* out) {
+    uint32_t w[MAX_SLOTS];
+    for (uint64_t t = 0; t < count; ++t) {
+        orc_words(seed, 0, begin + t, 3 + 2 * K, w);
+        int32_t* o = out + t * (2 + K);
+        int32_t v = go_alias(g->base.vthr, g->base.valias, g->base.V, w[0], w[1]);
+        o[0] = v;
+        o[1] = go_target(g, v, w[2]);
+        for (int j = 0; j < K; ++j) o[2 + j] = go_alias(g->base.nthr, g->base.nalias, g->base.V, w[3 + 2 * j], w[4 + 2 * j]);
+    }
+}
+
+static inline double go_fast_sigmoid(double x) { return orc_fast_sigmoid(x); }   /* pronet.go:98-109 */
+
+/* ---- fp64, the Go arithmetic ------------------------------------------------ */
+/* sgdUpdate (optimizer.go:61-84) */
+static void go_sgd_f64(const double* ve, const double* ce, double label, double alpha, int dim,
+                       double* vg, double* cg) {
+    double score = 0.0;
+    for (int d = 0; d < dim; ++d) score += ve[d] * ce[d];
+    double pred = go_fast_sigmoid(score);
+    double grad = alpha * (label - pred);
+    for (int d = 0; d < dim; ++d) { vg[d] += grad * ce[d]; cg[d] += grad * ve[d]; }
+}
+
+/* UpdatePair (optimizer.go:21-58) */
+static void go_update_pair_f64(double* W, double* C, int dim, int32_t v, int32_t c, const int32_t* negs, int K,
+                               double alpha, double* vg, double* cg, double* ng) {
+    double* wv = W + (int64_t)v * dim;
+    double* cc = C + (int64_t)c * dim;
+    for (int d = 0; d < dim; ++d) { vg[d] = 0.0; cg[d] = 0.0; }
+    go_sgd_f64(wv, cc, 1.0, alpha, dim, vg, cg);
+    for (int j = 0; j < K; ++j) {
+        if (negs[j] == c) continue;
+        double* cn = C + (int64_t)negs[j] * dim;
+        for (int d = 0; d < dim; ++d) ng[d] = 0.0;
+        go_sgd_f64(wv, cn, 0.0, alpha, dim, vg, ng);
+        for (int d = 0; d < dim; ++d) cn[d] += ng[d];
+    }
+    for (int d = 0; d < dim; ++d) { wv[d] += vg[d]; cc[d] += cg[d]; }
+}
+
+/* updateFirstOrder (internal/models/line/line.go:153-200) */
+static void go_first_order_f64(double* W, int dim, int32_t s, int32_t t, const int32_t* negs, int K, double alpha,
+                               double* vg, double* cg) {
+    double* ws = W + (int64_t)s * dim;
+    double* wt = W + (int64_t)t * dim;
+    double score = 0.0;
+    for (int d = 0; d < dim; ++d) score += ws[d] * wt[d];
+    double grad = alpha * (1.0 - go_fast_sigmoid(score));
+    for (int d = 0; d < dim; ++d) { vg[d] = grad * wt[d]; cg[d] = grad * ws[d]; }
+    for (int j = 0; j < K; ++j) {
+        int32_t n = negs[j];
+        if (n == t || n == s) continue;
+        double* wn = W + (int64_t)n * dim;
+        double sc = 0.0;
+        for (int d = 0; d < dim; ++d) sc += ws[d] * wn[d];
+        double gr = alpha * (0.0 - go_fast_sigmoid(sc));
+        for (int d = 0; d < dim; ++d) { vg[d] += gr * wn[d]; wn[d] += gr * ws[d]; }
+    }
+    for (int d = 0; d < dim; ++d) { ws[d] += vg[d]; wt[d] += cg[d]; }
+}
+
+/* UpdateBPRPair (optimizer.go:87-117): W users, C items */
+static void go_bpr_f64(double* W, double* C, int dim, int32_t u, int32_t i, int32_t j, double alpha, double lambda) {
+    double* wu = W + (int64_t)u * dim;
+    double* ci = C + (int64_t)i * dim;
+    double* cj = C + (int64_t)j * dim;
+    double pos = 0.0, neg = 0.0;
+    for (int d = 0; d < dim; ++d) { pos += wu[d] * ci[d]; neg += wu[d] * cj[d]; }
+    double gc = alpha * go_fast_sigmoid(neg - pos);
+    for (int d = 0; d < dim; ++d) {
+        double vgr = gc * (ci[d] - cj[d]);
+        double pg = gc * wu[d];
+        double ngr = -gc * wu[d];
+        wu[d] += vgr - lambda * alpha * wu[d];
+        ci[d] += pg - lambda * alpha * ci[d];
+        cj[d] += ngr - lambda * alpha * cj[d];
+    }
+}
+
+int orc_go_train_f64(const orc_go_graph* g, int model, double* W, double* C, int dim, int K, double alpha0,
+                     double lambda, uint64_t total, uint64_t begin, uint64_t end, uint64_t seed) {
+    sig_init();
+    double* buf = (double*)malloc(sizeof(double) * dim * 3);
+    uint32_t w[MAX_SLOTS];
+    int32_t negs[MAX_SLOTS];
+    int skipped = 0;
+    const int nk = model == 3 ? 1 : K;
+    for (uint64_t s = begin; s < end; ++s) {
+        orc_words(seed, 0, s, 3 + 2 * nk, w);
+        int32_t v = go_alias(g->base.vthr, g->base.valias, g->base.V, w[0], w[1]);
+        int32_t c = go_target(g, v, w[2]);
+        if (c < 0) { skipped++; continue; }
+        for (int j = 0; j < nk; ++j) negs[j] = go_alias(g->base.nthr, g->base.nalias, g->base.V, w[3 + 2 * j], w[4 + 2 * j]);
+        double alpha = orc_alpha_walk(s, alpha0, total);
+        if (model == 0) go_update_pair_f64(W, C, dim, v, c, negs, K, alpha, buf, buf + dim, buf + 2 * dim);
+        else if (model == 1) go_first_order_f64(W, dim, v, c, negs, K, alpha, buf, buf + dim);
+        else go_bpr_f64(W, C, dim, v, c, negs[0], alpha, lambda);
+    }
+    free(buf);
+    return skipped;
+}
+
+/* ---- fp32 spec of the Go rules (no fused multiply-add: amd64 Go does not fuse) -- */
+static void go_update_pair_f32(float* W, float* C, int dpad, int32_t v, int32_t c, const int32_t* negs, int K,
+                               float alpha, float* vg, float* cg) {
+    float* wv = W + (int64_t)v * dpad;
+    float* cc = C + (int64_t)c * dpad;
+    float f = dot_spec(wv, cc, dpad);
+    float grad = alpha * (1.0f - fast_sigmoid_f32(f));
+    for (int d = 0; d < dpad; ++d) { vg[d] = grad * cc[d]; cg[d] = grad * wv[d]; }
+    for (int j = 0; j < K; ++j) {
+        if (negs[j] == c) continue;
+        float* cn = C + (int64_t)negs[j] * dpad;
+        float fn = dot_spec(wv, cn, dpad);
+        float gr = alpha * (0.0f - fast_sigmoid_f32(fn));
+        for (int d = 0; d < dpad; ++d) {
+            float ng = gr * wv[d];
+            vg[d] = vg[d] + gr * cn[d];
+            cn[d] = cn[d] + ng;
+        }
+    }
+    for (int d = 0; d < dpad; ++d) { wv[d] = wv[d] + vg[d]; cc[d] = cc[d] + cg[d]; }
+}
+
+static void go_first_order_f32(float* W, int dpad, int32_t s, int32_t t, const int32_t* negs, int K, float alpha,
+                               float* vg, float* cg) {
+    float* ws = W + (int64_t)s * dpad;
+    float* wt = W + (int64_t)t * dpad;
+    float grad = alpha * (1.0f - fast_sigmoid_f32(dot_spec(ws, wt, dpad)));
+    for (int d = 0; d < dpad; ++d) { vg[d] = grad * wt[d]; cg[d] = grad * ws[d]; }
+    for (int j = 0; j < K; ++j) {
+        int32_t n = negs[j];
+        if (n == t || n == s) continue;
+        float* wn = W + (int64_t)n * dpad;
+        float gr = alpha * (0.0f - fast_sigmoid_f32(dot_spec(ws, wn, dpad)));
+        for (int d = 0; d < dpad; ++d) { vg[d] = vg[d] + gr * wn[d]; wn[d] = wn[d] + gr * ws[d]; }
+    }
+    for (int d = 0; d < dpad; ++d) { ws[d] = ws[d] + vg[d]; wt[d] = wt[d] + cg[d]; }
+}
+
+static void go_bpr_f32(float* W, float* C, int dpad, int32_t u, int32_t i, int32_t j, float alpha, float lambda) {
+    float* wu = W + (int64_t)u * dpad;
+    float* ci = C + (int64_t)i * dpad;
+    float* cj = C + (int64_t)j * dpad;
+    float pos = dot_spec(wu, ci, dpad), neg = dot_spec(wu, cj, dpad);
+    float gc = alpha * fast_sigmoid_f32(neg - pos);
+    float la = lambda * alpha;
+    for (int d = 0; d < dpad; ++d) {
+        float vgr = gc * (ci[d] - cj[d]);
+        float pg = gc * wu[d];
+        float ngr = -gc * wu[d];
+        wu[d] = wu[d] + (vgr - la * wu[d]);
+        ci[d] = ci[d] + (pg - la * ci[d]);
+        cj[d] = cj[d] + (ngr - la * cj[d]);
+    }
+}
+
+int orc_go_train_f32(const orc_go_graph* g, int model, float* W, float* C, int dim, int dpad, int K,
+                     double alpha0, double lambda, uint64_t total, uint64_t begin, uint64_t end, uint64_t seed) {
+    (void)dim;
+    sig_init();
+    float* buf = (float*)malloc(sizeof(float) * dpad * 2);
+    uint32_t w[MAX_SLOTS];
+    int32_t negs[MAX_SLOTS];
+    int skipped = 0;
+    const int nk = model == 3 ? 1 : K;
+    for (uint64_t s = begin; s < end; ++s) {
+        orc_words(seed, 0, s, 3 + 2 * nk, w);
+        int32_t v = go_alias(g->base.vthr, g->base.valias, g->base.V, w[0], w[1]);
+        int32_t c = go_target(g, v, w[2]);
+        if (c < 0) { skipped++; continue; }
+        for (int j = 0; j < nk; ++j) negs[j] = go_alias(g->base.nthr, g->base.nalias, g->base.V, w[3 + 2 * j], w[4 + 2 * j]);
+        float alpha = (float)orc_alpha_walk(s, alpha0, total);
+        if (model == 0) go_update_pair_f32(W, C, dpad, v, c, negs, K, alpha, buf, buf + dpad);
+        else if (model == 1) go_first_order_f32(W, dpad, v, c, negs, K, alpha, buf, buf + dpad);
+        else go_bpr_f32(W, C, dpad, v, c, negs[0], alpha, (float)lambda);
+    }
+    free(buf);
+    return skipped;
+}
+
+/* ---- Go DeepWalk ------------------------------------------------------------ */
+static int go_random_walk(const orc_go_graph* g, walk_rng* r, int32_t start, int steps, int32_t* walk) {
+    int L = 0;
+    int32_t cur = start;
+    walk[L++] = cur;
+    for (int i = 0; i < steps; ++i) {
+        if (g->base.offsets[cur + 1] - g->base.offsets[cur] == 0) break;   /* TargetSample -> -1 */
+        int32_t next = go_target(g, cur, walk_next(r));
+        walk[L++] = next;
+        cur = next;
+    }
+    return L;
+}
+
+static int go_skip_grams(const int32_t* walk, int L, int window, int32_t* pv, int32_t* pc) {
+    int n = 0;
+    for (int i = 0; i < L; ++i) {
+        int start = i - window; if (start < 0) start = 0;
+        int end = i + window + 1; if (end > L) end = L;
+        for (int j = start; j < end; ++j)
+            if (i != j) { pv[n] = walk[i]; pc[n] = walk[j]; n++; }
+    }
+    return n;
+}
+
+static int go_deepwalk(const orc_go_graph* g, double* W64, double* C64, float* W32, float* C32, int dim, int dpad,
+                       int walk_times, int walk_steps, int window, int K, double alpha0, uint64_t seed,
+                       const int64_t* order, uint64_t walk_begin, uint64_t walk_end) {
+    sig_init();
+    uint64_t total = (uint64_t)walk_times * (uint64_t)g->base.V;
+    if (walk_end > total) walk_end = total;
+    int32_t* walk = (int32_t*)malloc(sizeof(int32_t) * (walk_steps + 1));
+    int maxp = 2 * window * (walk_steps + 1) + 1;
+    int32_t* pv = (int32_t*)malloc(sizeof(int32_t) * maxp);
+    int32_t* pc = (int32_t*)malloc(sizeof(int32_t) * maxp);
+    int32_t negs[MAX_SLOTS];
+    int n = W64 ? dim : dpad;
+    double* b64 = (double*)malloc(sizeof(double) * n * 3);
+    float* b32 = (float*)malloc(sizeof(float) * n * 2);
+    for (uint64_t wk = walk_begin; wk < walk_end; ++wk) {
+        walk_rng r = {seed, wk, 0, {0, 0, 0, 0}, 0xFFFFFFFFu};
+        double alpha = orc_alpha_walk(wk, alpha0, total);
+        int L = go_random_walk(g, &r, (int32_t)order[wk], walk_steps, walk);
+        int np = go_skip_grams(walk, L, window, pv, pc);
+        for (int p = 0; p < np; ++p) {
+            for (int j = 0; j < K; ++j) {
+                uint32_t ki = walk_next(&r), kp = walk_next(&r);
+                negs[j] = go_alias(g->base.nthr, g->base.nalias, g->base.V, ki, kp);
+            }
+            if (W64) go_update_pair_f64(W64, C64, dim, pv[p], pc[p], negs, K, alpha, b64, b64 + n, b64 + 2 * n);
+            else go_update_pair_f32(W32, C32, dpad, pv[p], pc[p], negs, K, (float)alpha, b32, b32 + n);
+        }
+    }
+    free(walk); free(pv); free(pc); free(b64); free(b32);
+    return 0;
+}
+
+int orc_go_deepwalk_f32(const orc_go_graph* g, float* W, float* C, int dim, int dpad, int walk_times,
+                        int walk_steps, int window, int K, double alpha0, uint64_t seed,
+                        const int64_t* order, uint64_t walk_begin, uint64_t walk_end) {
+    return go_deepwalk(g, NULL, NULL, W, C, dim, dpad, walk_times, walk_steps, window, K, alpha0, seed, order,
+                       walk_begin, walk_end);
+}
+
+int orc_go_deepwalk_f64(const orc_go_graph* g, double* W, double* C, int dim, int walk_times, int walk_steps,
+                        int window, int K, double alpha0, uint64_t seed, const int64_t* order) {
+    return go_deepwalk(g, W, C, NULL, NULL, dim, dim, walk_times, walk_steps, window, K, alpha0, seed, order, 0,
+                       (uint64_t)-1);
+}

@@ -16,6 +16,7 @@ AT_VERTEX, AT_NEGATIVE, AT_CONTEXT = 0, 1, 2
 W, CTX = 0, 1
 MODEL = {"line2": 0, "line1": 1, "mf": 2, "bpr": 3}
 MODE = {"hogwild": 0, "atomic": 1, "serial": 2, "hybrid": 3}
+SEM = {"cpp": 0, "go": 1}
 
 
 class SmoreError(RuntimeError):
@@ -53,6 +54,7 @@ def _load():
         "smore_train_edges": (i32, [P, i32, u64, u64, u64, i32, dbl, dbl, u64, i32]),
         "smore_skipped": (i32, [P, C.POINTER(u64)]),
         "smore_set_hot_threshold": (i32, [P, dbl]),
+        "smore_set_semantics": (i32, [P, i32]),
         "smore_hot_rows": (i32, [P, C.POINTER(i64), C.POINTER(i64)]),
         "smore_last_kernel_ms": (C.c_float, [P]),
         "smore_train_deepwalk": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, u64, P, i32]),

@@ -55,6 +55,9 @@ struct smore_ctx {
     bool timed = false;
     int cus = 0;
     int64_t last_loaded = 0;
+    // semantics: SMORE_SEM_CPP (default) or SMORE_SEM_GO
+    int semantics = 0;
+    double* d_tcum = nullptr;
 };
 
 namespace {
@@ -173,7 +176,7 @@ void smore_destroy(smore_ctx* c) {
     dfree(c->d_offsets); dfree(c->d_targets); dfree(c->d_vtab); dfree(c->d_ntab); dfree(c->d_ctab);
     dfree(c->d_sig); dfree(c->d_skipped); dfree(c->d_table[0]); dfree(c->d_table[1]);
     dfree(c->d_hotW); dfree(c->d_hotC);
-    dfree(c->d_order); dfree(c->d_walks); dfree(c->d_lens);
+    dfree(c->d_order); dfree(c->d_walks); dfree(c->d_lens); dfree(c->d_tcum);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -204,6 +207,7 @@ int smore_set_graph_edges(smore_ctx* c, int64_t V, int64_t E, const int32_t* src
         return fail(c, SMORE_EINVAL, "bad arguments");
     c->g = HostGraph();
     c->hot_key.clear();
+    c->semantics = SMORE_SEM_CPP;
     if (!build_graph(V, E, src, dst, w, vm, nm, c->g, c->err)) return SMORE_EINVAL;
     return upload_graph(c);
 }
@@ -450,6 +454,27 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
     a.model = model;
     a.mode = mode;
     a.hotW = a.hotC = nullptr;
+    a.tcum = c->d_tcum;
+    if (c->semantics == SMORE_SEM_GO) {
+        if (model == SMORE_MF) return fail(c, SMORE_EINVAL, "Go semantics has no MF model");
+        if (mode == SMORE_HYBRID) return fail(c, SMORE_EINVAL, "Go semantics: hybrid scatter not built");
+        if (K > 10) return fail(c, SMORE_EINVAL, "Go semantics: K <= 10");
+        if (model == SMORE_BPR && c->ntables < 2) return fail(c, SMORE_ESTATE, "Go BPR needs W (users) and C (items)");
+        if (model == SMORE_BPR) a.C = c->d_table[1];
+        a.K = K;
+        const int G = lanes_of(c->dpad);
+        int grid = 1;
+        if (mode != SMORE_SERIAL) {
+            grid = c->cus * 4;
+            const int64_t need = ((int64_t)count + 256 / G - 1) / (256 / G);
+            if (need < grid) grid = (int)std::max<int64_t>(1, need);
+        }
+        HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+        HIPCHK(c, launch_go_edge(a, grid, c->stream));
+        HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+        c->timed = true;
+        return SMORE_OK;
+    }
     const int grid = edge_grid(c, a);
     if (mode == SMORE_HYBRID) {
         const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
@@ -470,6 +495,28 @@ int smore_train_edges(smore_ctx* c, int model, uint64_t begin, uint64_t count, u
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipGetLastError());
+    return SMORE_OK;
+}
+
+int smore_set_semantics(smore_ctx* c, int semantics) {
+    if (!c || (semantics != SMORE_SEM_CPP && semantics != SMORE_SEM_GO)) return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    if (semantics == c->semantics) return SMORE_OK;
+    std::vector<double> tcum;
+    if (semantics == SMORE_SEM_GO) build_go_tables(c->g, tcum);
+    else build_cpp_vn_tables(c->g);
+    c->semantics = semantics;
+    c->hot_key.clear();
+    if (c->device < 0) return SMORE_OK;
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    if ((rc = upload(c, c->d_vtab, c->g.vtab.data(), c->g.vtab.size()))) return rc;
+    if ((rc = upload(c, c->d_ntab, c->g.ntab.data(), c->g.ntab.size()))) return rc;
+    if (semantics == SMORE_SEM_GO) {
+        if ((rc = upload(c, c->d_tcum, tcum.data(), tcum.size()))) return rc;
+    } else {
+        dfree(c->d_tcum);
+    }
     return SMORE_OK;
 }
 
@@ -520,10 +567,12 @@ int smore_sample_edges(smore_ctx* c, int model, uint64_t begin, uint64_t count, 
     int rc;
     if ((rc = set_device(c))) return rc;
     const int bpr = model == SMORE_BPR;
-    const size_t width = bpr ? 7 : 2 + K;
+    const size_t width = c->semantics == SMORE_SEM_GO ? (bpr ? 3 : 2 + K) : (bpr ? 7 : 2 + K);
     int32_t* d = nullptr;
     HIPCHK(c, hipMalloc((void**)&d, count * width * sizeof(int32_t)));
-    hipError_t e = launch_sample(dev_graph(c), seed, begin, count, K, bpr, d, c->stream);
+    hipError_t e = c->semantics == SMORE_SEM_GO
+                       ? launch_go_sample(dev_graph(c), c->d_tcum, seed, begin, count, bpr ? 1 : K, d, c->stream)
+                       : launch_sample(dev_graph(c), seed, begin, count, K, bpr, d, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess) e = hipMemcpy(out, d, count * width * sizeof(int32_t), hipMemcpyDeviceToHost);
     (void)hipFree(d);
@@ -599,6 +648,8 @@ int smore_train_deepwalk(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, i
     a.begin = 0; a.count = 0; a.total = total; a.seed = seed; a.alpha0 = alpha0; a.reg = 0.0f;
     a.dpad = c->dpad; a.K = K; a.model = SMORE_LINE2; a.mode = mode;
     a.hotW = a.hotC = nullptr;
+    a.tcum = c->d_tcum;
+    if (c->semantics == SMORE_SEM_GO && mode == SMORE_HYBRID) return fail(c, SMORE_EINVAL, "Go semantics: no hybrid");
     int grid = 1;
     if (mode != SMORE_SERIAL) {
         int per_cu = 0;
@@ -624,12 +675,16 @@ int smore_train_deepwalk(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, i
         w.total_walks = total;
         w.steps = walk_steps;
         w.window = window;
-        HIPCHK(c, launch_walk_gen(a.g, w, seed, c->stream));
         const int64_t groups_per_block = 256 / lanes_of(c->dpad);
         int g2 = grid;
         if ((int64_t)g2 * groups_per_block > (int64_t)w.nwalks && mode != SMORE_SERIAL)
             g2 = (int)std::max<int64_t>(1, ((int64_t)w.nwalks + groups_per_block - 1) / groups_per_block);
-        HIPCHK(c, launch_walk_pairs(a, w, g2, c->stream));
+        if (c->semantics == SMORE_SEM_GO) {
+            HIPCHK(c, launch_go_walk(a, w, g2, c->stream));
+        } else {
+            HIPCHK(c, launch_walk_gen(a.g, w, seed, c->stream));
+            HIPCHK(c, launch_walk_pairs(a, w, g2, c->stream));
+        }
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;

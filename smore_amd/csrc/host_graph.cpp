@@ -57,6 +57,50 @@ void alias_encode(const double* prob, const int64_t* alias, int64_t n, const int
     }
 }
 
+void alias_go(const double* dist, int64_t n, double power, double* prob, int64_t* alias) {
+    std::vector<double> q((size_t)n);
+    double sum = 0.0;
+    for (int64_t i = 0; i < n; ++i) {
+        q[i] = dist[i] > 0 ? std::pow(dist[i], power) : 0.0;
+        sum += q[i];
+        prob[i] = 0.0;
+        alias[i] = 0;
+    }
+    if (sum == 0) {
+        for (int64_t i = 0; i < n; ++i) { prob[i] = 1.0; alias[i] = i; }
+        return;
+    }
+    for (int64_t i = 0; i < n; ++i) q[i] = q[i] * (double)n / sum;
+    std::vector<int64_t> small, large;
+    for (int64_t i = 0; i < n; ++i) (q[i] < 1.0 ? small : large).push_back(i);
+    while (!small.empty() && !large.empty()) {
+        int64_t l = small.back(); small.pop_back();
+        int64_t g = large.back(); large.pop_back();
+        prob[l] = q[l];
+        alias[l] = g;
+        q[g] = q[g] + q[l] - 1.0;
+        (q[g] < 1.0 ? small : large).push_back(g);
+    }
+    while (!large.empty()) { int64_t g = large.back(); large.pop_back(); prob[g] = 1.0; alias[g] = g; }
+    while (!small.empty()) { int64_t l = small.back(); small.pop_back(); prob[l] = 1.0; alias[l] = l; }
+}
+
+void build_go_tables(HostGraph& g, std::vector<double>& tcum) {
+    const int64_t V = g.V;
+    std::vector<double> dist((size_t)V);
+    for (int64_t v = 0; v < V; ++v) dist[v] = g.out_deg[v];
+    alias_go(dist.data(), V, 1.0, g.vprob.data(), g.valias.data());
+    for (int64_t v = 0; v < V; ++v) dist[v] = g.in_deg[v] + g.out_deg[v];
+    alias_go(dist.data(), V, 0.75, g.nprob.data(), g.nalias.data());
+    alias_encode(g.vprob.data(), g.valias.data(), V, nullptr, g.vtab.data());
+    alias_encode(g.nprob.data(), g.nalias.data(), V, nullptr, g.ntab.data());
+    tcum.resize((size_t)std::max<int64_t>(g.E, 1));
+    for (int64_t v = 0; v < V; ++v) {
+        double acc = 0.0;
+        for (int64_t e = g.offsets[v]; e < g.offsets[v + 1]; ++e) { acc += g.weights[e]; tcum[e] = acc; }
+    }
+}
+
 static void parallel_for(int64_t n, int64_t grain, const std::function<void(int64_t, int64_t)>& fn) {
     unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     unsigned nt = (unsigned)std::min<int64_t>(std::min<unsigned>(hw, 16u), (n + grain - 1) / grain);
@@ -102,27 +146,16 @@ bool build_graph(int64_t V, int64_t E, const int32_t* src, const int32_t* dst, c
         for (int64_t p = g.offsets[v]; p < g.offsets[v + 1]; ++p) g.out_deg[v] += g.weights[p];
     for (int64_t p = 0; p < E; ++p) g.in_deg[g.targets[p]] += g.weights[p];
 
-    std::vector<double> dist((size_t)V);
-    // vertex table (src/proNet.cpp:457-482)
-    for (int64_t v = 0; v < V; ++v) {
-        if (vertex_method == 0) dist[v] = g.out_deg[v];
-        else if (vertex_method == 1) dist[v] = g.out_deg[v] == 0 ? 0 : 1;
-        else dist[v] = g.in_deg[v] + g.out_deg[v];
-    }
+    g.vertex_method = vertex_method;
+    g.negative_method = negative_method;
     g.vprob.resize((size_t)V); g.valias.resize((size_t)V);
-    alias_cpp(dist.data(), V, g.vprob.data(), g.valias.data());
-    // negative table (src/proNet.cpp:485-510)
-    for (int64_t v = 0; v < V; ++v) {
-        if (negative_method == 0) dist[v] = g.in_deg[v] + g.out_deg[v];
-        else if (negative_method == 1) dist[v] = g.in_deg[v];
-        else dist[v] = g.in_deg[v] == 0 ? 0 : 1;
-    }
     g.nprob.resize((size_t)V); g.nalias.resize((size_t)V);
-    alias_cpp(dist.data(), V, g.nprob.data(), g.nalias.data());
+    g.vtab.resize((size_t)V); g.ntab.resize((size_t)V);
+    build_cpp_vn_tables(g);
     // per-vertex context tables, alias remapped to the target vid
     // (src/proNet.cpp:517-537); vertices are independent -> threads
     g.cprob.resize((size_t)E); g.calias.resize((size_t)E);
-    g.vtab.resize((size_t)V); g.ntab.resize((size_t)V); g.ctab.resize((size_t)E);
+    g.ctab.resize((size_t)E);
     parallel_for(V, 1 << 14, [&](int64_t b, int64_t e) {
         for (int64_t v = b; v < e; ++v) {
             int64_t off = g.offsets[v], br = g.offsets[v + 1] - off;
@@ -134,9 +167,28 @@ bool build_graph(int64_t V, int64_t E, const int32_t* src, const int32_t* dst, c
                          g.ctab.data() + off);
         }
     });
+    return true;
+}
+
+void build_cpp_vn_tables(HostGraph& g) {
+    const int64_t V = g.V;
+    std::vector<double> dist((size_t)V);
+    // vertex table (src/proNet.cpp:457-482)
+    for (int64_t v = 0; v < V; ++v) {
+        if (g.vertex_method == 0) dist[v] = g.out_deg[v];
+        else if (g.vertex_method == 1) dist[v] = g.out_deg[v] == 0 ? 0 : 1;
+        else dist[v] = g.in_deg[v] + g.out_deg[v];
+    }
+    alias_cpp(dist.data(), V, g.vprob.data(), g.valias.data());
+    // negative table (src/proNet.cpp:485-510)
+    for (int64_t v = 0; v < V; ++v) {
+        if (g.negative_method == 0) dist[v] = g.in_deg[v] + g.out_deg[v];
+        else if (g.negative_method == 1) dist[v] = g.in_deg[v];
+        else dist[v] = g.in_deg[v] == 0 ? 0 : 1;
+    }
+    alias_cpp(dist.data(), V, g.nprob.data(), g.nalias.data());
     alias_encode(g.vprob.data(), g.valias.data(), V, nullptr, g.vtab.data());
     alias_encode(g.nprob.data(), g.nalias.data(), V, nullptr, g.ntab.data());
-    return true;
 }
 
 static void alias_marginal(const std::vector<double>& prob, const std::vector<int64_t>& alias, int64_t off,

@@ -18,6 +18,7 @@ struct AliasEntry {          // device encoding of one alias-table entry (8 B)
 
 struct HostGraph {
     int64_t V = 0, E = 0;
+    int vertex_method = 0, negative_method = 0;
     std::vector<std::string> names;          // empty when built from ids
     std::vector<int64_t> offsets;            // V+1
     std::vector<int32_t> targets;            // E, push order per source
@@ -34,6 +35,16 @@ struct HostGraph {
 // (power argument ignored, :558,564), LIFO stacks, leftovers prob 1 alias -1.
 void alias_cpp(const double* dist, int64_t n, double* prob, int64_t* alias);
 
+// Vose alias method, Go rule (pkg/pronet/alias.go:10-90): q = d^power (0 for
+// d <= 0), sum 0 -> uniform, leftovers alias = self.
+void alias_go(const double* dist, int64_t n, double power, double* prob, int64_t* alias);
+
+// Go-semantics tables (pkg/pronet/pronet.go:191-249): VertexAT = alias_go(out,
+// 1.0), NegativeAT = alias_go(in+out, 0.75) written into vprob/valias/vtab and
+// nprob/nalias/ntab; tcum = per-vertex sequential prefix sums of the edge
+// weights (TargetSample's CDF scan, pronet.go:257-284).
+void build_go_tables(HostGraph& g, std::vector<double>& tcum);
+
 // {prob, alias} -> {ceil(prob * 2^32), alias}; always-accept entries store
 // {0xFFFFFFFF, self}; alias -1 -> self.  self_ids == nullptr: self = index.
 void alias_encode(const double* prob, const int64_t* alias, int64_t n, const int32_t* self_ids,
@@ -44,6 +55,10 @@ void alias_encode(const double* prob, const int64_t* alias, int64_t n, const int
 // an id out of range.
 bool build_graph(int64_t V, int64_t E, const int32_t* src, const int32_t* dst, const double* w,
                  int vertex_method, int negative_method, HostGraph& g, std::string& err);
+
+// (Re)build the C++-rule vertex and negative tables from the degrees and the
+// stored methods (src/proNet.cpp:457-510).
+void build_cpp_vn_tables(HostGraph& g);
 
 // Text edge list(s) -> names + directed slots (src/proNet.cpp:115-236).
 bool read_edgelist(const std::string& path, bool undirected, std::vector<std::string>& names,

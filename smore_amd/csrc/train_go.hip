@@ -1,0 +1,411 @@
+// train_go.hip -- Go-semantics kernels, the rules of
+// pkg/pronet/{pronet,alias,optimizer}.go and internal/models/{line,bpr,deepwalk}:
+//   * draws: aliasSample takes the index first (alias.go:99-100); TargetSample
+//     is a CDF scan over the raw weights (pronet.go:257-284), done here as a
+//     binary search over the same sequential fp64 prefix sums;
+//   * UpdatePair (optimizer.go:21-58): negatives equal to the positive are
+//     skipped (not redrawn), negatives update C_n immediately, the positive
+//     context's gradient and W_v's are applied at the end;
+//   * LINE order 1: updateFirstOrder (internal/models/line/line.go:153-200);
+//   * BPR: UpdateBPRPair with W (users) and C (items), lambda (optimizer.go:87-117);
+//   * DeepWalk: walks stop at a dead end, fixed window (pronet.go:292-333).
+// fp32 arithmetic without fused multiply-adds (amd64 Go does not fuse); the
+// oracle's orc_go_*_f32 is the bit-exact spec.  Same lane layout as
+// edge_kernels.h.
+#include "edge_kernels.h"
+
+namespace smore {
+
+__device__ __forceinline__ int32_t go_alias(const uint2* tab, uint32_t n, uint32_t ki, uint32_t kp) {
+    const uint32_t i = draw_index(ki, n);
+    const uint2 e = tab[i];
+    return kp < e.x ? (int32_t)i : (int32_t)e.y;
+}
+
+__device__ __forceinline__ int32_t go_target(const DevGraph& g, const double* tcum, int32_t v, uint32_t kr) {
+    const int64_t off = g.offsets[v];
+    const int64_t br = g.offsets[v + 1] - off;
+    if (br == 0) return -1;
+    const double r = ldexp((double)kr, -32) * tcum[off + br - 1];
+    int64_t lo = 0, hi = br - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (r <= tcum[off + mid]) hi = mid;
+        else lo = mid + 1;
+    }
+    return g.targets[off + lo];
+}
+
+template <int G, int M>
+__device__ __forceinline__ void load_row(float (&r)[M], const float* T, int64_t row, int dpad, int lane,
+                                         const bool (&ev)[M]) {
+    const float* p = T + row * dpad + lane;
+#pragma unroll
+    for (int m = 0; m < M; ++m) r[m] = ev[m] ? p[m * G] : 0.0f;
+}
+
+// scatter of a row: plain store of `val`, or atomic add of `delta`
+template <int G, int M, int MODE>
+__device__ __forceinline__ void put_row(float* T, int64_t row, int dpad, int lane, const bool (&ev)[M],
+                                        const float (&val)[M], const float (&delta)[M]) {
+    float* p = T + row * dpad + lane;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        if (!ev[m]) continue;
+        if constexpr (MODE == MODE_ATOMIC) unsafeAtomicAdd(p + m * G, delta[m]);
+        else p[m * G] = val[m];
+    }
+}
+
+template <int G, int M>
+__device__ __forceinline__ float dotg(const float (&a)[M], const float (&b)[M]) {
+    float p = 0.0f;
+#pragma unroll
+    for (int m = 0; m < M; ++m) p = __builtin_fmaf(a[m], b[m], p);
+    return group_sum<G>(p);
+}
+
+// Go UpdatePair on W (vertex) and C (context); negs[] already drawn.
+template <int G, int M, int KMAX, int MODE>
+__device__ __forceinline__ void go_update_pair(const EdgeArgs& a, const float* s_sig, int lane, const bool (&ev)[M],
+                                               int32_t v, int32_t c, const int32_t (&negs)[KMAX], float alpha) {
+    const int dpad = a.dpad;
+    float wv[M], cc[M], vg[M], cg[M];
+    load_row<G, M>(wv, a.W, v, dpad, lane, ev);
+    load_row<G, M>(cc, a.C, c, dpad, lane, ev);
+    float rows[KMAX][M];
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+        const bool use = negs[j] >= 0 && negs[j] != c;
+        const float* p = a.C + (int64_t)(use ? negs[j] : 0) * dpad + lane;
+#pragma unroll
+        for (int m = 0; m < M; ++m) rows[j][m] = (use && ev[m]) ? p[m * G] : 0.0f;
+    }
+#pragma unroll
+    for (int j = 1; j < KMAX; ++j)
+#pragma unroll
+        for (int j2 = 0; j2 < j; ++j2)
+            if (negs[j2] == negs[j]) {
+#pragma unroll
+                for (int m = 0; m < M; ++m) rows[j][m] = rows[j2][m];
+            }
+    {
+        const float grad = alpha * (1.0f - fast_sigmoid(dotg<G, M>(wv, cc), s_sig));
+#pragma unroll
+        for (int m = 0; m < M; ++m) { vg[m] = grad * cc[m]; cg[m] = grad * wv[m]; }
+    }
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+        if (negs[j] < 0 || negs[j] == c) continue;
+        const float gr = alpha * (0.0f - fast_sigmoid(dotg<G, M>(wv, rows[j]), s_sig));
+        float nk[M], dk[M];
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            dk[m] = gr * wv[m];
+            vg[m] = vg[m] + gr * rows[j][m];
+            nk[m] = rows[j][m] + dk[m];
+        }
+#pragma unroll
+        for (int j2 = j + 1; j2 < KMAX; ++j2)
+            if (negs[j2] == negs[j]) {
+#pragma unroll
+                for (int m = 0; m < M; ++m) rows[j2][m] = nk[m];
+            }
+        bool last = true;
+#pragma unroll
+        for (int j2 = j + 1; j2 < KMAX; ++j2) last = last && negs[j2] != negs[j];
+        if (MODE == MODE_ATOMIC || last) put_row<G, M, MODE>(a.C, negs[j], dpad, lane, ev, nk, dk);
+    }
+    float nw[M], nc[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) { nw[m] = wv[m] + vg[m]; nc[m] = cc[m] + cg[m]; }
+    put_row<G, M, MODE>(a.W, v, dpad, lane, ev, nw, vg);
+    put_row<G, M, MODE>(a.C, c, dpad, lane, ev, nc, cg);
+}
+
+// Go updateFirstOrder on one table W (source s, target t).
+template <int G, int M, int KMAX, int MODE>
+__device__ __forceinline__ void go_first_order(const EdgeArgs& a, const float* s_sig, int lane, const bool (&ev)[M],
+                                               int32_t s, int32_t t, const int32_t (&negs)[KMAX], float alpha) {
+    const int dpad = a.dpad;
+    float ws[M], wt[M], vg[M], cg[M];
+    load_row<G, M>(ws, a.W, s, dpad, lane, ev);
+    load_row<G, M>(wt, a.W, t, dpad, lane, ev);
+    float rows[KMAX][M];
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+        const bool use = negs[j] >= 0 && negs[j] != s && negs[j] != t;
+        const float* p = a.W + (int64_t)(use ? negs[j] : 0) * dpad + lane;
+#pragma unroll
+        for (int m = 0; m < M; ++m) rows[j][m] = (use && ev[m]) ? p[m * G] : 0.0f;
+    }
+#pragma unroll
+    for (int j = 1; j < KMAX; ++j)
+#pragma unroll
+        for (int j2 = 0; j2 < j; ++j2)
+            if (negs[j2] == negs[j]) {
+#pragma unroll
+                for (int m = 0; m < M; ++m) rows[j][m] = rows[j2][m];
+            }
+    {
+        const float grad = alpha * (1.0f - fast_sigmoid(dotg<G, M>(ws, wt), s_sig));
+#pragma unroll
+        for (int m = 0; m < M; ++m) { vg[m] = grad * wt[m]; cg[m] = grad * ws[m]; }
+    }
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+        if (negs[j] < 0 || negs[j] == s || negs[j] == t) continue;
+        const float gr = alpha * (0.0f - fast_sigmoid(dotg<G, M>(ws, rows[j]), s_sig));
+        float nk[M], dk[M];
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            vg[m] = vg[m] + gr * rows[j][m];
+            dk[m] = gr * ws[m];
+            nk[m] = rows[j][m] + dk[m];
+        }
+#pragma unroll
+        for (int j2 = j + 1; j2 < KMAX; ++j2)
+            if (negs[j2] == negs[j]) {
+#pragma unroll
+                for (int m = 0; m < M; ++m) rows[j2][m] = nk[m];
+            }
+        bool last = true;
+#pragma unroll
+        for (int j2 = j + 1; j2 < KMAX; ++j2) last = last && negs[j2] != negs[j];
+        if (MODE == MODE_ATOMIC || last) put_row<G, M, MODE>(a.W, negs[j], dpad, lane, ev, nk, dk);
+    }
+    float ns[M], nt[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) ns[m] = ws[m] + vg[m];
+    if (s == t) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) nt[m] = ns[m] + cg[m];
+        float d2[M];
+#pragma unroll
+        for (int m = 0; m < M; ++m) d2[m] = vg[m] + cg[m];
+        put_row<G, M, MODE>(a.W, s, dpad, lane, ev, nt, d2);
+    } else {
+#pragma unroll
+        for (int m = 0; m < M; ++m) nt[m] = wt[m] + cg[m];
+        put_row<G, M, MODE>(a.W, s, dpad, lane, ev, ns, vg);
+        put_row<G, M, MODE>(a.W, t, dpad, lane, ev, nt, cg);
+    }
+}
+
+// Go UpdateBPRPair: W users (u), C items (i, j).
+template <int G, int M, int MODE>
+__device__ __forceinline__ void go_bpr(const EdgeArgs& a, const float* s_sig, int lane, const bool (&ev)[M], int32_t u,
+                                       int32_t i, int32_t j, float alpha) {
+    const int dpad = a.dpad;
+    float wu[M], ci[M], cj[M];
+    load_row<G, M>(wu, a.W, u, dpad, lane, ev);
+    load_row<G, M>(ci, a.C, i, dpad, lane, ev);
+    load_row<G, M>(cj, a.C, j, dpad, lane, ev);
+    if (i == j) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) cj[m] = ci[m];
+    }
+    const float pos = dotg<G, M>(wu, ci), neg = dotg<G, M>(wu, cj);
+    const float gc = alpha * fast_sigmoid(neg - pos, s_sig);
+    const float la = a.reg * alpha;
+    float nu[M], ni[M], nj[M], du[M], di[M], dj[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        const float vgr = gc * (ci[m] - cj[m]);
+        const float pg = gc * wu[m];
+        const float ngr = -gc * wu[m];
+        nu[m] = wu[m] + (vgr - la * wu[m]);
+        ni[m] = ci[m] + (pg - la * ci[m]);
+        nj[m] = (i == j ? ni[m] : cj[m]) + (ngr - la * (i == j ? ni[m] : cj[m]));
+        du[m] = nu[m] - wu[m];
+        di[m] = ni[m] - ci[m];
+        dj[m] = nj[m] - (i == j ? ni[m] : cj[m]);
+    }
+    put_row<G, M, MODE>(a.W, u, dpad, lane, ev, nu, du);
+    if (i == j) {
+        float dd[M];
+#pragma unroll
+        for (int m = 0; m < M; ++m) dd[m] = nj[m] - ci[m];
+        put_row<G, M, MODE>(a.C, i, dpad, lane, ev, nj, dd);
+    } else {
+        put_row<G, M, MODE>(a.C, i, dpad, lane, ev, ni, di);
+        put_row<G, M, MODE>(a.C, j, dpad, lane, ev, nj, dj);
+    }
+}
+
+template <int G, int M, int KMAX, int MODE>
+__global__ void __launch_bounds__(256) go_edge_kernel(EdgeArgs a) {
+    __shared__ float s_sig[1001];
+    for (int i = threadIdx.x; i < 1001; i += blockDim.x) s_sig[i] = a.sig[i];
+    __syncthreads();
+    constexpr int NSLOT = 3 + 2 * KMAX;
+    const int lane = threadIdx.x & (G - 1);
+    uint64_t group = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+    uint64_t ngroups = ((uint64_t)gridDim.x * blockDim.x) / G;
+    if (a.mode == 2) {
+        if (group != 0) return;
+        ngroups = 1;
+    }
+    bool ev[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) ev[m] = lane + G * m < a.dpad;
+    const int nk = a.model == 3 ? 1 : a.K;
+    for (uint64_t t = group; t < a.count; t += ngroups) {
+        const uint64_t s = a.begin + t;
+        SampleWords<G, NSLOT> wd;
+        wd.draw(a.seed, 0, s, lane);
+        const int32_t v = go_alias(a.g.vtab, a.g.V, wd.w[0], wd.w[1]);
+        const int32_t c = go_target(a.g, a.tcum, v, wd.w[2]);
+        if (c < 0) {
+            if (lane == 0) atomicAdd(a.skipped, 1ull);
+            continue;
+        }
+        int32_t negs[KMAX];
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j)
+            negs[j] = j < nk ? go_alias(a.g.ntab, a.g.V, wd.w[3 + 2 * j], wd.w[4 + 2 * j]) : -1;
+        const float alpha = alpha_walk(s, a.alpha0, a.total);
+        if (a.model == 0) go_update_pair<G, M, KMAX, MODE>(a, s_sig, lane, ev, v, c, negs, alpha);
+        else if (a.model == 1) go_first_order<G, M, KMAX, MODE>(a, s_sig, lane, ev, v, c, negs, alpha);
+        else go_bpr<G, M, MODE>(a, s_sig, lane, ev, v, c, negs[0], alpha);
+    }
+}
+
+// Go RandomWalk: stops at a dead end; step s draws slot s (stream 1).
+__global__ void go_walk_gen_kernel(DevGraph g, const double* tcum, WalkArgs w, uint64_t seed) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= w.nwalks) return;
+    const uint64_t unit = w.walk_begin + t;
+    int32_t* out = w.walks + t * (uint64_t)(w.steps + 1);
+    int L = 0;
+    int32_t cur = (int32_t)w.order[unit];
+    out[L++] = cur;
+    uint4 b = make_uint4(0, 0, 0, 0);
+    for (int s = 0; s < w.steps; ++s) {
+        if (g.offsets[cur + 1] - g.offsets[cur] == 0) break;
+        if ((s & 3) == 0) b = philox_block(seed, 1, unit, (uint32_t)s >> 2);
+        cur = go_target(g, tcum, cur, comp(b, s & 3));
+        out[L++] = cur;
+    }
+    w.lens[t] = L;
+}
+
+// Go SkipGrams (fixed window) + Go UpdatePair per pair; negatives from slot L-1.
+template <int G, int M, int KMAX, int MODE>
+__global__ void __launch_bounds__(256) go_walk_pairs_kernel(EdgeArgs a, WalkArgs w) {
+    __shared__ float s_sig[1001];
+    for (int i = threadIdx.x; i < 1001; i += blockDim.x) s_sig[i] = a.sig[i];
+    __syncthreads();
+    const int lane = threadIdx.x & (G - 1);
+    uint64_t group = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+    uint64_t ngroups = ((uint64_t)gridDim.x * blockDim.x) / G;
+    if (a.mode == 2) {
+        if (group != 0) return;
+        ngroups = 1;
+    }
+    bool ev[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) ev[m] = lane + G * m < a.dpad;
+    const int stride = w.steps + 1;
+    for (uint64_t t = group; t < w.nwalks; t += ngroups) {
+        const uint64_t unit = w.walk_begin + t;
+        const int32_t* walk = w.walks + t * stride;
+        const int L = w.lens[t];
+        const float alpha = alpha_walk(unit, a.alpha0, w.total_walks);
+        uint32_t slot = (uint32_t)(L - 1);
+        for (int i = 0; i < L; ++i) {
+            const int lo = i - w.window < 0 ? 0 : i - w.window;
+            const int hi = i + w.window + 1 > L ? L : i + w.window + 1;
+            for (int j = lo; j < hi; ++j) {
+                if (j == i) continue;
+                SlotWords<G, 2 * KMAX> nw;
+                nw.draw(a.seed, 1, unit, slot, lane);
+                int32_t negs[KMAX];
+#pragma unroll
+                for (int n = 0; n < KMAX; ++n)
+                    negs[n] = n < a.K ? go_alias(a.g.ntab, a.g.V, nw.w[2 * n], nw.w[2 * n + 1]) : -1;
+                slot += 2 * a.K;
+                go_update_pair<G, M, KMAX, MODE>(a, s_sig, lane, ev, walk[i], walk[j], negs, alpha);
+            }
+        }
+    }
+}
+
+// draws only (parity tests): {v, c, n1..nK} per sample, Go slot layout
+__global__ void go_sample_kernel(DevGraph g, const double* tcum, uint64_t seed, uint64_t begin, uint64_t count, int K,
+                                 int32_t* out) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= count) return;
+    const uint64_t s = begin + t;
+    int32_t* o = out + t * (2 + K);
+    uint4 b = philox_block(seed, 0, s, 0);
+    uint32_t cur = 0;
+    auto word = [&](uint32_t j) -> uint32_t {
+        if ((j >> 2) != cur) { cur = j >> 2; b = philox_block(seed, 0, s, cur); }
+        return comp(b, (int)(j & 3));
+    };
+    const uint32_t w0 = word(0), w1 = word(1);
+    const int32_t v = go_alias(g.vtab, g.V, w0, w1);
+    o[0] = v;
+    o[1] = go_target(g, tcum, v, word(2));
+    for (int j = 0; j < K; ++j) {
+        const uint32_t ki = word(3 + 2 * j), kp = word(4 + 2 * j);
+        o[2 + j] = go_alias(g.ntab, g.V, ki, kp);
+    }
+}
+
+hipError_t launch_go_sample(const DevGraph& g, const double* tcum, uint64_t seed, uint64_t begin, uint64_t count,
+                            int K, int32_t* out, hipStream_t st) {
+    const int block = 256;
+    hipLaunchKernelGGL(go_sample_kernel, dim3((unsigned)((count + block - 1) / block)), dim3(block), 0, st, g, tcum,
+                       seed, begin, count, K, out);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ dispatch
+template <int G, int M, int KMAX>
+static hipError_t go_edge(const EdgeArgs& a, int grid, hipStream_t st) {
+    if (a.mode == 1) hipLaunchKernelGGL((go_edge_kernel<G, M, KMAX, MODE_ATOMIC>), dim3(grid), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((go_edge_kernel<G, M, KMAX, MODE_STORE>), dim3(grid), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+template <int G, int M, int KMAX>
+static hipError_t go_pairs(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st) {
+    if (a.mode == 1)
+        hipLaunchKernelGGL((go_walk_pairs_kernel<G, M, KMAX, MODE_ATOMIC>), dim3(grid), dim3(256), 0, st, a, w);
+    else
+        hipLaunchKernelGGL((go_walk_pairs_kernel<G, M, KMAX, MODE_STORE>), dim3(grid), dim3(256), 0, st, a, w);
+    return hipGetLastError();
+}
+
+hipError_t launch_go_edge(const EdgeArgs& a, int grid, hipStream_t st) {
+    const int G = lanes_of(a.dpad), M = (a.dpad + G - 1) / G;
+#define X(g, m)                                                  \
+    if (G == g && M == m) {                                      \
+        if (a.K <= 5 || a.model == 3) return go_edge<g, m, 5>(a, grid, st); \
+        return go_edge<g, m, 10>(a, grid, st);                   \
+    }
+    SMORE_FOR_EACH_GM(X)
+#undef X
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_go_walk(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st) {
+    const int block = 256;
+    hipLaunchKernelGGL(go_walk_gen_kernel, dim3((unsigned)((w.nwalks + block - 1) / block)), dim3(block), 0, st, a.g,
+                       a.tcum, w, a.seed);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int G = lanes_of(a.dpad), M = (a.dpad + G - 1) / G;
+#define X(g, m)                                                  \
+    if (G == g && M == m) {                                      \
+        if (a.K <= 5) return go_pairs<g, m, 5>(a, w, grid, st);  \
+        return go_pairs<g, m, 10>(a, w, grid, st);               \
+    }
+    SMORE_FOR_EACH_GM(X)
+#undef X
+    return hipErrorInvalidValue;
+}
+
+}  // namespace smore

@@ -14,6 +14,7 @@ struct EdgeArgs {
     unsigned long long* skipped;   // samples whose source had no out-edge
     const uint32_t* hotW;          // hybrid mode: 1 bit per row, atomic scatter if set
     const uint32_t* hotC;          //   (hotC == hotW for shared-table models)
+    const double* tcum;            // Go semantics: per-vertex prefix sums of edge weights
     uint64_t begin, count, total, seed;
     double alpha0;
     float reg;
@@ -30,6 +31,10 @@ struct WalkArgs {
 };
 
 int lanes_of(int dpad);
+hipError_t launch_go_edge(const EdgeArgs& a, int grid, hipStream_t st);
+hipError_t launch_go_walk(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st);
+hipError_t launch_go_sample(const DevGraph& g, const double* tcum, uint64_t seed, uint64_t begin, uint64_t count,
+                            int K, int32_t* out, hipStream_t st);
 hipError_t launch_walk_gen(const DevGraph& g, const WalkArgs& w, uint64_t seed, hipStream_t st);
 hipError_t launch_walk_pairs(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st);
 const void* walk_pairs_symbol(const EdgeArgs& a);

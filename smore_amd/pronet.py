@@ -123,8 +123,10 @@ class ProNet:
 
     # ---------------------------------------------------------------- samplers
     def sample_edges(self, model, begin, count, K, seed):
-        """Draws of samples [begin, begin+count): rows {v, c, n1..nK} (BPR: {u, i, j0..j4})."""
-        width = 7 if model == "bpr" else 2 + K
+        """Draws of samples [begin, begin+count): rows {v, c, n1..nK} (BPR: {u, i, j0..j4};
+        Go semantics BPR: {u, i, j})."""
+        go = getattr(self, "semantics", "cpp") == "go"
+        width = (3 if go else 7) if model == "bpr" else 2 + K
         out = np.zeros((count, width), np.int32)
         self._chk(lib.smore_sample_edges(self.ctx, _lib.MODEL[model], begin, count, K, seed, ptr(out)),
                   "sample_edges")
@@ -175,6 +177,11 @@ class ProNet:
         self._chk(lib.smore_train_deepwalk(self.ctx, int(walk_begin), int(walk_end), int(walk_times),
                                            int(walk_steps), int(window), int(K), float(alpha0), int(seed),
                                            ptr(order), _lib.MODE[mode]), "train_deepwalk")
+
+    def set_semantics(self, semantics):
+        """"cpp" (src/proNet.cpp rules, default) or "go" (pkg/pronet rules)."""
+        self._chk(lib.smore_set_semantics(self.ctx, _lib.SEM[semantics]), "set_semantics")
+        self.semantics = semantics
 
     def set_hot_threshold(self, tau):
         self._chk(lib.smore_set_hot_threshold(self.ctx, float(tau)), "set_hot_threshold")

@@ -132,3 +132,27 @@ def test_host_only_context_has_no_gpu_state():
     pn.LoadEdgeList(os.path.join(GOLDEN, "toy.txt"), 1)
     with pytest.raises(_lib.SmoreError):
         pn.alloc_tables(8, 2)
+
+
+@pytest.mark.parametrize("fname,und", [("pl1k.txt", 1), ("bip.txt", 0)])
+def test_go_semantics_tables_match_oracle(fname, und):
+    """smore_set_semantics(GO) rebuilds VertexAT (power 1) / NegativeAT (power
+    0.75, Go alias rule); switching back restores the C++ tables."""
+    from oracle import oracle as orc
+    from smore_amd import ProNet
+    from smore_amd import _lib
+    path = os.path.join(GOLDEN, fname)
+    gg = orc.GoGraph.from_file(path, und)
+    gc = orc.Graph.from_file(path, und)
+    pn = ProNet(device=-1)
+    pn.LoadEdgeList(path, und)
+    pn.set_semantics("go")
+    for which, t, a in ((_lib.AT_VERTEX, gg.vthr, gg.valias_enc), (_lib.AT_NEGATIVE, gg.nthr, gg.nalias_enc)):
+        tt, aa = pn.alias_encoded(which)
+        np.testing.assert_array_equal(tt, t)
+        np.testing.assert_array_equal(aa, a)
+    pn.set_semantics("cpp")
+    for which, t, a in ((_lib.AT_VERTEX, gc.vthr, gc.valias_enc), (_lib.AT_NEGATIVE, gc.nthr, gc.nalias_enc)):
+        tt, aa = pn.alias_encoded(which)
+        np.testing.assert_array_equal(tt, t)
+        np.testing.assert_array_equal(aa, a)

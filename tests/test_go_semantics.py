@@ -1,0 +1,100 @@
+"""Go-semantics mode of the oracle, pinned against an
+independent line-by-line Python restatement of the Go source
+(tests/go_semantics_ref.py).  CPU only; no Go toolchain exists here, so this
+mode's parity is "pinned by restatement" (DESIGN.md 6)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from tests import go_semantics_ref as ref
+from tests.conftest import GOLDEN
+
+SEED = 4242
+
+
+def graphs(name, und):
+    names, s, d, w = orc.read_edgelist(os.path.join(GOLDEN, name), und)
+    return orc.GoGraph(len(names), s, d, w, names), ref.ProNet(names, s, d, w)
+
+
+@pytest.mark.parametrize("dist,power", [([3.0, 1.0, 0.0, 2.0, 2.0], 1.0), ([0.0] * 4, 0.75), ([5.0], 1.0),
+                                        (list(np.random.default_rng(1).random(200) * 7), 0.75)])
+def test_go_alias_rule(dist, power):
+    p, a = orc.alias_go(dist, power)
+    rp, ra = ref.build_alias(dist, power)
+    np.testing.assert_array_equal(p, rp)
+    np.testing.assert_array_equal(a, ra)
+
+
+@pytest.mark.parametrize("name,und", [("pl100w.txt", 1), ("bip.txt", 0)])
+def test_go_draws(name, und):
+    g, pn = graphs(name, und)
+    got = orc.go_sample(g, SEED, 17, 3000, 4)
+    for t in range(3000):
+        rng = ref.Rng(SEED, 0, 17 + t, 11)
+        v = pn.source(rng)
+        c = pn.target(v, rng)
+        negs = [pn.negative(rng) for _ in range(4)]
+        assert list(got[t]) == [v, c] + negs, t
+
+
+def _tables(V, dim, seed):
+    rng = np.random.default_rng(seed)
+    return rng.random((V, dim)) - 0.5, rng.random((V, dim)) - 0.5
+
+
+@pytest.mark.parametrize("model,name,und", [("line2", "pl100w.txt", 1), ("line1", "pl100w.txt", 1),
+                                            ("bpr", "bip.txt", 0)])
+def test_go_train_f64_equals_restatement(model, name, und):
+    g, pn = graphs(name, und)
+    W0, C0 = _tables(g.V, 8, 3)
+    W, Cc = W0.copy(), C0.copy()
+    total = 50000
+    orc.go_train_f64(g, model, W, Cc, 5, 0.05, 0.001, total, 9990, 10990, SEED)   # crosses an alpha step
+    Wl, Cl = [list(r) for r in W0], [list(r) for r in C0]
+    ref.train(pn, model, Wl, Cl, 5, 0.05, 0.001, total, 9990, 10990, SEED)
+    np.testing.assert_array_equal(W, np.array(Wl))
+    np.testing.assert_array_equal(Cc, np.array(Cl))
+
+
+def test_go_deepwalk_f64_equals_restatement():
+    g, pn = graphs("pl100w.txt", 1)
+    W0, C0 = _tables(g.V, 8, 4)
+    order = orc.deepwalk_order(g.V, 1, 0)
+    W, Cc = W0.copy(), C0.copy()
+    orc.go_deepwalk_f64(g, W, Cc, 1, 6, 2, 3, 0.025, SEED, order)
+    Wl, Cl = [list(r) for r in W0], [list(r) for r in C0]
+    ref.deepwalk(pn, Wl, Cl, 1, 6, 2, 3, 0.025, SEED, order)
+    np.testing.assert_array_equal(W, np.array(Wl))
+    np.testing.assert_array_equal(Cc, np.array(Cl))
+
+
+@pytest.mark.parametrize("model,name,und", [("line2", "pl100w.txt", 1), ("line1", "pl100w.txt", 1),
+                                            ("bpr", "bip.txt", 0)])
+def test_go_fp32_spec_close_to_fp64(model, name, und):
+    g, _ = graphs(name, und)
+    W0, C0 = _tables(g.V, 16, 5)
+    for s in (3, 77, 12345):                        # one sample: 1e-5 (north-star criterion)
+        W, Cc = W0.copy(), C0.copy()
+        orc.go_train_f64(g, model, W, Cc, 5, 0.025, 0.001, 10 ** 6, s, s + 1, SEED)
+        W32, C32 = W0.astype(np.float32), C0.astype(np.float32)
+        orc.go_train_f32(g, model, W32, C32, 16, 5, 0.025, 0.001, 10 ** 6, s, s + 1, SEED)
+        np.testing.assert_allclose(W32, W, atol=1e-5, rtol=0)
+        np.testing.assert_allclose(C32, Cc, atol=1e-5, rtol=0)
+
+
+def test_go_semantics_differ_from_cpp():
+    """The Go rule really is different: skip-not-redraw duplicates, deferred
+    positive context, power-1 source sampling."""
+    g, _ = graphs("pl100w.txt", 1)
+    gc = orc.Graph.from_file(os.path.join(GOLDEN, "pl100w.txt"), 1)
+    assert not np.array_equal(g.vprob, gc.vprob)           # out_deg^1 vs ^0.75
+    np.testing.assert_array_equal(g.offsets, gc.offsets)
+    W0, C0 = _tables(g.V, 8, 6)
+    a, b = W0.copy(), C0.copy()
+    orc.go_train_f64(g, "line2", a, b, 5, 0.025, 0.0, 10 ** 6, 0, 2000, SEED)
+    c, d = W0.copy(), C0.copy()
+    orc.train_edge_f64(gc, "line2", c, d, 5, 0.025, 0.0, 10 ** 6, 0, 2000, SEED)
+    assert not np.allclose(a, c)

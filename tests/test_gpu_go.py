@@ -1,0 +1,190 @@
+"""Go-semantics mode (pkg/pronet + internal/models
+rules) of the HIP path against the oracle's orc_go_* functions, themselves
+pinned against an independent restatement of the Go source
+(tests/test_go_semantics.py).  Needs an MI355X.
+
+Tolerances: draws and serial mode bit-exact; one atomic sample 1e-6; a
+serial run vs the fp64 oracle 2e-3 max / 2e-4 median (as the C++ path)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from tests.conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+SEED = 777001
+
+
+@pytest.fixture(scope="module")
+def smore():
+    import smore_amd
+    return smore_amd
+
+
+def pair(smore, fname, und):
+    path = os.path.join(GOLDEN, fname)
+    g = orc.GoGraph.from_file(path, und)
+    pn = smore.ProNet(0)
+    pn.LoadEdgeList(path, und)
+    pn.set_semantics("go")
+    return g, pn
+
+
+def tables(V, dim, seed):
+    rng = np.random.default_rng(seed)
+    return [(rng.random((V, dim), dtype=np.float32) - 0.5) for _ in range(2)]
+
+
+def padded(T, dim):
+    out = np.zeros((T.shape[0], (dim + 3) // 4 * 4), np.float32)
+    out[:, :dim] = T
+    return out
+
+
+@pytest.mark.parametrize("fname,und,model,K", [("pl100w.txt", 1, "line2", 5), ("pl1k.txt", 1, "line2", 10),
+                                               ("toy.txt", 0, "line2", 3), ("bip.txt", 0, "bpr", 1)])
+def test_go_draws_bit_exact(smore, fname, und, model, K):
+    g, pn = pair(smore, fname, und)
+    got = pn.sample_edges(model, 31, 50000, K, SEED)
+    np.testing.assert_array_equal(got, orc.go_sample(g, SEED, 31, 50000, K))
+
+
+@pytest.mark.parametrize("model,dim,K", [("line2", 8, 5), ("line2", 64, 5), ("line2", 300, 10), ("line2", 128, 7),
+                                         ("line1", 20, 5), ("line1", 64, 10), ("bpr", 16, 1), ("bpr", 128, 1)])
+def test_go_serial_bit_exact_vs_oracle(smore, model, dim, K):
+    fname, und = ("bip.txt", 0) if model == "bpr" else ("pl100w.txt", 1)
+    g, pn = pair(smore, fname, und)
+    W0, C0 = tables(g.V, dim, dim + K)
+    ntab = 1 if model == "line1" else 2
+    pn.alloc_tables(dim, ntab)
+    pn.set_table(0, W0)
+    if ntab == 2:
+        pn.set_table(1, C0)
+    lam = 0.01 if model == "bpr" else 0.0
+    total, begin, n = 10 ** 6, 9000, 20000                  # crosses an alpha step
+    pn.train_edges(model, begin, n, total, K, 0.025, lam, SEED, "serial")
+    W, C = padded(W0, dim), padded(C0, dim)
+    orc.go_train_f32(g, model, W, C, dim, K, 0.025, lam, total, begin, begin + n, SEED)
+    np.testing.assert_array_equal(pn.get_table(0), W[:, :dim])
+    if ntab == 2:
+        np.testing.assert_array_equal(pn.get_table(1), C[:, :dim])
+
+
+def test_go_serial_skips_dead_ends(smore):
+    g, pn = pair(smore, "toy.txt", 0)
+    W0, C0 = tables(g.V, 8, 3)
+    pn.alloc_tables(8, 2)
+    pn.set_table(0, W0)
+    pn.set_table(1, C0)
+    pn.train_edges("line2", 0, 30000, 50000, 2, 0.025, 0.0, SEED, "serial")
+    W, C = padded(W0, 8), padded(C0, 8)
+    orc.go_train_f32(g, "line2", W, C, 8, 2, 0.025, 0.0, 50000, 0, 30000, SEED)
+    np.testing.assert_array_equal(pn.get_table(0), W)
+    np.testing.assert_array_equal(pn.get_table(1), C)
+
+
+@pytest.mark.parametrize("dim,K,window,steps", [(16, 5, 2, 10), (64, 5, 5, 40), (100, 10, 3, 20)])
+def test_go_deepwalk_serial_bit_exact(smore, dim, K, window, steps):
+    g, pn = pair(smore, "pl100w.txt", 1)
+    W0, C0 = tables(g.V, dim, dim)
+    pn.alloc_tables(dim, 2)
+    pn.set_table(0, W0)
+    pn.set_table(1, C0)
+    order = orc.deepwalk_order(g.V, 2, 5)
+    pn.train_deepwalk(0, 2 * g.V, 2, steps, window, K, 0.025, SEED, order, "serial")
+    W, C = padded(W0, dim), padded(C0, dim)
+    orc.go_deepwalk_f32(g, W, C, dim, 2, steps, window, K, 0.025, SEED, order)
+    np.testing.assert_array_equal(pn.get_table(0), W[:, :dim])
+    np.testing.assert_array_equal(pn.get_table(1), C[:, :dim])
+
+
+def test_go_deepwalk_directed_dead_ends(smore):
+    g, pn = pair(smore, "toy.txt", 0)
+    W0, C0 = tables(g.V, 8, 1)
+    pn.alloc_tables(8, 2)
+    pn.set_table(0, W0)
+    pn.set_table(1, C0)
+    order = orc.deepwalk_order(g.V, 3, 0)
+    pn.train_deepwalk(0, 3 * g.V, 3, 8, 2, 3, 0.025, SEED, order, "serial")
+    W, C = padded(W0, 8), padded(C0, 8)
+    orc.go_deepwalk_f32(g, W, C, 8, 3, 8, 2, 3, 0.025, SEED, order)
+    np.testing.assert_array_equal(pn.get_table(0), W)
+    np.testing.assert_array_equal(pn.get_table(1), C)
+
+
+@pytest.mark.parametrize("model", ["line2", "line1", "bpr"])
+def test_go_atomic_single_sample(smore, model):
+    fname, und = ("bip.txt", 0) if model == "bpr" else ("pl100w.txt", 1)
+    g, pn = pair(smore, fname, und)
+    W0, C0 = tables(g.V, 64, 9)
+    ntab = 1 if model == "line1" else 2
+    pn.alloc_tables(64, ntab)
+    K = 1 if model == "bpr" else 5
+    for s in (5, 99, 12345):
+        pn.set_table(0, W0)
+        if ntab == 2:
+            pn.set_table(1, C0)
+        pn.train_edges(model, s, 1, 10 ** 6, K, 0.025, 0.01, SEED, "atomic")
+        W, C = W0.copy(), C0.copy()
+        orc.go_train_f32(g, model, W, C, 64, K, 0.025, 0.01, 10 ** 6, s, s + 1, SEED)
+        np.testing.assert_allclose(pn.get_table(0), W, atol=1e-6, rtol=0)
+        if ntab == 2:
+            np.testing.assert_allclose(pn.get_table(1), C, atol=1e-6, rtol=0)
+
+
+@pytest.mark.parametrize("model", ["line2", "bpr"])
+def test_go_serial_close_to_fp64(smore, model):
+    """fp32 HIP path vs the fp64 Go rules over 2*10^5 dependent updates."""
+    fname, und = ("bip.txt", 0) if model == "bpr" else ("pl1k.txt", 1)
+    g, pn = pair(smore, fname, und)
+    dim = 32
+    W0, C0 = tables(g.V, dim, 2)
+    W0 *= 0.1
+    C0 *= 0.1
+    pn.alloc_tables(dim, 2)
+    pn.set_table(0, W0)
+    pn.set_table(1, C0)
+    total = 200000
+    K = 1 if model == "bpr" else 5
+    pn.train_edges(model, 0, total, total, K, 0.025, 0.001, SEED, "serial")
+    W, C = W0.astype(np.float64), C0.astype(np.float64)
+    orc.go_train_f64(g, model, W, C, K, 0.025, 0.001, total, 0, total, SEED)
+    for got, want in ((pn.get_table(0), W), (pn.get_table(1), C)):
+        err = np.abs(got - want)
+        assert err.max() < 2e-3 and np.median(err) < 2e-4, (err.max(), np.median(err))
+
+
+def test_go_rejects_mf(smore):
+    g, pn = pair(smore, "bip.txt", 0)
+    pn.alloc_tables(8, 2)
+    with pytest.raises(smore._lib.SmoreError):
+        pn.train_edges("mf", 0, 10, 10, 5, 0.025, 0.0, SEED, "atomic")
+
+
+def test_go_model_drivers(smore, tmp_path):
+    """internal/models/{line,bpr,deepwalk} mirrors: Go totals and Go save format."""
+    from smore_amd import go_models
+    path = os.path.join(GOLDEN, "pl1k.txt")
+    m = go_models.LINE.New()
+    m.LoadEdgeList(path, True)
+    assert m.MaxLine * 2 == m.pnet.MAX_line
+    m.Init(16, go_models.LINE.Second)
+    m.Train(2, 5, 0.025, 4)
+    out = tmp_path / "line.txt"
+    m.SaveWeights(str(out))
+    lines = out.read_text().splitlines()
+    assert len(lines) == m.pnet.MAX_vid + 1
+    assert np.isfinite(m.w_vertex).all() and np.abs(m.w_vertex).max() > 0
+    b = go_models.BPR.New()
+    b.LoadEdgeList(os.path.join(GOLDEN, "bip.txt"), False)
+    b.Init(8)
+    b.Train(3, 0.025, 0.001, 1)
+    assert np.isfinite(b.w_vertex).all()
+    d = go_models.DeepWalk.New()
+    d.LoadEdgeList(path, True)
+    d.Init(8)
+    d.Train(1, 10, 2, 3, 0.025, 1)
+    assert np.isfinite(d.w_context).all()
