@@ -2,13 +2,16 @@
 #   make            -> smore_amd/lib/libsmore_hip.so + smore_amd/bin/{line,bpr,mf,deepwalk}
 #   make oracle     -> oracle/build/liboracle.so (test infrastructure)
 #   make ref        -> oracle/_ref/ref_harness (needs /root/reference)
+#   tuning variants: make lib OBJ=build/obj_x LIB=build/x/libsmore_hip.so EXTRA=-DSMORE_WAVES_HYBRID=5
+#   (load one with SMORE_LIB=build/x/libsmore_hip.so)
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 CXXFLAGS := -std=c++17 -O3 -fPIC -ffp-contract=off -Wall -Wno-unused-function
-HIPFLAGS := $(CXXFLAGS) --offload-arch=$(ARCH) -Wno-pass-failed
+EXTRA    ?=
+HIPFLAGS := $(CXXFLAGS) --offload-arch=$(ARCH) -Wno-pass-failed $(EXTRA)
 SRC      := smore_amd/csrc
-OBJ      := build/obj
-LIB      := smore_amd/lib/libsmore_hip.so
+OBJ      ?= build/obj
+LIB      ?= smore_amd/lib/libsmore_hip.so
 BIN      := smore_amd/bin
 HDRS     := $(wildcard $(SRC)/*.h) include/smore_hip.h
 
@@ -25,11 +28,15 @@ $(OBJ)/capi.o: $(SRC)/capi.cpp $(HDRS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(CXXFLAGS) -c -o $@ $<
 
+$(OBJ)/graphgen.o: $(SRC)/graphgen.cpp $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(CXXFLAGS) -c -o $@ $<
+
 $(OBJ)/%.o: $(SRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-LIB_OBJS := $(OBJ)/host_graph.o $(OBJ)/capi.o $(patsubst $(SRC)/%.hip,$(OBJ)/%.o,$(wildcard $(SRC)/*.hip))
+LIB_OBJS := $(OBJ)/host_graph.o $(OBJ)/capi.o $(OBJ)/graphgen.o $(patsubst $(SRC)/%.hip,$(OBJ)/%.o,$(wildcard $(SRC)/*.hip))
 
 $(LIB): $(LIB_OBJS)
 	@mkdir -p $(dir $@)

@@ -95,9 +95,15 @@ def main():
     from smore_amd import graphgen
     from smore_amd.dist import ReplicaSync
 
+    t_gen = time.perf_counter()
     V, (src, dst, w) = graphgen.config_edges(args.config)
+    t_build = time.perf_counter()
     pn = smore_amd.ProNet(local)
     pn.set_graph_edges(V, src, dst, w)
+    t_ready = time.perf_counter()
+    if rank == 0:
+        print("[bench] %s: generated in %.1f s, graph built + uploaded in %.1f s"
+              % (args.config, t_build - t_gen, t_ready - t_build), file=sys.stderr, flush=True)
     E = pn.MAX_line
     pn.set_hot_threshold(args.hot_tau)
     pn.alloc_tables(args.dim, 2)

@@ -124,6 +124,14 @@ int smore_get_table(const smore_ctx* ctx, int which, float* host, int64_t rows, 
 /* device pointer + padded row stride (floats) of a table, for collectives */
 int smore_table_device(smore_ctx* ctx, int which, void** dptr, int64_t* stride);
 
+/* ---- benchmark inputs (not a reference interface) ------------------- */
+/* Seeded power-law edge list: both endpoints of each of `lines` records ~ Zipf(s)
+ * over V ranks, ranks mapped through a seeded permutation, weight 1.  Undirected:
+ * slots 2l, 2l+1 = (a,b), (b,a) (the loaders' push order); src/dst hold
+ * lines*(undirected ? 2 : 1) ids.  Independent of the host thread count. */
+int smore_gen_powerlaw(int64_t V, int64_t lines, int undirected, double s, uint64_t seed, int32_t* src,
+                       int32_t* dst);
+
 /* semantics of the sampling and update rules (SURVEY.md 8a "C++ vs Go"):
  * SMORE_SEM_CPP (default) = src/proNet.cpp; SMORE_SEM_GO = pkg/pronet +
  * internal/models: source alias out_degree^1, negatives (in+out)^0.75 with the Go

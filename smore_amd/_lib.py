@@ -7,7 +7,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libsmore_hip.so")
+LIB_PATH = os.environ.get("SMORE_LIB") or os.path.join(HERE, "lib", "libsmore_hip.so")   # SMORE_LIB: tuning variants
 
 OK, EINVAL, EHIP, ENOMEM, ESTATE, EIO = range(6)
 VM = {"out_degrees": 0, "no_degrees": 1, "degrees": 2}
@@ -55,6 +55,7 @@ def _load():
         "smore_skipped": (i32, [P, C.POINTER(u64)]),
         "smore_set_hot_threshold": (i32, [P, dbl]),
         "smore_set_semantics": (i32, [P, i32]),
+        "smore_gen_powerlaw": (i32, [i64, i64, i32, dbl, u64, P, P]),
         "smore_hot_rows": (i32, [P, C.POINTER(i64), C.POINTER(i64)]),
         "smore_last_kernel_ms": (C.c_float, [P]),
         "smore_train_deepwalk": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, u64, P, i32]),

@@ -38,8 +38,6 @@ struct smore_ctx {
     float* d_table[2] = {nullptr, nullptr};
     int dim = 0, dpad = 0, ntables = 0;
     // hybrid scatter: hot-row bitmaps (1 bit per row), keyed by what built them
-    uint32_t* d_hotW = nullptr;
-    uint32_t* d_hotC = nullptr;
     double hot_tau = 0.1;
     std::string hot_key;
     int64_t hot_rows[2] = {0, 0};
@@ -175,7 +173,7 @@ void smore_destroy(smore_ctx* c) {
     }
     dfree(c->d_offsets); dfree(c->d_targets); dfree(c->d_vtab); dfree(c->d_ntab); dfree(c->d_ctab);
     dfree(c->d_sig); dfree(c->d_skipped); dfree(c->d_table[0]); dfree(c->d_table[1]);
-    dfree(c->d_hotW); dfree(c->d_hotC);
+
     dfree(c->d_order); dfree(c->d_walks); dfree(c->d_lens); dfree(c->d_tcum);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -386,26 +384,62 @@ int smore_table_device(smore_ctx* c, int which, void** dptr, int64_t* stride) {
 // A row is "hot" when the expected number of resident sample groups touching
 // it at once, M * p(row), exceeds tau; hot rows take float atomics, the rest
 // plain stores (DESIGN.md "Scatter modes").
+// Hybrid scatter: rows whose expected number of concurrent updates M * p(row)
+// exceeds tau are tagged hot in the device graph's id words (device_common.h):
+// W-rows through the vertex table, C-rows through the negative and context
+// tables and the CSR targets (one union set for shared-table models).  Written
+// in place into the existing device arrays; the host graph stays untagged.
 static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
     char key[128];
     snprintf(key, sizeof key, "%d/%d/%lld/%.9g", model, K, (long long)M, c->hot_tau);
     if (c->hot_key == key) return SMORE_OK;
+    if (c->g.V >= ((int64_t)1 << 30)) return fail(c, SMORE_EINVAL, "hybrid scatter needs V < 2^30");
     std::vector<double> ps, pn, pc;
     draw_probabilities(c->g, ps, pn, pc);
-    const int64_t V = c->g.V, words = (V + 31) / 32;
-    std::vector<uint32_t> bw((size_t)words, 0), bc((size_t)words, 0);
+    const int64_t V = c->g.V, E = c->g.E;
+    std::vector<uint8_t> hw((size_t)V, 0), hc((size_t)V, 0);
     const int negs = model == SMORE_BPR ? 5 : K;
     c->hot_rows[0] = c->hot_rows[1] = 0;
     for (int64_t v = 0; v < V; ++v) {
         double pw, pcx;
         if (model == SMORE_LINE2) { pw = ps[v]; pcx = pc[v] + negs * pn[v]; }
         else { pw = pcx = ps[v] + pc[v] + negs * pn[v]; }
-        if ((double)M * pw > c->hot_tau) { bw[v >> 5] |= 1u << (v & 31); c->hot_rows[0]++; }
-        if ((double)M * pcx > c->hot_tau) { bc[v >> 5] |= 1u << (v & 31); c->hot_rows[1]++; }
+        if ((double)M * pw > c->hot_tau) { hw[v] = 1; c->hot_rows[0]++; }
+        if ((double)M * pcx > c->hot_tau) { hc[v] = 1; c->hot_rows[1]++; }
     }
+    const HostGraph& g = c->g;
+    auto tag_tab = [&](const std::vector<AliasEntry>& tab, const std::vector<uint8_t>& hot) {
+        std::vector<AliasEntry> t(tab);
+        for (int64_t i = 0; i < V; ++i) {
+            const uint32_t al = (uint32_t)t[i].alias;
+            t[i].alias = (int32_t)(al | ((uint32_t)hot[al] << 30) | ((uint32_t)hot[i] << 31));
+        }
+        return t;
+    };
     int rc;
-    if ((rc = upload(c, c->d_hotW, bw.data(), bw.size()))) return rc;
-    if ((rc = upload(c, c->d_hotC, bc.data(), bc.size()))) return rc;
+    if ((rc = set_device(c))) return rc;
+    {
+        const std::vector<AliasEntry> vt = tag_tab(g.vtab, hw), nt = tag_tab(g.ntab, hc);
+        HIPCHK(c, hipMemcpy(c->d_vtab, vt.data(), V * sizeof(AliasEntry), hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->d_ntab, nt.data(), V * sizeof(AliasEntry), hipMemcpyHostToDevice));
+    }
+    // targets and context alias words, in slices to bound the host copy
+    const int64_t slice = (int64_t)1 << 26;
+    std::vector<int32_t> tt;
+    std::vector<AliasEntry> ct;
+    for (int64_t b = 0; b < E; b += slice) {
+        const int64_t n = std::min(slice, E - b);
+        tt.resize((size_t)n);
+        ct.resize((size_t)n);
+        for (int64_t i = 0; i < n; ++i) {
+            const int32_t t = g.targets[b + i];
+            tt[i] = t | ((int32_t)hc[t] << 30);
+            const AliasEntry e = g.ctab[b + i];
+            ct[i] = {e.thresh, e.alias | ((int32_t)hc[e.alias] << 30)};
+        }
+        HIPCHK(c, hipMemcpy(c->d_targets + b, tt.data(), n * sizeof(int32_t), hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->d_ctab + b, ct.data(), n * sizeof(AliasEntry), hipMemcpyHostToDevice));
+    }
     c->hot_key = key;
     return SMORE_OK;
 }
@@ -453,7 +487,6 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
     a.K = model == SMORE_BPR ? 5 : K;
     a.model = model;
     a.mode = mode;
-    a.hotW = a.hotC = nullptr;
     a.tcum = c->d_tcum;
     if (c->semantics == SMORE_SEM_GO) {
         if (model == SMORE_MF) return fail(c, SMORE_EINVAL, "Go semantics has no MF model");
@@ -479,8 +512,6 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
     if (mode == SMORE_HYBRID) {
         const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
         if ((rc = build_hot_maps(c, model, a.K, M))) return rc;
-        a.hotW = c->d_hotW;
-        a.hotC = model == SMORE_LINE2 ? c->d_hotC : c->d_hotW;
     }
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     HIPCHK(c, launch_edge_train(a, grid, c->stream));
@@ -647,7 +678,6 @@ int smore_train_deepwalk(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, i
     a.skipped = c->d_skipped;
     a.begin = 0; a.count = 0; a.total = total; a.seed = seed; a.alpha0 = alpha0; a.reg = 0.0f;
     a.dpad = c->dpad; a.K = K; a.model = SMORE_LINE2; a.mode = mode;
-    a.hotW = a.hotC = nullptr;
     a.tcum = c->d_tcum;
     if (c->semantics == SMORE_SEM_GO && mode == SMORE_HYBRID) return fail(c, SMORE_EINVAL, "Go semantics: no hybrid");
     int grid = 1;
@@ -661,8 +691,6 @@ int smore_train_deepwalk(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, i
     if (mode == SMORE_HYBRID) {
         const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
         if ((rc = build_hot_maps(c, SMORE_LINE2, K, M))) return rc;
-        a.hotW = c->d_hotW;
-        a.hotC = c->d_hotC;
     }
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     for (uint64_t b = walk_begin; b < walk_end; b += chunk) {

@@ -31,27 +31,41 @@ __device__ __forceinline__ uint32_t comp(const uint4& b, int c) {
     return c == 0 ? b.x : c == 1 ? b.y : c == 2 ? b.z : b.w;
 }
 
-// Encoded graph in HBM (DESIGN.md "Data layout").
+// Encoded graph in HBM (DESIGN.md "Data layout").  Vertex ids stored in the
+// device graph are TAGGED: bits 0-29 the id, bit 30 = "hot row" (the hybrid
+// scatter adds to it atomically).  vtab/ntab alias words hold alias | tag(alias)
+// << 30 | tag(self) << 31, ctab alias words alias | tag << 30, targets t | tag
+// << 30.  Tags are all zero unless a hybrid run set them (capi build_hot_maps);
+// every kernel splits them off, so stale tags never change a result.
 struct DevGraph {
     const int64_t* offsets;   // V+1
-    const int32_t* targets;   // E
-    const uint2* vtab;        // V   {accept threshold, alias}
+    const int32_t* targets;   // E   tagged target vid
+    const uint2* vtab;        // V   {accept threshold, tagged alias word}
     const uint2* ntab;        // V
-    const uint2* ctab;        // E   alias already a target vid
+    const uint2* ctab;        // E   alias already a (tagged) target vid
     uint32_t V;
 };
+
+constexpr int32_t ID_MASK = 0x3FFFFFFF;
+__device__ __forceinline__ int32_t untag(int32_t t) { return t & ID_MASK; }
+__device__ __forceinline__ bool tag_hot(int32_t t) { return (t >> 30) & 1; }
 
 // index draw floor(k*n/2^32) == interposed random_gen(0, n) truncated.
 __device__ __forceinline__ uint32_t draw_index(uint32_t k, uint32_t n) { return __umulhi(k, n); }
 
-// SourceSample src/proNet.cpp:647-657 (p, then index)
-__device__ __forceinline__ int32_t source_sample(const DevGraph& g, uint32_t kp, uint32_t ki) {
-    const uint32_t i = draw_index(ki, g.V);
-    const uint2 e = g.vtab[i];
-    return kp < e.x ? (int32_t)i : (int32_t)e.y;
+// alias draw on a vtab/ntab entry -> tagged id
+__device__ __forceinline__ int32_t alias_pick(uint32_t i, uint2 e, uint32_t kp) {
+    return kp < e.x ? (int32_t)(i | ((e.y >> 31) << 30)) : (int32_t)(e.y & 0x7FFFFFFFu);
 }
 
-// TargetSample(vid) src/proNet.cpp:671-683 (branch 0 -> -1; p, then index)
+// SourceSample src/proNet.cpp:647-657 (p, then index); tagged id
+__device__ __forceinline__ int32_t source_sample(const DevGraph& g, uint32_t kp, uint32_t ki) {
+    const uint32_t i = draw_index(ki, g.V);
+    return alias_pick(i, g.vtab[i], kp);
+}
+
+// TargetSample(vid) src/proNet.cpp:671-683 (branch 0 -> -1; p, then index);
+// v untagged, result tagged
 __device__ __forceinline__ int32_t target_sample(const DevGraph& g, int32_t v, uint32_t kp,
                                                  uint32_t ki) {
     const int64_t off = g.offsets[v];
@@ -63,11 +77,10 @@ __device__ __forceinline__ int32_t target_sample(const DevGraph& g, int32_t v, u
     return kp < e.x ? t : (int32_t)e.y;
 }
 
-// NegativeSample src/proNet.cpp:623-633 (index FIRST, then p)
+// NegativeSample src/proNet.cpp:623-633 (index FIRST, then p); tagged id
 __device__ __forceinline__ int32_t negative_sample(const DevGraph& g, uint32_t ki, uint32_t kp) {
     const uint32_t i = draw_index(ki, g.V);
-    const uint2 e = g.ntab[i];
-    return kp < e.x ? (int32_t)i : (int32_t)e.y;
+    return alias_pick(i, g.ntab[i], kp);
 }
 
 // fastSigmoid src/proNet.cpp:62-71 on an fp32 dot: bucket index in fp64.

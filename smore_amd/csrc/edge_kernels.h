@@ -25,8 +25,27 @@ namespace smore {
 
 enum { MODE_STORE = 0, MODE_ATOMIC = 1, MODE_HYBRID = 3 };
 
-__device__ __forceinline__ bool hot_row(const uint32_t* bits, int32_t id) {
-    return (bits[id >> 5] >> (id & 31)) & 1u;
+// minimum waves per SIMD the register allocator must allow, per scatter mode
+// (0 = compiler default); overridable at build time for tuning.
+#ifndef SMORE_WAVES_STORE
+#define SMORE_WAVES_STORE 0
+#endif
+#ifndef SMORE_WAVES_ATOMIC
+#define SMORE_WAVES_ATOMIC 0
+#endif
+#ifndef SMORE_WAVES_HYBRID
+#define SMORE_WAVES_HYBRID 0
+#endif
+constexpr int waves_of(int mode) {
+    return mode == MODE_STORE ? SMORE_WAVES_STORE : mode == MODE_ATOMIC ? SMORE_WAVES_ATOMIC : SMORE_WAVES_HYBRID;
+}
+
+// hybrid scatter: a row is added atomically iff its id tag says hot
+template <int MODE>
+__device__ __forceinline__ bool scatter_atomic(int32_t tagged) {
+    if constexpr (MODE == MODE_ATOMIC) return true;
+    else if constexpr (MODE == MODE_HYBRID) return tagged >= 0 && tag_hot(tagged);
+    else return false;
 }
 
 // The 4+2K (or 14 for BPR) words of a sample: lane l of the group computes
@@ -89,6 +108,7 @@ struct SlotWords {
 // ------------------------------------------------------------------ update core
 // One UpdatePair / UpdateFactorizedPair on rows W_v and the K+1 context refs
 // id[0] (positive) and id[1..K] (negatives), done by the G lanes of a group.
+// Ids are untagged; hotw / hot[k] select the atomic scatter (MODE_HYBRID).
 //
 // Scatter bookkeeping without a copy of the original rows: after reference k
 // is processed its new value is propagated to the LATER references with the
@@ -100,7 +120,8 @@ struct SlotWords {
 template <int G, int M, int KMAX, int MODE>
 __device__ __forceinline__ void sgd_update(const EdgeArgs& a, const float* s_sig, int lane,
                                            const bool (&ev)[M], int32_t v, const int32_t (&id)[KMAX + 1],
-                                           float alpha, bool shared, bool mf) {
+                                           bool hotw, const bool (&hot)[KMAX + 1], float alpha, bool shared,
+                                           bool mf) {
     constexpr bool DELTA = MODE == MODE_ATOMIC || MODE == MODE_HYBRID;
     const int dpad = a.dpad;
     float* const Tw = a.W;
@@ -119,15 +140,6 @@ __device__ __forceinline__ void sgd_update(const EdgeArgs& a, const float* s_sig
         const float* cp = Tc + (int64_t)(id[k] < 0 ? 0 : id[k]) * dpad + lane;
 #pragma unroll
         for (int m = 0; m < M; ++m) rows[k][m] = (ev[m] && id[k] >= 0) ? cp[m * G] : 0.0f;
-    }
-    bool hot[KMAX + 1];
-    bool hotw = MODE == MODE_ATOMIC;
-#pragma unroll
-    for (int k = 0; k <= KMAX; ++k) hot[k] = MODE == MODE_ATOMIC;
-    if constexpr (MODE == MODE_HYBRID) {
-        hotw = hot_row(a.hotW, v);
-#pragma unroll
-        for (int k = 0; k <= KMAX; ++k) hot[k] = id[k] >= 0 && hot_row(a.hotC, id[k]);
     }
     // canonicalise repeated ids onto their first occurrence
 #pragma unroll
@@ -235,7 +247,8 @@ __device__ __forceinline__ void sgd_update(const EdgeArgs& a, const float* s_sig
 // LINE-2 (W,C), LINE-1 (W,W), MF (W,W, Opt_SGD): the model is a wave-uniform
 // runtime switch; the scatter MODE is compile-time.
 template <int G, int M, int KMAX, int MODE>
-__global__ void __launch_bounds__(256) edge_train_kernel(EdgeArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(waves_of(MODE))))
+edge_train_kernel(EdgeArgs a) {
     __shared__ float s_sig[1001];
     for (int i = threadIdx.x; i < 1001; i += blockDim.x) s_sig[i] = a.sig[i];
     __syncthreads();
@@ -260,19 +273,26 @@ __global__ void __launch_bounds__(256) edge_train_kernel(EdgeArgs a) {
         SampleWords<G, NSLOT> wd;
         wd.draw(a.seed, 0, s, lane);
 
-        const int32_t v = source_sample(a.g, wd.w[0], wd.w[1]);
+        const int32_t tv = source_sample(a.g, wd.w[0], wd.w[1]);
+        const int32_t v = untag(tv);
         const int32_t c = target_sample(a.g, v, wd.w[2], wd.w[3]);
         if (c < 0) {
             if (lane == 0) atomicAdd(a.skipped, 1ull);
             continue;
         }
         int32_t id[KMAX + 1];
+        bool hot[KMAX + 1];
         id[0] = c;
 #pragma unroll
         for (int j = 0; j < KMAX; ++j)
             id[j + 1] = (j < a.K) ? negative_sample(a.g, wd.w[4 + 2 * j], wd.w[5 + 2 * j]) : -1;
+#pragma unroll
+        for (int k = 0; k <= KMAX; ++k) {
+            hot[k] = scatter_atomic<MODE>(id[k]);
+            id[k] = id[k] < 0 ? -1 : untag(id[k]);
+        }
         const float alpha = alpha_at(s + base, a.alpha0, a.total);
-        sgd_update<G, M, KMAX, MODE>(a, s_sig, lane, ev, v, id, alpha, shared, mf);
+        sgd_update<G, M, KMAX, MODE>(a, s_sig, lane, ev, v, id, scatter_atomic<MODE>(tv), hot, alpha, shared, mf);
     }
 }
 
@@ -313,18 +333,25 @@ __global__ void __launch_bounds__(256) walk_pairs_kernel(EdgeArgs a, WalkArgs w)
             const int reduce = (int)draw_index(kw, (uint32_t)w.window) + 1;
             const int left = i - reduce < 0 ? 0 : i - reduce;
             const int right = i + reduce >= L ? L - 1 : i + reduce;
-            const int32_t vi = walk[i];
+            const int32_t tvi = walk[i];
             for (int j = left; j <= right; ++j) {
                 if (j == i) continue;
                 int32_t id[KMAX + 1];
+                bool hot[KMAX + 1];
                 id[0] = walk[j];
                 SlotWords<G, 2 * KMAX> nw;
                 nw.draw(a.seed, 1, unit, slot, lane);
 #pragma unroll
                 for (int n = 0; n < KMAX; ++n)
                     id[n + 1] = n < a.K ? negative_sample(a.g, nw.w[2 * n], nw.w[2 * n + 1]) : -1;
+#pragma unroll
+                for (int k = 0; k <= KMAX; ++k) {
+                    hot[k] = scatter_atomic<MODE>(id[k]);
+                    id[k] = id[k] < 0 ? -1 : untag(id[k]);
+                }
                 slot += 2 * a.K;
-                sgd_update<G, M, KMAX, MODE>(a, s_sig, lane, ev, vi, id, alpha, false, false);
+                sgd_update<G, M, KMAX, MODE>(a, s_sig, lane, ev, untag(tvi), id, scatter_atomic<MODE>(tvi), hot,
+                                             alpha, false, false);
             }
         }
     }
@@ -358,14 +385,20 @@ __global__ void __launch_bounds__(256) bpr_train_kernel(EdgeArgs a) {
         SampleWords<G, 14> wd;
         wd.draw(a.seed, 0, s, lane);
         int32_t id[NS];
+        bool hot[NS];
         id[0] = source_sample(a.g, wd.w[0], wd.w[1]);
-        id[1] = target_sample(a.g, id[0], wd.w[2], wd.w[3]);
+        id[1] = target_sample(a.g, untag(id[0]), wd.w[2], wd.w[3]);
         if (id[1] < 0) {
             if (lane == 0) atomicAdd(a.skipped, 1ull);
             continue;
         }
 #pragma unroll
         for (int n = 0; n < 5; ++n) id[2 + n] = negative_sample(a.g, wd.w[4 + 2 * n], wd.w[5 + 2 * n]);
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            hot[k] = scatter_atomic<MODE>(id[k]);
+            id[k] = untag(id[k]);
+        }
 
         float row[NS][M];
 #pragma unroll
@@ -443,8 +476,7 @@ __global__ void __launch_bounds__(256) bpr_train_kernel(EdgeArgs a) {
             for (int k2 = k + 1; k2 < NS; ++k2) last = last && (id[k2] != id[k]);
             if (last) {
                 float* q = T + (int64_t)id[k] * dpad + lane;
-                bool atom = MODE == MODE_ATOMIC;
-                if constexpr (MODE == MODE_HYBRID) atom = hot_row(a.hotC, id[k]);
+                const bool atom = hot[k];
 #pragma unroll
                 for (int m = 0; m < M; ++m) {
                     if (!ev[m]) continue;

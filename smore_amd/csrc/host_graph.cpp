@@ -114,11 +114,70 @@ static void parallel_for(int64_t n, int64_t grain, const std::function<void(int6
     for (auto& x : th) x.join();
 }
 
+// Stable sort of edge slots by source: LSD radix over the source id (two
+// passes up to 2^26 vertices, else 11-bit digits) of packed (src << 32 | slot) words, threads over contiguous slot
+// ranges with per-thread digit counts -- stable, so each source keeps its
+// push order.  Returns the slot order.
+static std::vector<uint64_t> sort_slots_by_source(int64_t V, int64_t E, const int32_t* src) {
+    std::vector<uint64_t> a((size_t)E), b((size_t)E);
+    parallel_for(E, 1 << 16, [&](int64_t lo, int64_t hi) {
+        for (int64_t e = lo; e < hi; ++e) a[e] = ((uint64_t)(uint32_t)src[e] << 32) | (uint64_t)e;
+    });
+    int bits = 1;
+    while (bits < 31 && ((int64_t)1 << bits) < V) ++bits;
+    const int D = bits <= 26 ? (bits + 1) / 2 : 11;     // two passes up to 2^26 vertices
+    const int NB = 1 << D;
+    const int64_t nt = std::max<int64_t>(1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(),
+                                                               E >> 16}));
+    const int64_t chunk = (E + nt - 1) / std::max<int64_t>(nt, 1);
+    std::vector<int64_t> cnt((size_t)(nt * NB));
+    for (int shift = 32; shift < 32 + bits; shift += D) {
+        std::fill(cnt.begin(), cnt.end(), 0);
+        auto run = [&](auto&& fn) {
+            std::vector<std::thread> th;
+            for (int64_t t = 0; t < nt; ++t) th.emplace_back(fn, t);
+            for (auto& x : th) x.join();
+        };
+        run([&](int64_t t) {
+            int64_t* c = cnt.data() + t * NB;
+            for (int64_t e = t * chunk, end = std::min(E, e + chunk); e < end; ++e) c[(a[e] >> shift) & (NB - 1)]++;
+        });
+        int64_t sum = 0;                               // digit-major, thread-minor offsets
+        for (int d = 0; d < NB; ++d)
+            for (int64_t t = 0; t < nt; ++t) {
+                const int64_t x = cnt[t * NB + d];
+                cnt[t * NB + d] = sum;
+                sum += x;
+            }
+        run([&](int64_t t) {
+            int64_t* c = cnt.data() + t * NB;
+            for (int64_t e = t * chunk, end = std::min(E, e + chunk); e < end; ++e)
+                b[c[(a[e] >> shift) & (NB - 1)]++] = a[e];
+        });
+        a.swap(b);
+    }
+    return a;
+}
+
 bool build_graph(int64_t V, int64_t E, const int32_t* src, const int32_t* dst, const double* w,
                  int vertex_method, int negative_method, HostGraph& g, std::string& err) {
-    if (V <= 0 || V >= (int64_t)1 << 31 || E < 0) { err = "bad graph size"; return false; }
-    for (int64_t e = 0; e < E; ++e)
-        if (src[e] < 0 || src[e] >= V || dst[e] < 0 || dst[e] >= V) {
+    if (V <= 0 || V >= (int64_t)1 << 30 || E < 0 || E >= (int64_t)1 << 32) {   // ids carry a tag in bit 30
+        err = "bad graph size (V < 2^30, E < 2^32)";
+        return false;
+    }
+    std::vector<int64_t> bad(16, -1);
+    {
+        std::vector<std::thread> th;
+        const int64_t nt = 16, chunk = (E + nt - 1) / nt;
+        for (int64_t t = 0; t < nt; ++t)
+            th.emplace_back([&, t] {
+                for (int64_t e = t * chunk, end = std::min(E, e + chunk); e < end; ++e)
+                    if (src[e] < 0 || src[e] >= V || dst[e] < 0 || dst[e] >= V) { bad[t] = e; break; }
+            });
+        for (auto& x : th) x.join();
+    }
+    for (int64_t e : bad)
+        if (e >= 0) {
             err = "edge " + std::to_string(e) + " has a vertex id out of range";
             return false;
         }
@@ -127,24 +186,53 @@ bool build_graph(int64_t V, int64_t E, const int32_t* src, const int32_t* dst, c
     g.offsets.assign((size_t)V + 1, 0);
     g.targets.resize((size_t)E);
     g.weights.resize((size_t)E);
-    // CSR by a stable counting sort: per source, targets keep push order
+    // CSR by a stable sort on the source: per source, targets keep push order
     // (graph[vid1].push_back(vid2), src/proNet.cpp:208-215 and :427-437)
-    for (int64_t e = 0; e < E; ++e) g.offsets[src[e] + 1]++;
-    for (int64_t v = 0; v < V; ++v) g.offsets[v + 1] += g.offsets[v];
     {
-        std::vector<int64_t> cur(g.offsets.begin(), g.offsets.end() - 1);
-        for (int64_t e = 0; e < E; ++e) {
-            int64_t p = cur[src[e]]++;
-            g.targets[p] = dst[e];
-            g.weights[p] = w[e];
-        }
+        const std::vector<uint64_t> order = sort_slots_by_source(V, E, src);
+        parallel_for(E, 1 << 16, [&](int64_t lo, int64_t hi) {
+            for (int64_t p = lo; p < hi; ++p) {
+                const int64_t e = (int64_t)(order[p] & 0xFFFFFFFFu);
+                g.targets[p] = dst[e];
+                g.weights[p] = w[e];
+                const int64_t v = (int64_t)(order[p] >> 32);
+                if (p == E - 1 || (int64_t)(order[p + 1] >> 32) != v) g.offsets[v + 1] = p + 1;
+            }
+        });
+        for (int64_t v = 0; v < V; ++v)                // sources without edges
+            if (g.offsets[v + 1] < g.offsets[v]) g.offsets[v + 1] = g.offsets[v];
     }
     // degrees (src/proNet.cpp:431-443): out in adjacency order, in over the CSR
     g.out_deg.assign((size_t)V, 0.0);
     g.in_deg.assign((size_t)V, 0.0);
-    for (int64_t v = 0; v < V; ++v)
-        for (int64_t p = g.offsets[v]; p < g.offsets[v + 1]; ++p) g.out_deg[v] += g.weights[p];
-    for (int64_t p = 0; p < E; ++p) g.in_deg[g.targets[p]] += g.weights[p];
+    parallel_for(V, 1 << 14, [&](int64_t lo, int64_t hi) {
+        for (int64_t v = lo; v < hi; ++v)
+            for (int64_t p = g.offsets[v]; p < g.offsets[v + 1]; ++p) g.out_deg[v] += g.weights[p];
+    });
+    // in-degrees sum in CSR order; with integer weights (sums exact in fp64,
+    // so any order gives the same bits) threads keep private partial sums
+    bool integral = E < ((int64_t)1 << 40);
+    for (int64_t p = 0; p < E && integral; ++p)
+        integral = g.weights[p] == std::floor(g.weights[p]) && g.weights[p] >= 0 && g.weights[p] < 4096.0;
+    const int64_t nt = std::min<int64_t>(16, std::max(1u, std::thread::hardware_concurrency()));
+    if (!integral || E < ((int64_t)1 << 22) || nt == 1) {
+        for (int64_t p = 0; p < E; ++p) g.in_deg[g.targets[p]] += g.weights[p];
+    } else {
+        std::vector<std::vector<double>> part((size_t)nt);
+        std::vector<std::thread> th;
+        const int64_t chunk = (E + nt - 1) / nt;
+        for (int64_t t = 0; t < nt; ++t)
+            th.emplace_back([&, t] {
+                part[t].assign((size_t)V, 0.0);
+                for (int64_t p = t * chunk, end = std::min(E, p + chunk); p < end; ++p)
+                    part[t][g.targets[p]] += g.weights[p];
+            });
+        for (auto& x : th) x.join();
+        parallel_for(V, 1 << 16, [&](int64_t lo, int64_t hi) {
+            for (int64_t t = 0; t < nt; ++t)
+                for (int64_t v = lo; v < hi; ++v) g.in_deg[v] += part[t][v];
+        });
+    }
 
     g.vertex_method = vertex_method;
     g.negative_method = negative_method;

@@ -19,7 +19,7 @@ namespace smore {
 __device__ __forceinline__ int32_t go_alias(const uint2* tab, uint32_t n, uint32_t ki, uint32_t kp) {
     const uint32_t i = draw_index(ki, n);
     const uint2 e = tab[i];
-    return kp < e.x ? (int32_t)i : (int32_t)e.y;
+    return kp < e.x ? (int32_t)i : untag((int32_t)e.y);   // ids untagged (no hybrid scatter here)
 }
 
 __device__ __forceinline__ int32_t go_target(const DevGraph& g, const double* tcum, int32_t v, uint32_t kr) {
@@ -33,7 +33,7 @@ __device__ __forceinline__ int32_t go_target(const DevGraph& g, const double* tc
         if (r <= tcum[off + mid]) hi = mid;
         else lo = mid + 1;
     }
-    return g.targets[off + lo];
+    return untag(g.targets[off + lo]);
 }
 
 template <int G, int M>

@@ -12,8 +12,6 @@ struct EdgeArgs {
     float* W;                      // [V][dpad]
     float* C;                      // [V][dpad] (== W for shared-table models)
     unsigned long long* skipped;   // samples whose source had no out-edge
-    const uint32_t* hotW;          // hybrid mode: 1 bit per row, atomic scatter if set
-    const uint32_t* hotC;          //   (hotC == hotW for shared-table models)
     const double* tcum;            // Go semantics: per-vertex prefix sums of edge weights
     uint64_t begin, count, total, seed;
     double alpha0;

@@ -26,14 +26,15 @@ __global__ void sample_kernel(DevGraph g, uint64_t seed, uint64_t begin, uint64_
         return w[j & 3];
     };
     (void)nslot;
-    const int32_t v = source_sample(g, word(0), word(1));
+    const int32_t v = untag(source_sample(g, word(0), word(1)));
     o[0] = v;
     const uint32_t tp = word(2), ti = word(3);
-    o[1] = target_sample(g, v, tp, ti);
+    const int32_t c = target_sample(g, v, tp, ti);
+    o[1] = c < 0 ? -1 : untag(c);
     const int nn = bpr ? 5 : K;
     for (int j = 0; j < nn; ++j) {
         const uint32_t ki = word(4 + 2 * j), kp = word(5 + 2 * j);
-        o[2 + j] = negative_sample(g, ki, kp);
+        o[2 + j] = untag(negative_sample(g, ki, kp));
     }
 }
 

@@ -11,10 +11,12 @@ __global__ void walk_gen_kernel(DevGraph g, WalkArgs w, uint64_t seed) {
     if (t >= w.nwalks) return;
     const uint64_t unit = w.walk_begin + t;
     const int32_t start = (int32_t)w.order[unit];
+    // walks hold tagged ids; the start vertex's tag is the self tag of its vtab entry
+    const int32_t tstart = start | (int32_t)((g.vtab[start].y >> 31) << 30);
     int32_t* out = w.walks + t * (uint64_t)(w.steps + 1);
     int L = 0;
-    int32_t next = start;
-    out[L++] = next;
+    int32_t next = start, tnext = tstart;
+    out[L++] = tnext;
     uint4 b = make_uint4(0, 0, 0, 0);
     for (int s = 0; s < w.steps; ++s) {
         if (g.offsets[next + 1] - g.offsets[next] == 0) {
@@ -24,8 +26,9 @@ __global__ void walk_gen_kernel(DevGraph g, WalkArgs w, uint64_t seed) {
         const uint32_t s0 = 2u * (uint32_t)s;
         if ((s0 & 3) == 0) b = philox_block(seed, 1, unit, s0 >> 2);
         const uint32_t kp = comp(b, (int)(s0 & 3)), ki = comp(b, (int)((s0 + 1) & 3));
-        next = target_sample(g, next, kp, ki);
-        out[L++] = next;
+        tnext = target_sample(g, next, kp, ki);
+        next = untag(tnext);
+        out[L++] = tnext;
     }
     w.lens[t] = L;
 }

@@ -324,3 +324,61 @@ def test_replica_sync_rccl_single_rank(smore):
         assert torch.equal(sync.snaps[0][:, :64].cpu(), torch.from_numpy(pn.get_table(0)))
     finally:
         dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------- hybrid scatter (tagged ids)
+def test_hybrid_tags_keep_draws_and_serial_bit_exact(smore):
+    """A hybrid run tags hot rows in the device graph's id words; draws and
+    every other mode must be unaffected (tags are split off before use)."""
+    g, pn = make_pair(smore, "pl100w.txt", 1)
+    W0, C0 = rand_tables(g.V, 64, 2, 21)
+    pn.alloc_tables(64, 2)
+    pn.set_table(0, W0)
+    pn.set_table(1, C0)
+    pn.set_hot_threshold(1e-3)                     # many hot rows
+    pn.train_edges("line2", 0, 200000, 10 ** 6, 5, 0.025, 0.0, SEED, "hybrid")
+    hw, hc = pn.hot_rows()
+    assert 0 < hw <= g.V and 0 < hc <= g.V
+    assert np.isfinite(pn.get_table(0)).all()
+    np.testing.assert_array_equal(pn.sample_edges("line2", 7, 20000, 5, SEED), orc.sample_line(g, SEED, 7, 20000, 5))
+    pn.set_table(0, W0)
+    pn.set_table(1, C0)
+    pn.train_edges("line2", 12345, 20000, 10 ** 6, 5, 0.025, 0.0, SEED, "serial")
+    W, C = padded(W0, 64), padded(C0, 64)
+    orc.train_edge_f32(g, "line2", W, C, 64, 5, 0.025, 0.0, 10 ** 6, 12345, 12345 + 20000, SEED)
+    np.testing.assert_array_equal(pn.get_table(0), W)
+    np.testing.assert_array_equal(pn.get_table(1), C)
+
+
+@pytest.mark.parametrize("tau", [0.0, 1e30])
+def test_hybrid_single_sample(smore, tau):
+    """tau 0: every row hot (atomic deltas); tau huge: no row hot (stores)."""
+    g, pn = make_pair(smore, "pl100w.txt", 1)
+    W0, C0 = rand_tables(g.V, 64, 2, 12)
+    pn.alloc_tables(64, 2)
+    pn.set_hot_threshold(tau)
+    for s in (5, 99, 12345):
+        pn.set_table(0, W0)
+        pn.set_table(1, C0)
+        pn.train_edges("line2", s, 1, 10 ** 6, 5, 0.025, 0.0, SEED, "hybrid")
+        W, C = padded(W0, 64), padded(C0, 64)
+        orc.train_edge_f32(g, "line2", W, C, 64, 5, 0.025, 0.0, 10 ** 6, s, s + 1, SEED)
+        np.testing.assert_allclose(pn.get_table(0), W, atol=1e-6, rtol=0)
+        np.testing.assert_allclose(pn.get_table(1), C, atol=1e-6, rtol=0)
+
+
+def test_hybrid_deepwalk_and_bpr_run(smore):
+    g, pn = make_pair(smore, "pl100w.txt", 1)
+    pn.alloc_tables(32, 2)
+    pn.init_table_uniform(0, 1)
+    pn.zero_table(1)
+    pn.set_hot_threshold(1e-3)
+    order = orc.deepwalk_order(g.V, 1, 0)
+    pn.train_deepwalk(0, g.V, 1, 20, 3, 5, 0.025, SEED, order, "hybrid")
+    assert np.isfinite(pn.get_table(0)).all() and np.isfinite(pn.get_table(1)).all()
+    gb, pb = make_pair(smore, "bip.txt", 0, nm="no_degrees")
+    pb.alloc_tables(16, 1)
+    pb.init_table_uniform(0, 1)
+    pb.set_hot_threshold(1e-3)
+    pb.train_edges("bpr", 0, 100000, 100000, 5, 0.05, 0.0, SEED, "hybrid")
+    assert np.isfinite(pb.get_table(0)).all()
