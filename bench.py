@@ -3,8 +3,11 @@
 
 A "step" is one launch of the fused sample->gather->update kernel over
 `--samples` edge samples (default 2^27) of the synthetic power-law graph of
-config c2 (1M vertices / 20M undirected lines = 40M directed slots, d=64,
-K=5), inputs resident in HBM.  One process per GPU; with N > 1
+config c4 (10M vertices / 200M undirected lines = 400M directed slots, d=64,
+K=5; the north star's 1/2/4/8-GPU graph), inputs resident in
+HBM.  Default scatter: hybrid (atomic adds for the hot rows, the 32 hottest
+write-combined per workgroup in LDS, plain stores for the rest), whose
+training objective matches the lossless atomic scatter.  One process per GPU; with N > 1
 each rank runs its own disjoint global-sample range on a replicated graph and
 replicated tables, and the tables' deltas are all-reduced over RCCL every
 `--sync-every` steps (weak scaling).  Rank 0 prints one JSON line.
@@ -38,13 +41,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c2")
+    ap.add_argument("--config", default="c4")
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--negative", type=int, default=5)
     ap.add_argument("--samples", type=int, default=1 << 27, help="edge samples per step per GPU")
-    ap.add_argument("--mode", default="atomic", choices=["hogwild", "atomic", "hybrid"],
-                    help="scatter: atomic (default; lock-free, no lost updates), hybrid, hogwild (plain stores)")
-    ap.add_argument("--hot-tau", type=float, default=0.1, help="hybrid: hot-row threshold")
+    ap.add_argument("--mode", default="hybrid", choices=["hogwild", "atomic", "hybrid"],
+                    help="scatter: hybrid (default), atomic (every row), hogwild (plain stores, loses updates)")
+    ap.add_argument("--hot-tau", type=float, default=0.03, help="hybrid: hot-row threshold")
+    ap.add_argument("--combine-rows", type=int, default=32, help="hybrid: LDS write-combined hottest rows")
+    ap.add_argument("--combine-flush", type=int, default=16, help="hybrid: rounds between LDS flushes")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
     ap.add_argument("--sync-every", type=int, default=1)
     ap.add_argument("--sync", default="sum", choices=["sum", "mean"])
@@ -54,7 +59,7 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(V, src, dst, w, dim, K, seconds):
+def cpu_baseline(V, src, dst, w, dim, K, seconds, config):
     """The oracle's fp32 spec with OpenMP Hogwild threads on this host (the
     reference sources do not travel to the GPU box), bounded in time."""
     from oracle import oracle as orc
@@ -71,8 +76,8 @@ def cpu_baseline(V, src, dst, w, dim, K, seconds):
         done += chunk
     el = time.perf_counter() - t0
     return {"value": round(done / el / 1e6, 4), "unit": "M edge-updates/s", "cores": threads, "kind": "port",
-            "sample": "%d LINE-2 samples (d=%d, K=%d) on the same c2 graph, %d OpenMP Hogwild threads, %.1f s"
-                      % (done, dim, K, threads, el)}
+            "sample": "%d LINE-2 samples (d=%d, K=%d) on the same %s graph, %d OpenMP Hogwild threads, %.1f s"
+                      % (done, dim, K, config, threads, el)}
 
 
 def main():
@@ -106,6 +111,7 @@ def main():
               % (args.config, t_build - t_gen, t_ready - t_build), file=sys.stderr, flush=True)
     E = pn.MAX_line
     pn.set_hot_threshold(args.hot_tau)
+    pn.set_write_combine(args.combine_rows, args.combine_flush)
     pn.alloc_tables(args.dim, 2)
     pn.init_table_uniform(0, args.seed)     # W ~ (u-0.5)/d, as the reference Init law
     pn.zero_table(1)                        # C = 0 (src/model/LINE.cpp:92)
@@ -163,7 +169,7 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline and args.cpu_baseline_seconds > 0:
-            cpu = cpu_baseline(V, src, dst, w, args.dim, K, args.cpu_baseline_seconds)
+            cpu = cpu_baseline(V, src, dst, w, args.dim, K, args.cpu_baseline_seconds, args.config)
         out = {
             "metric": "M edge-updates/sec (d=64, neg=5)",
             "value": round(updates / el / 1e6, 3),

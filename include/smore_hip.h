@@ -164,6 +164,12 @@ int smore_train_edges(smore_ctx* ctx, int model, uint64_t begin, uint64_t count,
  * (its per-sample touch probability) > tau (default 0.1); see DESIGN.md */
 int smore_set_hot_threshold(smore_ctx* ctx, double tau);
 /* rows marked hot in W and C by the last hybrid launch */
+/* hybrid scatter: the `rows` hottest hot context rows (default 32; 0 = off; at
+ * most 8192/dim) are write-combined per workgroup in LDS and added to HBM every
+ * `flush_rounds` rounds of the persistent loop (default 16) -- bounded extra
+ * staleness on those rows only, in exchange for not serialising every sample's
+ * atomic adds on the same few HBM lines. */
+int smore_set_write_combine(smore_ctx* ctx, int rows, int flush_rounds);
 int smore_hot_rows(const smore_ctx* ctx, int64_t* hot_w, int64_t* hot_c);
 /* samples whose source had no out-edge (reference: TargetSample -> -1) */
 int smore_skipped(smore_ctx* ctx, uint64_t* skipped);

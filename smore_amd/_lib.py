@@ -55,6 +55,7 @@ def _load():
         "smore_skipped": (i32, [P, C.POINTER(u64)]),
         "smore_set_hot_threshold": (i32, [P, dbl]),
         "smore_set_semantics": (i32, [P, i32]),
+        "smore_set_write_combine": (i32, [P, i32, i32]),
         "smore_gen_powerlaw": (i32, [i64, i64, i32, dbl, u64, P, P]),
         "smore_hot_rows": (i32, [P, C.POINTER(i64), C.POINTER(i64)]),
         "smore_last_kernel_ms": (C.c_float, [P]),

@@ -38,7 +38,7 @@ struct smore_ctx {
     float* d_table[2] = {nullptr, nullptr};
     int dim = 0, dpad = 0, ntables = 0;
     // hybrid scatter: hot-row bitmaps (1 bit per row), keyed by what built them
-    double hot_tau = 0.1;
+    double hot_tau = 0.03;
     std::string hot_key;
     int64_t hot_rows[2] = {0, 0};
     // DeepWalk buffers
@@ -56,6 +56,11 @@ struct smore_ctx {
     // semantics: SMORE_SEM_CPP (default) or SMORE_SEM_GO
     int semantics = 0;
     double* d_tcum = nullptr;
+    // hybrid write-combining: super-hot context rows (hash + slot ids)
+    int2* d_sh_hash = nullptr;
+    int32_t* d_sh_ids = nullptr;
+    int sh_rows = 0;
+    int sh_max = 32, sh_flush = 16;
 };
 
 namespace {
@@ -174,7 +179,7 @@ void smore_destroy(smore_ctx* c) {
     dfree(c->d_offsets); dfree(c->d_targets); dfree(c->d_vtab); dfree(c->d_ntab); dfree(c->d_ctab);
     dfree(c->d_sig); dfree(c->d_skipped); dfree(c->d_table[0]); dfree(c->d_table[1]);
 
-    dfree(c->d_order); dfree(c->d_walks); dfree(c->d_lens); dfree(c->d_tcum);
+    dfree(c->d_order); dfree(c->d_walks); dfree(c->d_lens); dfree(c->d_tcum); dfree(c->d_sh_hash); dfree(c->d_sh_ids);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -407,6 +412,33 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
         if ((double)M * pw > c->hot_tau) { hw[v] = 1; c->hot_rows[0]++; }
         if ((double)M * pcx > c->hot_tau) { hc[v] = 1; c->hot_rows[1]++; }
     }
+    // super-hot rows: the hottest hot context rows, write-combined per block
+    {
+        std::vector<std::pair<double, int32_t>> r;
+        for (int64_t v = 0; v < V; ++v) {
+            const double p = model == SMORE_LINE2 ? pc[v] + negs * pn[v] : ps[v] + pc[v] + negs * pn[v];
+            if (hc[v]) r.push_back({p, (int32_t)v});
+        }
+        const int64_t cap = std::max<int64_t>(0, std::min<int64_t>(c->sh_max, 8192 / std::max(1, c->dpad)));
+        const int64_t n = std::min<int64_t>(cap, (int64_t)r.size());
+        std::partial_sort(r.begin(), r.begin() + n, r.end(), [](const auto& x, const auto& y) {
+            return x.first > y.first || (x.first == y.first && x.second < y.second);
+        });
+        std::vector<int2> hash(SH_HASH, make_int2(-1, -1));
+        std::vector<int32_t> ids((size_t)std::max<int64_t>(n, 1), -1);
+        for (int64_t i = 0; i < n; ++i) {
+            const int32_t id = r[i].second;
+            ids[i] = id;
+            uint32_t p = sh_hash_of(id);
+            while (hash[p & (SH_HASH - 1)].x >= 0) ++p;
+            hash[p & (SH_HASH - 1)] = make_int2(id, (int)i);
+        }
+        int rc2;
+        if ((rc2 = set_device(c))) return rc2;
+        if ((rc2 = upload(c, c->d_sh_hash, hash.data(), hash.size()))) return rc2;
+        if ((rc2 = upload(c, c->d_sh_ids, ids.data(), ids.size()))) return rc2;
+        c->sh_rows = (int)n;
+    }
     const HostGraph& g = c->g;
     auto tag_tab = [&](const std::vector<AliasEntry>& tab, const std::vector<uint8_t>& hot) {
         std::vector<AliasEntry> t(tab);
@@ -449,7 +481,10 @@ static int edge_grid(smore_ctx* c, const EdgeArgs& a) {
     if (a.mode == SMORE_SERIAL) return 1;
     int per_cu = 0;
     const void* sym = edge_kernel_symbol(a);
-    if (!sym || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sym, 256, 0) != hipSuccess || per_cu < 1)
+    if (!sym ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sym, 256, sh_lds_bytes(a.sh_rows, a.dpad)) !=
+            hipSuccess ||
+        per_cu < 1)
         per_cu = 1;
     int64_t grid = (int64_t)c->cus * per_cu;
     const int G = lanes_of(a.dpad);
@@ -471,7 +506,7 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
     if (count == 0) return SMORE_OK;
     int rc;
     if ((rc = set_device(c))) return rc;
-    EdgeArgs a;
+    EdgeArgs a{};
     a.g = dev_graph(c);
     a.sig = c->d_sig;
     a.W = c->d_table[0];
@@ -508,11 +543,17 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
         c->timed = true;
         return SMORE_OK;
     }
+    const bool combine = mode == SMORE_HYBRID && model != SMORE_BPR;
+    a.sh_rows = combine ? std::min(c->sh_max, 8192 / std::max(1, c->dpad)) : 0;   // LDS bound for the grid
     const int grid = edge_grid(c, a);
     if (mode == SMORE_HYBRID) {
         const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
         if ((rc = build_hot_maps(c, model, a.K, M))) return rc;
     }
+    a.sh_rows = combine ? c->sh_rows : 0;
+    a.sh_hash = c->d_sh_hash;
+    a.sh_ids = c->d_sh_ids;
+    a.sh_flush = std::max(1, c->sh_flush);
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     HIPCHK(c, launch_edge_train(a, grid, c->stream));
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
@@ -554,6 +595,14 @@ int smore_set_semantics(smore_ctx* c, int semantics) {
 int smore_set_hot_threshold(smore_ctx* c, double tau) {
     if (!c || !(tau >= 0)) return SMORE_EINVAL;
     c->hot_tau = tau;
+    return SMORE_OK;
+}
+
+int smore_set_write_combine(smore_ctx* c, int rows, int flush_rounds) {
+    if (!c || rows < 0 || rows > 1024 || flush_rounds < 1) return SMORE_EINVAL;
+    c->sh_max = rows;
+    c->sh_flush = flush_rounds;
+    c->hot_key.clear();
     return SMORE_OK;
 }
 
@@ -670,7 +719,7 @@ int smore_train_deepwalk(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, i
         HIPCHK(c, hipMalloc((void**)&c->d_lens, chunk * sizeof(int32_t)));
         c->walk_buf_n = need;
     }
-    EdgeArgs a;
+    EdgeArgs a{};
     a.g = dev_graph(c);
     a.sig = c->d_sig;
     a.W = c->d_table[0];

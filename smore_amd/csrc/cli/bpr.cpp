@@ -16,7 +16,7 @@ int main(int argc, char** argv) {
     }
     char network_file[4096] = "", rep_file[4096] = "";
     int dimensions = 64, negative_samples = 5, sample_times = 10, threads = 1, device = 0, fmt = 0;
-    int mode = SMORE_ATOMIC;
+    int mode = SMORE_HYBRID;
     unsigned long long seed = 1;
     double init_alpha = 0.025, reg = 0.01;
     if ((i = ArgPos("-train", argc, argv)) > 0) snprintf(network_file, sizeof network_file, "%s", argv[i + 1]);

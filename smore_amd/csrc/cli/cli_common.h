@@ -23,8 +23,8 @@ static int ArgPos(const char* str, int argc, char** argv) {
 static int mode_of(const char* s) {
     if (!strcmp(s, "hogwild")) return SMORE_HOGWILD;
     if (!strcmp(s, "serial")) return SMORE_SERIAL;
-    if (!strcmp(s, "hybrid")) return SMORE_HYBRID;
-    return SMORE_ATOMIC;
+    if (!strcmp(s, "atomic")) return SMORE_ATOMIC;
+    return SMORE_HYBRID;
 }
 
 #define SMORE_CLI_CHECK(ctx, expr)                                                    \

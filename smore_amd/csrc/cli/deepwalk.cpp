@@ -22,7 +22,7 @@ int main(int argc, char** argv) {
     char network_file[4096] = "", rep_file[4096] = "", load_v[4096] = "", load_c[4096] = "";
     // defaults of cli/deepwalk.cpp:56-57 (walk_steps 5 in the C++ CLI)
     int dimensions = 64, undirected = 1, window_size = 5, negative_samples = 5, walk_times = 10, walk_steps = 5;
-    int threads = 1, device = 0, fmt = 0, mode = SMORE_ATOMIC;
+    int threads = 1, device = 0, fmt = 0, mode = SMORE_HYBRID;
     unsigned long long seed = 1;
     double init_alpha = 0.025;
     if ((i = ArgPos("-train", argc, argv)) > 0) snprintf(network_file, sizeof network_file, "%s", argv[i + 1]);

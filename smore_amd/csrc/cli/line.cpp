@@ -26,7 +26,7 @@ int main(int argc, char** argv) {
     }
     char network_file[4096] = "", rep_file[4096] = "";
     int dimensions = 64, undirected = 1, negative_samples = 5, sample_times = 10, threads = 1, order = 2;
-    int device = 0, mode = SMORE_ATOMIC, fmt = 0;
+    int device = 0, mode = SMORE_HYBRID, fmt = 0;
     unsigned long long seed = 1;
     double init_alpha = 0.025;
     if ((i = ArgPos("-train", argc, argv)) > 0) snprintf(network_file, sizeof network_file, "%s", argv[i + 1]);

@@ -48,6 +48,27 @@ __device__ __forceinline__ bool scatter_atomic(int32_t tagged) {
     else return false;
 }
 
+// Block-local write-combining of the super-hot context rows (hybrid scatter):
+// their deltas accumulate in LDS and a block adds them to HBM every sh_flush
+// rounds (one 256-B atomic wave-instruction per row) instead of every sample
+// adding to the same few HBM lines.  The block reads such a row as HBM value +
+// its own pending delta.
+struct ShState {
+    const int2* hash;      // LDS, SH_HASH entries {id, slot}
+    float* pend;           // LDS, [n][dpad]
+    int n;
+};
+
+__device__ __forceinline__ int sh_lookup(const int2* h, int32_t id) {
+    uint32_t p = ((uint32_t)id * 2654435761u) >> 24;
+    for (int i = 0; i < SH_HASH; ++i) {
+        const int2 e = h[(p + (uint32_t)i) & (SH_HASH - 1)];
+        if (e.x == id) return e.y;
+        if (e.x < 0) return -1;
+    }
+    return -1;
+}
+
 // The 4+2K (or 14 for BPR) words of a sample: lane l of the group computes
 // Philox block (l % NBLK) of unit s; word j is broadcast from lane j/4.
 template <int G, int NSLOT>
@@ -121,7 +142,7 @@ template <int G, int M, int KMAX, int MODE>
 __device__ __forceinline__ void sgd_update(const EdgeArgs& a, const float* s_sig, int lane,
                                            const bool (&ev)[M], int32_t v, const int32_t (&id)[KMAX + 1],
                                            bool hotw, const bool (&hot)[KMAX + 1], float alpha, bool shared,
-                                           bool mf) {
+                                           bool mf, const ShState& sh) {
     constexpr bool DELTA = MODE == MODE_ATOMIC || MODE == MODE_HYBRID;
     const int dpad = a.dpad;
     float* const Tw = a.W;
@@ -140,6 +161,34 @@ __device__ __forceinline__ void sgd_update(const EdgeArgs& a, const float* s_sig
         const float* cp = Tc + (int64_t)(id[k] < 0 ? 0 : id[k]) * dpad + lane;
 #pragma unroll
         for (int m = 0; m < M; ++m) rows[k][m] = (ev[m] && id[k] >= 0) ? cp[m * G] : 0.0f;
+    }
+    // super-hot rows: add this block's pending deltas
+    int slot[KMAX + 1];
+    int slotw = -1;
+#pragma unroll
+    for (int k = 0; k <= KMAX; ++k) slot[k] = -1;
+    if constexpr (MODE == MODE_HYBRID) {
+        if (sh.n > 0) {
+#pragma unroll
+            for (int k = 0; k <= KMAX; ++k) {
+                if (id[k] >= 0 && hot[k]) slot[k] = sh_lookup(sh.hash, id[k]);
+                if (slot[k] >= 0) {
+                    const float* pp = sh.pend + slot[k] * dpad + lane;
+#pragma unroll
+                    for (int m = 0; m < M; ++m)
+                        if (ev[m]) rows[k][m] += pp[m * G];
+                }
+            }
+            if (shared && hotw) {
+                slotw = sh_lookup(sh.hash, v);
+                if (slotw >= 0) {
+                    const float* pp = sh.pend + slotw * dpad + lane;
+#pragma unroll
+                    for (int m = 0; m < M; ++m)
+                        if (ev[m]) wv[m] += pp[m * G];
+                }
+            }
+        }
     }
     // canonicalise repeated ids onto their first occurrence
 #pragma unroll
@@ -217,18 +266,30 @@ __device__ __forceinline__ void sgd_update(const EdgeArgs& a, const float* s_sig
 #pragma unroll
         for (int m = 0; m < M; ++m) {
             if (!ev[m]) continue;
-            if (DELTA && hotw) unsafeAtomicAdd(wq + m * G, shared ? wv[m] - wv0[m] : e[m]);
-            else wq[m * G] = wv[m];
+            if (DELTA && hotw) {
+                const float d = shared ? wv[m] - wv0[m] : e[m];
+                if (MODE == MODE_HYBRID && slotw >= 0) atomicAdd(sh.pend + slotw * dpad + lane + m * G, d);
+                else unsafeAtomicAdd(wq + m * G, d);
+            } else {
+                wq[m * G] = wv[m];
+            }
         }
     }
 #pragma unroll
     for (int k = 0; k <= KMAX; ++k) {
         if (id[k] < 0 || id[k] == vs) continue;
         if (DELTA && hot[k]) {
-            float* cq = Tc + (int64_t)id[k] * dpad + lane;
+            if (MODE == MODE_HYBRID && slot[k] >= 0) {
+                float* pq = sh.pend + slot[k] * dpad + lane;
 #pragma unroll
-            for (int m = 0; m < M; ++m)
-                if (ev[m]) unsafeAtomicAdd(cq + m * G, rows[k][m]);
+                for (int m = 0; m < M; ++m)
+                    if (ev[m]) atomicAdd(pq + m * G, rows[k][m]);
+            } else {
+                float* cq = Tc + (int64_t)id[k] * dpad + lane;
+#pragma unroll
+                for (int m = 0; m < M; ++m)
+                    if (ev[m]) unsafeAtomicAdd(cq + m * G, rows[k][m]);
+            }
         } else {
             bool last = true;
 #pragma unroll
@@ -250,15 +311,31 @@ template <int G, int M, int KMAX, int MODE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(waves_of(MODE))))
 edge_train_kernel(EdgeArgs a) {
     __shared__ float s_sig[1001];
+    extern __shared__ float s_dyn[];   // hybrid: int2 hash[SH_HASH], int ids[n], float pend[n][dpad]
     for (int i = threadIdx.x; i < 1001; i += blockDim.x) s_sig[i] = a.sig[i];
+    ShState sh{nullptr, nullptr, 0};
+    int32_t* sh_ids = nullptr;
+    if constexpr (MODE == MODE_HYBRID) {
+        if (a.sh_rows > 0) {
+            int2* h = reinterpret_cast<int2*>(s_dyn);
+            sh_ids = reinterpret_cast<int32_t*>(h + SH_HASH);
+            float* pend = reinterpret_cast<float*>(sh_ids + a.sh_rows);
+            for (int i = threadIdx.x; i < SH_HASH; i += blockDim.x) h[i] = a.sh_hash[i];
+            for (int i = threadIdx.x; i < a.sh_rows; i += blockDim.x) sh_ids[i] = a.sh_ids[i];
+            for (int i = threadIdx.x; i < a.sh_rows * a.dpad; i += blockDim.x) pend[i] = 0.0f;
+            sh = ShState{h, pend, a.sh_rows};
+        }
+    }
     __syncthreads();
 
     constexpr int NSLOT = 4 + 2 * KMAX;
     const int lane = threadIdx.x & (G - 1);
-    uint64_t group = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
-    uint64_t ngroups = ((uint64_t)gridDim.x * blockDim.x) / G;
+    const uint64_t gpb = blockDim.x / G;                 // groups per block
+    uint64_t r0 = (uint64_t)blockIdx.x * gpb;            // block-uniform round base
+    uint64_t ngroups = (uint64_t)gridDim.x * gpb;
+    const uint64_t gib = threadIdx.x / G;
     if (a.mode == 2) {               // serial: one group, samples in order
-        if (group != 0) return;
+        if (blockIdx.x != 0 || gib != 0) return;
         ngroups = 1;
     }
     const bool shared = a.model != 0;
@@ -267,32 +344,62 @@ edge_train_kernel(EdgeArgs a) {
 #pragma unroll
     for (int m = 0; m < M; ++m) ev[m] = lane + G * m < a.dpad;
     const uint64_t base = mf ? 0 : 1;   // LINE counts from 1, MF from 0
+    float* const Tc = a.C;
 
-    for (uint64_t t = group; t < a.count; t += ngroups) {
-        const uint64_t s = a.begin + t;
-        SampleWords<G, NSLOT> wd;
-        wd.draw(a.seed, 0, s, lane);
+    // adds the block's pending super-hot deltas to HBM (one row per wave-instruction)
+    auto flush = [&]() {
+        __syncthreads();
+        const int n = sh.n * a.dpad;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const float x = sh.pend[i];
+            if (x != 0.0f) {
+                const int s = i / a.dpad, e = i - s * a.dpad;
+                unsafeAtomicAdd(Tc + (int64_t)sh_ids[s] * a.dpad + e, x);
+                sh.pend[i] = 0.0f;
+            }
+        }
+        __syncthreads();
+    };
 
-        const int32_t tv = source_sample(a.g, wd.w[0], wd.w[1]);
-        const int32_t v = untag(tv);
-        const int32_t c = target_sample(a.g, v, wd.w[2], wd.w[3]);
-        if (c < 0) {
-            if (lane == 0) atomicAdd(a.skipped, 1ull);
-            continue;
-        }
-        int32_t id[KMAX + 1];
-        bool hot[KMAX + 1];
-        id[0] = c;
+    uint32_t round = 0;
+    for (; r0 < a.count; r0 += ngroups) {
+        const uint64_t t = a.mode == 2 ? r0 : r0 + gib;
+        if (t < a.count) {
+            const uint64_t s = a.begin + t;
+            SampleWords<G, NSLOT> wd;
+            wd.draw(a.seed, 0, s, lane);
+
+            const int32_t tv = source_sample(a.g, wd.w[0], wd.w[1]);
+            const int32_t v = untag(tv);
+            const int32_t c = target_sample(a.g, v, wd.w[2], wd.w[3]);
+            if (c < 0) {
+                if (lane == 0) atomicAdd(a.skipped, 1ull);
+            } else {
+                int32_t id[KMAX + 1];
+                bool hot[KMAX + 1];
+                id[0] = c;
 #pragma unroll
-        for (int j = 0; j < KMAX; ++j)
-            id[j + 1] = (j < a.K) ? negative_sample(a.g, wd.w[4 + 2 * j], wd.w[5 + 2 * j]) : -1;
+                for (int j = 0; j < KMAX; ++j)
+                    id[j + 1] = (j < a.K) ? negative_sample(a.g, wd.w[4 + 2 * j], wd.w[5 + 2 * j]) : -1;
 #pragma unroll
-        for (int k = 0; k <= KMAX; ++k) {
-            hot[k] = scatter_atomic<MODE>(id[k]);
-            id[k] = id[k] < 0 ? -1 : untag(id[k]);
+                for (int k = 0; k <= KMAX; ++k) {
+                    hot[k] = scatter_atomic<MODE>(id[k]);
+                    id[k] = id[k] < 0 ? -1 : untag(id[k]);
+                }
+                const float alpha = alpha_at(s + base, a.alpha0, a.total);
+                sgd_update<G, M, KMAX, MODE>(a, s_sig, lane, ev, v, id, scatter_atomic<MODE>(tv), hot, alpha, shared,
+                                             mf, sh);
+            }
         }
-        const float alpha = alpha_at(s + base, a.alpha0, a.total);
-        sgd_update<G, M, KMAX, MODE>(a, s_sig, lane, ev, v, id, scatter_atomic<MODE>(tv), hot, alpha, shared, mf);
+        if constexpr (MODE == MODE_HYBRID) {
+            if (sh.n > 0 && ++round == (uint32_t)a.sh_flush) {
+                flush();
+                round = 0;
+            }
+        }
+    }
+    if constexpr (MODE == MODE_HYBRID) {
+        if (sh.n > 0) flush();
     }
 }
 
@@ -351,7 +458,7 @@ __global__ void __launch_bounds__(256) walk_pairs_kernel(EdgeArgs a, WalkArgs w)
                 }
                 slot += 2 * a.K;
                 sgd_update<G, M, KMAX, MODE>(a, s_sig, lane, ev, untag(tvi), id, scatter_atomic<MODE>(tvi), hot,
-                                             alpha, false, false);
+                                             alpha, false, false, ShState{nullptr, nullptr, 0});
             }
         }
     }

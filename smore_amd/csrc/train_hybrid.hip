@@ -6,9 +6,11 @@ namespace smore {
 
 template <int G, int M>
 static hipError_t go(const EdgeArgs& a, int grid, hipStream_t st) {
-    if (a.K <= 5) hipLaunchKernelGGL((edge_train_kernel<G, M, 5, MODE_HYBRID>), dim3(grid), dim3(256), 0, st, a);
-    else if (a.K <= 10) hipLaunchKernelGGL((edge_train_kernel<G, M, 10, MODE_HYBRID>), dim3(grid), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((edge_train_kernel<G, M, 20, MODE_HYBRID>), dim3(grid), dim3(256), 0, st, a);
+    const size_t lds = sh_lds_bytes(a.sh_rows, a.dpad);
+    if (a.K <= 5) hipLaunchKernelGGL((edge_train_kernel<G, M, 5, MODE_HYBRID>), dim3(grid), dim3(256), lds, st, a);
+    else if (a.K <= 10)
+        hipLaunchKernelGGL((edge_train_kernel<G, M, 10, MODE_HYBRID>), dim3(grid), dim3(256), lds, st, a);
+    else hipLaunchKernelGGL((edge_train_kernel<G, M, 20, MODE_HYBRID>), dim3(grid), dim3(256), lds, st, a);
     return hipGetLastError();
 }
 

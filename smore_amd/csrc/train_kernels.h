@@ -13,6 +13,12 @@ struct EdgeArgs {
     float* C;                      // [V][dpad] (== W for shared-table models)
     unsigned long long* skipped;   // samples whose source had no out-edge
     const double* tcum;            // Go semantics: per-vertex prefix sums of edge weights
+    // hybrid write-combining of the super-hot context rows (edge kernel only):
+    // open-addressing hash {id, slot} (SH_HASH entries, id -1 = empty), the
+    // slot -> id list, sh_rows slots (0 = off), a block flush every sh_flush rounds
+    const int2* sh_hash;
+    const int32_t* sh_ids;
+    int sh_rows, sh_flush;
     uint64_t begin, count, total, seed;
     double alpha0;
     float reg;
@@ -29,6 +35,12 @@ struct WalkArgs {
 };
 
 int lanes_of(int dpad);
+constexpr int SH_HASH = 256;   // entries of the super-hot row hash (power of two)
+// dynamic LDS of the hybrid edge kernel: hash, slot ids, pending deltas
+inline size_t sh_lds_bytes(int sh_rows, int dpad) {
+    return sh_rows > 0 ? SH_HASH * 8 + (size_t)sh_rows * 4 + (size_t)sh_rows * dpad * 4 : 0;
+}
+inline uint32_t sh_hash_of(int32_t id) { return ((uint32_t)id * 2654435761u) >> 24; }
 hipError_t launch_go_edge(const EdgeArgs& a, int grid, hipStream_t st);
 hipError_t launch_go_walk(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st);
 hipError_t launch_go_sample(const DevGraph& g, const double* tcum, uint64_t seed, uint64_t begin, uint64_t count,

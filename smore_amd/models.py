@@ -6,7 +6,8 @@ loop is one HIP launch per chunk through the C ABI.
 Differences from the reference, all deliberate and documented in DESIGN.md:
   * draws come from the seeded Philox spec (`seed`), not random_device;
   * `workers` is accepted for signature parity; the GPU runs one Hogwild
-    stream of samples whose learning rate follows the 1-worker schedule;
+    stream of samples whose learning rate follows the 1-worker schedule
+    (scatter "hybrid" by default: atomic adds for hot rows, DESIGN.md 8);
   * embeddings are fp32.
 """
 import sys
@@ -34,7 +35,7 @@ class _EdgeModel:
     model = None
     count_base = 0
 
-    def __init__(self, device=0, mode="hogwild", seed=1):
+    def __init__(self, device=0, mode="hybrid", seed=1):
         self.pnet = ProNet(device)
         self.mode = mode
         self.seed = seed
@@ -96,7 +97,7 @@ class MF(_EdgeModel):
     """MF (src/model/MF.{h,cpp}): UpdateFactorizedPair on one table."""
     model = "mf"
 
-    def __init__(self, device=0, mode="hogwild", seed=1):
+    def __init__(self, device=0, mode="hybrid", seed=1):
         super().__init__(device, mode, seed)
         self.pnet.SetNegativeMethod("no_degrees")   # src/model/MF.cpp:4-7
 
@@ -119,7 +120,7 @@ class BPR(_EdgeModel):
     """BPR (src/model/BPR.{h,cpp}): UpdateBPRPair, 5 rounds, one table."""
     model = "bpr"
 
-    def __init__(self, device=0, mode="hogwild", seed=1):
+    def __init__(self, device=0, mode="hybrid", seed=1):
         super().__init__(device, mode, seed)
         self.pnet.SetNegativeMethod("no_degrees")   # src/model/BPR.cpp:4-7
 

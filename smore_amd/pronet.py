@@ -183,6 +183,10 @@ class ProNet:
         self._chk(lib.smore_set_semantics(self.ctx, _lib.SEM[semantics]), "set_semantics")
         self.semantics = semantics
 
+    def set_write_combine(self, rows, flush_rounds=64):
+        """Hybrid scatter: LDS write-combining of the `rows` hottest context rows."""
+        self._chk(lib.smore_set_write_combine(self.ctx, int(rows), int(flush_rounds)), "set_write_combine")
+
     def set_hot_threshold(self, tau):
         self._chk(lib.smore_set_hot_threshold(self.ctx, float(tau)), "set_hot_threshold")
 

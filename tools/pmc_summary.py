@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 outputs of the bench into profiles/: per-launch HBM
+traffic of the hot kernel from separate FETCH_SIZE / WRITE_SIZE passes
+(MI355X_MICROARCH.md "HBM": FETCH_SIZE / WRITE_SIZE in KB, from the L2's
+memory-side request counters; WRITE_SIZE exact for float atomics and dword
+stores, FETCH_SIZE uncalibrated for 4-B-per-lane 64-B-segment gathers, so it
+is reported uncorrected) and the kernel-trace average duration.
+
+    python tools/pmc_summary.py --fetch F.csv --write W.csv --stats S.csv \
+        --config c4 --samples 134217728 --mode hybrid --out profiles/pmc_traffic.json
+"""
+import argparse
+import csv
+import json
+
+
+def per_dispatch(path, kernel):
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
+    if not vals:
+        raise SystemExit("no %s dispatches in %s" % (kernel, path))
+    return sum(vals) / len(vals), len(vals)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--stats", required=True)
+    ap.add_argument("--kernel", default="edge_train_kernel")
+    ap.add_argument("--config", required=True)
+    ap.add_argument("--samples", type=int, required=True)
+    ap.add_argument("--mode", required=True)
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    f, nf = per_dispatch(a.fetch, a.kernel)
+    w, nw = per_dispatch(a.write, a.kernel)
+    stats = [r for r in csv.DictReader(open(a.stats)) if a.kernel in r["Name"]]
+    avg_ns = float(stats[0]["AverageNs"]) if stats else None
+    out = {
+        "config": a.config, "samples": a.samples, "mode": a.mode,
+        "kernel": stats[0]["Name"] if stats else a.kernel,
+        "dispatches_fetch": nf, "dispatches_write": nw,
+        "fetch_size_kb": f, "write_size_kb": w,
+        "hbm_bytes_per_launch": (f + w) * 1024.0,
+        "fetch_bytes_per_sample": f * 1024.0 / a.samples,
+        "write_bytes_per_sample": w * 1024.0 / a.samples,
+        "kernel_avg_ns": avg_ns,
+        "note": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; units KB; "
+                "FETCH_SIZE uncorrected (uncalibrated for this access shape) and includes Infinity-Cache hits",
+    }
+    json.dump(out, open(a.out, "w"), indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -51,9 +51,11 @@ def main():
     draws = pn.sample_edges("line2", 1 << 40, 200000, 5, 99991)   # held-out draws
     total = args.samples + 1
     for spec in args.modes:
-        mode, _, tau = spec.partition(":")
-        if tau:
-            pn.set_hot_threshold(float(tau))
+        parts = spec.split(":")          # mode[:tau[:combine_rows[:flush_rounds]]]
+        mode = parts[0]
+        if len(parts) > 1:
+            pn.set_hot_threshold(float(parts[1]))
+        pn.set_write_combine(int(parts[2]) if len(parts) > 2 else 32, int(parts[3]) if len(parts) > 3 else 64)
         pn.alloc_tables(args.dim, 2)
         pn.init_table_uniform(0, 3)
         pn.zero_table(1)
