@@ -29,6 +29,15 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
 
+def rec_width(K):
+    """int32 words of a pre-drawn sample record (train_kernels.h rec_width)."""
+    kmax = 5 if K <= 5 else 10 if K <= 10 else 20
+    r = 4
+    while r < 2 + kmax:
+        r *= 2
+    return r
+
+
 def algorithmic_bytes(dim, K):
     """R = (2+K)*d*4 + 8 (vertex alias) + 16 (offset pair)
     + 8 (context alias) + 4 (target vid) + 8K (negative alias); W = (2+K)*d*4."""
@@ -138,8 +147,13 @@ def main():
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
+    draw_ms = upd_ms = 0.0
     for k in range(args.warmup, args.warmup + args.steps):
         step(k)
+        ph = pn.last_phase_ms()      # waits for this step's events (a few us of host gap)
+        if ph is not None:
+            draw_ms += ph[0]
+            upd_ms += ph[1]
     ev1.record(stream)
     torch.cuda.synchronize()
     if dist:
@@ -155,8 +169,13 @@ def main():
 
     updates = S * args.steps * world
     R, Wb = algorithmic_bytes(args.dim, K)
-    launch_s = gpu_ms / 1e3 / args.steps            # avg per-launch time on the launch stream
-    achieved = R * S / launch_s / 1e9
+    step_s = gpu_ms / 1e3 / args.steps              # avg per-step time on the launch stream
+    # dominant kernel = the update kernel (gather/update/scatter); its algorithmic
+    # reads are the K+2 rows plus the 32-B pre-drawn record of each sample
+    rec_b = 4 * rec_width(K)
+    R_upd = (2 + K) * args.dim * 4 + rec_b
+    launch_s = upd_ms / 1e3 / args.steps if upd_ms > 0 else step_s
+    achieved = R_upd * S / launch_s / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
@@ -188,11 +207,16 @@ def main():
                        "samples_per_step_per_gpu": S, "scatter": args.mode,
                        "sync": ("%s every %d steps" % (args.sync, args.sync_every)) if world > 1 else "none",
                        "parallelism": "replicas%d" % world},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "roofline": {"bound": "hbm", "kernel": "edge_train_kernel (gather/update/scatter)",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "bytes_per_update_read": R, "bytes_per_update_write": Wb,
-                         "achieved_rw": round((R + Wb) * S / launch_s / 1e9, 1),
-                         "kernel_ms_per_launch": round(launch_s * 1e3, 3)},
+                         "bytes_per_update_read": R_upd, "bytes_per_update_write": Wb,
+                         "achieved_rw": round((R_upd + Wb) * S / launch_s / 1e9, 1),
+                         "kernel_ms_per_launch": round(launch_s * 1e3, 3),
+                         "draw_kernel_ms_per_launch": round(draw_ms / args.steps, 3),
+                         "path": {"bytes_per_update_read": R, "achieved": round(R * S / step_s / 1e9, 1),
+                                  "frac": round(R * S / step_s / 1e9 / HBM_PEAK_GBS, 4),
+                                  "ms_per_step": round(step_s * 1e3, 3)}},
             "cpu_baseline": cpu,
             "skipped_samples": int(skipped),
         }

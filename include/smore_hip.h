@@ -175,6 +175,10 @@ int smore_hot_rows(const smore_ctx* ctx, int64_t* hot_w, int64_t* hot_c);
 int smore_skipped(smore_ctx* ctx, uint64_t* skipped);
 /* milliseconds of the last training launch (HIP events on the launch stream) */
 float smore_last_kernel_ms(const smore_ctx* ctx);
+/* the last LINE/MF edge launch split by phase: total ms of the draw kernels
+ * (sampling, train_draw.hip) and of the update kernels (gather/update/scatter);
+ * SMORE_ESTATE if the last launch was not an edge launch */
+int smore_last_phase_ms(const smore_ctx* ctx, float* draw_ms, float* update_ms);
 
 /* replaces: DeepWalk::Train (src/model/DeepWalk.cpp:98-155): walks
  * [walk_begin, walk_end) of walk_times*V, start vertices order[] (host,

@@ -61,6 +61,11 @@ struct smore_ctx {
     int32_t* d_sh_ids = nullptr;
     int sh_rows = 0;
     int sh_max = 32, sh_flush = 16;
+    // pre-drawn edge-sample records (train_draw.hip) and per-phase timing
+    int32_t* d_rec = nullptr;
+    size_t rec_cap = 0;                 // int32 words
+    std::vector<hipEvent_t> phase_ev;   // {before draw 0, after draw 0, after update 0, after draw 1, ...}
+    int phase_n = 0;                    // chunks of the last edge launch
 };
 
 namespace {
@@ -180,6 +185,8 @@ void smore_destroy(smore_ctx* c) {
     dfree(c->d_sig); dfree(c->d_skipped); dfree(c->d_table[0]); dfree(c->d_table[1]);
 
     dfree(c->d_order); dfree(c->d_walks); dfree(c->d_lens); dfree(c->d_tcum); dfree(c->d_sh_hash); dfree(c->d_sh_ids);
+    dfree(c->d_rec);
+    for (hipEvent_t e : c->phase_ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -394,9 +401,11 @@ int smore_table_device(smore_ctx* c, int which, void** dptr, int64_t* stride) {
 // W-rows through the vertex table, C-rows through the negative and context
 // tables and the CSR targets (one union set for shared-table models).  Written
 // in place into the existing device arrays; the host graph stays untagged.
+constexpr double SH_STALE_MAX = 4096.0;
+
 static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
     char key[128];
-    snprintf(key, sizeof key, "%d/%d/%lld/%.9g", model, K, (long long)M, c->hot_tau);
+    snprintf(key, sizeof key, "%d/%d/%lld/%.9g/%d/%d", model, K, (long long)M, c->hot_tau, c->sh_max, c->sh_flush);
     if (c->hot_key == key) return SMORE_OK;
     if (c->g.V >= ((int64_t)1 << 30)) return fail(c, SMORE_EINVAL, "hybrid scatter needs V < 2^30");
     std::vector<double> ps, pn, pc;
@@ -417,7 +426,11 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
         std::vector<std::pair<double, int32_t>> r;
         for (int64_t v = 0; v < V; ++v) {
             const double p = model == SMORE_LINE2 ? pc[v] + negs * pn[v] : ps[v] + pc[v] + negs * pn[v];
-            if (hc[v]) r.push_back({p, (int32_t)v});
+            // bounded staleness: a combined row's pending deltas are invisible to
+            // other workgroups for up to sh_flush rounds, i.e. about
+            // M * p * sh_flush updates; rows above SH_STALE_MAX stay on atomics
+            // (on small graphs that is every hot row)
+            if (hc[v] && (double)M * p * c->sh_flush <= SH_STALE_MAX) r.push_back({p, (int32_t)v});
         }
         const int64_t cap = std::max<int64_t>(0, std::min<int64_t>(c->sh_max, 8192 / std::max(1, c->dpad)));
         const int64_t n = std::min<int64_t>(cap, (int64_t)r.size());
@@ -491,6 +504,13 @@ static int edge_grid(smore_ctx* c, const EdgeArgs& a) {
     const int64_t groups_per_block = 256 / G;
     const int64_t need = ((int64_t)a.count + groups_per_block - 1) / groups_per_block;
     if (need < grid) grid = need;
+    // Hogwild concurrency cap: at most V/16 resident sample groups (each keeps
+    // two samples in flight), so that on small graphs the expected number of
+    // in-flight updates per row stays O(1) as in the reference's few-thread
+    // Hogwild; the benchmark graphs (V >= 1M) are far from the cap.
+    const int64_t cap_groups = std::max<int64_t>(1, c->g.V / 16);
+    const int64_t cap = (cap_groups + groups_per_block - 1) / groups_per_block;
+    if (cap < grid) grid = cap;
     return (int)(grid < 1 ? 1 : grid);
 }
 
@@ -554,10 +574,80 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
     a.sh_hash = c->d_sh_hash;
     a.sh_ids = c->d_sh_ids;
     a.sh_flush = std::max(1, c->sh_flush);
+    if (model == SMORE_BPR) {
+        HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+        HIPCHK(c, launch_edge_train(a, grid, c->stream));
+        HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+        c->timed = true;
+        c->phase_n = 0;
+        return SMORE_OK;
+    }
+    if (SMORE_PIPE_DRAWS && pipe_draws(lanes_of(c->dpad), kmax_of(a.K))) {
+        // the update kernel draws its own samples (software-pipelined)
+        while (c->phase_ev.size() < 3) {
+            hipEvent_t e;
+            HIPCHK(c, hipEventCreate(&e));
+            c->phase_ev.push_back(e);
+        }
+        HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+        HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream));
+        HIPCHK(c, hipEventRecord(c->phase_ev[1], c->stream));
+        HIPCHK(c, launch_edge_train(a, grid, c->stream));
+        HIPCHK(c, hipEventRecord(c->phase_ev[2], c->stream));
+        HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+        c->timed = true;
+        c->phase_n = 1;
+        return SMORE_OK;
+    }
+    // edge models with few lanes per sample: draw kernel -> update kernel per
+    // chunk of samples (the record buffer is bounded at 4 GiB)
+    const int RW = rec_width(kmax_of(a.K));
+    const uint64_t chunk_max = ((uint64_t)1 << 30) / (uint64_t)RW;
+    const uint64_t chunk = std::min<uint64_t>(count, chunk_max);
+    if (c->rec_cap < chunk * RW) {
+        dfree(c->d_rec);
+        c->rec_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_rec, chunk * RW * sizeof(int32_t)));
+        c->rec_cap = chunk * RW;
+    }
+    const int nch = (int)((count + chunk - 1) / chunk);
+    while ((int)c->phase_ev.size() < 2 * nch + 1) {
+        hipEvent_t e;
+        HIPCHK(c, hipEventCreate(&e));
+        c->phase_ev.push_back(e);
+    }
+    const DevGraph dg = dev_graph(c);
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    HIPCHK(c, launch_edge_train(a, grid, c->stream));
+    HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream));
+    for (int k = 0; k < nch; ++k) {
+        const uint64_t b = (uint64_t)k * chunk, n = std::min<uint64_t>(chunk, count - b);
+        HIPCHK(c, launch_draw(dg, seed, begin + b, n, a.K, c->d_rec, c->d_skipped, c->stream));
+        HIPCHK(c, hipEventRecord(c->phase_ev[2 * k + 1], c->stream));
+        EdgeArgs ak = a;
+        ak.begin = begin + b;
+        ak.count = n;
+        ak.rec = c->d_rec;
+        HIPCHK(c, launch_edge_train(ak, grid, c->stream));
+        HIPCHK(c, hipEventRecord(c->phase_ev[2 * k + 2], c->stream));
+    }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
+    c->phase_n = nch;
+    return SMORE_OK;
+}
+
+int smore_last_phase_ms(const smore_ctx* c, float* draw_ms, float* update_ms) {
+    if (!c || !c->timed || c->phase_n <= 0) return SMORE_ESTATE;
+    float d = 0.0f, u = 0.0f, ms = 0.0f;
+    if (hipEventSynchronize(c->phase_ev[2 * c->phase_n]) != hipSuccess) return SMORE_EHIP;
+    for (int k = 0; k < c->phase_n; ++k) {
+        if (hipEventElapsedTime(&ms, c->phase_ev[2 * k], c->phase_ev[2 * k + 1]) != hipSuccess) return SMORE_EHIP;
+        d += ms;
+        if (hipEventElapsedTime(&ms, c->phase_ev[2 * k + 1], c->phase_ev[2 * k + 2]) != hipSuccess) return SMORE_EHIP;
+        u += ms;
+    }
+    if (draw_ms) *draw_ms = d;
+    if (update_ms) *update_ms = u;
     return SMORE_OK;
 }
 

@@ -125,6 +125,8 @@ __device__ __forceinline__ float group_sum(float p) {
     return p;
 }
 
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, const float4& v) { *reinterpret_cast<float4*>(p) = v; }
 

@@ -1,0 +1,47 @@
+// edge_inst.h -- instantiation helper for edge_train_kernel: one translation
+// unit per (scatter MODE, KMAX) (train_edge_<mode>_k<KMAX>.hip) so the build
+// compiles them in parallel.  Dispatch over (G, M) and the table layout
+// (SH = 0: LINE-2's two tables, 1: one shared table, LINE-1 / MF).
+#pragma once
+#include "edge_kernels.h"
+
+namespace smore {
+
+template <int KMAX, int MODE>
+struct EdgeInst {
+    template <int G, int M, int SH>
+    static hipError_t go(const EdgeArgs& a, int grid, hipStream_t st) {
+        const size_t lds = MODE == MODE_HYBRID ? sh_lds_bytes(a.sh_rows, a.dpad) : 0;
+        hipLaunchKernelGGL((edge_train_kernel<G, M, KMAX, MODE, SH>), dim3(grid), dim3(256), lds, st, a);
+        return hipGetLastError();
+    }
+    static hipError_t launch(const EdgeArgs& a, int grid, hipStream_t st) {
+        const int G = lanes_of(a.dpad), M = (a.dpad + G - 1) / G;
+#define X(g, m) \
+    if (G == g && M == m) return a.model == 0 ? go<g, m, 0>(a, grid, st) : go<g, m, 1>(a, grid, st);
+        SMORE_FOR_EACH_GM(X)
+#undef X
+        return hipErrorInvalidValue;
+    }
+    static const void* symbol(const EdgeArgs& a) {
+        const int G = lanes_of(a.dpad), M = (a.dpad + G - 1) / G;
+#define X(g, m)                                                                          \
+    if (G == g && M == m)                                                                \
+        return a.model == 0 ? (const void*)edge_train_kernel<g, m, KMAX, MODE, 0>        \
+                            : (const void*)edge_train_kernel<g, m, KMAX, MODE, 1>;
+        SMORE_FOR_EACH_GM(X)
+#undef X
+        return nullptr;
+    }
+};
+
+}  // namespace smore
+
+// defines launch_edge_<name>(a, grid, st) and edge_symbol_<name>(a)
+#define SMORE_EDGE_INST(name, KMAX, MODE)                                                  \
+    namespace smore {                                                                      \
+    hipError_t launch_edge_##name(const EdgeArgs& a, int grid, hipStream_t st) {           \
+        return EdgeInst<KMAX, MODE>::launch(a, grid, st);                                  \
+    }                                                                                      \
+    const void* edge_symbol_##name(const EdgeArgs& a) { return EdgeInst<KMAX, MODE>::symbol(a); } \
+    }

@@ -7,9 +7,10 @@
 // wave instruction; d=128: G=32, two 128-B segments).
 //
 // Per sample:
-//   Philox draws (each lane computes one 4-word block, broadcast by shuffle)
-//   -> alias draws: source, target (CSR + per-vertex context table), K
-//      negatives (all independent 8-B / 4-B loads)
+//   [edge models: the draws come pre-drawn from train_draw.hip, one 32-B
+//    record per sample, prefetched one round ahead; BPR / DeepWalk draw here:
+//    Philox words (each lane computes one 4-word block, broadcast by shuffle)
+//    -> alias draws: source, target, K negatives]
 //   -> gather of the K+2 rows into registers
 //   -> K+1 sequential Opt_SigmoidSGD / Opt_SGD steps (fmaf chain + pairwise
 //      lane tree; fastSigmoid table in LDS)
@@ -25,6 +26,14 @@ namespace smore {
 
 enum { MODE_STORE = 0, MODE_ATOMIC = 1, MODE_HYBRID = 3 };
 
+// 1: edge kernels with a lane per negative draw their own samples
+// (software-pipelined); 0 (default): every edge launch runs draw_kernel first.
+// Measured at C4 (2^27 samples, hybrid): fused-pipelined 127 ms vs
+// draw 22 + update 110 ms -- kept as an option.
+#ifndef SMORE_PIPE_DRAWS
+#define SMORE_PIPE_DRAWS 0
+#endif
+
 // minimum waves per SIMD the register allocator must allow, per scatter mode
 // (0 = compiler default); overridable at build time for tuning.
 #ifndef SMORE_WAVES_STORE
@@ -34,7 +43,7 @@ enum { MODE_STORE = 0, MODE_ATOMIC = 1, MODE_HYBRID = 3 };
 #define SMORE_WAVES_ATOMIC 0
 #endif
 #ifndef SMORE_WAVES_HYBRID
-#define SMORE_WAVES_HYBRID 0
+#define SMORE_WAVES_HYBRID 4
 #endif
 constexpr int waves_of(int mode) {
     return mode == MODE_STORE ? SMORE_WAVES_STORE : mode == MODE_ATOMIC ? SMORE_WAVES_ATOMIC : SMORE_WAVES_HYBRID;
@@ -138,23 +147,16 @@ struct SlotWords {
 // delta), or kept as the value if it is stored (only the last occurrence of an
 // id stores, and it holds the final value).  A reference to W_v's own row in
 // a shared table is never scattered itself: W_v's scatter carries it.
-template <int G, int M, int KMAX, int MODE>
-__device__ __forceinline__ void sgd_update(const EdgeArgs& a, const float* s_sig, int lane,
-                                           const bool (&ev)[M], int32_t v, const int32_t (&id)[KMAX + 1],
-                                           bool hotw, const bool (&hot)[KMAX + 1], float alpha, bool shared,
-                                           bool mf, const ShState& sh) {
-    constexpr bool DELTA = MODE == MODE_ATOMIC || MODE == MODE_HYBRID;
+template <int G, int M, int KMAX>
+__device__ __forceinline__ void gather_rows(const EdgeArgs& a, int lane, const bool (&ev)[M], int32_t v,
+                                            const int32_t (&id)[KMAX + 1], bool shared, float (&wv)[M],
+                                            float (&rows)[KMAX + 1][M]) {
     const int dpad = a.dpad;
-    float* const Tw = a.W;
-    float* const Tc = shared ? a.W : a.C;
-    const int32_t vs = shared ? v : -2;   // id of W_v inside the context table
-
-    // ---- gather
-    float wv[M], rows[KMAX + 1][M];
+    const float* const Tc = shared ? a.W : a.C;
     {
-        const float* wp = Tw + (int64_t)v * dpad + lane;
+        const float* wp = a.W + (int64_t)(v < 0 ? 0 : v) * dpad + lane;
 #pragma unroll
-        for (int m = 0; m < M; ++m) wv[m] = ev[m] ? wp[m * G] : 0.0f;
+        for (int m = 0; m < M; ++m) wv[m] = (ev[m] && v >= 0) ? wp[m * G] : 0.0f;
     }
 #pragma unroll
     for (int k = 0; k <= KMAX; ++k) {
@@ -162,6 +164,24 @@ __device__ __forceinline__ void sgd_update(const EdgeArgs& a, const float* s_sig
 #pragma unroll
         for (int m = 0; m < M; ++m) rows[k][m] = (ev[m] && id[k] >= 0) ? cp[m * G] : 0.0f;
     }
+}
+
+// sgd_update on rows already gathered by gather_rows (wv, rows are consumed).
+// SHARED: -1 = runtime (a.model), 0 = two tables (LINE-2), 1 = one table.
+template <int G, int M, int KMAX, int MODE, int SHARED = -1>
+__device__ __forceinline__ void sgd_update_rows(const EdgeArgs& a, const float* s_sig, int lane,
+                                                const bool (&ev)[M], int32_t v, const int32_t (&id)[KMAX + 1],
+                                                bool hotw, const bool (&hot)[KMAX + 1], float alpha, bool shared_rt,
+                                                bool mf_rt, const ShState& sh, float (&wv)[M],
+                                                float (&rows)[KMAX + 1][M]) {
+    constexpr bool DELTA = MODE == MODE_ATOMIC || MODE == MODE_HYBRID;
+    const bool shared = SHARED < 0 ? shared_rt : SHARED == 1;
+    const bool mf = SHARED == 0 ? false : mf_rt;
+    const int dpad = a.dpad;
+    float* const Tw = a.W;
+    float* const Tc = shared ? a.W : a.C;
+    const int32_t vs = shared ? v : -2;   // id of W_v inside the context table
+
     // super-hot rows: add this block's pending deltas
     int slot[KMAX + 1];
     int slotw = -1;
@@ -205,8 +225,8 @@ __device__ __forceinline__ void sgd_update(const EdgeArgs& a, const float* s_sig
 #pragma unroll
             for (int m = 0; m < M; ++m) rows[k][m] = wv[m];
         }
-    float wv0[DELTA ? M : 1];
-    if constexpr (DELTA) {
+    float wv0[(DELTA && SHARED != 0) ? M : 1];
+    if constexpr (DELTA && SHARED != 0) {
 #pragma unroll
         for (int m = 0; m < M; ++m) wv0[m] = wv[m];
     }
@@ -267,7 +287,9 @@ __device__ __forceinline__ void sgd_update(const EdgeArgs& a, const float* s_sig
         for (int m = 0; m < M; ++m) {
             if (!ev[m]) continue;
             if (DELTA && hotw) {
-                const float d = shared ? wv[m] - wv0[m] : e[m];
+                float d = e[m];
+                if constexpr (SHARED != 0)
+                    if (shared) d = wv[m] - wv0[m];
                 if (MODE == MODE_HYBRID && slotw >= 0) atomicAdd(sh.pend + slotw * dpad + lane + m * G, d);
                 else unsafeAtomicAdd(wq + m * G, d);
             } else {
@@ -304,10 +326,21 @@ __device__ __forceinline__ void sgd_update(const EdgeArgs& a, const float* s_sig
     }
 }
 
+// gather + update (callers without row prefetch)
+template <int G, int M, int KMAX, int MODE>
+__device__ __forceinline__ void sgd_update(const EdgeArgs& a, const float* s_sig, int lane, const bool (&ev)[M],
+                                           int32_t v, const int32_t (&id)[KMAX + 1], bool hotw,
+                                           const bool (&hot)[KMAX + 1], float alpha, bool shared, bool mf,
+                                           const ShState& sh) {
+    float wv[M], rows[KMAX + 1][M];
+    gather_rows<G, M, KMAX>(a, lane, ev, v, id, shared, wv, rows);
+    sgd_update_rows<G, M, KMAX, MODE>(a, s_sig, lane, ev, v, id, hotw, hot, alpha, shared, mf, sh, wv, rows);
+}
+
 // ------------------------------------------------------------------ edge kernel
 // LINE-2 (W,C), LINE-1 (W,W), MF (W,W, Opt_SGD): the model is a wave-uniform
 // runtime switch; the scatter MODE is compile-time.
-template <int G, int M, int KMAX, int MODE>
+template <int G, int M, int KMAX, int MODE, int SHARED>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(waves_of(MODE))))
 edge_train_kernel(EdgeArgs a) {
     __shared__ float s_sig[1001];
@@ -328,7 +361,6 @@ edge_train_kernel(EdgeArgs a) {
     }
     __syncthreads();
 
-    constexpr int NSLOT = 4 + 2 * KMAX;
     const int lane = threadIdx.x & (G - 1);
     const uint64_t gpb = blockDim.x / G;                 // groups per block
     uint64_t r0 = (uint64_t)blockIdx.x * gpb;            // block-uniform round base
@@ -338,8 +370,8 @@ edge_train_kernel(EdgeArgs a) {
         if (blockIdx.x != 0 || gib != 0) return;
         ngroups = 1;
     }
-    const bool shared = a.model != 0;
-    const bool mf = a.model == 2;
+    const bool shared = SHARED == 1;  // LINE-1 / MF: one table (host dispatches on a.model)
+    const bool mf = SHARED == 1 && a.model == 2;
     bool ev[M];                      // element lane + G*m exists
 #pragma unroll
     for (int m = 0; m < M; ++m) ev[m] = lane + G * m < a.dpad;
@@ -361,41 +393,184 @@ edge_train_kernel(EdgeArgs a) {
         __syncthreads();
     };
 
+    const uint64_t step = a.mode == 2 ? 1 : ngroups;
     uint32_t round = 0;
-    for (; r0 < a.count; r0 += ngroups) {
-        const uint64_t t = a.mode == 2 ? r0 : r0 + gib;
-        if (t < a.count) {
-            const uint64_t s = a.begin + t;
-            SampleWords<G, NSLOT> wd;
-            wd.draw(a.seed, 0, s, lane);
-
-            const int32_t tv = source_sample(a.g, wd.w[0], wd.w[1]);
-            const int32_t v = untag(tv);
-            const int32_t c = target_sample(a.g, v, wd.w[2], wd.w[3]);
-            if (c < 0) {
-                if (lane == 0) atomicAdd(a.skipped, 1ull);
-            } else {
-                int32_t id[KMAX + 1];
-                bool hot[KMAX + 1];
-                id[0] = c;
+    // the update of one sample, ids tagged as drawn (c < 0: source without out-edges)
+    auto process = [&](uint64_t t, int32_t tv, int32_t c, const int32_t (&negs)[KMAX]) {
+        const int32_t v = untag(tv);
+        int32_t id[KMAX + 1];
+        bool hot[KMAX + 1];
+        id[0] = c;
 #pragma unroll
-                for (int j = 0; j < KMAX; ++j)
-                    id[j + 1] = (j < a.K) ? negative_sample(a.g, wd.w[4 + 2 * j], wd.w[5 + 2 * j]) : -1;
+        for (int j = 0; j < KMAX; ++j) id[j + 1] = (j < a.K) ? negs[j] : -1;
 #pragma unroll
-                for (int k = 0; k <= KMAX; ++k) {
-                    hot[k] = scatter_atomic<MODE>(id[k]);
-                    id[k] = id[k] < 0 ? -1 : untag(id[k]);
-                }
-                const float alpha = alpha_at(s + base, a.alpha0, a.total);
-                sgd_update<G, M, KMAX, MODE>(a, s_sig, lane, ev, v, id, scatter_atomic<MODE>(tv), hot, alpha, shared,
-                                             mf, sh);
-            }
+        for (int k = 0; k <= KMAX; ++k) {
+            hot[k] = scatter_atomic<MODE>(id[k]);
+            id[k] = id[k] < 0 ? -1 : untag(id[k]);
         }
+        const float alpha = alpha_at(a.begin + t + base, a.alpha0, a.total);
+        float wv[M], rows[KMAX + 1][M];
+        gather_rows<G, M, KMAX>(a, lane, ev, v, id, shared, wv, rows);
+        sgd_update_rows<G, M, KMAX, MODE, SHARED>(a, s_sig, lane, ev, v, id, scatter_atomic<MODE>(tv), hot, alpha,
+                                                  shared, mf, sh, wv, rows);
+    };
+    auto maybe_flush = [&]() {
         if constexpr (MODE == MODE_HYBRID) {
             if (sh.n > 0 && ++round == (uint32_t)a.sh_flush) {
                 flush();
                 round = 0;
             }
+        }
+    };
+
+    if constexpr (SMORE_PIPE_DRAWS && pipe_draws(G, KMAX)) {
+        // Fused, software-pipelined draws.  A sample's draws are a dependent
+        // chain: vertex alias (A) -> CSR offsets of the source (B) -> context
+        // alias + target (C); its K negative-alias reads are independent.  Each
+        // round of this group issues stage A for sample t+3S, B for t+2S and C
+        // (with the negatives) for t+S before gathering the rows of sample t
+        // (stage D), so the chain overlaps the update and a round costs one
+        // memory round trip.  Lane K of the group carries the source/target
+        // chain, lane j < K negative j; each lane computes the one Philox
+        // block its draw needs (slots of DESIGN.md "RNG spec").  The ids reach
+        // the update by group shuffles.  Same draws as train_draw.hip.
+        const int64_t S = (int64_t)step, n = (int64_t)a.count;
+        const int64_t g_off = a.mode == 2 ? 0 : (int64_t)gib;
+        const bool srcl = lane == a.K, negl = lane < a.K;
+        const uint2* atab = srcl ? a.g.vtab : a.g.ntab;
+        const uint32_t ablk = srcl ? 0u : 1u + (uint32_t)(lane >> 1);
+        const bool odd = lane & 1;
+        int32_t vB = -1, vC = -1, vD = -1, cD = -1, nD = -1;
+        uint32_t w2B = 0, w3B = 0, w2C = 0;
+        int64_t eC = -1;
+        for (int64_t rr = (int64_t)r0 - 3 * S; rr < n; rr += S) {
+            const int64_t tD = rr + g_off, tC = tD + S, tB = tD + 2 * S, tA = tD + 3 * S;
+            // A (lane K): vertex alias of sample tA; lanes < K: negative alias of tC
+            const int64_t tx = srcl ? tA : tC;
+            const bool ax = (srcl || negl) && tx >= 0 && tx < n;
+            const uint4 b = philox_block(a.seed, 0, a.begin + (uint64_t)(ax ? tx : 0), ablk);
+            const uint32_t kidx = srcl ? b.y : (odd ? b.z : b.x);
+            const uint32_t kp = srcl ? b.x : (odd ? b.w : b.y);
+            const uint32_t ai = draw_index(kidx, a.g.V);
+            uint2 ae = make_uint2(0xFFFFFFFFu, 0u);
+            if (ax) ae = atab[ai];
+            // B (lane K): CSR offsets of the source of sample tB
+            int64_t o0 = 0, o1 = 0;
+            const bool bx = srcl && tB >= 0 && tB < n;
+            if (bx) {
+                const int32_t v = untag(vB);
+                o0 = a.g.offsets[v];
+                o1 = a.g.offsets[v + 1];
+            }
+            // C (lane K): context alias entry and target of sample tC
+            uint2 ce = make_uint2(0u, 0u);
+            int32_t tt = -1;
+            const bool cx = srcl && tC >= 0 && tC < n && eC >= 0;
+            if (cx) {
+                ce = a.g.ctab[eC];
+                tt = a.g.targets[eC];
+            }
+            // D: update sample tD
+            const int32_t tv = __shfl(vD, a.K, G);
+            const int32_t c = __shfl(cD, a.K, G);
+            int32_t negs[KMAX];
+#pragma unroll
+            for (int j = 0; j < KMAX; ++j) negs[j] = __shfl(nD, j, G);
+            if (tD >= 0 && tD < n) {
+                if (c < 0) {
+                    if (lane == 0) atomicAdd(a.skipped, 1ull);
+                } else {
+                    process((uint64_t)tD, tv, c, negs);
+                }
+            }
+            // advance the stages
+            const int32_t pick = alias_pick(ai, ae, kp);
+            vD = vC;
+            cD = cx ? (w2C < ce.x ? tt : (int32_t)ce.y) : -1;
+            nD = pick;
+            vC = vB;
+            w2C = w2B;
+            eC = (bx && o1 > o0) ? o0 + (int64_t)draw_index(w3B, (uint32_t)(o1 - o0)) : -1;
+            vB = pick;
+            w2B = b.z;
+            w3B = b.w;
+            maybe_flush();
+        }
+    } else if (a.mode == 2) {
+        // serial: records in order, gather after the previous sample's scatter
+        constexpr int RW = rec_width(KMAX);
+        for (; r0 < a.count; ++r0) {
+            const i32x4* p = reinterpret_cast<const i32x4*>(a.rec + r0 * RW);
+            i32x4 r[RW / 4];
+#pragma unroll
+            for (int q = 0; q < RW / 4; ++q) r[q] = p[q];
+            if (r[0][1] >= 0) {   // c < 0: counted by the draw kernel
+                int32_t negs[KMAX];
+#pragma unroll
+                for (int j = 0; j < KMAX; ++j) negs[j] = r[(j + 2) / 4][(j + 2) % 4];
+                process(r0, r[0][0], r[0][1], negs);
+            }
+        }
+    } else {
+        // Hogwild modes: pre-drawn records (train_draw.hip), and the rows of
+        // the group's next sample are gathered BEFORE this sample's scatter:
+        // vector-memory ops retire in issue order (one vmcnt for loads, stores
+        // and atomics), so a gather issued after a scatter would wait for the
+        // scatter's acknowledgements too.  The next sample may thus read a row
+        // this sample is about to write -- the staleness every other resident
+        // group already has (Hogwild); the serial mode above keeps strict order.
+        constexpr int RW = rec_width(KMAX);
+        const uint64_t S = step;
+        struct Ids {
+            int32_t v, id[KMAX + 1];
+            bool hotw, hot[KMAX + 1], live;
+        };
+        auto decode = [&](uint64_t t, const i32x4 (&r)[RW / 4], Ids& x) {
+            x.live = t < a.count && r[0][1] >= 0;   // c < 0: counted by the draw kernel
+            x.hotw = scatter_atomic<MODE>(r[0][0]);
+            x.v = x.live ? untag(r[0][0]) : -1;
+#pragma unroll
+            for (int k = 0; k <= KMAX; ++k) {
+                const int32_t w = (k == 0) ? r[0][1] : (k - 1 < a.K ? r[(k + 1) / 4][(k + 1) % 4] : -1);
+                x.hot[k] = scatter_atomic<MODE>(w);
+                x.id[k] = (!x.live || w < 0) ? -1 : untag(w);
+            }
+        };
+        auto load_rec = [&](uint64_t t, i32x4 (&r)[RW / 4]) {
+#pragma unroll
+            for (int q = 0; q < RW / 4; ++q) r[q] = i32x4{-1, -1, -1, -1};
+            if (t < a.count) {
+                const i32x4* p = reinterpret_cast<const i32x4*>(a.rec + t * RW);
+#pragma unroll
+                for (int q = 0; q < RW / 4; ++q) r[q] = __builtin_nontemporal_load(p + q);
+            }
+        };
+        i32x4 rr[RW / 4];
+        Ids xa, xb;
+        float wva[M], rowsa[KMAX + 1][M], wvb[M], rowsb[KMAX + 1][M];
+        uint64_t t = r0 + gib;
+        load_rec(t, rr);
+        decode(t, rr, xa);
+        gather_rows<G, M, KMAX>(a, lane, ev, xa.v, xa.id, shared, wva, rowsa);
+        load_rec(t + S, rr);
+        for (; r0 < a.count; r0 += S) {
+            t = r0 + gib;
+            decode(t + S, rr, xb);
+            load_rec(t + 2 * S, rr);
+            gather_rows<G, M, KMAX>(a, lane, ev, xb.v, xb.id, shared, wvb, rowsb);
+            if (xa.live) {
+                const float alpha = alpha_at(a.begin + t + base, a.alpha0, a.total);
+                sgd_update_rows<G, M, KMAX, MODE, SHARED>(a, s_sig, lane, ev, xa.v, xa.id, xa.hotw, xa.hot, alpha,
+                                                         shared, mf, sh, wva, rowsa);
+            }
+            xa = xb;
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+                wva[m] = wvb[m];
+#pragma unroll
+                for (int k = 0; k <= KMAX; ++k) rowsa[k][m] = rowsb[k][m];
+            }
+            maybe_flush();
         }
     }
     if constexpr (MODE == MODE_HYBRID) {
@@ -600,10 +775,18 @@ __global__ void __launch_bounds__(256) bpr_train_kernel(EdgeArgs a) {
 }
 
 // ---------------------------------------------------------------- dispatch
-// (G, M) pairs for dpad in [4, 512]: G = min(64, pow2ceil(dpad/4)),
-// M = ceil(dpad / G).
+// (G, M) pairs for dpad in [4, 512]: G = min(64, pow2ceil(dpad / SMORE_EPL)),
+// M = ceil(dpad / G) (train_kernels.hip lanes_of; oracle orc_lane_width).
+#if SMORE_EPL == 1
+#define SMORE_FOR_EACH_GM(X) \
+    X(4, 1) X(8, 1) X(16, 1) X(32, 1) X(64, 1) X(64, 2) X(64, 3) X(64, 4) X(64, 5) X(64, 6) X(64, 7) X(64, 8)
+#elif SMORE_EPL == 2
+#define SMORE_FOR_EACH_GM(X) \
+    X(2, 2) X(4, 2) X(8, 2) X(16, 2) X(32, 2) X(64, 2) X(64, 3) X(64, 4) X(64, 5) X(64, 6) X(64, 7) X(64, 8)
+#else
 #define SMORE_FOR_EACH_GM(X) \
     X(1, 4) X(2, 4) X(4, 3) X(4, 4) X(8, 3) X(8, 4) X(16, 3) X(16, 4) X(32, 3) X(32, 4) \
     X(64, 3) X(64, 4) X(64, 5) X(64, 6) X(64, 7) X(64, 8)
+#endif
 
 }  // namespace smore

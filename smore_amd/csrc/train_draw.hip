@@ -1,0 +1,120 @@
+// train_draw.hip -- the sampling half of the edge hot path.
+//
+// LINE::Train's per-sample draws (src/model/LINE.cpp:171-176 -> SourceSample
+// src/proNet.cpp:647-657, TargetSample :671-683, and UpdatePair's K
+// NegativeSample calls :623-633; MF::Train and LINE order 1 the same) for a
+// range of global sample indices, written as one record per sample for the
+// update kernel (edge_kernels.h edge_train_kernel):
+//     rec[t] = {v, c, n_1 .. n_K, -1 ...}   (rec_width(KMAX) int32, tagged ids)
+// c = -1 when the source has no out-edge (the reference's TargetSample -1;
+// such samples are counted in *skipped and skipped by the update).
+//
+// Why a separate kernel: the draws are a 3-deep chain of dependent random
+// 8-16 B reads (vertex alias -> CSR offsets -> context alias + target) plus K
+// independent negative-alias reads.  Inside the update kernel every sample
+// waited on that chain before its row gathers; here one thread per sample
+// keeps thousands of chains in flight per CU (few registers), and the update
+// kernel sees one streaming 32-B read per sample.  Draws are identical to the
+// fused form (same Philox slots, same compares), so results are unchanged.
+#include "train_kernels.h"
+
+namespace smore {
+
+// PART: 0 = the whole record; 1 = {v, c} only; 2 = negatives only (a pass
+// whose only random reads are the negative table, small enough to stay in the
+// Infinity Cache while it runs)
+template <int KMAX, int PART>
+__global__ void __launch_bounds__(256) draw_kernel(DevGraph g, uint64_t seed, uint64_t begin, uint64_t count,
+                                                   int K, int32_t* rec, unsigned long long* skipped) {
+    constexpr int RW = rec_width(KMAX);
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= count) return;
+    const uint64_t s = begin + t;
+    // slots 0-3: source p, source index, target p, target index
+    int32_t* const r = rec + t * RW;
+    if constexpr (PART == 1) {
+        const uint4 b0 = philox_block(seed, 0, s, 0);
+        const uint32_t vi = draw_index(b0.y, g.V);
+        const int32_t tv = alias_pick(vi, g.vtab[vi], b0.x);
+        const int32_t c = target_sample(g, untag(tv), b0.z, b0.w);
+        __builtin_nontemporal_store(tv, r);
+        __builtin_nontemporal_store(c, r + 1);
+        if (c < 0) atomicAdd(skipped, 1ull);
+        return;
+    }
+    if constexpr (PART == 2) {
+#pragma unroll
+        for (int j = 0; j < KMAX; j += 2) {
+            if (j < K) {
+                const uint4 b = philox_block(seed, 0, s, 1 + j / 2);
+                const uint32_t i0 = draw_index(b.x, g.V);
+                __builtin_nontemporal_store(alias_pick(i0, g.ntab[i0], b.y), r + 2 + j);
+                if (j + 1 < K) {
+                    const uint32_t i1 = draw_index(b.z, g.V);
+                    __builtin_nontemporal_store(alias_pick(i1, g.ntab[i1], b.w), r + 3 + j);
+                }
+            }
+        }
+        return;
+    }
+    const uint4 b0 = philox_block(seed, 0, s, 0);
+    const uint32_t vi = draw_index(b0.y, g.V);
+    const uint2 ve = g.vtab[vi];
+    // slots 4+2j (index), 5+2j (p): block 1 + j/2, components 2(j&1), 2(j&1)+1
+    uint32_t nidx[KMAX], np[KMAX];
+    uint2 ne[KMAX];
+#pragma unroll
+    for (int j = 0; j < KMAX; j += 2) {
+        if (j < K) {
+            const uint4 b = philox_block(seed, 0, s, 1 + j / 2);
+            nidx[j] = draw_index(b.x, g.V);
+            np[j] = b.y;
+            if (j + 1 < KMAX) {
+                nidx[j + 1] = draw_index(b.z, g.V);
+                np[j + 1] = b.w;
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j)
+        if (j < K) ne[j] = g.ntab[nidx[j]];
+    const int32_t tv = alias_pick(vi, ve, b0.x);
+    const int32_t c = target_sample(g, untag(tv), b0.z, b0.w);
+    int32_t w[RW];
+    w[0] = tv;
+    w[1] = c;
+#pragma unroll
+    for (int j = 0; j < RW - 2; ++j) w[2 + j] = (j < KMAX && j < K) ? alias_pick(nidx[j], ne[j], np[j]) : -1;
+    i32x4* o = reinterpret_cast<i32x4*>(rec + t * RW);
+#pragma unroll
+    for (int q = 0; q < RW / 4; ++q) {
+        const i32x4 x = {w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
+        __builtin_nontemporal_store(x, o + q);
+    }
+    if (c < 0) atomicAdd(skipped, 1ull);
+}
+
+hipError_t launch_draw(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K, int32_t* rec,
+                       unsigned long long* skipped, hipStream_t st) {
+    const int block = 256;
+    const dim3 grid((unsigned)((count + block - 1) / block));
+#if SMORE_DRAW_SPLIT
+    // negatives first, then source/target (unused record words stay as written by
+    // the previous launch; the update kernel reads only words 0 .. 1+K)
+#define SMORE_DRAW(KM)                                                                                        \
+    hipLaunchKernelGGL((draw_kernel<KM, 2>), grid, dim3(block), 0, st, g, seed, begin, count, K, rec, skipped); \
+    hipLaunchKernelGGL((draw_kernel<KM, 1>), grid, dim3(block), 0, st, g, seed, begin, count, K, rec, skipped);
+#else
+#define SMORE_DRAW(KM) \
+    hipLaunchKernelGGL((draw_kernel<KM, 0>), grid, dim3(block), 0, st, g, seed, begin, count, K, rec, skipped);
+#endif
+    switch (kmax_of(K)) {
+        case 5: SMORE_DRAW(5) break;
+        case 10: SMORE_DRAW(10) break;
+        default: SMORE_DRAW(20) break;
+    }
+#undef SMORE_DRAW
+    return hipGetLastError();
+}
+
+}  // namespace smore

@@ -19,6 +19,9 @@ struct EdgeArgs {
     const int2* sh_hash;
     const int32_t* sh_ids;
     int sh_rows, sh_flush;
+    // edge kernels: the pre-drawn sample records of samples [begin, begin+count)
+    // (draw_kernel), rec_width(KMAX) int32 each
+    const int32_t* rec;
     uint64_t begin, count, total, seed;
     double alpha0;
     float reg;
@@ -34,7 +37,29 @@ struct WalkArgs {
     int steps, window;
 };
 
+// lanes per sample group: G = min(64, pow2ceil(dpad / SMORE_EPL)); lane l owns
+// row elements l, l+G, l+2G, ... (DESIGN.md "Arithmetic spec")
+#ifndef SMORE_EPL
+#define SMORE_EPL 4
+#endif
 int lanes_of(int dpad);
+// int32 words per pre-drawn edge-sample record {v, c, n_1..n_K, pad}: the
+// smallest power of two >= 2 + KMAX, at least 4 (whole 16-B words)
+constexpr int rec_width(int kmax) {
+    int r = 4;
+    while (r < 2 + kmax) r <<= 1;
+    return r;
+}
+// edge kernels whose group has a lane per negative plus one draw the samples
+// themselves (software-pipelined, edge_kernels.h); the others read records
+// written by draw_kernel
+constexpr bool pipe_draws(int G, int kmax) { return kmax + 1 <= G; }
+#ifndef SMORE_PIPE_DRAWS
+#define SMORE_PIPE_DRAWS 0
+#endif
+inline int kmax_of(int K) { return K <= 5 ? 5 : K <= 10 ? 10 : 20; }
+hipError_t launch_draw(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K, int32_t* rec,
+                       unsigned long long* skipped, hipStream_t st);
 constexpr int SH_HASH = 256;   // entries of the super-hot row hash (power of two)
 // dynamic LDS of the hybrid edge kernel: hash, slot ids, pending deltas
 inline size_t sh_lds_bytes(int sh_rows, int dpad) {
@@ -48,13 +73,15 @@ hipError_t launch_go_sample(const DevGraph& g, const double* tcum, uint64_t seed
 hipError_t launch_walk_gen(const DevGraph& g, const WalkArgs& w, uint64_t seed, hipStream_t st);
 hipError_t launch_walk_pairs(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st);
 const void* walk_pairs_symbol(const EdgeArgs& a);
-hipError_t launch_edge_store(const EdgeArgs& a, int grid, hipStream_t st);
-hipError_t launch_edge_atomic(const EdgeArgs& a, int grid, hipStream_t st);
-hipError_t launch_edge_hybrid(const EdgeArgs& a, int grid, hipStream_t st);
-const void* edge_symbol_hybrid(const EdgeArgs& a);
+// edge kernel instantiations, one per (scatter mode s/a/h, KMAX) (train_edge_*.hip)
+#define SMORE_DECL_EDGE(name)                                                   \
+    hipError_t launch_edge_##name(const EdgeArgs& a, int grid, hipStream_t st); \
+    const void* edge_symbol_##name(const EdgeArgs& a);
+SMORE_DECL_EDGE(s5) SMORE_DECL_EDGE(s10) SMORE_DECL_EDGE(s20)
+SMORE_DECL_EDGE(a5) SMORE_DECL_EDGE(a10) SMORE_DECL_EDGE(a20)
+SMORE_DECL_EDGE(h5) SMORE_DECL_EDGE(h10) SMORE_DECL_EDGE(h20)
+#undef SMORE_DECL_EDGE
 hipError_t launch_bpr(const EdgeArgs& a, int grid, hipStream_t st);
-const void* edge_symbol_store(const EdgeArgs& a);
-const void* edge_symbol_atomic(const EdgeArgs& a);
 const void* bpr_symbol(const EdgeArgs& a);
 hipError_t launch_edge_train(const EdgeArgs& a, int grid, hipStream_t st);
 const void* edge_kernel_symbol(const EdgeArgs& a);

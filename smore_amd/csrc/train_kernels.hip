@@ -55,24 +55,29 @@ __global__ void init_uniform_kernel(float* T, int64_t rows, int dim, int dpad, u
 
 // ------------------------------------------------------------------ dispatch
 int lanes_of(int dpad) {
-    int nq = dpad / 4, G = 1;
+    int nq = (dpad + SMORE_EPL - 1) / SMORE_EPL, G = 1;
     while (G < nq && G < 64) G <<= 1;
     return G;
 }
 
+#define SMORE_EDGE_DISPATCH(fn, ...)                                           \
+    {                                                                          \
+        const int k = kmax_of(a.K);                                            \
+        if (a.mode == 1) return k == 5 ? fn##a5(__VA_ARGS__) : k == 10 ? fn##a10(__VA_ARGS__) : fn##a20(__VA_ARGS__); \
+        if (a.mode == 3) return k == 5 ? fn##h5(__VA_ARGS__) : k == 10 ? fn##h10(__VA_ARGS__) : fn##h20(__VA_ARGS__); \
+        return k == 5 ? fn##s5(__VA_ARGS__) : k == 10 ? fn##s10(__VA_ARGS__) : fn##s20(__VA_ARGS__);                \
+    }
+
 hipError_t launch_edge_train(const EdgeArgs& a, int grid, hipStream_t st) {
     if (a.model == 3) return launch_bpr(a, grid, st);
-    if (a.mode == 1) return launch_edge_atomic(a, grid, st);
-    if (a.mode == 3) return launch_edge_hybrid(a, grid, st);
-    return launch_edge_store(a, grid, st);
+    SMORE_EDGE_DISPATCH(launch_edge_, a, grid, st)
 }
 
 const void* edge_kernel_symbol(const EdgeArgs& a) {
     if (a.model == 3) return bpr_symbol(a);
-    if (a.mode == 1) return edge_symbol_atomic(a);
-    if (a.mode == 3) return edge_symbol_hybrid(a);
-    return edge_symbol_store(a);
+    SMORE_EDGE_DISPATCH(edge_symbol_, a)
 }
+#undef SMORE_EDGE_DISPATCH
 
 hipError_t launch_sample(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K,
                          int bpr, int32_t* out, hipStream_t st) {

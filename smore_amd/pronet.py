@@ -206,6 +206,14 @@ class ProNet:
     def last_kernel_ms(self):
         return float(lib.smore_last_kernel_ms(self.ctx))
 
+    def last_phase_ms(self):
+        """(draw_ms, update_ms) of the last LINE/MF edge launch, or None."""
+        import ctypes
+        d, u = ctypes.c_float(), ctypes.c_float()
+        if lib.smore_last_phase_ms(self.ctx, ctypes.byref(d), ctypes.byref(u)) != 0:
+            return None
+        return float(d.value), float(u.value)
+
     def load_pretrain(self, which, path):
         """proNet::LoadPreTrain (src/proNet.cpp:238-286)."""
         self._chk(lib.smore_load_pretrain(self.ctx, which, path.encode()), "load_pretrain")
