@@ -63,6 +63,10 @@ struct smore_ctx {
     int sh_max = 32, sh_flush = 16;
     // pre-drawn edge-sample records (train_draw.hip) and per-phase timing
     int32_t* d_rec = nullptr;
+    // packed draw tables (train_draw.hip), rebuilt when the graph tables change
+    uint4* d_vt32 = nullptr;
+    uint4* d_ct16 = nullptr;
+    bool packed_ok = false;
     size_t rec_cap = 0;                 // int32 words
     std::vector<hipEvent_t> phase_ev;   // {before draw 0, after draw 0, after update 0, after draw 1, ...}
     int phase_n = 0;                    // chunks of the last edge launch
@@ -111,6 +115,9 @@ int upload_graph(smore_ctx* c) {
     }
     if ((rc = set_device(c))) return rc;
     HostGraph& g = c->g;
+    c->packed_ok = false;
+    dfree(c->d_vt32);
+    dfree(c->d_ct16);
     if ((rc = upload(c, c->d_offsets, g.offsets.data(), g.offsets.size()))) return rc;
     if ((rc = upload(c, c->d_targets, g.targets.data(), g.targets.size()))) return rc;
     if ((rc = upload(c, c->d_vtab, g.vtab.data(), g.vtab.size()))) return rc;
@@ -135,6 +142,8 @@ DevGraph dev_graph(const smore_ctx* c) {
     d.vtab = reinterpret_cast<const uint2*>(c->d_vtab);
     d.ntab = reinterpret_cast<const uint2*>(c->d_ntab);
     d.ctab = reinterpret_cast<const uint2*>(c->d_ctab);
+    d.vt32 = c->packed_ok ? c->d_vt32 : nullptr;
+    d.ct16 = c->packed_ok ? c->d_ct16 : nullptr;
     d.V = (uint32_t)c->g.V;
     return d;
 }
@@ -185,7 +194,7 @@ void smore_destroy(smore_ctx* c) {
     dfree(c->d_sig); dfree(c->d_skipped); dfree(c->d_table[0]); dfree(c->d_table[1]);
 
     dfree(c->d_order); dfree(c->d_walks); dfree(c->d_lens); dfree(c->d_tcum); dfree(c->d_sh_hash); dfree(c->d_sh_ids);
-    dfree(c->d_rec);
+    dfree(c->d_rec); dfree(c->d_vt32); dfree(c->d_ct16);
     for (hipEvent_t e : c->phase_ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -277,6 +286,7 @@ int smore_set_alias(smore_ctx* c, int which, const double* prob, const int64_t* 
     int rc;
     if ((rc = set_device(c))) return rc;
     AliasEntry*& d = which == 0 ? c->d_vtab : which == 1 ? c->d_ntab : c->d_ctab;
+    c->packed_ok = false;
     return upload(c, d, T.data(), T.size());
 }
 
@@ -486,6 +496,20 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
         HIPCHK(c, hipMemcpy(c->d_ctab + b, ct.data(), n * sizeof(AliasEntry), hipMemcpyHostToDevice));
     }
     c->hot_key = key;
+    c->packed_ok = false;
+    return SMORE_OK;
+}
+
+// packed draw tables (DevGraph::vt32 / ct16): built on the device from the
+// current (tagged) tables; skipped when offsets do not fit 32 bits
+static int ensure_packed(smore_ctx* c) {
+    if (c->packed_ok) return SMORE_OK;
+    const int64_t V = c->g.V, E = c->g.E;
+    if (E >= ((int64_t)1 << 32)) return SMORE_OK;
+    if (!c->d_vt32) HIPCHK(c, hipMalloc(&c->d_vt32, (size_t)std::max<int64_t>(V, 1) * 2 * sizeof(uint4)));
+    if (!c->d_ct16) HIPCHK(c, hipMalloc(&c->d_ct16, (size_t)std::max<int64_t>(E, 1) * sizeof(uint4)));
+    HIPCHK(c, launch_pack(dev_graph(c), (uint64_t)E, c->d_vt32, c->d_ct16, c->stream));
+    c->packed_ok = true;
     return SMORE_OK;
 }
 
@@ -616,6 +640,7 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
         HIPCHK(c, hipEventCreate(&e));
         c->phase_ev.push_back(e);
     }
+    if ((rc = ensure_packed(c))) return rc;
     const DevGraph dg = dev_graph(c);
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream));
@@ -664,6 +689,7 @@ int smore_set_semantics(smore_ctx* c, int semantics) {
     if (!c || (semantics != SMORE_SEM_CPP && semantics != SMORE_SEM_GO)) return SMORE_EINVAL;
     if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
     if (semantics == c->semantics) return SMORE_OK;
+    c->packed_ok = false;
     std::vector<double> tcum;
     if (semantics == SMORE_SEM_GO) build_go_tables(c->g, tcum);
     else build_cpp_vn_tables(c->g);

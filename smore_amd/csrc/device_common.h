@@ -43,6 +43,12 @@ struct DevGraph {
     const uint2* vtab;        // V   {accept threshold, tagged alias word}
     const uint2* ntab;        // V
     const uint2* ctab;        // E   alias already a (tagged) target vid
+    // packed copies for the draw kernel (nullptr when E >= 2^32): per vertex
+    // entry i two uint4 {thresh, alias word, off(i), deg(i)}, {off(a), deg(a),
+    // 0, 0} (a = alias(i)) -- a source draw plus its CSR row in one 32-B read;
+    // per edge slot {thresh, tagged alias vid, tagged target, 0}
+    const uint4* vt32;
+    const uint4* ct16;
     uint32_t V;
 };
 

@@ -378,19 +378,27 @@ edge_train_kernel(EdgeArgs a) {
     const uint64_t base = mf ? 0 : 1;   // LINE counts from 1, MF from 0
     float* const Tc = a.C;
 
-    // adds the block's pending super-hot deltas to HBM (one row per wave-instruction)
-    auto flush = [&]() {
-        __syncthreads();
+    // adds pending super-hot deltas to HBM (one row per wave-instruction).
+    // Wave w of the block drains its share of the pending rows with an LDS
+    // exchange (read-and-zero in one atomic), so there is no workgroup barrier
+    // in the loop: an LDS add racing with the drain lands either in this
+    // flush or in the wave's next one, never lost.
+    const int nwaves = blockDim.x / 64, wave = threadIdx.x / 64;
+    auto drain = [&]() {
         const int n = sh.n * a.dpad;
-        for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            const float x = sh.pend[i];
+        const int per = (n + nwaves - 1) / nwaves;
+        const int lo = wave * per, hi = n < lo + per ? n : lo + per;
+        for (int i = lo + (threadIdx.x & 63); i < hi; i += 64) {
+            const float x = atomicExch(&sh.pend[i], 0.0f);
             if (x != 0.0f) {
                 const int s = i / a.dpad, e = i - s * a.dpad;
                 unsafeAtomicAdd(Tc + (int64_t)sh_ids[s] * a.dpad + e, x);
-                sh.pend[i] = 0.0f;
             }
         }
+    };
+    auto flush = [&]() {   // end of the kernel: every wave is done adding
         __syncthreads();
+        drain();
     };
 
     const uint64_t step = a.mode == 2 ? 1 : ngroups;
@@ -417,7 +425,7 @@ edge_train_kernel(EdgeArgs a) {
     auto maybe_flush = [&]() {
         if constexpr (MODE == MODE_HYBRID) {
             if (sh.n > 0 && ++round == (uint32_t)a.sh_flush) {
-                flush();
+                drain();
                 round = 0;
             }
         }

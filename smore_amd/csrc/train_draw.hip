@@ -59,7 +59,14 @@ __global__ void __launch_bounds__(256) draw_kernel(DevGraph g, uint64_t seed, ui
     }
     const uint4 b0 = philox_block(seed, 0, s, 0);
     const uint32_t vi = draw_index(b0.y, g.V);
-    const uint2 ve = g.vtab[vi];
+    uint2 ve = make_uint2(0u, 0u);
+    uint4 p0 = make_uint4(0u, 0u, 0u, 0u), p1 = p0;
+    if (g.vt32) {
+        p0 = g.vt32[2 * (uint64_t)vi];
+        p1 = g.vt32[2 * (uint64_t)vi + 1];
+    } else {
+        ve = g.vtab[vi];
+    }
     // slots 4+2j (index), 5+2j (p): block 1 + j/2, components 2(j&1), 2(j&1)+1
     uint32_t nidx[KMAX], np[KMAX];
     uint2 ne[KMAX];
@@ -78,8 +85,21 @@ __global__ void __launch_bounds__(256) draw_kernel(DevGraph g, uint64_t seed, ui
 #pragma unroll
     for (int j = 0; j < KMAX; ++j)
         if (j < K) ne[j] = g.ntab[nidx[j]];
-    const int32_t tv = alias_pick(vi, ve, b0.x);
-    const int32_t c = target_sample(g, untag(tv), b0.z, b0.w);
+    int32_t tv, c;
+    if (g.vt32) {
+        // source draw and its CSR row from one packed entry; one context read
+        const bool acc = b0.x < p0.x;
+        tv = alias_pick(vi, make_uint2(p0.x, p0.y), b0.x);
+        const uint32_t off = acc ? p0.z : p1.x, br = acc ? p0.w : p1.y;
+        c = -1;
+        if (br != 0) {
+            const uint4 ce = g.ct16[(uint64_t)off + draw_index(b0.w, br)];
+            c = b0.z < ce.x ? (int32_t)ce.z : (int32_t)ce.y;
+        }
+    } else {
+        tv = alias_pick(vi, ve, b0.x);
+        c = target_sample(g, untag(tv), b0.z, b0.w);
+    }
     int32_t w[RW];
     w[0] = tv;
     w[1] = c;
@@ -92,6 +112,31 @@ __global__ void __launch_bounds__(256) draw_kernel(DevGraph g, uint64_t seed, ui
         __builtin_nontemporal_store(x, o + q);
     }
     if (c < 0) atomicAdd(skipped, 1ull);
+}
+
+// packed draw tables from the device graph (after any re-tagging)
+__global__ void pack_vertex_kernel(DevGraph g, uint4* vt32) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= g.V) return;
+    const uint2 e = g.vtab[i];
+    const int32_t al = (int32_t)(e.y & (uint32_t)ID_MASK);
+    const int64_t oi = g.offsets[i], oa = g.offsets[al];
+    vt32[2 * i] = make_uint4(e.x, e.y, (uint32_t)oi, (uint32_t)(g.offsets[i + 1] - oi));
+    vt32[2 * i + 1] = make_uint4((uint32_t)oa, (uint32_t)(g.offsets[al + 1] - oa), 0u, 0u);
+}
+
+__global__ void pack_edge_kernel(DevGraph g, uint64_t E, uint4* ct16) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= E) return;
+    const uint2 e = g.ctab[i];
+    ct16[i] = make_uint4(e.x, e.y, (uint32_t)g.targets[i], 0u);
+}
+
+hipError_t launch_pack(const DevGraph& g, uint64_t E, uint4* vt32, uint4* ct16, hipStream_t st) {
+    const int block = 256;
+    hipLaunchKernelGGL(pack_vertex_kernel, dim3((unsigned)((g.V + block - 1) / block)), dim3(block), 0, st, g, vt32);
+    hipLaunchKernelGGL(pack_edge_kernel, dim3((unsigned)((E + block - 1) / block)), dim3(block), 0, st, g, E, ct16);
+    return hipGetLastError();
 }
 
 hipError_t launch_draw(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K, int32_t* rec,

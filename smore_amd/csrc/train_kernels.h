@@ -58,6 +58,7 @@ constexpr bool pipe_draws(int G, int kmax) { return kmax + 1 <= G; }
 #define SMORE_PIPE_DRAWS 0
 #endif
 inline int kmax_of(int K) { return K <= 5 ? 5 : K <= 10 ? 10 : 20; }
+hipError_t launch_pack(const DevGraph& g, uint64_t E, uint4* vt32, uint4* ct16, hipStream_t st);
 hipError_t launch_draw(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K, int32_t* rec,
                        unsigned long long* skipped, hipStream_t st);
 constexpr int SH_HASH = 256;   // entries of the super-hot row hash (power of two)
