@@ -1,16 +1,18 @@
 #!/usr/bin/env python3
 """Benchmark: LINE order-2 edge-updates/s on MI355X (BASELINE.json metric).
 
-A "step" is one launch of the fused sample->gather->update kernel over
+A "step" is one pass of the hot path over
 `--samples` edge samples (default 2^27) of the synthetic power-law graph of
 config c4 (10M vertices / 200M undirected lines = 400M directed slots, d=64,
 K=5; the north star's 1/2/4/8-GPU graph), inputs resident in
-HBM.  Default scatter: hybrid (atomic adds for the hot rows, the 32 hottest
-write-combined per workgroup in LDS, plain stores for the rest), whose
-training objective matches the lossless atomic scatter.  One process per GPU; with N > 1
-each rank runs its own disjoint global-sample range on a replicated graph and
-replicated tables, and the tables' deltas are all-reduced over RCCL every
-`--sync-every` steps (weak scaling).  Rank 0 prints one JSON line.
+HBM.  A step is the draw kernel (train_draw.hip) and the update kernel
+(edge_kernels.h).  Default scatter: hybrid (atomic adds for the hot rows, the
+32 hottest write-combined per workgroup in LDS, plain stores for the rest),
+whose training objective matches the lossless atomic scatter.
+One process per GPU; with N > 1 each rank runs its own disjoint global-sample
+range on a replicated graph and replicated tables, and the tables' deltas are
+all-reduced over RCCL every `--sync-every` steps, overlapping the next step
+(smore_amd/dist.py OverlapSync; weak scaling).  Rank 0 prints one JSON line.
 
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -56,7 +58,7 @@ def parse():
     ap.add_argument("--samples", type=int, default=1 << 27, help="edge samples per step per GPU")
     ap.add_argument("--mode", default="hybrid", choices=["hogwild", "atomic", "hybrid"],
                     help="scatter: hybrid (default), atomic (every row), hogwild (plain stores, loses updates)")
-    ap.add_argument("--hot-tau", type=float, default=0.03, help="hybrid: hot-row threshold")
+    ap.add_argument("--hot-tau", type=float, default=0.3, help="hybrid: hot-row threshold")
     ap.add_argument("--combine-rows", type=int, default=32, help="hybrid: LDS write-combined hottest rows")
     ap.add_argument("--combine-flush", type=int, default=16, help="hybrid: rounds between LDS flushes")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
@@ -136,10 +138,12 @@ def main():
         begin = (k * world + rank) * S
         pn.train_edges("line2", begin, S, total, K, 0.025, 0.0, args.seed, args.mode, sync=False)
         if sync is not None and (k + 1) % args.sync_every == 0:
-            sync.allreduce()
+            sync.begin()      # folds the previous exchange in; this one overlaps the next step
 
     for k in range(args.warmup):
         step(k)
+    if sync is not None:
+        sync.end()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -154,6 +158,8 @@ def main():
         if ph is not None:
             draw_ms += ph[0]
             upd_ms += ph[1]
+    if sync is not None:
+        sync.end()            # the last exchange lands inside the timed region
     ev1.record(stream)
     torch.cuda.synchronize()
     if dist:

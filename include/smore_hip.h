@@ -161,7 +161,7 @@ int smore_train_edges(smore_ctx* ctx, int model, uint64_t begin, uint64_t count,
                       uint64_t total, int K, double alpha0, double reg, uint64_t seed,
                       int mode);
 /* SMORE_HYBRID: a row takes float atomics when (resident sample groups) x
- * (its per-sample touch probability) > tau (default 0.1); see DESIGN.md */
+ * (its per-sample touch probability) > tau (default 0.3); see DESIGN.md */
 int smore_set_hot_threshold(smore_ctx* ctx, double tau);
 /* rows marked hot in W and C by the last hybrid launch */
 /* hybrid scatter: the `rows` hottest hot context rows (default 32; 0 = off; at
@@ -179,6 +179,16 @@ float smore_last_kernel_ms(const smore_ctx* ctx);
  * (sampling, train_draw.hip) and of the update kernels (gather/update/scatter);
  * SMORE_ESTATE if the last launch was not an edge launch */
 int smore_last_phase_ms(const smore_ctx* ctx, float* draw_ms, float* update_ms);
+
+/* ---- multi-GPU replica exchange (new: the reference is single-process Hogwild,
+ * src/model/LINE.cpp:162) -------------------------------------------
+ * Fused passes around an all-reduce of R, on the context stream, over n floats
+ * of device memory laid out like a table (n % 4 == 0, 16-byte aligned):
+ *   begin:  D = T - S;  R = D;  S = T          (this rank's delta since the last exchange)
+ *   end:    X = scale*R - D;  T += X;  S += X  (R = sum over ranks; scale 1 or 1/world)
+ * Driven by smore_amd/dist.py (RCCL all-reduce overlapping the next step). */
+int smore_delta_begin(smore_ctx* ctx, const void* T, void* S, void* D, void* R, int64_t n);
+int smore_delta_end(smore_ctx* ctx, void* T, void* S, const void* D, const void* R, float scale, int64_t n);
 
 /* replaces: DeepWalk::Train (src/model/DeepWalk.cpp:98-155): walks
  * [walk_begin, walk_end) of walk_times*V, start vertices order[] (host,

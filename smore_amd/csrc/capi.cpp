@@ -34,11 +34,12 @@ struct smore_ctx {
     AliasEntry* d_ctab = nullptr;
     float* d_sig = nullptr;
     unsigned long long* d_skipped = nullptr;
+    unsigned long long* d_work = nullptr;   // chunk counter of the Hogwild edge kernels
     // tables
     float* d_table[2] = {nullptr, nullptr};
     int dim = 0, dpad = 0, ntables = 0;
     // hybrid scatter: hot-row bitmaps (1 bit per row), keyed by what built them
-    double hot_tau = 0.03;
+    double hot_tau = 0.3;
     std::string hot_key;
     int64_t hot_rows[2] = {0, 0};
     // DeepWalk buffers
@@ -174,6 +175,7 @@ int smore_create(int device, smore_ctx** out) {
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
     if (e == hipSuccess) e = hipMalloc((void**)&c->d_skipped, sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(c->d_skipped, 0, sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->d_work, sizeof(unsigned long long));
     if (e == hipSuccess) e = hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device);
     if (e != hipSuccess) {
         delete c;
@@ -191,7 +193,7 @@ void smore_destroy(smore_ctx* c) {
         (void)hipStreamSynchronize(c->stream);
     }
     dfree(c->d_offsets); dfree(c->d_targets); dfree(c->d_vtab); dfree(c->d_ntab); dfree(c->d_ctab);
-    dfree(c->d_sig); dfree(c->d_skipped); dfree(c->d_table[0]); dfree(c->d_table[1]);
+    dfree(c->d_sig); dfree(c->d_skipped); dfree(c->d_work); dfree(c->d_table[0]); dfree(c->d_table[1]);
 
     dfree(c->d_order); dfree(c->d_walks); dfree(c->d_lens); dfree(c->d_tcum); dfree(c->d_sh_hash); dfree(c->d_sh_ids);
     dfree(c->d_rec); dfree(c->d_vt32); dfree(c->d_ct16);
@@ -606,25 +608,8 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
         c->phase_n = 0;
         return SMORE_OK;
     }
-    if (SMORE_PIPE_DRAWS && pipe_draws(lanes_of(c->dpad), kmax_of(a.K))) {
-        // the update kernel draws its own samples (software-pipelined)
-        while (c->phase_ev.size() < 3) {
-            hipEvent_t e;
-            HIPCHK(c, hipEventCreate(&e));
-            c->phase_ev.push_back(e);
-        }
-        HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-        HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream));
-        HIPCHK(c, hipEventRecord(c->phase_ev[1], c->stream));
-        HIPCHK(c, launch_edge_train(a, grid, c->stream));
-        HIPCHK(c, hipEventRecord(c->phase_ev[2], c->stream));
-        HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-        c->timed = true;
-        c->phase_n = 1;
-        return SMORE_OK;
-    }
-    // edge models with few lanes per sample: draw kernel -> update kernel per
-    // chunk of samples (the record buffer is bounded at 4 GiB)
+    // edge models: draw kernel -> update kernel per chunk of samples (the
+    // record buffer is bounded at 4 GiB; a 2^27-sample launch is one chunk)
     const int RW = rec_width(kmax_of(a.K));
     const uint64_t chunk_max = ((uint64_t)1 << 30) / (uint64_t)RW;
     const uint64_t chunk = std::min<uint64_t>(count, chunk_max);
@@ -652,6 +637,8 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
         ak.begin = begin + b;
         ak.count = n;
         ak.rec = c->d_rec;
+        ak.work = c->d_work;
+        HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
         HIPCHK(c, launch_edge_train(ak, grid, c->stream));
         HIPCHK(c, hipEventRecord(c->phase_ev[2 * k + 2], c->stream));
     }
@@ -881,7 +868,31 @@ int smore_train_deepwalk(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, i
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
+    c->phase_n = 0;
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return SMORE_OK;
+}
+
+// ---------------------------------------------------------------- replica exchange
+static int delta_args(smore_ctx* c, const void* T, const void* S, const void* D, const void* R, int64_t n) {
+    if (!c || !T || !S || !D || !R || n < 0 || (n & 3)) return fail(c, SMORE_EINVAL, "delta: bad buffers");
+    for (const void* p : {T, S, D, R})
+        if ((uintptr_t)p & 15) return fail(c, SMORE_EINVAL, "delta: buffers must be 16-byte aligned");
+    return set_device(c);
+}
+
+int smore_delta_begin(smore_ctx* c, const void* T, void* S, void* D, void* R, int64_t n) {
+    int rc;
+    if ((rc = delta_args(c, T, S, D, R, n))) return rc;
+    HIPCHK(c, launch_delta_begin((const float*)T, (float*)S, (float*)D, (float*)R, (uint64_t)n, c->cus, c->stream));
+    return SMORE_OK;
+}
+
+int smore_delta_end(smore_ctx* c, void* T, void* S, const void* D, const void* R, float scale, int64_t n) {
+    int rc;
+    if ((rc = delta_args(c, T, S, D, R, n))) return rc;
+    HIPCHK(c, launch_delta_end((float*)T, (float*)S, (const float*)D, (const float*)R, scale, (uint64_t)n, c->cus,
+                               c->stream));
     return SMORE_OK;
 }
 

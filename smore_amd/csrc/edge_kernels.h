@@ -26,13 +26,6 @@ namespace smore {
 
 enum { MODE_STORE = 0, MODE_ATOMIC = 1, MODE_HYBRID = 3 };
 
-// 1: edge kernels with a lane per negative draw their own samples
-// (software-pipelined); 0 (default): every edge launch runs draw_kernel first.
-// Measured at C4 (2^27 samples, hybrid): fused-pipelined 127 ms vs
-// draw 22 + update 110 ms -- kept as an option.
-#ifndef SMORE_PIPE_DRAWS
-#define SMORE_PIPE_DRAWS 0
-#endif
 
 // minimum waves per SIMD the register allocator must allow, per scatter mode
 // (0 = compiler default); overridable at build time for tuning.
@@ -431,80 +424,7 @@ edge_train_kernel(EdgeArgs a) {
         }
     };
 
-    if constexpr (SMORE_PIPE_DRAWS && pipe_draws(G, KMAX)) {
-        // Fused, software-pipelined draws.  A sample's draws are a dependent
-        // chain: vertex alias (A) -> CSR offsets of the source (B) -> context
-        // alias + target (C); its K negative-alias reads are independent.  Each
-        // round of this group issues stage A for sample t+3S, B for t+2S and C
-        // (with the negatives) for t+S before gathering the rows of sample t
-        // (stage D), so the chain overlaps the update and a round costs one
-        // memory round trip.  Lane K of the group carries the source/target
-        // chain, lane j < K negative j; each lane computes the one Philox
-        // block its draw needs (slots of DESIGN.md "RNG spec").  The ids reach
-        // the update by group shuffles.  Same draws as train_draw.hip.
-        const int64_t S = (int64_t)step, n = (int64_t)a.count;
-        const int64_t g_off = a.mode == 2 ? 0 : (int64_t)gib;
-        const bool srcl = lane == a.K, negl = lane < a.K;
-        const uint2* atab = srcl ? a.g.vtab : a.g.ntab;
-        const uint32_t ablk = srcl ? 0u : 1u + (uint32_t)(lane >> 1);
-        const bool odd = lane & 1;
-        int32_t vB = -1, vC = -1, vD = -1, cD = -1, nD = -1;
-        uint32_t w2B = 0, w3B = 0, w2C = 0;
-        int64_t eC = -1;
-        for (int64_t rr = (int64_t)r0 - 3 * S; rr < n; rr += S) {
-            const int64_t tD = rr + g_off, tC = tD + S, tB = tD + 2 * S, tA = tD + 3 * S;
-            // A (lane K): vertex alias of sample tA; lanes < K: negative alias of tC
-            const int64_t tx = srcl ? tA : tC;
-            const bool ax = (srcl || negl) && tx >= 0 && tx < n;
-            const uint4 b = philox_block(a.seed, 0, a.begin + (uint64_t)(ax ? tx : 0), ablk);
-            const uint32_t kidx = srcl ? b.y : (odd ? b.z : b.x);
-            const uint32_t kp = srcl ? b.x : (odd ? b.w : b.y);
-            const uint32_t ai = draw_index(kidx, a.g.V);
-            uint2 ae = make_uint2(0xFFFFFFFFu, 0u);
-            if (ax) ae = atab[ai];
-            // B (lane K): CSR offsets of the source of sample tB
-            int64_t o0 = 0, o1 = 0;
-            const bool bx = srcl && tB >= 0 && tB < n;
-            if (bx) {
-                const int32_t v = untag(vB);
-                o0 = a.g.offsets[v];
-                o1 = a.g.offsets[v + 1];
-            }
-            // C (lane K): context alias entry and target of sample tC
-            uint2 ce = make_uint2(0u, 0u);
-            int32_t tt = -1;
-            const bool cx = srcl && tC >= 0 && tC < n && eC >= 0;
-            if (cx) {
-                ce = a.g.ctab[eC];
-                tt = a.g.targets[eC];
-            }
-            // D: update sample tD
-            const int32_t tv = __shfl(vD, a.K, G);
-            const int32_t c = __shfl(cD, a.K, G);
-            int32_t negs[KMAX];
-#pragma unroll
-            for (int j = 0; j < KMAX; ++j) negs[j] = __shfl(nD, j, G);
-            if (tD >= 0 && tD < n) {
-                if (c < 0) {
-                    if (lane == 0) atomicAdd(a.skipped, 1ull);
-                } else {
-                    process((uint64_t)tD, tv, c, negs);
-                }
-            }
-            // advance the stages
-            const int32_t pick = alias_pick(ai, ae, kp);
-            vD = vC;
-            cD = cx ? (w2C < ce.x ? tt : (int32_t)ce.y) : -1;
-            nD = pick;
-            vC = vB;
-            w2C = w2B;
-            eC = (bx && o1 > o0) ? o0 + (int64_t)draw_index(w3B, (uint32_t)(o1 - o0)) : -1;
-            vB = pick;
-            w2B = b.z;
-            w3B = b.w;
-            maybe_flush();
-        }
-    } else if (a.mode == 2) {
+    if (a.mode == 2) {
         // serial: records in order, gather after the previous sample's scatter
         constexpr int RW = rec_width(KMAX);
         for (; r0 < a.count; ++r0) {
@@ -528,13 +448,12 @@ edge_train_kernel(EdgeArgs a) {
         // this sample is about to write -- the staleness every other resident
         // group already has (Hogwild); the serial mode above keeps strict order.
         constexpr int RW = rec_width(KMAX);
-        const uint64_t S = step;
         struct Ids {
             int32_t v, id[KMAX + 1];
             bool hotw, hot[KMAX + 1], live;
         };
-        auto decode = [&](uint64_t t, const i32x4 (&r)[RW / 4], Ids& x) {
-            x.live = t < a.count && r[0][1] >= 0;   // c < 0: counted by the draw kernel
+        auto decode = [&](uint64_t t, uint64_t lim, const i32x4 (&r)[RW / 4], Ids& x) {
+            x.live = t < lim && r[0][1] >= 0;   // c < 0: counted by the draw kernel
             x.hotw = scatter_atomic<MODE>(r[0][0]);
             x.v = x.live ? untag(r[0][0]) : -1;
 #pragma unroll
@@ -544,10 +463,10 @@ edge_train_kernel(EdgeArgs a) {
                 x.id[k] = (!x.live || w < 0) ? -1 : untag(w);
             }
         };
-        auto load_rec = [&](uint64_t t, i32x4 (&r)[RW / 4]) {
+        auto load_rec = [&](uint64_t t, uint64_t lim, i32x4 (&r)[RW / 4]) {
 #pragma unroll
             for (int q = 0; q < RW / 4; ++q) r[q] = i32x4{-1, -1, -1, -1};
-            if (t < a.count) {
+            if (t < lim) {
                 const i32x4* p = reinterpret_cast<const i32x4*>(a.rec + t * RW);
 #pragma unroll
                 for (int q = 0; q < RW / 4; ++q) r[q] = __builtin_nontemporal_load(p + q);
@@ -556,29 +475,46 @@ edge_train_kernel(EdgeArgs a) {
         i32x4 rr[RW / 4];
         Ids xa, xb;
         float wva[M], rowsa[KMAX + 1][M], wvb[M], rowsb[KMAX + 1][M];
-        uint64_t t = r0 + gib;
-        load_rec(t, rr);
-        decode(t, rr, xa);
-        gather_rows<G, M, KMAX>(a, lane, ev, xa.v, xa.id, shared, wva, rowsa);
-        load_rec(t + S, rr);
-        for (; r0 < a.count; r0 += S) {
-            t = r0 + gib;
-            decode(t + S, rr, xb);
-            load_rec(t + 2 * S, rr);
-            gather_rows<G, M, KMAX>(a, lane, ev, xb.v, xb.id, shared, wvb, rowsb);
-            if (xa.live) {
-                const float alpha = alpha_at(a.begin + t + base, a.alpha0, a.total);
-                sgd_update_rows<G, M, KMAX, MODE, SHARED>(a, s_sig, lane, ev, xa.v, xa.id, xa.hotw, xa.hot, alpha,
-                                                         shared, mf, sh, wva, rowsa);
-            }
-            xa = xb;
+        // Work is handed out in chunks of CH_ROUNDS rounds (CH_ROUNDS * gpb
+        // consecutive samples per block) from a per-launch counter: a block
+        // that starts late (a collective's kernel holding CU slots, uneven
+        // XCD clocks) takes fewer chunks instead of stretching the launch by
+        // a whole fixed share.  Within a chunk the block's groups take samples
+        // c0 + gib, c0 + gib + gpb, ... with the row prefetch above.
+        __shared__ uint64_t s_next;
+        const uint64_t span = CH_ROUNDS * gpb;
+        auto grab = [&]() -> uint64_t {
+            __syncthreads();   // every wave has read the previous s_next
+            if (threadIdx.x == 0) s_next = atomicAdd(a.work, 1ull) * span;
+            __syncthreads();
+            return s_next;
+        };
+        for (uint64_t c0 = grab(); c0 < a.count; c0 = grab()) {
+            const uint64_t lim = c0 + span < a.count ? c0 + span : a.count;
+            uint64_t t = c0 + gib;
+            load_rec(t, lim, rr);
+            decode(t, lim, rr, xa);
+            gather_rows<G, M, KMAX>(a, lane, ev, xa.v, xa.id, shared, wva, rowsa);
+            load_rec(t + gpb, lim, rr);
+            for (uint64_t r = c0; r < lim; r += gpb) {
+                t = r + gib;
+                decode(t + gpb, lim, rr, xb);
+                load_rec(t + 2 * gpb, lim, rr);
+                gather_rows<G, M, KMAX>(a, lane, ev, xb.v, xb.id, shared, wvb, rowsb);
+                if (xa.live) {
+                    const float alpha = alpha_at(a.begin + t + base, a.alpha0, a.total);
+                    sgd_update_rows<G, M, KMAX, MODE, SHARED>(a, s_sig, lane, ev, xa.v, xa.id, xa.hotw, xa.hot,
+                                                             alpha, shared, mf, sh, wva, rowsa);
+                }
+                xa = xb;
 #pragma unroll
-            for (int m = 0; m < M; ++m) {
-                wva[m] = wvb[m];
+                for (int m = 0; m < M; ++m) {
+                    wva[m] = wvb[m];
 #pragma unroll
-                for (int k = 0; k <= KMAX; ++k) rowsa[k][m] = rowsb[k][m];
+                    for (int k = 0; k <= KMAX; ++k) rowsa[k][m] = rowsb[k][m];
+                }
+                maybe_flush();
             }
-            maybe_flush();
         }
     }
     if constexpr (MODE == MODE_HYBRID) {

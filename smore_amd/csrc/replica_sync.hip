@@ -1,0 +1,66 @@
+// replica_sync.hip -- the two fused passes of the multi-GPU replica exchange
+// (new in this build -- the reference is single-process Hogwild,
+// src/model/LINE.cpp:162).  Every rank holds the whole table T; S is the
+// snapshot at the previous exchange.  Per exchange:
+//   begin (compute stream):  D = T - S;  R = D;  S = T
+//   all-reduce R (SUM) over RCCL, asynchronously, overlapping the next
+//   compute step (smore_amd/dist.py OverlapSync)
+//   end (compute stream):    X = scale * R - D;  T += X;  S += X
+// so every rank's samples land once on every replica (one exchange late),
+// and the next begin's D is again only this rank's own updates.  Streaming,
+// 16 B per lane, HBM-bound (begin moves 5 and end 6 table-sized streams).
+#include "train_kernels.h"
+
+namespace smore {
+
+__global__ void __launch_bounds__(256) delta_begin_kernel(const float4* __restrict__ T, float4* __restrict__ S,
+                                                          float4* __restrict__ D, float4* __restrict__ R,
+                                                          uint64_t n4) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const float4 t = T[i], s = S[i];
+        const float4 d = make_float4(t.x - s.x, t.y - s.y, t.z - s.z, t.w - s.w);
+        D[i] = d;
+        R[i] = d;
+        S[i] = t;
+    }
+}
+
+__global__ void __launch_bounds__(256) delta_end_kernel(float4* __restrict__ T, float4* __restrict__ S,
+                                                        const float4* __restrict__ D,
+                                                        const float4* __restrict__ R, float scale, uint64_t n4) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const float4 r = R[i], d = D[i];
+        const float4 x = make_float4(scale * r.x - d.x, scale * r.y - d.y, scale * r.z - d.z, scale * r.w - d.w);
+        float4 t = T[i], s = S[i];
+        t.x += x.x; t.y += x.y; t.z += x.z; t.w += x.w;
+        s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
+        T[i] = t;
+        S[i] = s;
+    }
+}
+
+static unsigned stream_grid(uint64_t n4, int cus) {
+    const uint64_t want = (n4 + 255) / 256, cap = (uint64_t)(cus > 0 ? cus : 256) * 16;
+    return (unsigned)(want < cap ? (want ? want : 1) : cap);
+}
+
+hipError_t launch_delta_begin(const float* T, float* S, float* D, float* R, uint64_t n, int cus, hipStream_t st) {
+    const uint64_t n4 = n / 4;
+    hipLaunchKernelGGL(delta_begin_kernel, dim3(stream_grid(n4, cus)), dim3(256), 0, st,
+                       reinterpret_cast<const float4*>(T), reinterpret_cast<float4*>(S),
+                       reinterpret_cast<float4*>(D), reinterpret_cast<float4*>(R), n4);
+    return hipGetLastError();
+}
+
+hipError_t launch_delta_end(float* T, float* S, const float* D, const float* R, float scale, uint64_t n, int cus,
+                            hipStream_t st) {
+    const uint64_t n4 = n / 4;
+    hipLaunchKernelGGL(delta_end_kernel, dim3(stream_grid(n4, cus)), dim3(256), 0, st, reinterpret_cast<float4*>(T),
+                       reinterpret_cast<float4*>(S), reinterpret_cast<const float4*>(D),
+                       reinterpret_cast<const float4*>(R), scale, n4);
+    return hipGetLastError();
+}
+
+}  // namespace smore

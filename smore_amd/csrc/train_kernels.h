@@ -22,6 +22,7 @@ struct EdgeArgs {
     // edge kernels: the pre-drawn sample records of samples [begin, begin+count)
     // (draw_kernel), rec_width(KMAX) int32 each
     const int32_t* rec;
+    unsigned long long* work;      // Hogwild edge kernels: chunk counter, zeroed per launch
     uint64_t begin, count, total, seed;
     double alpha0;
     float reg;
@@ -50,14 +51,11 @@ constexpr int rec_width(int kmax) {
     while (r < 2 + kmax) r <<= 1;
     return r;
 }
-// edge kernels whose group has a lane per negative plus one draw the samples
-// themselves (software-pipelined, edge_kernels.h); the others read records
-// written by draw_kernel
-constexpr bool pipe_draws(int G, int kmax) { return kmax + 1 <= G; }
-#ifndef SMORE_PIPE_DRAWS
-#define SMORE_PIPE_DRAWS 0
-#endif
+constexpr uint64_t CH_ROUNDS = 128;   // rounds per dynamically handed-out chunk
 inline int kmax_of(int K) { return K <= 5 ? 5 : K <= 10 ? 10 : 20; }
+hipError_t launch_delta_begin(const float* T, float* S, float* D, float* R, uint64_t n, int cus, hipStream_t st);
+hipError_t launch_delta_end(float* T, float* S, const float* D, const float* R, float scale, uint64_t n, int cus,
+                            hipStream_t st);
 hipError_t launch_pack(const DevGraph& g, uint64_t E, uint4* vt32, uint4* ct16, hipStream_t st);
 hipError_t launch_draw(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K, int32_t* rec,
                        unsigned long long* skipped, hipStream_t st);

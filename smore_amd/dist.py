@@ -3,16 +3,25 @@ Hogwild only, src/model/LINE.cpp:162).
 
 One process per GPU.  Every rank holds the whole graph and both embedding
 tables, runs its own disjoint range of global sample indices (Hogwild inside
-the GPU), and every few steps the ranks exchange what they learned:
+the GPU), and the ranks exchange what they learned through the snapshot-delta
+rule
 
     delta_r = T_r - T_snap ;  all_reduce(delta, SUM) over RCCL (xGMI)
     T = T_snap + sum_r delta_r      (or the mean, --sync mean)
-    T_snap = T
 
-With sum, every sample's update lands on the shared table exactly once --
-the multi-GPU analogue of the reference's single shared table.  The
-all-reduce works in place on the context's own device tables (zero-copy
-through __cuda_array_interface__), one collective per table.
+With sum, every sample's update lands on every replica exactly once -- the
+multi-GPU analogue of the reference's single shared table.
+
+Two schedules:
+  DeltaAllReduce  synchronous: the collective runs between two steps.
+  OverlapSync     one exchange late: begin() snapshots this rank's delta and
+                  starts its all-reduce asynchronously (ProcessGroupNCCL runs it
+                  on its own stream, ordered after the compute stream's current
+                  point), the next training step runs meanwhile, and end()
+                  makes the compute stream wait for it and folds the other
+                  ranks' deltas in.  ReplicaSync = OverlapSync over a ProNet
+                  context's device tables with the fused HIP passes of
+                  replica_sync.hip.
 """
 import torch
 import torch.distributed as dist
@@ -35,7 +44,7 @@ def table_tensor(pn, which):
 
 
 class DeltaAllReduce:
-    """Snapshot-delta exchange over a list of same-shaped tensors on every rank."""
+    """Synchronous snapshot-delta exchange over same-shaped tensors on every rank."""
 
     def __init__(self, tensors, mean=False, group=None):
         self.tensors = list(tensors)
@@ -54,8 +63,84 @@ class DeltaAllReduce:
             s.copy_(t)
 
 
-class ReplicaSync(DeltaAllReduce):
-    """DeltaAllReduce over a ProNet context's device tables (W and C)."""
+class TorchPasses:
+    """The exchange passes as torch ops (CPU tensors in the gloo tests)."""
+
+    @staticmethod
+    def begin(T, S, D, R):
+        torch.sub(T, S, out=D)
+        R.copy_(D)
+        S.copy_(T)
+
+    @staticmethod
+    def end(T, S, D, R, scale):
+        R.mul_(scale).sub_(D)
+        T.add_(R)
+        S.add_(R)
+
+
+class HipPasses:
+    """The same passes as one fused HIP kernel each (replica_sync.hip), on the
+    context stream."""
+
+    def __init__(self, pn):
+        self.pn = pn
+
+    def begin(self, T, S, D, R):
+        self.pn.delta_begin(T.data_ptr(), S.data_ptr(), D.data_ptr(), R.data_ptr(), T.numel())
+
+    def end(self, T, S, D, R, scale):
+        self.pn.delta_end(T.data_ptr(), S.data_ptr(), D.data_ptr(), R.data_ptr(), scale, T.numel())
+
+
+class OverlapSync:
+    """One-exchange-late snapshot-delta exchange whose collective overlaps the
+    next compute step (see the module docstring).
+
+        begin():  [end() of the previous exchange]; D = T - S; R = D; S = T;
+                  all_reduce(R) started asynchronously
+        end():    wait for the collective; X = scale*R - D; T += X; S += X
+
+    After end() every replica holds every rank's updates up to the matching
+    begin(), plus its own since."""
+
+    def __init__(self, tensors, mean=False, group=None, passes=None):
+        self.T = list(tensors)
+        self.S = [t.clone() for t in self.T]
+        self.D = [torch.zeros_like(t) for t in self.T]
+        self.R = [torch.zeros_like(t) for t in self.T]
+        self.mean = mean
+        self.group = group
+        self.passes = passes or TorchPasses()
+        self.works = None
+
+    def begin(self):
+        self.end()
+        for T, S, D, R in zip(self.T, self.S, self.D, self.R):
+            self.passes.begin(T, S, D, R)
+        self.works = [dist.all_reduce(R, op=dist.ReduceOp.SUM, group=self.group, async_op=True) for R in self.R]
+
+    def end(self):
+        if self.works is None:
+            return
+        for w in self.works:
+            w.wait()
+        scale = 1.0 / dist.get_world_size(self.group) if self.mean else 1.0
+        for T, S, D, R in zip(self.T, self.S, self.D, self.R):
+            self.passes.end(T, S, D, R, scale)
+        self.works = None
+
+    def allreduce(self):
+        """Synchronous use: begin() then end()."""
+        self.begin()
+        self.end()
+
+
+class ReplicaSync(OverlapSync):
+    """OverlapSync over a ProNet context's device tables (W and C), with the
+    fused HIP passes; the context runs on torch's current stream so the
+    passes, the training kernels and the collective are ordered on it."""
 
     def __init__(self, pn, mean=False, tables=(0, 1), group=None):
-        super().__init__([table_tensor(pn, w) for w in tables], mean=mean, group=group)
+        pn.set_stream(torch.cuda.current_stream().cuda_stream)
+        super().__init__([table_tensor(pn, w) for w in tables], mean=mean, group=group, passes=HipPasses(pn))

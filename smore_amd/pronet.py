@@ -206,6 +206,14 @@ class ProNet:
     def last_kernel_ms(self):
         return float(lib.smore_last_kernel_ms(self.ctx))
 
+    def delta_begin(self, T, S, D, R, n):
+        """Replica exchange pass D = T - S; R = D; S = T (device pointers, n floats)."""
+        self._chk(lib.smore_delta_begin(self.ctx, T, S, D, R, int(n)), "delta_begin")
+
+    def delta_end(self, T, S, D, R, scale, n):
+        """Replica exchange pass X = scale*R - D; T += X; S += X."""
+        self._chk(lib.smore_delta_end(self.ctx, T, S, D, R, float(scale), int(n)), "delta_end")
+
     def last_phase_ms(self):
         """(draw_ms, update_ms) of the last LINE/MF edge launch, or None."""
         import ctypes

@@ -18,15 +18,15 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, mean, out):
+def _worker(rank, world, port, mean, out, overlap=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from smore_amd.dist import DeltaAllReduce
+    from smore_amd.dist import DeltaAllReduce, OverlapSync
     torch.manual_seed(0)
     base = [torch.randn(50, 8), torch.randn(50, 8)]
     tabs = [b.clone() for b in base]
-    sync = DeltaAllReduce(tabs, mean=mean)
+    sync = OverlapSync(tabs, mean=mean) if overlap else DeltaAllReduce(tabs, mean=mean)
     expect = [b.clone() for b in base]
     for step in range(3):
         # each rank updates disjoint and overlapping rows with its own deltas
@@ -36,24 +36,37 @@ def _worker(rank, world, port, mean, out):
             deltas.append([torch.randn(50, 8, generator=g) * 0.01 for _ in tabs])
         for t, d in zip(tabs, deltas[rank]):
             t.add_(d)
-        sync.allreduce()
+        if overlap:
+            sync.begin()     # folds the previous exchange in, starts this one
+        else:
+            sync.allreduce()
         for i in range(len(tabs)):
             tot = sum(deltas[r][i] for r in range(world))
             expect[i] += tot / world if mean else tot
+    if overlap:
+        sync.end()
     ok = all(torch.allclose(t, e, atol=1e-5) for t, e in zip(tabs, expect))
     same = [torch.empty_like(tabs[0]) for _ in range(world)]
     dist.all_gather(same, tabs[0])
-    ok = ok and all(torch.equal(same[0], x) for x in same)
+    # synchronous: snap + sum on every rank, bit-identical replicas; overlapped:
+    # each rank adds (sum - own delta) to its own values, equal within rounding
+    if overlap:
+        ok = ok and all(torch.allclose(same[0], x, atol=1e-6, rtol=0) for x in same)
+    else:
+        ok = ok and all(torch.equal(same[0], x) for x in same)
     out[rank] = int(ok)
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("overlap", [False, True])
 @pytest.mark.parametrize("mean", [False, True])
-def test_delta_allreduce_gloo_world2(mean):
+def test_delta_allreduce_gloo_world2(mean, overlap):
+    """Synchronous (DeltaAllReduce) and one-exchange-late (OverlapSync)
+    schedules end with every rank's updates applied once on every rank."""
     ctx = mp.get_context("spawn")
     out = ctx.Array("i", [0, 0])
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, mean, out)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, mean, out, overlap)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:

@@ -312,8 +312,9 @@ def test_save_weights_format(smore, tmp_path):
 
 
 def test_replica_sync_rccl_single_rank(smore):
-    """RCCL all-reduce path of smore_amd/dist.py on the context's own device
-    tables (zero-copy views), world size 1: W_snap + sum(delta) == W."""
+    """RCCL all-reduce path of smore_amd/dist.py (fused HIP passes,
+    replica_sync.hip) on the context's own device tables (zero-copy views),
+    world size 1: W_snap + sum(delta) == W, synchronous and overlapped."""
     import socket
 
     import torch
@@ -339,7 +340,19 @@ def test_replica_sync_rccl_single_rank(smore):
         torch.cuda.synchronize()
         np.testing.assert_allclose(pn.get_table(0), before[0], atol=1e-6)
         np.testing.assert_allclose(pn.get_table(1), before[1], atol=1e-6)
-        assert torch.equal(sync.snaps[0][:, :64].cpu(), torch.from_numpy(pn.get_table(0)))
+        assert torch.equal(sync.S[0][:, :64].cpu(), torch.from_numpy(pn.get_table(0)))
+        # overlapped schedule: a step runs while the exchange is in flight
+        pn.train_edges("line2", 100000, 100000, 10 ** 6, 5, 0.025, 0.0, SEED, "atomic", sync=False)
+        sync.begin()
+        torch.cuda.synchronize()
+        at_begin = pn.get_table(1)
+        np.testing.assert_array_equal(sync.S[1][:, :64].cpu().numpy(), at_begin)
+        pn.train_edges("line2", 200000, 100000, 10 ** 6, 5, 0.025, 0.0, SEED, "atomic", sync=False)
+        sync.end()             # world 1: adds (R - D) = 0 to T and S
+        torch.cuda.synchronize()
+        assert np.isfinite(pn.get_table(0)).all()
+        np.testing.assert_array_equal(sync.S[1][:, :64].cpu().numpy(), at_begin)
+        assert not np.array_equal(pn.get_table(1), at_begin)
     finally:
         dist.destroy_process_group()
 
