@@ -175,10 +175,13 @@ int smore_hot_rows(const smore_ctx* ctx, int64_t* hot_w, int64_t* hot_c);
 int smore_skipped(smore_ctx* ctx, uint64_t* skipped);
 /* milliseconds of the last training launch (HIP events on the launch stream) */
 float smore_last_kernel_ms(const smore_ctx* ctx);
-/* the last LINE/MF edge launch split by phase: total ms of the draw kernels
- * (sampling, train_draw.hip) and of the update kernels (gather/update/scatter);
- * SMORE_ESTATE if the last launch was not an edge launch */
-int smore_last_phase_ms(const smore_ctx* ctx, float* draw_ms, float* update_ms);
+/* the last LINE/MF edge call split by phase (HIP events on the context stream):
+ * update_ms = total time of its `launches` update-kernel launches (gather/update/
+ * scatter), draw_ms = time the context stream waited for draw kernels
+ * (train_draw.hip) that did not overlap an update (the draws of chunk k+1 run on
+ * a second stream during the update of chunk k); SMORE_ESTATE if the last call
+ * was not an edge call */
+int smore_last_phase_ms(const smore_ctx* ctx, float* draw_ms, float* update_ms, int* launches);
 
 /* ---- multi-GPU replica exchange (new: the reference is single-process Hogwild,
  * src/model/LINE.cpp:162) -------------------------------------------

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -23,6 +24,8 @@ struct smore_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
+    hipStream_t draw_stream = nullptr;   // draw kernels overlapping the previous chunk's update
+    std::vector<hipEvent_t> sync_ev;     // draw-done / update-done hand-offs between the two streams
     std::string err;
     HostGraph g;
     bool has_graph = false;
@@ -171,6 +174,7 @@ int smore_create(int device, smore_ctx** out) {
     }
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->draw_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&c->ev0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev1);
     if (e == hipSuccess) e = hipMalloc((void**)&c->d_skipped, sizeof(unsigned long long));
@@ -201,6 +205,8 @@ void smore_destroy(smore_ctx* c) {
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    if (c->draw_stream) (void)hipStreamDestroy(c->draw_stream);
+    for (hipEvent_t e : c->sync_ev) (void)hipEventDestroy(e);
     delete c;
 }
 
@@ -516,7 +522,7 @@ static int ensure_packed(smore_ctx* c) {
 }
 
 // ---------------------------------------------------------------- training
-static int edge_grid(smore_ctx* c, const EdgeArgs& a) {
+static int edge_grid(smore_ctx* c, const EdgeArgs& a, bool leave_slot = false) {
     if (a.mode == SMORE_SERIAL) return 1;
     int per_cu = 0;
     const void* sym = edge_kernel_symbol(a);
@@ -525,6 +531,14 @@ static int edge_grid(smore_ctx* c, const EdgeArgs& a) {
             hipSuccess ||
         per_cu < 1)
         per_cu = 1;
+    // leave one block slot per CU to the concurrent draw kernel (measured at C4:
+    // 3 of 4 update blocks per CU run the update as fast as 4)
+    if (leave_slot && per_cu > 1) per_cu -= 1;
+    // tuning knob: SMORE_BLOCKS_PER_CU caps the resident blocks per CU
+    if (const char* e = getenv("SMORE_BLOCKS_PER_CU")) {
+        const int cap = atoi(e);
+        if (cap > 0 && cap < per_cu) per_cu = cap;
+    }
     int64_t grid = (int64_t)c->cus * per_cu;
     const int G = lanes_of(a.dpad);
     const int64_t groups_per_block = 256 / G;
@@ -608,39 +622,66 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
         c->phase_n = 0;
         return SMORE_OK;
     }
-    // edge models: draw kernel -> update kernel per chunk of samples (the
-    // record buffer is bounded at 4 GiB; a 2^27-sample launch is one chunk)
+    // edge models: draw kernel -> update kernel per chunk of samples.  With
+    // several chunks the draws of chunk k+1 run on a second stream while
+    // chunk k updates (two record buffers; the update kernel leaves one block
+    // slot per CU for them).  Both kernels are bound by HBM, so the overlap
+    // buys little (C4 hybrid, 2^25-sample chunks: 120.4 ms per 2^27 samples
+    // vs 122 sequential; plain stores 116.6 vs 108): chunks default to 2^27
+    // samples (SMORE_DRAW_CHUNK overrides), i.e. sequential for a bench step.
     const int RW = rec_width(kmax_of(a.K));
-    const uint64_t chunk_max = ((uint64_t)1 << 30) / (uint64_t)RW;
+    uint64_t chunk_max = (uint64_t)1 << 27;
+    if (const char* e = getenv("SMORE_DRAW_CHUNK")) chunk_max = std::max<uint64_t>(1024, strtoull(e, nullptr, 10));
+    if (a.mode == SMORE_SERIAL) chunk_max = ((uint64_t)1 << 30) / (uint64_t)RW;
     const uint64_t chunk = std::min<uint64_t>(count, chunk_max);
-    if (c->rec_cap < chunk * RW) {
+    const int nch = (int)((count + chunk - 1) / chunk);
+    const int nbuf = nch > 1 ? 2 : 1;
+    if (c->rec_cap < chunk * RW * nbuf) {
         dfree(c->d_rec);
         c->rec_cap = 0;
-        HIPCHK(c, hipMalloc(&c->d_rec, chunk * RW * sizeof(int32_t)));
-        c->rec_cap = chunk * RW;
+        HIPCHK(c, hipMalloc(&c->d_rec, chunk * RW * nbuf * sizeof(int32_t)));
+        c->rec_cap = chunk * RW * nbuf;
     }
-    const int nch = (int)((count + chunk - 1) / chunk);
-    while ((int)c->phase_ev.size() < 2 * nch + 1) {
-        hipEvent_t e;
-        HIPCHK(c, hipEventCreate(&e));
-        c->phase_ev.push_back(e);
-    }
+    auto grow = [&](std::vector<hipEvent_t>& v, size_t n) -> int {
+        while (v.size() < n) {
+            hipEvent_t e;
+            HIPCHK(c, hipEventCreate(&e));
+            v.push_back(e);
+        }
+        return SMORE_OK;
+    };
+    if ((rc = grow(c->phase_ev, 2 * (size_t)nch + 1))) return rc;
+    if ((rc = grow(c->sync_ev, 2 * (size_t)nch))) return rc;
     if ((rc = ensure_packed(c))) return rc;
     const DevGraph dg = dev_graph(c);
+    const int ugrid = nch > 1 ? edge_grid(c, a, true) : grid;
+    hipStream_t ds = nch > 1 ? c->draw_stream : c->stream;
+    auto recbuf = [&](int k) { return c->d_rec + (size_t)(k % nbuf) * chunk * RW; };
+    auto draw = [&](int k) -> int {
+        const uint64_t b = (uint64_t)k * chunk, n = std::min<uint64_t>(chunk, count - b);
+        if (k >= 2) HIPCHK(c, hipStreamWaitEvent(ds, c->sync_ev[2 * (k - 2) + 1], 0));   // buffer free
+        HIPCHK(c, launch_draw(dg, seed, begin + b, n, a.K, recbuf(k), c->d_skipped, ds));
+        HIPCHK(c, hipEventRecord(c->sync_ev[2 * k], ds));
+        return SMORE_OK;
+    };
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream));
+    if (ds != c->stream) HIPCHK(c, hipStreamWaitEvent(ds, c->phase_ev[0], 0));   // after earlier work
+    if ((rc = draw(0))) return rc;
     for (int k = 0; k < nch; ++k) {
-        const uint64_t b = (uint64_t)k * chunk, n = std::min<uint64_t>(chunk, count - b);
-        HIPCHK(c, launch_draw(dg, seed, begin + b, n, a.K, c->d_rec, c->d_skipped, c->stream));
+        if (k + 1 < nch && (rc = draw(k + 1))) return rc;
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->sync_ev[2 * k], 0));
         HIPCHK(c, hipEventRecord(c->phase_ev[2 * k + 1], c->stream));
+        const uint64_t b = (uint64_t)k * chunk, n = std::min<uint64_t>(chunk, count - b);
         EdgeArgs ak = a;
         ak.begin = begin + b;
         ak.count = n;
-        ak.rec = c->d_rec;
+        ak.rec = recbuf(k);
         ak.work = c->d_work;
         HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
-        HIPCHK(c, launch_edge_train(ak, grid, c->stream));
+        HIPCHK(c, launch_edge_train(ak, ugrid, c->stream));
         HIPCHK(c, hipEventRecord(c->phase_ev[2 * k + 2], c->stream));
+        HIPCHK(c, hipEventRecord(c->sync_ev[2 * k + 1], c->stream));
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
@@ -648,7 +689,7 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
     return SMORE_OK;
 }
 
-int smore_last_phase_ms(const smore_ctx* c, float* draw_ms, float* update_ms) {
+int smore_last_phase_ms(const smore_ctx* c, float* draw_ms, float* update_ms, int* launches) {
     if (!c || !c->timed || c->phase_n <= 0) return SMORE_ESTATE;
     float d = 0.0f, u = 0.0f, ms = 0.0f;
     if (hipEventSynchronize(c->phase_ev[2 * c->phase_n]) != hipSuccess) return SMORE_EHIP;
@@ -660,6 +701,7 @@ int smore_last_phase_ms(const smore_ctx* c, float* draw_ms, float* update_ms) {
     }
     if (draw_ms) *draw_ms = d;
     if (update_ms) *update_ms = u;
+    if (launches) *launches = c->phase_n;
     return SMORE_OK;
 }
 

@@ -215,12 +215,13 @@ class ProNet:
         self._chk(lib.smore_delta_end(self.ctx, T, S, D, R, float(scale), int(n)), "delta_end")
 
     def last_phase_ms(self):
-        """(draw_ms, update_ms) of the last LINE/MF edge launch, or None."""
+        """(exposed draw ms, update ms, update launches) of the last LINE/MF
+        edge call, or None."""
         import ctypes
-        d, u = ctypes.c_float(), ctypes.c_float()
-        if lib.smore_last_phase_ms(self.ctx, ctypes.byref(d), ctypes.byref(u)) != 0:
+        d, u, n = ctypes.c_float(), ctypes.c_float(), ctypes.c_int()
+        if lib.smore_last_phase_ms(self.ctx, ctypes.byref(d), ctypes.byref(u), ctypes.byref(n)) != 0:
             return None
-        return float(d.value), float(u.value)
+        return float(d.value), float(u.value), int(n.value)
 
     def load_pretrain(self, which, path):
         """proNet::LoadPreTrain (src/proNet.cpp:238-286)."""
