@@ -413,3 +413,29 @@ def test_hybrid_deepwalk_and_bpr_run(smore):
     pb.set_hot_threshold(1e-3)
     pb.train_edges("bpr", 0, 100000, 100000, 5, 0.05, 0.0, SEED, "hybrid")
     assert np.isfinite(pb.get_table(0)).all()
+
+
+def test_chunked_overlapped_draws(smore):
+    """Calls larger than one record chunk: the draws of chunk k+1 run on a
+    second stream during the update of chunk k (double-buffered records).
+    Serial mode is unaffected (one chunk); a chunked atomic run trains as
+    well as an unchunked one and leaves finite tables."""
+    g, pn = make_pair(smore, "pl1k.txt", 1)
+    total = 2 * 10 ** 6
+    res = {}
+    for chunk in (None, "65536"):
+        if chunk:
+            os.environ["SMORE_DRAW_CHUNK"] = chunk
+        try:
+            pn.alloc_tables(32, 2)
+            pn.init_table_glibc(0, 0)
+            pn.zero_table(1)
+            pn.train_edges("line2", 0, total - 1, total, 5, 0.025, 0.0, SEED, "atomic")
+            ph = pn.last_phase_ms()
+            W, C = pn.get_table(0), pn.get_table(1)
+        finally:
+            os.environ.pop("SMORE_DRAW_CHUNK", None)
+        assert np.isfinite(W).all() and np.isfinite(C).all()
+        assert ph is not None and ph[2] == (1 if chunk is None else -(-(total - 1) // int(chunk)))
+        res[chunk] = _auc(W, C, g, np.random.default_rng(0))
+    assert abs(res[None] - res["65536"]) < 0.02, res
