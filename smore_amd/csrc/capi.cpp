@@ -419,11 +419,13 @@ int smore_table_device(smore_ctx* c, int which, void** dptr, int64_t* stride) {
 // W-rows through the vertex table, C-rows through the negative and context
 // tables and the CSR targets (one union set for shared-table models).  Written
 // in place into the existing device arrays; the host graph stays untagged.
-constexpr double SH_STALE_MAX = 4096.0;
+constexpr double SH_STALE_MAX = 65536.0;
 
 static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
     char key[128];
-    snprintf(key, sizeof key, "%d/%d/%lld/%.9g/%d/%d", model, K, (long long)M, c->hot_tau, c->sh_max, c->sh_flush);
+    const char* stale_env = getenv("SMORE_SH_STALE");
+    snprintf(key, sizeof key, "%d/%d/%lld/%.9g/%d/%d/%s", model, K, (long long)M, c->hot_tau, c->sh_max, c->sh_flush,
+             stale_env ? stale_env : "");
     if (c->hot_key == key) return SMORE_OK;
     if (c->g.V >= ((int64_t)1 << 30)) return fail(c, SMORE_EINVAL, "hybrid scatter needs V < 2^30");
     std::vector<double> ps, pn, pc;
@@ -441,6 +443,8 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
     }
     // super-hot rows: the hottest hot context rows, write-combined per block
     {
+        double stale_max = SH_STALE_MAX;   // SMORE_SH_STALE overrides (tuning)
+        if (const char* e = getenv("SMORE_SH_STALE")) stale_max = atof(e);
         std::vector<std::pair<double, int32_t>> r;
         for (int64_t v = 0; v < V; ++v) {
             const double p = model == SMORE_LINE2 ? pc[v] + negs * pn[v] : ps[v] + pc[v] + negs * pn[v];
@@ -448,7 +452,7 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
             // other workgroups for up to sh_flush rounds, i.e. about
             // M * p * sh_flush updates; rows above SH_STALE_MAX stay on atomics
             // (on small graphs that is every hot row)
-            if (hc[v] && (double)M * p * c->sh_flush <= SH_STALE_MAX) r.push_back({p, (int32_t)v});
+            if (hc[v] && (double)M * p * c->sh_flush <= stale_max) r.push_back({p, (int32_t)v});
         }
         const int64_t cap = std::max<int64_t>(0, std::min<int64_t>(c->sh_max, 8192 / std::max(1, c->dpad)));
         const int64_t n = std::min<int64_t>(cap, (int64_t)r.size());

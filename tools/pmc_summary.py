@@ -1,10 +1,15 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 outputs of the bench into profiles/: per-launch HBM
-traffic of the hot kernel from separate FETCH_SIZE / WRITE_SIZE passes
+traffic of a kernel from separate FETCH_SIZE / WRITE_SIZE passes
 (MI355X_MICROARCH.md "HBM": FETCH_SIZE / WRITE_SIZE in KB, from the L2's
-memory-side request counters; WRITE_SIZE exact for float atomics and dword
-stores, FETCH_SIZE uncalibrated for 4-B-per-lane 64-B-segment gathers, so it
-is reported uncorrected) and the kernel-trace average duration.
+memory-side request counters, Infinity-Cache hits included) and the
+kernel-trace average duration.
+
+gfx950 correction, calibrated on this path's own access shape
+(profiles/pmc_calibration.json: tools/probe_scatter's dword-per-lane gathers of
+random 256-B rows from a 5-GB table, known byte counts): FETCH_SIZE reads
+0.51 x the bytes fetched, WRITE_SIZE 1.000 x the bytes written (stores and
+float atomics).  Fetched bytes are therefore FETCH_SIZE x 2.
 
     python tools/pmc_summary.py --fetch F.csv --write W.csv --stats S.csv \
         --config c4 --samples 134217728 --mode hybrid --out profiles/pmc_traffic.json
@@ -12,6 +17,9 @@ is reported uncorrected) and the kernel-trace average duration.
 import argparse
 import csv
 import json
+
+
+FETCH_CORRECTION = 2.0
 
 
 def per_dispatch(path, kernel):
@@ -33,6 +41,8 @@ def main():
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     f, nf = per_dispatch(a.fetch, a.kernel)
+    f_raw = f
+    f = f * FETCH_CORRECTION
     w, nw = per_dispatch(a.write, a.kernel)
     stats = [r for r in csv.DictReader(open(a.stats)) if a.kernel in r["Name"]]
     avg_ns = float(stats[0]["AverageNs"]) if stats else None
@@ -40,13 +50,14 @@ def main():
         "config": a.config, "samples": a.samples, "mode": a.mode,
         "kernel": stats[0]["Name"] if stats else a.kernel,
         "dispatches_fetch": nf, "dispatches_write": nw,
-        "fetch_size_kb": f, "write_size_kb": w,
+        "fetch_size_kb_raw": f_raw, "fetch_kb_corrected": f, "write_size_kb": w,
         "hbm_bytes_per_launch": (f + w) * 1024.0,
         "fetch_bytes_per_sample": f * 1024.0 / a.samples,
         "write_bytes_per_sample": w * 1024.0 / a.samples,
         "kernel_avg_ns": avg_ns,
         "note": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; units KB; "
-                "FETCH_SIZE uncorrected (uncalibrated for this access shape) and includes Infinity-Cache hits",
+                "fetch = FETCH_SIZE x 2 (gfx950 half-count, calibrated in profiles/pmc_calibration.json); "
+                "includes Infinity-Cache hits",
     }
     json.dump(out, open(a.out, "w"), indent=1)
     print(json.dumps(out))
