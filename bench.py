@@ -7,7 +7,7 @@ config c4 (10M vertices / 200M undirected lines = 400M directed slots, d=64,
 K=5; the north star's 1/2/4/8-GPU graph), inputs resident in
 HBM.  A step is the draw kernel (train_draw.hip) and the update kernel
 (edge_kernels.h).  Default scatter: hybrid (atomic adds for the hot rows, the
-32 hottest write-combined per workgroup in LDS, plain stores for the rest),
+128 hottest write-combined per workgroup in LDS, plain stores for the rest),
 whose training objective matches the lossless atomic scatter.
 One process per GPU; with N > 1 each rank runs its own disjoint global-sample
 range on a replicated graph and replicated tables, and the tables' deltas are
@@ -59,8 +59,8 @@ def parse():
     ap.add_argument("--mode", default="hybrid", choices=["hogwild", "atomic", "hybrid"],
                     help="scatter: hybrid (default), atomic (every row), hogwild (plain stores, loses updates)")
     ap.add_argument("--hot-tau", type=float, default=0.3, help="hybrid: hot-row threshold")
-    ap.add_argument("--combine-rows", type=int, default=32, help="hybrid: LDS write-combined hottest rows")
-    ap.add_argument("--combine-flush", type=int, default=16, help="hybrid: rounds between LDS flushes")
+    ap.add_argument("--combine-rows", type=int, default=128, help="hybrid: LDS write-combined hottest rows")
+    ap.add_argument("--combine-flush", type=int, default=32, help="hybrid: rounds between LDS flushes")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
     ap.add_argument("--sync-every", type=int, default=1)
     ap.add_argument("--sync", default="sum", choices=["sum", "mean"])

@@ -164,11 +164,12 @@ int smore_train_edges(smore_ctx* ctx, int model, uint64_t begin, uint64_t count,
  * (its per-sample touch probability) > tau (default 0.3); see DESIGN.md */
 int smore_set_hot_threshold(smore_ctx* ctx, double tau);
 /* rows marked hot in W and C by the last hybrid launch */
-/* hybrid scatter: the `rows` hottest hot context rows (default 32; 0 = off; at
- * most 8192/dim) are write-combined per workgroup in LDS and added to HBM every
- * `flush_rounds` rounds of the persistent loop (default 16) -- bounded extra
- * staleness on those rows only, in exchange for not serialising every sample's
- * atomic adds on the same few HBM lines. */
+/* hybrid scatter: the `rows` hottest hot context rows (default 128; 0 = off; at
+ * most 8192/dim) are write-combined per workgroup in LDS and drained to HBM every
+ * `flush_rounds` rounds of a wave's loop (default 32) -- bounded extra staleness on
+ * those rows only (rows whose expected updates per flush window exceed 65536 stay
+ * on atomics), in exchange for not serialising every sample's atomic adds on the
+ * same few HBM lines. */
 int smore_set_write_combine(smore_ctx* ctx, int rows, int flush_rounds);
 int smore_hot_rows(const smore_ctx* ctx, int64_t* hot_w, int64_t* hot_c);
 /* samples whose source had no out-edge (reference: TargetSample -> -1) */

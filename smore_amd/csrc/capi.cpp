@@ -64,7 +64,7 @@ struct smore_ctx {
     int2* d_sh_hash = nullptr;
     int32_t* d_sh_ids = nullptr;
     int sh_rows = 0;
-    int sh_max = 32, sh_flush = 16;
+    int sh_max = 128, sh_flush = 32;
     // pre-drawn edge-sample records (train_draw.hip) and per-phase timing
     int32_t* d_rec = nullptr;
     // packed draw tables (train_draw.hip), rebuilt when the graph tables change

@@ -183,7 +183,7 @@ class ProNet:
         self._chk(lib.smore_set_semantics(self.ctx, _lib.SEM[semantics]), "set_semantics")
         self.semantics = semantics
 
-    def set_write_combine(self, rows, flush_rounds=64):
+    def set_write_combine(self, rows, flush_rounds=32):
         """Hybrid scatter: LDS write-combining of the `rows` hottest context rows."""
         self._chk(lib.smore_set_write_combine(self.ctx, int(rows), int(flush_rounds)), "set_write_combine")
 

@@ -55,7 +55,7 @@ def main():
         mode = parts[0]
         if len(parts) > 1:
             pn.set_hot_threshold(float(parts[1]))
-        pn.set_write_combine(int(parts[2]) if len(parts) > 2 else 32, int(parts[3]) if len(parts) > 3 else 64)
+        pn.set_write_combine(int(parts[2]) if len(parts) > 2 else 128, int(parts[3]) if len(parts) > 3 else 32)
         pn.alloc_tables(args.dim, 2)
         pn.init_table_uniform(0, 3)
         pn.zero_table(1)
