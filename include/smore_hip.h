@@ -193,6 +193,10 @@ int smore_last_phase_ms(const smore_ctx* ctx, float* draw_ms, float* update_ms, 
  * Driven by smore_amd/dist.py (RCCL all-reduce overlapping the next step). */
 int smore_delta_begin(smore_ctx* ctx, const void* T, void* S, void* D, void* R, int64_t n);
 int smore_delta_end(smore_ctx* ctx, void* T, void* S, const void* D, const void* R, float scale, int64_t n);
+/* end of one exchange fused with the begin of the next (one pass instead of two):
+ * X = scale*R - D; T += X; then D = T - S (the rank's delta since the last begin),
+ * R = D, S = T */
+int smore_delta_cycle(smore_ctx* ctx, void* T, void* S, void* D, void* R, float scale, int64_t n);
 
 /* replaces: DeepWalk::Train (src/model/DeepWalk.cpp:98-155): walks
  * [walk_begin, walk_end) of walk_times*V, start vertices order[] (host,

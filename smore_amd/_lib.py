@@ -62,6 +62,7 @@ def _load():
         "smore_last_phase_ms": (i32, [P, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(i32)]),
         "smore_delta_begin": (i32, [P, P, P, P, P, i64]),
         "smore_delta_end": (i32, [P, P, P, P, P, C.c_float, i64]),
+        "smore_delta_cycle": (i32, [P, P, P, P, P, C.c_float, i64]),
         "smore_train_deepwalk": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, u64, P, i32]),
         "smore_deepwalk_order": (i32, [i64, i32, u64, P]),
         "smore_sample_edges": (i32, [P, i32, u64, u64, i32, u64, P]),

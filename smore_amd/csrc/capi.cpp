@@ -942,4 +942,11 @@ int smore_delta_end(smore_ctx* c, void* T, void* S, const void* D, const void* R
     return SMORE_OK;
 }
 
+int smore_delta_cycle(smore_ctx* c, void* T, void* S, void* D, void* R, float scale, int64_t n) {
+    int rc;
+    if ((rc = delta_args(c, T, S, D, R, n))) return rc;
+    HIPCHK(c, launch_delta_cycle((float*)T, (float*)S, (float*)D, (float*)R, scale, (uint64_t)n, c->cus, c->stream));
+    return SMORE_OK;
+}
+
 }  // extern "C"

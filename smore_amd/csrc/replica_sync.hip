@@ -41,6 +41,26 @@ __global__ void __launch_bounds__(256) delta_end_kernel(float4* __restrict__ T, 
     }
 }
 
+// end of exchange k fused with begin of exchange k+1 (8 streams instead of
+// 5 + 6): X = scale*R - D; T' = T + X; then D' = T' - (S + X) = T - S,
+// R' = D', S' = T'
+__global__ void __launch_bounds__(256) delta_cycle_kernel(float4* __restrict__ T, float4* __restrict__ S,
+                                                          float4* __restrict__ D, float4* __restrict__ R, float scale,
+                                                          uint64_t n4) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const float4 r = R[i], d = D[i], t = T[i], s = S[i];
+        const float4 x = make_float4(scale * r.x - d.x, scale * r.y - d.y, scale * r.z - d.z, scale * r.w - d.w);
+        const float4 tn = make_float4(t.x + x.x, t.y + x.y, t.z + x.z, t.w + x.w);
+        const float4 sn = make_float4(s.x + x.x, s.y + x.y, s.z + x.z, s.w + x.w);
+        const float4 dn = make_float4(tn.x - sn.x, tn.y - sn.y, tn.z - sn.z, tn.w - sn.w);
+        T[i] = tn;
+        D[i] = dn;
+        R[i] = dn;
+        S[i] = tn;
+    }
+}
+
 static unsigned stream_grid(uint64_t n4, int cus) {
     const uint64_t want = (n4 + 255) / 256, cap = (uint64_t)(cus > 0 ? cus : 256) * 16;
     return (unsigned)(want < cap ? (want ? want : 1) : cap);
@@ -60,6 +80,15 @@ hipError_t launch_delta_end(float* T, float* S, const float* D, const float* R, 
     hipLaunchKernelGGL(delta_end_kernel, dim3(stream_grid(n4, cus)), dim3(256), 0, st, reinterpret_cast<float4*>(T),
                        reinterpret_cast<float4*>(S), reinterpret_cast<const float4*>(D),
                        reinterpret_cast<const float4*>(R), scale, n4);
+    return hipGetLastError();
+}
+
+hipError_t launch_delta_cycle(float* T, float* S, float* D, float* R, float scale, uint64_t n, int cus,
+                              hipStream_t st) {
+    const uint64_t n4 = n / 4;
+    hipLaunchKernelGGL(delta_cycle_kernel, dim3(stream_grid(n4, cus)), dim3(256), 0, st, reinterpret_cast<float4*>(T),
+                       reinterpret_cast<float4*>(S), reinterpret_cast<float4*>(D), reinterpret_cast<float4*>(R), scale,
+                       n4);
     return hipGetLastError();
 }
 

@@ -56,6 +56,8 @@ inline int kmax_of(int K) { return K <= 5 ? 5 : K <= 10 ? 10 : 20; }
 hipError_t launch_delta_begin(const float* T, float* S, float* D, float* R, uint64_t n, int cus, hipStream_t st);
 hipError_t launch_delta_end(float* T, float* S, const float* D, const float* R, float scale, uint64_t n, int cus,
                             hipStream_t st);
+hipError_t launch_delta_cycle(float* T, float* S, float* D, float* R, float scale, uint64_t n, int cus,
+                              hipStream_t st);
 hipError_t launch_pack(const DevGraph& g, uint64_t E, uint4* vt32, uint4* ct16, hipStream_t st);
 hipError_t launch_draw(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K, int32_t* rec,
                        unsigned long long* skipped, hipStream_t st);

@@ -78,6 +78,11 @@ class TorchPasses:
         T.add_(R)
         S.add_(R)
 
+    @classmethod
+    def cycle(cls, T, S, D, R, scale):
+        cls.end(T, S, D, R, scale)
+        cls.begin(T, S, D, R)
+
 
 class HipPasses:
     """The same passes as one fused HIP kernel each (replica_sync.hip), on the
@@ -92,13 +97,16 @@ class HipPasses:
     def end(self, T, S, D, R, scale):
         self.pn.delta_end(T.data_ptr(), S.data_ptr(), D.data_ptr(), R.data_ptr(), scale, T.numel())
 
+    def cycle(self, T, S, D, R, scale):
+        self.pn.delta_cycle(T.data_ptr(), S.data_ptr(), D.data_ptr(), R.data_ptr(), scale, T.numel())
+
 
 class OverlapSync:
     """One-exchange-late snapshot-delta exchange whose collective overlaps the
     next compute step (see the module docstring).
 
-        begin():  [end() of the previous exchange]; D = T - S; R = D; S = T;
-                  all_reduce(R) started asynchronously
+        begin():  [end() of the previous exchange, fused with this begin];
+                  D = T - S; R = D; S = T; all_reduce(R) started asynchronously
         end():    wait for the collective; X = scale*R - D; T += X; S += X
 
     After end() every replica holds every rank's updates up to the matching
@@ -115,17 +123,26 @@ class OverlapSync:
         self.works = None
 
     def begin(self):
-        self.end()
-        for T, S, D, R in zip(self.T, self.S, self.D, self.R):
-            self.passes.begin(T, S, D, R)
+        if self.works is not None:      # fold the previous exchange in and start this one: one pass
+            for w in self.works:
+                w.wait()
+            scale = self._scale()
+            for T, S, D, R in zip(self.T, self.S, self.D, self.R):
+                self.passes.cycle(T, S, D, R, scale)
+        else:
+            for T, S, D, R in zip(self.T, self.S, self.D, self.R):
+                self.passes.begin(T, S, D, R)
         self.works = [dist.all_reduce(R, op=dist.ReduceOp.SUM, group=self.group, async_op=True) for R in self.R]
+
+    def _scale(self):
+        return 1.0 / dist.get_world_size(self.group) if self.mean else 1.0
 
     def end(self):
         if self.works is None:
             return
         for w in self.works:
             w.wait()
-        scale = 1.0 / dist.get_world_size(self.group) if self.mean else 1.0
+        scale = self._scale()
         for T, S, D, R in zip(self.T, self.S, self.D, self.R):
             self.passes.end(T, S, D, R, scale)
         self.works = None

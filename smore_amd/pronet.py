@@ -214,6 +214,10 @@ class ProNet:
         """Replica exchange pass X = scale*R - D; T += X; S += X."""
         self._chk(lib.smore_delta_end(self.ctx, T, S, D, R, float(scale), int(n)), "delta_end")
 
+    def delta_cycle(self, T, S, D, R, scale, n):
+        """delta_end then delta_begin in one pass."""
+        self._chk(lib.smore_delta_cycle(self.ctx, T, S, D, R, float(scale), int(n)), "delta_cycle")
+
     def last_phase_ms(self):
         """(exposed draw ms, update ms, update launches) of the last LINE/MF
         edge call, or None."""

@@ -353,6 +353,13 @@ def test_replica_sync_rccl_single_rank(smore):
         assert np.isfinite(pn.get_table(0)).all()
         np.testing.assert_array_equal(sync.S[1][:, :64].cpu().numpy(), at_begin)
         assert not np.array_equal(pn.get_table(1), at_begin)
+        # begin() while an exchange is in flight: the fused end+begin pass
+        sync.begin()
+        pn.train_edges("line2", 300000, 100000, 10 ** 6, 5, 0.025, 0.0, SEED, "atomic", sync=False)
+        sync.begin()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(sync.S[0][:, :64].cpu().numpy(), pn.get_table(0))
+        sync.end()
     finally:
         dist.destroy_process_group()
 
