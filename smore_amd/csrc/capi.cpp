@@ -618,14 +618,6 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
     a.sh_hash = c->d_sh_hash;
     a.sh_ids = c->d_sh_ids;
     a.sh_flush = std::max(1, c->sh_flush);
-    if (model == SMORE_BPR) {
-        HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-        HIPCHK(c, launch_edge_train(a, grid, c->stream));
-        HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-        c->timed = true;
-        c->phase_n = 0;
-        return SMORE_OK;
-    }
     // edge models: draw kernel -> update kernel per chunk of samples.  With
     // several chunks the draws of chunk k+1 run on a second stream while
     // chunk k updates (two record buffers; the update kernel leaves one block

@@ -1,7 +1,7 @@
 // edge_inst.h -- instantiation helper for edge_train_kernel: one translation
 // unit per (scatter MODE, KMAX) (train_edge_<mode>_k<KMAX>.hip) so the build
-// compiles them in parallel.  Dispatch over (G, M) and the table layout
-// (SH = 0: LINE-2's two tables, 1: one shared table, LINE-1 / MF).
+// compiles them in parallel.  Dispatch over (G, M) and the rule (SH = 0:
+// LINE-2's two tables, 1: one shared table, LINE-1 / MF, 2: BPR, KMAX 5 only).
 #pragma once
 #include "edge_kernels.h"
 
@@ -17,8 +17,14 @@ struct EdgeInst {
     }
     static hipError_t launch(const EdgeArgs& a, int grid, hipStream_t st) {
         const int G = lanes_of(a.dpad), M = (a.dpad + G - 1) / G;
-#define X(g, m) \
-    if (G == g && M == m) return a.model == 0 ? go<g, m, 0>(a, grid, st) : go<g, m, 1>(a, grid, st);
+#define X(g, m)                                                                           \
+    if (G == g && M == m) {                                                               \
+        if (a.model == 3) {                                                               \
+            if constexpr (KMAX == 5) return go<g, m, 2>(a, grid, st);                     \
+            else return hipErrorInvalidValue;                                             \
+        }                                                                                 \
+        return a.model == 0 ? go<g, m, 0>(a, grid, st) : go<g, m, 1>(a, grid, st);        \
+    }
         SMORE_FOR_EACH_GM(X)
 #undef X
         return hipErrorInvalidValue;
@@ -26,9 +32,14 @@ struct EdgeInst {
     static const void* symbol(const EdgeArgs& a) {
         const int G = lanes_of(a.dpad), M = (a.dpad + G - 1) / G;
 #define X(g, m)                                                                          \
-    if (G == g && M == m)                                                                \
+    if (G == g && M == m) {                                                              \
+        if (a.model == 3) {                                                              \
+            if constexpr (KMAX == 5) return (const void*)edge_train_kernel<g, m, 5, MODE, 2>; \
+            else return nullptr;                                                         \
+        }                                                                                \
         return a.model == 0 ? (const void*)edge_train_kernel<g, m, KMAX, MODE, 0>        \
-                            : (const void*)edge_train_kernel<g, m, KMAX, MODE, 1>;
+                            : (const void*)edge_train_kernel<g, m, KMAX, MODE, 1>;       \
+    }
         SMORE_FOR_EACH_GM(X)
 #undef X
         return nullptr;

@@ -38,8 +38,12 @@ enum { MODE_STORE = 0, MODE_ATOMIC = 1, MODE_HYBRID = 3 };
 #ifndef SMORE_WAVES_HYBRID
 #define SMORE_WAVES_HYBRID 4
 #endif
-constexpr int waves_of(int mode) {
-    return mode == MODE_STORE ? SMORE_WAVES_STORE : mode == MODE_ATOMIC ? SMORE_WAVES_ATOMIC : SMORE_WAVES_HYBRID;
+#ifndef SMORE_WAVES_BPR
+#define SMORE_WAVES_BPR 0
+#endif
+constexpr int waves_of(int mode, int shared = 0) {
+    return shared == 2 ? SMORE_WAVES_BPR   // BPR: 7 rows and their originals
+                       : mode == MODE_STORE ? SMORE_WAVES_STORE : mode == MODE_ATOMIC ? SMORE_WAVES_ATOMIC : SMORE_WAVES_HYBRID;
 }
 
 // hybrid scatter: a row is added atomically iff its id tag says hot
@@ -330,11 +334,121 @@ __device__ __forceinline__ void sgd_update(const EdgeArgs& a, const float* s_sig
     sgd_update_rows<G, M, KMAX, MODE>(a, s_sig, lane, ev, v, id, hotw, hot, alpha, shared, mf, sh, wv, rows);
 }
 
+// ------------------------------------------------------------------ BPR update
+// UpdateBPRPair (src/proNet.cpp:1406-1455), one shared table, 5 rounds, on
+// rows gathered by gather_rows: wv = W[u], rows[0] = W[i], rows[1+n] = W[j_n].
+template <int G, int M, int KMAX, int MODE>
+__device__ __forceinline__ void bpr_update_rows(const EdgeArgs& a, const float* s_sig, int lane,
+                                                const bool (&ev)[M], int32_t u, const int32_t (&idc)[KMAX + 1],
+                                                bool hotu, const bool (&hotc)[KMAX + 1], float alpha,
+                                                float (&wv)[M], float (&rows)[KMAX + 1][M]) {
+    static_assert(KMAX == 5, "BPR: 5 rounds");
+    constexpr int NS = 7;
+    const int dpad = a.dpad;
+    float* const T = a.W;
+    int32_t id[NS];
+    bool hot[NS];
+    float row[NS][M];
+    id[0] = u;
+    hot[0] = hotu;
+#pragma unroll
+    for (int m = 0; m < M; ++m) row[0][m] = wv[m];
+#pragma unroll
+    for (int k = 0; k <= KMAX; ++k) {
+        id[1 + k] = idc[k];
+        hot[1 + k] = hotc[k];
+#pragma unroll
+        for (int m = 0; m < M; ++m) row[1 + k][m] = rows[k][m];
+    }
+#pragma unroll
+    for (int k = 1; k < NS; ++k)
+#pragma unroll
+        for (int k2 = 0; k2 < k; ++k2)
+            if (id[k2] == id[k]) {
+#pragma unroll
+                for (int m = 0; m < M; ++m) row[k][m] = row[k2][m];
+            }
+    constexpr bool DELTA = MODE == MODE_ATOMIC || MODE == MODE_HYBRID;
+    float orig[DELTA ? NS : 1][M];
+    if constexpr (DELTA) {
+#pragma unroll
+        for (int k = 0; k < NS; ++k)
+#pragma unroll
+            for (int m = 0; m < M; ++m) orig[k][m] = row[k][m];
+    }
+    const float r1 = alpha * 0.0025f, r2 = alpha * 0.025f;
+    float ve[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) ve[m] = 0.0f;
+
+#define SMORE_PROPAGATE(K_)                                                              \
+_Pragma("unroll") for (int k2 = 0; k2 < NS; ++k2) if (k2 != (K_) && id[k2] == id[(K_)]) { \
+    _Pragma("unroll") for (int m = 0; m < M; ++m) row[k2][m] = row[(K_)][m];                \
+}
+
+#pragma unroll
+    for (int n = 0; n < 5; ++n) {
+        const int J = 2 + n;
+        float x[M], ce[M];
+        float p = 0.0f;
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            x[m] = row[1][m] - row[J][m];
+            p = __builtin_fmaf(row[0][m], x[m], p);
+        }
+        const float f = group_sum<G>(p);
+        const float gg = fast_sigmoid(-f, s_sig) * alpha;
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            ve[m] = __builtin_fmaf(gg, x[m], ve[m]);
+            ce[m] = gg * row[0][m];
+        }
+#pragma unroll
+        for (int m = 0; m < M; ++m) row[1][m] = __builtin_fmaf(-r1, row[1][m], row[1][m]);
+        SMORE_PROPAGATE(1)
+#pragma unroll
+        for (int m = 0; m < M; ++m) row[J][m] = __builtin_fmaf(-r1, row[J][m], row[J][m]);
+        SMORE_PROPAGATE(J)
+#pragma unroll
+        for (int m = 0; m < M; ++m) row[1][m] = row[1][m] + ce[m];
+        SMORE_PROPAGATE(1)
+#pragma unroll
+        for (int m = 0; m < M; ++m) row[J][m] = row[J][m] - ce[m];
+        SMORE_PROPAGATE(J)
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) row[0][m] = __builtin_fmaf(-r2, row[0][m], row[0][m]) + ve[m];
+    SMORE_PROPAGATE(0)
+#undef SMORE_PROPAGATE
+
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        bool last = true;
+#pragma unroll
+        for (int k2 = k + 1; k2 < NS; ++k2) last = last && (id[k2] != id[k]);
+        if (last) {
+            float* q = T + (int64_t)id[k] * dpad + lane;
+            const bool atom = hot[k];
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+                if (!ev[m]) continue;
+                if constexpr (DELTA) {
+                    if (atom) unsafeAtomicAdd(q + m * G, row[k][m] - orig[k][m]);
+                    else q[m * G] = row[k][m];
+                } else {
+                    q[m * G] = row[k][m];
+                }
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------ edge kernel
-// LINE-2 (W,C), LINE-1 (W,W), MF (W,W, Opt_SGD): the model is a wave-uniform
-// runtime switch; the scatter MODE is compile-time.
+// LINE-2 (W,C; SHARED 0), LINE-1 / MF (W,W; SHARED 1, Opt_SGD for MF at run
+// time) and BPR (W,W; SHARED 2, UpdateBPRPair); the scatter MODE is
+// compile-time.
 template <int G, int M, int KMAX, int MODE, int SHARED>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(waves_of(MODE))))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(waves_of(MODE, SHARED))))
 edge_train_kernel(EdgeArgs a) {
     __shared__ float s_sig[1001];
     extern __shared__ float s_dyn[];   // hybrid: int2 hash[SH_HASH], int ids[n], float pend[n][dpad]
@@ -357,18 +471,16 @@ edge_train_kernel(EdgeArgs a) {
     const int lane = threadIdx.x & (G - 1);
     const uint64_t gpb = blockDim.x / G;                 // groups per block
     uint64_t r0 = (uint64_t)blockIdx.x * gpb;            // block-uniform round base
-    uint64_t ngroups = (uint64_t)gridDim.x * gpb;
     const uint64_t gib = threadIdx.x / G;
     if (a.mode == 2) {               // serial: one group, samples in order
         if (blockIdx.x != 0 || gib != 0) return;
-        ngroups = 1;
     }
-    const bool shared = SHARED == 1;  // LINE-1 / MF: one table (host dispatches on a.model)
+    const bool shared = SHARED >= 1;  // LINE-1 / MF / BPR: one table (host dispatches on a.model)
     const bool mf = SHARED == 1 && a.model == 2;
     bool ev[M];                      // element lane + G*m exists
 #pragma unroll
     for (int m = 0; m < M; ++m) ev[m] = lane + G * m < a.dpad;
-    const uint64_t base = mf ? 0 : 1;   // LINE counts from 1, MF from 0
+    const uint64_t base = (mf || SHARED == 2) ? 0 : 1;   // LINE counts from 1, MF and BPR from 0
     float* const Tc = a.C;
 
     // adds pending super-hot deltas to HBM (one row per wave-instruction).
@@ -394,8 +506,17 @@ edge_train_kernel(EdgeArgs a) {
         drain();
     };
 
-    const uint64_t step = a.mode == 2 ? 1 : ngroups;
     uint32_t round = 0;
+    // the update rule on gathered rows
+    auto update_rows = [&](int32_t v, const int32_t (&id)[KMAX + 1], bool hotw, const bool (&hot)[KMAX + 1],
+                           float alpha, float (&wv)[M], float (&rows)[KMAX + 1][M]) {
+        if constexpr (SHARED == 2) {
+            if constexpr (KMAX == 5) bpr_update_rows<G, M, KMAX, MODE>(a, s_sig, lane, ev, v, id, hotw, hot, alpha, wv, rows);
+        } else {
+            sgd_update_rows<G, M, KMAX, MODE, SHARED>(a, s_sig, lane, ev, v, id, hotw, hot, alpha, shared, mf, sh, wv,
+                                                      rows);
+        }
+    };
     // the update of one sample, ids tagged as drawn (c < 0: source without out-edges)
     auto process = [&](uint64_t t, int32_t tv, int32_t c, const int32_t (&negs)[KMAX]) {
         const int32_t v = untag(tv);
@@ -412,8 +533,7 @@ edge_train_kernel(EdgeArgs a) {
         const float alpha = alpha_at(a.begin + t + base, a.alpha0, a.total);
         float wv[M], rows[KMAX + 1][M];
         gather_rows<G, M, KMAX>(a, lane, ev, v, id, shared, wv, rows);
-        sgd_update_rows<G, M, KMAX, MODE, SHARED>(a, s_sig, lane, ev, v, id, scatter_atomic<MODE>(tv), hot, alpha,
-                                                  shared, mf, sh, wv, rows);
+        update_rows(v, id, scatter_atomic<MODE>(tv), hot, alpha, wv, rows);
     };
     auto maybe_flush = [&]() {
         if constexpr (MODE == MODE_HYBRID) {
@@ -491,6 +611,26 @@ edge_train_kernel(EdgeArgs a) {
         };
         for (uint64_t c0 = grab(); c0 < a.count; c0 = grab()) {
             const uint64_t lim = c0 + span < a.count ? c0 + span : a.count;
+            if constexpr (SHARED == 2) {
+                // BPR: no row prefetch (a second set of 7 rows would halve the
+                // resident waves); the next record is still loaded one round ahead
+                uint64_t t = c0 + gib;
+                load_rec(t, lim, rr);
+                for (uint64_t r = c0; r < lim; r += gpb) {
+                    t = r + gib;
+                    decode(t, lim, rr, xa);
+                    load_rec(t + gpb, lim, rr);
+                    if (xa.live) {
+                        gather_rows<G, M, KMAX>(a, lane, ev, xa.v, xa.id, shared, wva, rowsa);
+                        const float alpha = alpha_at(a.begin + t + base, a.alpha0, a.total);
+                        if constexpr (KMAX == 5)
+                            bpr_update_rows<G, M, KMAX, MODE>(a, s_sig, lane, ev, xa.v, xa.id, xa.hotw, xa.hot, alpha,
+                                                              wva, rowsa);
+                    }
+                    maybe_flush();
+                }
+                continue;
+            }
             uint64_t t = c0 + gib;
             load_rec(t, lim, rr);
             decode(t, lim, rr, xa);
@@ -503,8 +643,9 @@ edge_train_kernel(EdgeArgs a) {
                 gather_rows<G, M, KMAX>(a, lane, ev, xb.v, xb.id, shared, wvb, rowsb);
                 if (xa.live) {
                     const float alpha = alpha_at(a.begin + t + base, a.alpha0, a.total);
-                    sgd_update_rows<G, M, KMAX, MODE, SHARED>(a, s_sig, lane, ev, xa.v, xa.id, xa.hotw, xa.hot,
-                                                             alpha, shared, mf, sh, wva, rowsa);
+                    if constexpr (SHARED != 2)
+                        sgd_update_rows<G, M, KMAX, MODE, SHARED>(a, s_sig, lane, ev, xa.v, xa.id, xa.hotw, xa.hot,
+                                                                 alpha, shared, mf, sh, wva, rowsa);
                 }
                 xa = xb;
 #pragma unroll
@@ -578,141 +719,6 @@ __global__ void __launch_bounds__(256) walk_pairs_kernel(EdgeArgs a, WalkArgs w)
                 slot += 2 * a.K;
                 sgd_update<G, M, KMAX, MODE>(a, s_sig, lane, ev, untag(tvi), id, scatter_atomic<MODE>(tvi), hot,
                                              alpha, false, false, ShState{nullptr, nullptr, 0});
-            }
-        }
-    }
-}
-
-// ------------------------------------------------------------------ BPR kernel
-// UpdateBPRPair (src/proNet.cpp:1406-1455), one shared table, 5 rounds.
-// Slots: 0 = u, 1 = i, 2+n = j_n.
-template <int G, int M, int MODE>
-__global__ void __launch_bounds__(256) bpr_train_kernel(EdgeArgs a) {
-    __shared__ float s_sig[1001];
-    for (int i = threadIdx.x; i < 1001; i += blockDim.x) s_sig[i] = a.sig[i];
-    __syncthreads();
-
-    constexpr int NS = 7;
-    const int lane = threadIdx.x & (G - 1);
-    uint64_t group = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
-    uint64_t ngroups = ((uint64_t)gridDim.x * blockDim.x) / G;
-    if (a.mode == 2) {
-        if (group != 0) return;
-        ngroups = 1;
-    }
-    const int dpad = a.dpad;
-    bool ev[M];
-#pragma unroll
-    for (int m = 0; m < M; ++m) ev[m] = lane + G * m < dpad;
-    float* const T = a.W;
-
-    for (uint64_t t = group; t < a.count; t += ngroups) {
-        const uint64_t s = a.begin + t;
-        SampleWords<G, 14> wd;
-        wd.draw(a.seed, 0, s, lane);
-        int32_t id[NS];
-        bool hot[NS];
-        id[0] = source_sample(a.g, wd.w[0], wd.w[1]);
-        id[1] = target_sample(a.g, untag(id[0]), wd.w[2], wd.w[3]);
-        if (id[1] < 0) {
-            if (lane == 0) atomicAdd(a.skipped, 1ull);
-            continue;
-        }
-#pragma unroll
-        for (int n = 0; n < 5; ++n) id[2 + n] = negative_sample(a.g, wd.w[4 + 2 * n], wd.w[5 + 2 * n]);
-#pragma unroll
-        for (int k = 0; k < NS; ++k) {
-            hot[k] = scatter_atomic<MODE>(id[k]);
-            id[k] = untag(id[k]);
-        }
-
-        float row[NS][M];
-#pragma unroll
-        for (int k = 0; k < NS; ++k) {
-            const float* p = T + (int64_t)id[k] * dpad + lane;
-#pragma unroll
-            for (int m = 0; m < M; ++m) row[k][m] = ev[m] ? p[m * G] : 0.0f;
-        }
-#pragma unroll
-        for (int k = 1; k < NS; ++k)
-#pragma unroll
-            for (int k2 = 0; k2 < k; ++k2)
-                if (id[k2] == id[k]) {
-#pragma unroll
-                    for (int m = 0; m < M; ++m) row[k][m] = row[k2][m];
-                }
-        constexpr bool DELTA = MODE == MODE_ATOMIC || MODE == MODE_HYBRID;
-        float orig[DELTA ? NS : 1][M];
-        if constexpr (DELTA) {
-#pragma unroll
-            for (int k = 0; k < NS; ++k)
-#pragma unroll
-                for (int m = 0; m < M; ++m) orig[k][m] = row[k][m];
-        }
-        const float alpha = alpha_at(s, a.alpha0, a.total);
-        const float r1 = alpha * 0.0025f, r2 = alpha * 0.025f;
-        float ve[M];
-#pragma unroll
-        for (int m = 0; m < M; ++m) ve[m] = 0.0f;
-
-#define SMORE_PROPAGATE(K_)                                                              \
-    _Pragma("unroll") for (int k2 = 0; k2 < NS; ++k2) if (k2 != (K_) && id[k2] == id[(K_)]) { \
-        _Pragma("unroll") for (int m = 0; m < M; ++m) row[k2][m] = row[(K_)][m];                \
-    }
-
-#pragma unroll
-        for (int n = 0; n < 5; ++n) {
-            const int J = 2 + n;
-            float x[M], ce[M];
-            float p = 0.0f;
-#pragma unroll
-            for (int m = 0; m < M; ++m) {
-                x[m] = row[1][m] - row[J][m];
-                p = __builtin_fmaf(row[0][m], x[m], p);
-            }
-            const float f = group_sum<G>(p);
-            const float gg = fast_sigmoid(-f, s_sig) * alpha;
-#pragma unroll
-            for (int m = 0; m < M; ++m) {
-                ve[m] = __builtin_fmaf(gg, x[m], ve[m]);
-                ce[m] = gg * row[0][m];
-            }
-#pragma unroll
-            for (int m = 0; m < M; ++m) row[1][m] = __builtin_fmaf(-r1, row[1][m], row[1][m]);
-            SMORE_PROPAGATE(1)
-#pragma unroll
-            for (int m = 0; m < M; ++m) row[J][m] = __builtin_fmaf(-r1, row[J][m], row[J][m]);
-            SMORE_PROPAGATE(J)
-#pragma unroll
-            for (int m = 0; m < M; ++m) row[1][m] = row[1][m] + ce[m];
-            SMORE_PROPAGATE(1)
-#pragma unroll
-            for (int m = 0; m < M; ++m) row[J][m] = row[J][m] - ce[m];
-            SMORE_PROPAGATE(J)
-        }
-#pragma unroll
-        for (int m = 0; m < M; ++m) row[0][m] = __builtin_fmaf(-r2, row[0][m], row[0][m]) + ve[m];
-        SMORE_PROPAGATE(0)
-#undef SMORE_PROPAGATE
-
-#pragma unroll
-        for (int k = 0; k < NS; ++k) {
-            bool last = true;
-#pragma unroll
-            for (int k2 = k + 1; k2 < NS; ++k2) last = last && (id[k2] != id[k]);
-            if (last) {
-                float* q = T + (int64_t)id[k] * dpad + lane;
-                const bool atom = hot[k];
-#pragma unroll
-                for (int m = 0; m < M; ++m) {
-                    if (!ev[m]) continue;
-                    if constexpr (DELTA) {
-                        if (atom) unsafeAtomicAdd(q + m * G, row[k][m] - orig[k][m]);
-                        else q[m * G] = row[k][m];
-                    } else {
-                        q[m * G] = row[k][m];
-                    }
-                }
             }
         }
     }

@@ -82,8 +82,6 @@ SMORE_DECL_EDGE(s5) SMORE_DECL_EDGE(s10) SMORE_DECL_EDGE(s20)
 SMORE_DECL_EDGE(a5) SMORE_DECL_EDGE(a10) SMORE_DECL_EDGE(a20)
 SMORE_DECL_EDGE(h5) SMORE_DECL_EDGE(h10) SMORE_DECL_EDGE(h20)
 #undef SMORE_DECL_EDGE
-hipError_t launch_bpr(const EdgeArgs& a, int grid, hipStream_t st);
-const void* bpr_symbol(const EdgeArgs& a);
 hipError_t launch_edge_train(const EdgeArgs& a, int grid, hipStream_t st);
 const void* edge_kernel_symbol(const EdgeArgs& a);
 hipError_t launch_sample(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K,

@@ -1,6 +1,6 @@
 // train_kernels.hip -- sampler / init kernels and the launch dispatch of the
-// fused sampled-SGD kernels (edge_kernels.h; instantiated in train_store.hip,
-// train_atomic.hip, train_bpr.hip).
+// sampled-SGD update kernels (edge_kernels.h; instantiated in
+// train_edge_<mode>_k<KMAX>.hip).
 
 #include "train_kernels.h"
 
@@ -69,12 +69,10 @@ int lanes_of(int dpad) {
     }
 
 hipError_t launch_edge_train(const EdgeArgs& a, int grid, hipStream_t st) {
-    if (a.model == 3) return launch_bpr(a, grid, st);
     SMORE_EDGE_DISPATCH(launch_edge_, a, grid, st)
 }
 
 const void* edge_kernel_symbol(const EdgeArgs& a) {
-    if (a.model == 3) return bpr_symbol(a);
     SMORE_EDGE_DISPATCH(edge_symbol_, a)
 }
 #undef SMORE_EDGE_DISPATCH
