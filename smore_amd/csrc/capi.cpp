@@ -67,6 +67,12 @@ struct smore_ctx {
     int sh_max = 128, sh_flush = 32;
     // pre-drawn edge-sample records (train_draw.hip) and per-phase timing
     int32_t* d_rec = nullptr;
+    // DeepWalk pair records: per-walk pair counts, their exclusive scan, scan scratch
+    uint32_t* d_pcount = nullptr;
+    uint64_t* d_poff = nullptr;
+    size_t pair_walks = 0;
+    void* d_scan_tmp = nullptr;
+    size_t scan_tmp_bytes = 0;
     // packed draw tables (train_draw.hip), rebuilt when the graph tables change
     uint4* d_vt32 = nullptr;
     uint4* d_ct16 = nullptr;
@@ -201,6 +207,8 @@ void smore_destroy(smore_ctx* c) {
 
     dfree(c->d_order); dfree(c->d_walks); dfree(c->d_lens); dfree(c->d_tcum); dfree(c->d_sh_hash); dfree(c->d_sh_ids);
     dfree(c->d_rec); dfree(c->d_vt32); dfree(c->d_ct16);
+    dfree(c->d_pcount); dfree(c->d_poff);
+    if (c->d_scan_tmp) (void)hipFree(c->d_scan_tmp);
     for (hipEvent_t e : c->phase_ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -851,7 +859,10 @@ int smore_train_deepwalk(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, i
         c->walk_order_n = total;
         c->walk_order_host = order;
     }
-    const uint64_t chunk = std::min<uint64_t>(walk_end - walk_begin, (uint64_t)1 << 20);
+    // C++ semantics: walks -> pair records -> update kernel, 2^18 walks per chunk
+    // (~61M pairs at walk_steps 40, window 5); Go semantics: fused walk kernel
+    const bool cpp = c->semantics != SMORE_SEM_GO;
+    const uint64_t chunk = std::min<uint64_t>(walk_end - walk_begin, (uint64_t)1 << (cpp ? 18 : 20));
     const size_t need = chunk * (size_t)(walk_steps + 1);
     if (c->walk_buf_n < need) {
         dfree(c->d_walks);
@@ -878,9 +889,32 @@ int smore_train_deepwalk(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, i
             per_cu = 1;
         grid = c->cus * per_cu;
     }
-    if (mode == SMORE_HYBRID) {
-        const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
-        if ((rc = build_hot_maps(c, SMORE_LINE2, K, M))) return rc;
+    EdgeArgs ar = a;   // the update kernel over pair records (C++ semantics)
+    int ugrid = 1;
+    if (cpp) {
+        if (c->pair_walks < chunk) {
+            dfree(c->d_pcount);
+            dfree(c->d_poff);
+            c->pair_walks = 0;
+            HIPCHK(c, hipMalloc((void**)&c->d_pcount, chunk * sizeof(uint32_t)));
+            HIPCHK(c, hipMalloc((void**)&c->d_poff, chunk * sizeof(uint64_t)));
+            c->pair_walks = chunk;
+        }
+        const bool combine = mode == SMORE_HYBRID;
+        ar.sh_rows = combine ? std::min(c->sh_max, 8192 / std::max(1, c->dpad)) : 0;
+        ar.alpha_rec = 1;
+        ar.work = c->d_work;
+        ar.count = (uint64_t)1 << 40;   // grid for a full chunk of pairs (a launch never needs more)
+        ugrid = edge_grid(c, ar);
+        if (mode == SMORE_HYBRID) {
+            const int64_t M = (int64_t)ugrid * (256 / lanes_of(c->dpad));
+            if ((rc = build_hot_maps(c, SMORE_LINE2, K, M))) return rc;
+        }
+        ar.g = dev_graph(c);
+        ar.sh_rows = combine ? c->sh_rows : 0;
+        ar.sh_hash = c->d_sh_hash;
+        ar.sh_ids = c->d_sh_ids;
+        ar.sh_flush = std::max(1, c->sh_flush);
     }
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     for (uint64_t b = walk_begin; b < walk_end; b += chunk) {
@@ -900,8 +934,33 @@ int smore_train_deepwalk(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, i
         if (c->semantics == SMORE_SEM_GO) {
             HIPCHK(c, launch_go_walk(a, w, g2, c->stream));
         } else {
-            HIPCHK(c, launch_walk_gen(a.g, w, seed, c->stream));
-            HIPCHK(c, launch_walk_pairs(a, w, g2, c->stream));
+            HIPCHK(c, launch_walk_gen(ar.g, w, seed, c->stream));
+            HIPCHK(c, launch_pair_count(w, seed, c->d_pcount, c->stream));
+            HIPCHK(c, scan_pair_counts(c->d_pcount, c->d_poff, w.nwalks, &c->d_scan_tmp, &c->scan_tmp_bytes,
+                                       c->stream));
+            uint64_t last_off = 0;
+            uint32_t last_cnt = 0;
+            HIPCHK(c, hipMemcpyAsync(&last_off, c->d_poff + (w.nwalks - 1), sizeof last_off, hipMemcpyDeviceToHost,
+                                     c->stream));
+            HIPCHK(c, hipMemcpyAsync(&last_cnt, c->d_pcount + (w.nwalks - 1), sizeof last_cnt,
+                                     hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            const uint64_t npairs = last_off + last_cnt;
+            if (npairs == 0) continue;
+            const int RW = rec_width(kmax_of(K));
+            if (c->rec_cap < npairs * RW) {
+                dfree(c->d_rec);
+                c->rec_cap = 0;
+                HIPCHK(c, hipMalloc(&c->d_rec, npairs * RW * sizeof(int32_t)));
+                c->rec_cap = npairs * RW;
+            }
+            HIPCHK(c, launch_pair_emit(ar.g, w, seed, K, alpha0, c->d_poff, c->d_rec, c->stream));
+            EdgeArgs ak = ar;
+            ak.begin = 0;
+            ak.count = npairs;
+            ak.rec = c->d_rec;
+            HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
+            HIPCHK(c, launch_edge_train(ak, mode == SMORE_SERIAL ? 1 : ugrid, c->stream));
         }
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));

@@ -518,7 +518,7 @@ edge_train_kernel(EdgeArgs a) {
         }
     };
     // the update of one sample, ids tagged as drawn (c < 0: source without out-edges)
-    auto process = [&](uint64_t t, int32_t tv, int32_t c, const int32_t (&negs)[KMAX]) {
+    auto process = [&](float alpha, int32_t tv, int32_t c, const int32_t (&negs)[KMAX]) {
         const int32_t v = untag(tv);
         int32_t id[KMAX + 1];
         bool hot[KMAX + 1];
@@ -530,7 +530,6 @@ edge_train_kernel(EdgeArgs a) {
             hot[k] = scatter_atomic<MODE>(id[k]);
             id[k] = id[k] < 0 ? -1 : untag(id[k]);
         }
-        const float alpha = alpha_at(a.begin + t + base, a.alpha0, a.total);
         float wv[M], rows[KMAX + 1][M];
         gather_rows<G, M, KMAX>(a, lane, ev, v, id, shared, wv, rows);
         update_rows(v, id, scatter_atomic<MODE>(tv), hot, alpha, wv, rows);
@@ -544,6 +543,12 @@ edge_train_kernel(EdgeArgs a) {
         }
     };
 
+    // learning rate of record t: from the global sample index (LINE / MF / BPR),
+    // or carried in the record's word 2 + KMAX (DeepWalk pairs, per walk)
+    auto rec_alpha = [&](uint64_t t, const i32x4* r) -> float {
+        if (a.alpha_rec) return __int_as_float(r[(2 + KMAX) / 4][(2 + KMAX) % 4]);
+        return alpha_at(a.begin + t + base, a.alpha0, a.total);
+    };
     if (a.mode == 2) {
         // serial: records in order, gather after the previous sample's scatter
         constexpr int RW = rec_width(KMAX);
@@ -556,7 +561,7 @@ edge_train_kernel(EdgeArgs a) {
                 int32_t negs[KMAX];
 #pragma unroll
                 for (int j = 0; j < KMAX; ++j) negs[j] = r[(j + 2) / 4][(j + 2) % 4];
-                process(r0, r[0][0], r[0][1], negs);
+                process(rec_alpha(r0, r), r[0][0], r[0][1], negs);
             }
         }
     } else {
@@ -571,9 +576,11 @@ edge_train_kernel(EdgeArgs a) {
         struct Ids {
             int32_t v, id[KMAX + 1];
             bool hotw, hot[KMAX + 1], live;
+            float alpha;
         };
         auto decode = [&](uint64_t t, uint64_t lim, const i32x4 (&r)[RW / 4], Ids& x) {
             x.live = t < lim && r[0][1] >= 0;   // c < 0: counted by the draw kernel
+            x.alpha = rec_alpha(t, r);
             x.hotw = scatter_atomic<MODE>(r[0][0]);
             x.v = x.live ? untag(r[0][0]) : -1;
 #pragma unroll
@@ -622,10 +629,9 @@ edge_train_kernel(EdgeArgs a) {
                     load_rec(t + gpb, lim, rr);
                     if (xa.live) {
                         gather_rows<G, M, KMAX>(a, lane, ev, xa.v, xa.id, shared, wva, rowsa);
-                        const float alpha = alpha_at(a.begin + t + base, a.alpha0, a.total);
                         if constexpr (KMAX == 5)
-                            bpr_update_rows<G, M, KMAX, MODE>(a, s_sig, lane, ev, xa.v, xa.id, xa.hotw, xa.hot, alpha,
-                                                              wva, rowsa);
+                            bpr_update_rows<G, M, KMAX, MODE>(a, s_sig, lane, ev, xa.v, xa.id, xa.hotw, xa.hot,
+                                                              xa.alpha, wva, rowsa);
                     }
                     maybe_flush();
                 }
@@ -642,10 +648,9 @@ edge_train_kernel(EdgeArgs a) {
                 load_rec(t + 2 * gpb, lim, rr);
                 gather_rows<G, M, KMAX>(a, lane, ev, xb.v, xb.id, shared, wvb, rowsb);
                 if (xa.live) {
-                    const float alpha = alpha_at(a.begin + t + base, a.alpha0, a.total);
                     if constexpr (SHARED != 2)
                         sgd_update_rows<G, M, KMAX, MODE, SHARED>(a, s_sig, lane, ev, xa.v, xa.id, xa.hotw, xa.hot,
-                                                                 alpha, shared, mf, sh, wva, rowsa);
+                                                                 xa.alpha, shared, mf, sh, wva, rowsa);
                 }
                 xa = xb;
 #pragma unroll

@@ -23,6 +23,7 @@ struct EdgeArgs {
     // (draw_kernel), rec_width(KMAX) int32 each
     const int32_t* rec;
     unsigned long long* work;      // Hogwild edge kernels: chunk counter, zeroed per launch
+    int alpha_rec;                 // 1: learning rate in record word 2 + KMAX (DeepWalk pairs)
     uint64_t begin, count, total, seed;
     double alpha0;
     float reg;
@@ -58,6 +59,11 @@ hipError_t launch_delta_end(float* T, float* S, const float* D, const float* R, 
                             hipStream_t st);
 hipError_t launch_delta_cycle(float* T, float* S, float* D, float* R, float scale, uint64_t n, int cus,
                               hipStream_t st);
+hipError_t launch_pair_count(const WalkArgs& w, uint64_t seed, uint32_t* count, hipStream_t st);
+hipError_t scan_pair_counts(const uint32_t* count, uint64_t* off, uint64_t n, void** temp, size_t* temp_bytes,
+                            hipStream_t st);
+hipError_t launch_pair_emit(const DevGraph& g, const WalkArgs& w, uint64_t seed, int K, double alpha0,
+                            const uint64_t* off, int32_t* rec, hipStream_t st);
 hipError_t launch_pack(const DevGraph& g, uint64_t E, uint4* vt32, uint4* ct16, hipStream_t st);
 hipError_t launch_draw(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K, int32_t* rec,
                        unsigned long long* skipped, hipStream_t st);
