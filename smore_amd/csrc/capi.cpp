@@ -881,14 +881,7 @@ int smore_train_deepwalk(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, i
     a.dpad = c->dpad; a.K = K; a.model = SMORE_LINE2; a.mode = mode;
     a.tcum = c->d_tcum;
     if (c->semantics == SMORE_SEM_GO && mode == SMORE_HYBRID) return fail(c, SMORE_EINVAL, "Go semantics: no hybrid");
-    int grid = 1;
-    if (mode != SMORE_SERIAL) {
-        int per_cu = 0;
-        const void* sym = walk_pairs_symbol(a);
-        if (!sym || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sym, 256, 0) != hipSuccess || per_cu < 1)
-            per_cu = 1;
-        grid = c->cus * per_cu;
-    }
+    const int grid = mode != SMORE_SERIAL ? c->cus * 4 : 1;   // Go walk kernel (as the Go edge path)
     EdgeArgs ar = a;   // the update kernel over pair records (C++ semantics)
     int ugrid = 1;
     if (cpp) {

@@ -668,67 +668,6 @@ edge_train_kernel(EdgeArgs a) {
     }
 }
 
-// ------------------------------------------------------------------ DeepWalk pairs
-// DeepWalk::Train's per-walk body after RandomWalk (src/model/DeepWalk.cpp:
-// 133-139): SkipGrams with the random window shrink (src/proNet.cpp:769-809)
-// and UpdatePairs -> UpdatePair per pair (src/proNet.cpp:2741-2753), one
-// group per walk, pairs in the reference's order.  Draw slots of walk w
-// (stream 1): after the 2(L-1) walk draws, L window draws, then 2K per pair.
-template <int G, int M, int KMAX, int MODE>
-__global__ void __launch_bounds__(256) walk_pairs_kernel(EdgeArgs a, WalkArgs w) {
-    __shared__ float s_sig[1001];
-    for (int i = threadIdx.x; i < 1001; i += blockDim.x) s_sig[i] = a.sig[i];
-    __syncthreads();
-
-    const int lane = threadIdx.x & (G - 1);
-    uint64_t group = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
-    uint64_t ngroups = ((uint64_t)gridDim.x * blockDim.x) / G;
-    if (a.mode == 2) {
-        if (group != 0) return;
-        ngroups = 1;
-    }
-    bool ev[M];
-#pragma unroll
-    for (int m = 0; m < M; ++m) ev[m] = lane + G * m < a.dpad;
-    const int stride = w.steps + 1;
-
-    for (uint64_t t = group; t < w.nwalks; t += ngroups) {
-        const uint64_t unit = w.walk_begin + t;
-        const int32_t* walk = w.walks + t * stride;
-        const int L = w.lens[t];
-        const float alpha = alpha_walk(unit, a.alpha0, w.total_walks);
-        const uint32_t win_base = 2u * (uint32_t)(L - 1);
-        uint32_t slot = win_base + (uint32_t)L;          // first negative slot
-        for (int i = 0; i < L; ++i) {
-            const uint32_t sw = win_base + (uint32_t)i;
-            const uint32_t kw = comp(philox_block(a.seed, 1, unit, sw >> 2), (int)(sw & 3));
-            const int reduce = (int)draw_index(kw, (uint32_t)w.window) + 1;
-            const int left = i - reduce < 0 ? 0 : i - reduce;
-            const int right = i + reduce >= L ? L - 1 : i + reduce;
-            const int32_t tvi = walk[i];
-            for (int j = left; j <= right; ++j) {
-                if (j == i) continue;
-                int32_t id[KMAX + 1];
-                bool hot[KMAX + 1];
-                id[0] = walk[j];
-                SlotWords<G, 2 * KMAX> nw;
-                nw.draw(a.seed, 1, unit, slot, lane);
-#pragma unroll
-                for (int n = 0; n < KMAX; ++n)
-                    id[n + 1] = n < a.K ? negative_sample(a.g, nw.w[2 * n], nw.w[2 * n + 1]) : -1;
-#pragma unroll
-                for (int k = 0; k <= KMAX; ++k) {
-                    hot[k] = scatter_atomic<MODE>(id[k]);
-                    id[k] = id[k] < 0 ? -1 : untag(id[k]);
-                }
-                slot += 2 * a.K;
-                sgd_update<G, M, KMAX, MODE>(a, s_sig, lane, ev, untag(tvi), id, scatter_atomic<MODE>(tvi), hot,
-                                             alpha, false, false, ShState{nullptr, nullptr, 0});
-            }
-        }
-    }
-}
-
 // ---------------------------------------------------------------- dispatch
 // (G, M) pairs for dpad in [4, 512]: G = min(64, pow2ceil(dpad / SMORE_EPL)),
 // M = ceil(dpad / G) (train_kernels.hip lanes_of; oracle orc_lane_width).

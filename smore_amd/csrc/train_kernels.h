@@ -78,8 +78,6 @@ hipError_t launch_go_walk(const EdgeArgs& a, const WalkArgs& w, int grid, hipStr
 hipError_t launch_go_sample(const DevGraph& g, const double* tcum, uint64_t seed, uint64_t begin, uint64_t count,
                             int K, int32_t* out, hipStream_t st);
 hipError_t launch_walk_gen(const DevGraph& g, const WalkArgs& w, uint64_t seed, hipStream_t st);
-hipError_t launch_walk_pairs(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st);
-const void* walk_pairs_symbol(const EdgeArgs& a);
 // edge kernel instantiations, one per (scatter mode s/a/h, KMAX) (train_edge_*.hip)
 #define SMORE_DECL_EDGE(name)                                                   \
     hipError_t launch_edge_##name(const EdgeArgs& a, int grid, hipStream_t st); \

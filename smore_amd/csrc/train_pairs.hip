@@ -7,7 +7,7 @@
 // and UpdatePairs -> UpdatePair per pair (src/proNet.cpp:2741-2753).  Per walk
 // (one thread): the window draws (slots 2(L-1) + i, stream 1), then for each
 // pair in the reference's order its K negatives (2K consecutive slots from
-// 2(L-1) + L: index, then p) -- the draws of walk_pairs_kernel.  Two passes:
+// 2(L-1) + L: index, then p), as the oracle restates them.  Two passes:
 // count the pairs of each walk, exclusive-scan the counts, emit the records
 //     {walk[i], walk[j], n_1 .. n_K, .., alpha bits at word 2 + KMAX}
 // walk-major in pair order, so a serial update over them is the reference's

@@ -1,6 +1,7 @@
-// train_walk.hip -- DeepWalk on the GPU: walk generation (RandomWalk,
-// src/proNet.cpp:704-724) and the skip-gram pair updates (walk_pairs_kernel).
-#include "edge_kernels.h"
+// train_walk.hip -- DeepWalk walk generation on the GPU (RandomWalk,
+// src/proNet.cpp:704-724); the skip-gram pairs become sample records
+// (train_pairs.hip) for the update kernel.
+#include "train_kernels.h"
 
 namespace smore {
 
@@ -38,48 +39,6 @@ hipError_t launch_walk_gen(const DevGraph& g, const WalkArgs& w, uint64_t seed, 
     hipLaunchKernelGGL(walk_gen_kernel, dim3((unsigned)((w.nwalks + block - 1) / block)), dim3(block), 0, st, g,
                        w, seed);
     return hipGetLastError();
-}
-
-template <int G, int M, int KMAX>
-static hipError_t go(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st) {
-    if (a.mode == 1)
-        hipLaunchKernelGGL((walk_pairs_kernel<G, M, KMAX, MODE_ATOMIC>), dim3(grid), dim3(256), 0, st, a, w);
-    else if (a.mode == 3)
-        hipLaunchKernelGGL((walk_pairs_kernel<G, M, KMAX, MODE_HYBRID>), dim3(grid), dim3(256), 0, st, a, w);
-    else
-        hipLaunchKernelGGL((walk_pairs_kernel<G, M, KMAX, MODE_STORE>), dim3(grid), dim3(256), 0, st, a, w);
-    return hipGetLastError();
-}
-
-template <int G, int M, int KMAX>
-static const void* sym(const EdgeArgs& a) {
-    if (a.mode == 1) return (const void*)walk_pairs_kernel<G, M, KMAX, MODE_ATOMIC>;
-    if (a.mode == 3) return (const void*)walk_pairs_kernel<G, M, KMAX, MODE_HYBRID>;
-    return (const void*)walk_pairs_kernel<G, M, KMAX, MODE_STORE>;
-}
-
-hipError_t launch_walk_pairs(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st) {
-    const int G = lanes_of(a.dpad), M = (a.dpad + G - 1) / G;
-#define X(g, m)                                          \
-    if (G == g && M == m) {                              \
-        if (a.K <= 5) return go<g, m, 5>(a, w, grid, st); \
-        return go<g, m, 10>(a, w, grid, st);              \
-    }
-    SMORE_FOR_EACH_GM(X)
-#undef X
-    return hipErrorInvalidValue;
-}
-
-const void* walk_pairs_symbol(const EdgeArgs& a) {
-    const int G = lanes_of(a.dpad), M = (a.dpad + G - 1) / G;
-#define X(g, m)                                   \
-    if (G == g && M == m) {                       \
-        if (a.K <= 5) return sym<g, m, 5>(a);     \
-        return sym<g, m, 10>(a);                  \
-    }
-    SMORE_FOR_EACH_GM(X)
-#undef X
-    return nullptr;
 }
 
 }  // namespace smore
