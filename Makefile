@@ -13,34 +13,29 @@ SRC      := smore_amd/csrc
 OBJ      ?= build/obj
 LIB      ?= smore_amd/lib/libsmore_hip.so
 BIN      := smore_amd/bin
-HDRS     := $(wildcard $(SRC)/*.h) include/smore_hip.h
+# kernels depend on the device headers only; host objects on the host headers
+DEV_HDRS := $(SRC)/device_common.h $(SRC)/train_kernels.h $(SRC)/edge_kernels.h $(SRC)/edge_inst.h
+HOST_HDRS := $(SRC)/host_graph.h $(SRC)/ctx.h $(SRC)/train_kernels.h $(SRC)/device_common.h include/smore_hip.h
 
-.PHONY: all lib cli oracle ref clean
-all: lib cli
+.PHONY: all lib cli goshape oracle ref clean
+all: lib cli goshape
 
 lib: $(LIB)
 
-$(OBJ)/host_graph.o: $(SRC)/host_graph.cpp $(HDRS)
+HOST_SRCS := host_graph capi exchange graphgen
+$(OBJ)/%.o: $(SRC)/%.cpp $(HOST_HDRS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(CXXFLAGS) -c -o $@ $<
 
-$(OBJ)/capi.o: $(SRC)/capi.cpp $(HDRS)
-	@mkdir -p $(OBJ)
-	$(HIPCC) $(CXXFLAGS) -c -o $@ $<
-
-$(OBJ)/graphgen.o: $(SRC)/graphgen.cpp $(HDRS)
-	@mkdir -p $(OBJ)
-	$(HIPCC) $(CXXFLAGS) -c -o $@ $<
-
-$(OBJ)/%.o: $(SRC)/%.hip $(HDRS)
+$(OBJ)/%.o: $(SRC)/%.hip $(DEV_HDRS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-LIB_OBJS := $(OBJ)/host_graph.o $(OBJ)/capi.o $(OBJ)/graphgen.o $(patsubst $(SRC)/%.hip,$(OBJ)/%.o,$(wildcard $(SRC)/*.hip))
+LIB_OBJS := $(patsubst %,$(OBJ)/%.o,$(HOST_SRCS)) $(patsubst $(SRC)/%.hip,$(OBJ)/%.o,$(wildcard $(SRC)/*.hip))
 
 $(LIB): $(LIB_OBJS)
 	@mkdir -p $(dir $@)
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread -ldl
 
 CLIS := $(patsubst $(SRC)/cli/%.cpp,$(BIN)/%,$(wildcard $(SRC)/cli/*.cpp))
 cli: $(CLIS)
@@ -57,3 +52,8 @@ ref:
 
 clean:
 	rm -rf build smore_amd/lib smore_amd/bin
+
+# the Go shim's call sequence as a C program (tests/test_gpu_goshape.py)
+goshape: tests/c/go_shape
+tests/c/go_shape: tests/c/go_shape.c include/smore_hip.h $(LIB)
+	gcc -std=c11 -O2 -Wall -Iinclude -o $@ $< -L$(dir $(LIB)) -lsmore_hip -Wl,-rpath,'$$ORIGIN/../../smore_amd/lib'

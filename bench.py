@@ -50,8 +50,8 @@ def algorithmic_bytes(dim, K):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4")
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--negative", type=int, default=5)
@@ -70,25 +70,56 @@ def parse():
     return ap.parse_args()
 
 
+def host_cores():
+    """(cores this process may run on, cores of the machine)."""
+    try:
+        mine = len(os.sched_getaffinity(0))
+    except AttributeError:
+        mine = os.cpu_count() or 1
+    return mine, os.cpu_count() or mine
+
+
 def cpu_baseline(V, src, dst, w, dim, K, seconds, config):
-    """The oracle's fp32 spec with OpenMP Hogwild threads on this host (the
-    reference sources do not travel to the GPU box), bounded in time."""
+    """The reference's arithmetic and CPU structure -- fp64 rows, OpenMP Hogwild
+    threads over contiguous sample blocks (src/model/LINE.cpp:160-191) -- as
+    restated by the oracle (the reference sources do not travel to the GPU box),
+    on this host's cores, bounded in time."""
     from oracle import oracle as orc
-    threads = min(16, os.cpu_count() or 1)
+    mine, machine = host_cores()
+    threads = max(1, min(16, mine))
     g = orc.Graph(V, src, dst, w)
-    dpad = (dim + 3) // 4 * 4
-    W = ((np.random.default_rng(1).random((V, dpad), dtype=np.float32) - 0.5) / dim).astype(np.float32)
-    W[:, dim:] = 0
+    W = (np.random.default_rng(1).random((V, dim)) - 0.5) / dim
     C = np.zeros_like(W)
     total = 1 << 40
     chunk, done, t0 = 2_000_000, 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        orc.train_edge_f32(g, "line2", W, C, dim, K, 0.025, 0.0, total, done, done + chunk, 7, threads)
+        orc.train_edge_f64(g, "line2", W, C, K, 0.025, 0.0, total, done, done + chunk, 7, threads)
         done += chunk
     el = time.perf_counter() - t0
     return {"value": round(done / el / 1e6, 4), "unit": "M edge-updates/s", "cores": threads, "kind": "port",
-            "sample": "%d LINE-2 samples (d=%d, K=%d) on the same %s graph, %d OpenMP Hogwild threads, %.1f s"
-                      % (done, dim, K, config, threads, el)}
+            "arithmetic": "f64 (the reference's)", "host_cpus_available": mine, "host_cpus_machine": machine,
+            "sample": "%d LINE-2 samples (d=%d, K=%d) on the same %s graph, fp64 rows, %d OpenMP Hogwild threads "
+                      "(%d CPUs available to this process, %d on the machine), %.1f s"
+                      % (done, dim, K, config, threads, mine, machine, el)}
+
+
+def measured_copy_peak(torch, gib=4, reps=5):
+    """Device-to-device copy bandwidth on this GPU (read + write bytes / time)."""
+    n = (gib << 30) // 4
+    x = torch.empty(n, dtype=torch.float32, device="cuda").fill_(1.0)
+    y = torch.empty_like(x)
+    y.copy_(x)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        y.copy_(x)
+    e1.record()
+    torch.cuda.synchronize()
+    gbs = 2 * 4 * n * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
+    del x, y
+    torch.cuda.empty_cache()
+    return gbs
 
 
 def main():
@@ -185,12 +216,14 @@ def main():
     upd_s = upd_ms / 1e3 / args.steps if upd_ms > 0 else step_s       # update-kernel time per step
     launch_s = upd_ms / 1e3 / launches if launches else step_s         # per update launch (rocprof average)
     achieved = R_upd * S / upd_s / 1e9
-    traffic = None
+    traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         p = json.load(open(pmc))
         if p.get("config") == args.config and p.get("samples") == S and p.get("mode") == args.mode:
             traffic = p.get("hbm_bytes_per_launch")   # FETCH_SIZE + WRITE_SIZE per update launch
+            traffic_src = "profiles/pmc_traffic.json: rocprofv3 --pmc of this config (%s)" % p.get("round", "")
+    copy_peak = measured_copy_peak(torch) if rank == 0 else 0.0
     Wt = pn.get_table(0)
     assert np.isfinite(Wt).all(), "non-finite embeddings"
 
@@ -216,18 +249,26 @@ def main():
                        "samples_per_step_per_gpu": S, "scatter": args.mode,
                        "sync": ("%s every %d steps" % (args.sync, args.sync_every)) if world > 1 else "none",
                        "parallelism": "replicas%d" % world},
-            "roofline": {"bound": "hbm", "kernel": "edge_train_kernel (gather/update/scatter)",
-                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "bytes_per_update_read": R_upd, "bytes_per_update_write": Wb,
-                         "achieved_rw": round((R_upd + Wb) * S / upd_s / 1e9, 1),
-                         "kernel_ms_per_launch": round(launch_s * 1e3, 3),
-                         "launches_per_step": round(launches / args.steps, 2),
-                         "update_ms_per_step": round(upd_s * 1e3, 3),
-                         "exposed_draw_ms_per_step": round(draw_ms / args.steps, 3),
-                         "path": {"bytes_per_update_read": R, "achieved": round(R * S / step_s / 1e9, 1),
-                                  "frac": round(R * S / step_s / 1e9 / HBM_PEAK_GBS, 4),
-                                  "ms_per_step": round(step_s * 1e3, 3)}},
+            # achieved = updates/s x 1868 B (the whole path's algorithmic
+            # reads) over the 8 TB/s HBM read roofline; the dominant kernel's own
+            # figure (its per-launch time, as rocprof reports it) is "kernel"
+            "roofline": {"bound": "hbm", "achieved": round(R * S / step_s / 1e9, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(R * S / step_s / 1e9 / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "bytes_per_update_read": R, "bytes_per_update_write": Wb,
+                         "ms_per_step": round(step_s * 1e3, 3),
+                         "measured_peak": {"copy_GBs": round(copy_peak, 1),
+                                           "frac": round(R * S / step_s / 1e9 / copy_peak, 4),
+                                           "note": "device-to-device copy, read+write bytes / time"},
+                         "kernel": {"name": "edge_train_kernel (gather/update/scatter)",
+                                    "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
+                                    "bytes_per_update_read": R_upd, "bytes_per_update_write": Wb,
+                                    "achieved_rw": round((R_upd + Wb) * S / upd_s / 1e9, 1),
+                                    "ms_per_launch": round(launch_s * 1e3, 3),
+                                    "launches_per_step": round(launches / args.steps, 2),
+                                    "update_ms_per_step": round(upd_s * 1e3, 3),
+                                    "exposed_draw_ms_per_step": round(draw_ms / args.steps, 3)}},
             "cpu_baseline": cpu,
             "skipped_samples": int(skipped),
         }

@@ -1,0 +1,310 @@
+//go:build smore_hip
+
+// hip.go -- the MI355X drop-in under the Go models' training loops.
+//
+// Drop this file into pkg/pronet of the Go tree (RainBoltz/smore) and build
+// with `-tags smore_hip`; point cgo at this repository's header and library:
+//
+//	CGO_CFLAGS="-I<repo>/include" \
+//	CGO_LDFLAGS="-L<repo>/smore_amd/lib -Wl,-rpath,<repo>/smore_amd/lib" \
+//	go build -tags smore_hip ./cmd/line ./cmd/bpr ./cmd/deepwalk
+//
+// What stays Go: NewProNet, LoadEdgeList (pkg/pronet/pronet.go:77,112), the
+// models' Init and SaveWeights.  What moves to the GPU: the per-sample loops of
+// (*LINE).Train (internal/models/line/line.go:73-150), (*BPR).Train
+// (internal/models/bpr/bpr.go:61-135) and (*DeepWalk).Train
+// (internal/models/deepwalk/deepwalk.go:61-141), i.e. SourceSample /
+// TargetSample / NegativeSample (pronet.go:252-289) and UpdatePair /
+// UpdateBPRPair (optimizer.go:21-117) -- one C call per training run instead
+// of one Go call per sample.  The library runs them with the GO rules
+// (smore_set_semantics(SMORE_SEM_GO)): source ~ out_degree^1, CDF target scan
+// over the adjacency order of pn.Graph, NegativeAT from pn (so callers that
+// assign their own NegativeAT keep it), duplicate negatives skipped, deferred
+// positive context, BPR on W (users) and C (items) with lambda, fixed-window
+// SkipGrams.  Draws come from the library's seeded Philox stream instead of
+// time-seeded math/rand; tables are fp32 on the GPU.
+//
+// cgo may not hold Go memory that contains Go pointers, so the [][]float64
+// tables are flattened into C-allocated fp32 buffers and copied back.
+package pronet
+
+/*
+#cgo LDFLAGS: -lsmore_hip
+#include <stdlib.h>
+#include "smore_hip.h"
+*/
+import "C"
+
+import (
+	"fmt"
+	"os"
+	"strconv"
+	"unsafe"
+)
+
+// HIP models (include/smore_hip.h)
+const (
+	HIPLine2 = int(C.SMORE_LINE2) // UpdatePair(W, C)       -- LINE 2nd order, DeepWalk pairs
+	HIPLine1 = int(C.SMORE_LINE1) // updateFirstOrder(W)    -- LINE 1st order
+	HIPBPR   = int(C.SMORE_BPR)   // UpdateBPRPair(W, C, λ) -- BPR
+)
+
+// HIP scatter modes: Hogwild plain stores, float atomics (lossless; the default
+// for Go callers), strict serial order (parity runs).
+const (
+	HIPHogwild = int(C.SMORE_HOGWILD)
+	HIPAtomic  = int(C.SMORE_ATOMIC)
+	HIPSerial  = int(C.SMORE_SERIAL)
+)
+
+// HIPConfig selects the GPUs and the scatter mode of a run.
+type HIPConfig struct {
+	Device int    // first GPU
+	GPUs   int    // replicas on Device .. Device+GPUs-1 (tables all-reduced over RCCL)
+	Mode   int    // HIPAtomic unless set
+	Seed   uint64 // Philox seed of the draws
+}
+
+// HIPConfigFromEnv reads SMORE_HIP_DEVICE, SMORE_HIP_GPUS, SMORE_HIP_MODE
+// (hogwild|atomic|serial) and SMORE_HIP_SEED; defaults 0, 1, atomic, seed.
+func HIPConfigFromEnv(seed uint64) HIPConfig {
+	c := HIPConfig{Device: 0, GPUs: 1, Mode: HIPAtomic, Seed: seed}
+	if v, err := strconv.Atoi(os.Getenv("SMORE_HIP_DEVICE")); err == nil {
+		c.Device = v
+	}
+	if v, err := strconv.Atoi(os.Getenv("SMORE_HIP_GPUS")); err == nil && v > 0 {
+		c.GPUs = v
+	}
+	switch os.Getenv("SMORE_HIP_MODE") {
+	case "hogwild":
+		c.Mode = HIPHogwild
+	case "serial":
+		c.Mode = HIPSerial
+	}
+	if v, err := strconv.ParseUint(os.Getenv("SMORE_HIP_SEED"), 10, 64); err == nil {
+		c.Seed = v
+	}
+	return c
+}
+
+// HIP is one library context (or a replica group) holding pn's graph.
+type HIP struct {
+	group  *C.smore_group
+	ctx    *C.smore_ctx // replica 0
+	maxVid int64
+	cfg    HIPConfig
+	dim    int
+	ntab   int
+}
+
+func (h *HIP) err(what string) error {
+	if h.group != nil {
+		return fmt.Errorf("%s: %s", what, C.GoString(C.smore_group_last_error(h.group)))
+	}
+	return fmt.Errorf("%s: %s", what, C.GoString(C.smore_last_error(h.ctx)))
+}
+
+// NewHIP uploads pn's graph to the GPUs of cfg in Go semantics: the directed
+// edge slots of pn.Graph / pn.EdgeWeights in vertex order (the adjacency order
+// TargetSample's CDF scan walks, pronet.go:257-284), then pn.NegativeAT.
+func (pn *ProNet) NewHIP(cfg HIPConfig) (*HIP, error) {
+	if cfg.GPUs < 1 {
+		cfg.GPUs = 1
+	}
+	h := &HIP{maxVid: pn.MaxVid, cfg: cfg}
+	devs := make([]C.int, cfg.GPUs)
+	for i := range devs {
+		devs[i] = C.int(cfg.Device + i)
+	}
+	if rc := C.smore_group_create(&devs[0], C.int(cfg.GPUs), &h.group); rc != C.SMORE_OK {
+		return nil, fmt.Errorf("smore_group_create(%d GPUs from %d): status %d", cfg.GPUs, cfg.Device, int(rc))
+	}
+	h.ctx = C.smore_group_ctx(h.group, 0)
+	E := 0
+	for v := int64(0); v < pn.MaxVid; v++ {
+		E += len(pn.Graph[v])
+	}
+	n := E
+	if n == 0 {
+		n = 1
+	}
+	src := (*[1 << 40]C.int32_t)(C.malloc(C.size_t(4 * n)))[:n:n]
+	dst := (*[1 << 40]C.int32_t)(C.malloc(C.size_t(4 * n)))[:n:n]
+	wgt := (*[1 << 40]C.double)(C.malloc(C.size_t(8 * n)))[:n:n]
+	defer C.free(unsafe.Pointer(&src[0]))
+	defer C.free(unsafe.Pointer(&dst[0]))
+	defer C.free(unsafe.Pointer(&wgt[0]))
+	e := 0
+	for v := int64(0); v < pn.MaxVid; v++ {
+		ws := pn.EdgeWeights[v]
+		for i, t := range pn.Graph[v] {
+			src[e], dst[e], wgt[e] = C.int32_t(v), C.int32_t(t), C.double(ws[i])
+			e++
+		}
+	}
+	if rc := C.smore_group_set_graph_edges(h.group, C.int64_t(pn.MaxVid), C.int64_t(E), &src[0], &dst[0], &wgt[0],
+		C.SMORE_VM_OUT_DEGREES, C.SMORE_NM_DEGREES); rc != C.SMORE_OK {
+		h.Close()
+		return nil, h.err("smore_group_set_graph_edges")
+	}
+	if rc := C.smore_group_set_semantics(h.group, C.SMORE_SEM_GO); rc != C.SMORE_OK {
+		h.Close()
+		return nil, h.err("smore_group_set_semantics")
+	}
+	if int64(len(pn.NegativeAT)) == pn.MaxVid && pn.MaxVid > 0 {
+		prob := (*[1 << 40]C.double)(C.malloc(C.size_t(8 * pn.MaxVid)))[:pn.MaxVid:pn.MaxVid]
+		alias := (*[1 << 40]C.int64_t)(C.malloc(C.size_t(8 * pn.MaxVid)))[:pn.MaxVid:pn.MaxVid]
+		defer C.free(unsafe.Pointer(&prob[0]))
+		defer C.free(unsafe.Pointer(&alias[0]))
+		for i, a := range pn.NegativeAT {
+			prob[i], alias[i] = C.double(a.Prob), C.int64_t(a.Alias)
+		}
+		for r := 0; r < cfg.GPUs; r++ {
+			c := C.smore_group_ctx(h.group, C.int(r))
+			if rc := C.smore_set_alias(c, C.SMORE_AT_NEGATIVE, &prob[0], &alias[0], C.int64_t(pn.MaxVid)); rc != C.SMORE_OK {
+				err := fmt.Errorf("smore_set_alias: %s", C.GoString(C.smore_last_error(c)))
+				h.Close()
+				return nil, err
+			}
+		}
+	}
+	return h, nil
+}
+
+// Close releases the GPUs.
+func (h *HIP) Close() {
+	if h.group != nil {
+		C.smore_group_destroy(h.group)
+	}
+	h.group, h.ctx = nil, nil
+}
+
+func (h *HIP) alloc(dim, ntab int) error {
+	if h.dim == dim && h.ntab == ntab {
+		return nil
+	}
+	if rc := C.smore_group_alloc_tables(h.group, C.int(dim), C.int(ntab)); rc != C.SMORE_OK {
+		return h.err("smore_group_alloc_tables")
+	}
+	h.dim, h.ntab = dim, ntab
+	return nil
+}
+
+// put copies Go tables into replica 0 (fp64 -> fp32), get copies them back.
+func (h *HIP) transfer(tables [][][]float64, toGPU bool) error {
+	n := int(h.maxVid) * h.dim
+	if n == 0 {
+		return nil
+	}
+	buf := (*[1 << 40]C.float)(C.malloc(C.size_t(4 * n)))[:n:n]
+	defer C.free(unsafe.Pointer(&buf[0]))
+	for which, t := range tables {
+		if t == nil {
+			continue
+		}
+		if toGPU {
+			for v := 0; v < int(h.maxVid); v++ {
+				row := t[v]
+				for d := 0; d < h.dim; d++ {
+					buf[v*h.dim+d] = C.float(row[d])
+				}
+			}
+			if rc := C.smore_set_table(h.ctx, C.int(which), &buf[0], C.int64_t(h.maxVid), C.int(h.dim)); rc != C.SMORE_OK {
+				return h.err("smore_set_table")
+			}
+		} else {
+			if rc := C.smore_get_table(h.ctx, C.int(which), &buf[0], C.int64_t(h.maxVid), C.int(h.dim)); rc != C.SMORE_OK {
+				return h.err("smore_get_table")
+			}
+			for v := 0; v < int(h.maxVid); v++ {
+				row := t[v]
+				for d := 0; d < h.dim; d++ {
+					row[d] = float64(buf[v*h.dim+d])
+				}
+			}
+		}
+	}
+	if toGPU {
+		if rc := C.smore_group_broadcast_tables(h.group); rc != C.SMORE_OK {
+			return h.err("smore_group_broadcast_tables")
+		}
+	}
+	return nil
+}
+
+// hipChunk: samples per replica per library call (progress granularity)
+const hipChunk = uint64(1) << 27
+
+// TrainEdges runs samples [0, total) of an edge model (HIPLine2 on w, c;
+// HIPLine1 on w; HIPBPR on w = users, c = items with lambda; K negatives, 1 for
+// BPR) with the Go learning-rate schedule over `total`, and copies the trained
+// tables back.  progress(done) is called between library calls.
+func (h *HIP) TrainEdges(model int, w, c [][]float64, dim int, total uint64, K int, alpha, lambda float64,
+	progress func(done uint64)) error {
+	ntab := 2
+	if model == HIPLine1 {
+		ntab, c = 1, nil
+	}
+	if err := h.alloc(dim, ntab); err != nil {
+		return err
+	}
+	if err := h.transfer([][][]float64{w, c}, true); err != nil {
+		return err
+	}
+	step := hipChunk * uint64(h.cfg.GPUs)
+	for done := uint64(0); done < total; {
+		n := total - done
+		if n > step {
+			n = step
+		}
+		if rc := C.smore_group_train_edges(h.group, C.int(model), C.uint64_t(done), C.uint64_t(n), C.uint64_t(total),
+			C.int(K), C.double(alpha), C.double(lambda), C.uint64_t(h.cfg.Seed), C.int(h.cfg.Mode), 0, 0); rc != C.SMORE_OK {
+			return h.err("smore_group_train_edges")
+		}
+		done += n
+		if progress != nil {
+			progress(done)
+		}
+	}
+	return h.transfer([][][]float64{w, c}, false)
+}
+
+// TrainDeepWalk runs walks [0, len(order)) of the Go DeepWalk (walk from
+// order[i], dead-end stop, fixed-window SkipGrams, UpdatePair per pair) and
+// copies W and C back.  order holds walkTimes x MaxVid start vertices, built
+// by the caller exactly as (*DeepWalk).Train shuffles them.
+func (h *HIP) TrainDeepWalk(w, c [][]float64, dim int, order []int64, walkTimes, walkSteps, window, K int,
+	alpha float64, progress func(done uint64)) error {
+	if err := h.alloc(dim, 2); err != nil {
+		return err
+	}
+	if err := h.transfer([][][]float64{w, c}, true); err != nil {
+		return err
+	}
+	total := uint64(len(order))
+	if total == 0 {
+		return nil
+	}
+	ord := (*[1 << 40]C.int64_t)(C.malloc(C.size_t(8 * total)))[:total:total]
+	defer C.free(unsafe.Pointer(&ord[0]))
+	for i, v := range order {
+		ord[i] = C.int64_t(v)
+	}
+	step := uint64(1<<20) * uint64(h.cfg.GPUs)
+	for done := uint64(0); done < total; {
+		n := total - done
+		if n > step {
+			n = step
+		}
+		if rc := C.smore_group_train_deepwalk(h.group, C.uint64_t(done), C.uint64_t(done+n), C.int(walkTimes),
+			C.int(walkSteps), C.int(window), C.int(K), C.double(alpha), C.uint64_t(h.cfg.Seed), &ord[0],
+			C.int(h.cfg.Mode), 0, 0); rc != C.SMORE_OK {
+			return h.err("smore_group_train_deepwalk")
+		}
+		done += n
+		if progress != nil {
+			progress(done)
+		}
+	}
+	return h.transfer([][][]float64{w, c}, false)
+}

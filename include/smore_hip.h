@@ -2,9 +2,10 @@
  * smore_hip.h -- C ABI of the MI355X-native SMORe hot path (libsmore_hip.so).
  *
  * The drop-in boundary: plain pointers and sizes, int status codes, no torch
- * and no HIP types in the signatures.  A context owns device memory on ONE GPU
- * (one process per GPU; multi-GPU replication is driven from above, see
- * smore_amd/dist.py).  Calls are synchronous unless named *_async; a context is
+ * and no HIP types in the signatures.  A context owns device memory on ONE GPU;
+ * N GPUs are N replicas exchanging table deltas over RCCL, driven either one
+ * process per GPU (smore_comm_init / smore_exchange_*) or from one process
+ * (smore_group_*).  Calls are synchronous unless named *_async; a context is
  * not thread-safe.  Host buffers are owned by the caller and copied in/out.
  *
  * Each entry point names the reference interface it replaces
@@ -198,6 +199,57 @@ int smore_delta_end(smore_ctx* ctx, void* T, void* S, const void* D, const void*
  * R = D, S = T */
 int smore_delta_cycle(smore_ctx* ctx, void* T, void* S, void* D, void* R, float scale, int64_t n);
 
+/* ---- multi-GPU replicas over RCCL, in the library (smore_amd/csrc/exchange.cpp) ------
+ * replaces: the fan-out of one training run over the reference's workers
+ * (LINE::Train `#pragma omp parallel for`, src/model/LINE.cpp:162; MF.cpp /
+ * BPR.cpp / DeepWalk.cpp Train likewise; Go goroutines per worker,
+ * internal/models/line/line.go:96-146) -- here across GPUs.  Every GPU holds a
+ * replica of graph and tables and trains a disjoint range of global sample
+ * indices; the replicas exchange table deltas (all-reduce over xGMI), one
+ * exchange late, overlapping the next step:
+ *   begin: D = T - S; R = D; S = T; all-reduce(R) on the exchange stream
+ *   end:   X = scale*R - D; T += X; S += X          (scale 1, or 1/nranks if mean)
+ * One process per GPU: every rank calls smore_comm_init with the same id (made
+ * by one rank with smore_comm_unique_id and shared out of band), then after the
+ * tables are initialised smore_exchange_reset (S = T), after each training step
+ * smore_exchange_begin (an in-flight exchange is folded in first), and at the
+ * end smore_exchange_end.  RCCL is loaded on first use (librccl.so.1). */
+#define SMORE_COMM_ID_BYTES 128
+int smore_comm_unique_id(unsigned char* id /* SMORE_COMM_ID_BYTES */);
+int smore_comm_init(smore_ctx* ctx, int nranks, int rank, const unsigned char* id);
+int smore_exchange_reset(smore_ctx* ctx);
+int smore_exchange_begin(smore_ctx* ctx, int mean);
+int smore_exchange_end(smore_ctx* ctx);
+
+/* One process driving N GPUs (`smore_create(dev_ids, n_dev)` with
+ * internal fan-out): a group of N contexts with one communicator each
+ * (ncclCommInitAll).  Replica 0 is the primary: graph / table / save calls that
+ * are not group calls go to smore_group_ctx(g, 0); smore_group_broadcast_tables
+ * then copies its tables to every replica.  Group training splits the global
+ * sample (walk) range in rounds: in round k replica r runs
+ * [begin + (k*N + r)*per, +per), then all replicas exchange; the last exchange
+ * completes before the call returns, when all replicas agree (float rounding). */
+typedef struct smore_group smore_group;
+int smore_group_create(const int* devices, int n, smore_group** out);
+void smore_group_destroy(smore_group* g);
+int smore_group_size(const smore_group* g);
+smore_ctx* smore_group_ctx(smore_group* g, int rank);
+const char* smore_group_last_error(const smore_group* g);
+int smore_group_load_edgelist(smore_group* g, const char* path, int undirected, int vertex_method,
+                              int negative_method);
+int smore_group_set_graph_edges(smore_group* g, int64_t V, int64_t E, const int32_t* src, const int32_t* dst,
+                                const double* w, int vertex_method, int negative_method);
+int smore_group_set_semantics(smore_group* g, int semantics);
+int smore_group_alloc_tables(smore_group* g, int dim, int ntables);
+int smore_group_broadcast_tables(smore_group* g);
+/* per = samples per replica per exchange (0: 2^27) */
+int smore_group_train_edges(smore_group* g, int model, uint64_t begin, uint64_t count, uint64_t total, int K,
+                            double alpha0, double reg, uint64_t seed, int mode, uint64_t per, int mean);
+/* per = walks per replica per exchange (0: 2^18) */
+int smore_group_train_deepwalk(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
+                               int walk_steps, int window, int K, double alpha0, uint64_t seed,
+                               const int64_t* order, int mode, uint64_t per, int mean);
+
 /* replaces: DeepWalk::Train (src/model/DeepWalk.cpp:98-155): walks
  * [walk_begin, walk_end) of walk_times*V, start vertices order[] (host,
  * walk_times*V entries, see smore_deepwalk_order), RandomWalk + SkipGrams +
@@ -205,6 +257,11 @@ int smore_delta_cycle(smore_ctx* ctx, void* T, void* S, void* D, void* R, float 
 int smore_train_deepwalk(smore_ctx* ctx, uint64_t walk_begin, uint64_t walk_end,
                          int walk_times, int walk_steps, int window, int K, double alpha0,
                          uint64_t seed, const int64_t* order, int mode);
+/* the same, returning once the work is queued on the context stream (order[]
+ * must stay valid until the context synchronizes) */
+int smore_train_deepwalk_async(smore_ctx* ctx, uint64_t walk_begin, uint64_t walk_end,
+                               int walk_times, int walk_steps, int window, int K, double alpha0,
+                               uint64_t seed, const int64_t* order, int mode);
 /* the reference's walk start order: per walk_time a Fisher-Yates shuffle with
  * glibc rand() after `skip` Init draws (src/model/DeepWalk.cpp:122-131) */
 int smore_deepwalk_order(int64_t V, int walk_times, uint64_t skip, int64_t* order);

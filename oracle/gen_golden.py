@@ -8,6 +8,7 @@ synthetic edge lists it was run on.  Re-run only in a container that has
 /root/reference; the committed fixtures are what the tests read.
 
     python oracle/gen_golden.py            # regenerate everything
+    python oracle/gen_golden.py --only e2e_deepwalk_d128_pl100w   # one end-to-end fixture
 """
 import os
 import struct
@@ -109,6 +110,10 @@ def main():
     zipf_graph(graphs["pl1k"], 1000, 3000, seed=11, weighted=False)
     zipf_graph(graphs["pl100w"], 100, 400, seed=12, weighted=True)
     bipartite_graph(graphs["bip"], 200, 100, 2000, seed=13)
+    only = sys.argv[sys.argv.index("--only") + 1:] if "--only" in sys.argv else None
+    if only:
+        gen_e2e(graphs, 20251015, only)
+        return
 
     # ---- G1: AliasMethod on hand-made distributions (src/proNet.cpp:544-620)
     rng = np.random.default_rng(21)
@@ -184,6 +189,11 @@ def main():
         rec["meta_model"] = np.frombuffer(model.encode(), np.uint8)
         np.savez_compressed(os.path.join(GOLD, name + ".npz"), **rec)
 
+    gen_e2e(graphs, seed, None)
+    print("golden fixtures written to", GOLD)
+
+
+def gen_e2e(graphs, seed, only):
     # ---- G5: end-to-end 1-thread runs ----------------------------------------
     e2e = [
         ("e2e_mf_toy", ["mf", graphs["toy"], 5, 1, 5, 0.025, 0.01, seed]),         # config 1
@@ -191,14 +201,17 @@ def main():
         ("e2e_line1_pl100w", ["line", graphs["pl100w"], 1, 1, 8, 1, 5, 0.025, seed]),
         ("e2e_bpr_bip", ["bpr", graphs["bip"], 8, 1, 0.025, 0.01, seed]),
         ("e2e_deepwalk_pl100w", ["deepwalk", graphs["pl100w"], 1, 8, 2, 10, 3, 2, 0.025, seed]),
+        # config 5's model shape: d=128, walk_steps 40, window 5, K 5
+        ("e2e_deepwalk_d128_pl100w", ["deepwalk", graphs["pl100w"], 1, 128, 1, 40, 5, 5, 0.025, seed]),
     ]
     for name, args in e2e:
+        if only and name not in only:
+            continue
         out = os.path.join(TMP, name + ".bin")
         run(*(args + [out]))
         o = read_smrf(out)
         o["meta_args"] = np.frombuffer(" ".join(str(a) for a in args[:1] + args[2:]).encode(), np.uint8)
         np.savez_compressed(os.path.join(GOLD, name + ".npz"), **o)
-    print("golden fixtures written to", GOLD)
 
 
 if __name__ == "__main__":

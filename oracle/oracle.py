@@ -63,6 +63,8 @@ def _declare(L):
     L.orc_alpha_walk.argtypes = [u64, dbl, u64]
     L.orc_train_edge_f64.restype = C.c_int
     L.orc_train_edge_f64.argtypes = [P, C.c_int, P, P, C.c_int, C.c_int, dbl, dbl, u64, u64, u64, u64]
+    L.orc_train_edge_f64_mt.restype = C.c_int
+    L.orc_train_edge_f64_mt.argtypes = [P, C.c_int, P, P, C.c_int, C.c_int, dbl, dbl, u64, u64, u64, u64, C.c_int]
     L.orc_train_bpr_f64.restype = C.c_int
     L.orc_train_bpr_f64.argtypes = [P, P, C.c_int, dbl, u64, u64, u64, u64]
     L.orc_train_deepwalk_f64.restype = C.c_int
@@ -226,8 +228,11 @@ def lane_width(dpad):
 MODEL = {"line2": 0, "line1": 1, "mf": 2}
 
 
-def train_edge_f64(g, model, W, C_, K, alpha0, reg, total, begin, end, seed):
+def train_edge_f64(g, model, W, C_, K, alpha0, reg, total, begin, end, seed, threads=1):
     dim = W.shape[1]
+    if threads > 1:
+        return lib().orc_train_edge_f64_mt(g.ref, MODEL[model], ptr(W), ptr(C_), dim, K, alpha0, reg, total, begin,
+                                           end, seed, threads)
     return lib().orc_train_edge_f64(g.ref, MODEL[model], ptr(W), ptr(C_), dim, K, alpha0, reg, total, begin, end, seed)
 
 

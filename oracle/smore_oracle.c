@@ -448,6 +448,39 @@ int orc_train_edge_f64(const orc_graph* g, int model, double* W, double* C, int 
     return skipped;
 }
 
+/* The same loop with OpenMP Hogwild threads over contiguous sample blocks:
+ * the reference's own CPU structure (src/model/LINE.cpp:162, racy shared fp64
+ * rows) -- bench.py's reference-arithmetic CPU baseline. */
+int orc_train_edge_f64_mt(const orc_graph* g, int model, double* W, double* C, int dim,
+                          int K, double alpha0, double reg, uint64_t total, uint64_t begin,
+                          uint64_t end, uint64_t seed, int threads) {
+    if (threads <= 1) return orc_train_edge_f64(g, model, W, C, dim, K, alpha0, reg, total, begin, end, seed);
+    int skipped = 0;
+#ifdef _OPENMP
+    sig_init();
+    uint64_t base = (model == 2) ? 0 : 1;
+    #pragma omp parallel num_threads(threads) reduction(+:skipped)
+    {
+        double* err = (double*)malloc(sizeof(double) * dim);
+        uint32_t w[MAX_SLOTS];
+        int32_t negs[MAX_SLOTS];
+        #pragma omp for schedule(static)
+        for (int64_t si = (int64_t)begin; si < (int64_t)end; ++si) {
+            uint64_t s = (uint64_t)si;
+            orc_words(seed, 0, s, 4 + 2 * K, w);
+            int32_t v = source_sample(g, w[0], w[1]);
+            int32_t c = target_sample(g, v, w[2], w[3]);
+            if (c < 0) { skipped++; continue; }
+            for (int j = 0; j < K; ++j) negs[j] = negative_sample(g, w[4 + 2 * j], w[5 + 2 * j]);
+            double alpha = orc_alpha_line(s + base, alpha0, total);
+            update_edge_f64(model, W, C, dim, v, c, negs, K, alpha, reg, err);
+        }
+        free(err);
+    }
+#endif
+    return skipped;
+}
+
 /* UpdateBPRPair src/proNet.cpp:1406-1455 with Opt_BPRSGD :1053-1068; one
  * shared table (BPR::Train passes w_vertex twice, src/model/BPR.cpp:91). */
 static void update_bpr_f64(double* W, int dim, int32_t u, int32_t i, const int32_t* js,

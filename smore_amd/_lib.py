@@ -64,6 +64,24 @@ def _load():
         "smore_delta_end": (i32, [P, P, P, P, P, C.c_float, i64]),
         "smore_delta_cycle": (i32, [P, P, P, P, P, C.c_float, i64]),
         "smore_train_deepwalk": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, u64, P, i32]),
+        "smore_train_deepwalk_async": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, u64, P, i32]),
+        "smore_comm_unique_id": (i32, [P]),
+        "smore_comm_init": (i32, [P, i32, i32, P]),
+        "smore_exchange_reset": (i32, [P]),
+        "smore_exchange_begin": (i32, [P, i32]),
+        "smore_exchange_end": (i32, [P]),
+        "smore_group_create": (i32, [P, i32, C.POINTER(P)]),
+        "smore_group_destroy": (None, [P]),
+        "smore_group_size": (i32, [P]),
+        "smore_group_ctx": (C.c_void_p, [P, i32]),
+        "smore_group_last_error": (C.c_char_p, [P]),
+        "smore_group_load_edgelist": (i32, [P, C.c_char_p, i32, i32, i32]),
+        "smore_group_set_graph_edges": (i32, [P, i64, i64, P, P, P, i32, i32]),
+        "smore_group_set_semantics": (i32, [P, i32]),
+        "smore_group_alloc_tables": (i32, [P, i32, i32]),
+        "smore_group_broadcast_tables": (i32, [P]),
+        "smore_group_train_edges": (i32, [P, i32, u64, u64, u64, i32, dbl, dbl, u64, i32, u64, i32]),
+        "smore_group_train_deepwalk": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, u64, P, i32, u64, i32]),
         "smore_deepwalk_order": (i32, [i64, i32, u64, P]),
         "smore_sample_edges": (i32, [P, i32, u64, u64, i32, u64, P]),
         "smore_save_weights": (i32, [P, i32, C.c_char_p, i32]),

@@ -3,9 +3,7 @@
 // A context owns one GPU's copy of the graph (CSR, encoded alias tables, the
 // fastSigmoid table) and the embedding tables.  Everything on the device is
 // uploaded once; training calls only launch kernels on the context stream.
-#include "../../include/smore_hip.h"
-
-#include <hip/hip_runtime.h>
+#include "ctx.h"
 
 #include <algorithm>
 #include <cmath>
@@ -15,155 +13,7 @@
 #include <string>
 #include <vector>
 
-#include "host_graph.h"
-#include "train_kernels.h"
-
-using namespace smore;
-
-struct smore_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    hipStream_t own_stream = nullptr;
-    hipStream_t draw_stream = nullptr;   // draw kernels overlapping the previous chunk's update
-    std::vector<hipEvent_t> sync_ev;     // draw-done / update-done hand-offs between the two streams
-    std::string err;
-    HostGraph g;
-    bool has_graph = false;
-    // device graph
-    int64_t* d_offsets = nullptr;
-    int32_t* d_targets = nullptr;
-    AliasEntry* d_vtab = nullptr;
-    AliasEntry* d_ntab = nullptr;
-    AliasEntry* d_ctab = nullptr;
-    float* d_sig = nullptr;
-    unsigned long long* d_skipped = nullptr;
-    unsigned long long* d_work = nullptr;   // chunk counter of the Hogwild edge kernels
-    // tables
-    float* d_table[2] = {nullptr, nullptr};
-    int dim = 0, dpad = 0, ntables = 0;
-    // hybrid scatter: hot-row bitmaps (1 bit per row), keyed by what built them
-    double hot_tau = 0.3;
-    std::string hot_key;
-    int64_t hot_rows[2] = {0, 0};
-    // DeepWalk buffers
-    int64_t* d_order = nullptr;
-    uint64_t walk_order_n = 0;
-    const int64_t* walk_order_host = nullptr;
-    int32_t* d_walks = nullptr;
-    int32_t* d_lens = nullptr;
-    size_t walk_buf_n = 0;
-    // timing
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    bool timed = false;
-    int cus = 0;
-    int64_t last_loaded = 0;
-    // semantics: SMORE_SEM_CPP (default) or SMORE_SEM_GO
-    int semantics = 0;
-    double* d_tcum = nullptr;
-    // hybrid write-combining: super-hot context rows (hash + slot ids)
-    int2* d_sh_hash = nullptr;
-    int32_t* d_sh_ids = nullptr;
-    int sh_rows = 0;
-    int sh_max = 128, sh_flush = 32;
-    // pre-drawn edge-sample records (train_draw.hip) and per-phase timing
-    int32_t* d_rec = nullptr;
-    // DeepWalk pair records: per-walk pair counts, their exclusive scan, scan scratch
-    uint32_t* d_pcount = nullptr;
-    uint64_t* d_poff = nullptr;
-    size_t pair_walks = 0;
-    void* d_scan_tmp = nullptr;
-    size_t scan_tmp_bytes = 0;
-    // packed draw tables (train_draw.hip), rebuilt when the graph tables change
-    uint4* d_vt32 = nullptr;
-    uint4* d_ct16 = nullptr;
-    bool packed_ok = false;
-    size_t rec_cap = 0;                 // int32 words
-    std::vector<hipEvent_t> phase_ev;   // {before draw 0, after draw 0, after update 0, after draw 1, ...}
-    int phase_n = 0;                    // chunks of the last edge launch
-};
-
-namespace {
-
-int fail(smore_ctx* c, int code, const std::string& msg) {
-    if (c) c->err = msg;
-    return code;
-}
-
-#define HIPCHK(c, expr)                                                                     \
-    do {                                                                                    \
-        hipError_t e_ = (expr);                                                             \
-        if (e_ != hipSuccess)                                                               \
-            return fail((c), SMORE_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
-    } while (0)
-
-template <class T>
-void dfree(T*& p) {
-    if (p) (void)hipFree((void*)p);
-    p = nullptr;
-}
-
-template <class T>
-int upload(smore_ctx* c, T*& d, const T* h, size_t n) {
-    dfree(d);
-    if (n == 0) n = 1;
-    HIPCHK(c, hipMalloc((void**)&d, n * sizeof(T)));
-    if (h) HIPCHK(c, hipMemcpy(d, h, n * sizeof(T), hipMemcpyHostToDevice));
-    return SMORE_OK;
-}
-
-int set_device(smore_ctx* c) {
-    if (c->device < 0) return fail(c, SMORE_ESTATE, "host-only context (device < 0) has no GPU state");
-    HIPCHK(c, hipSetDevice(c->device));
-    return SMORE_OK;
-}
-
-int upload_graph(smore_ctx* c) {
-    int rc;
-    if (c->device < 0) {
-        c->has_graph = true;
-        return SMORE_OK;
-    }
-    if ((rc = set_device(c))) return rc;
-    HostGraph& g = c->g;
-    c->packed_ok = false;
-    dfree(c->d_vt32);
-    dfree(c->d_ct16);
-    if ((rc = upload(c, c->d_offsets, g.offsets.data(), g.offsets.size()))) return rc;
-    if ((rc = upload(c, c->d_targets, g.targets.data(), g.targets.size()))) return rc;
-    if ((rc = upload(c, c->d_vtab, g.vtab.data(), g.vtab.size()))) return rc;
-    if ((rc = upload(c, c->d_ntab, g.ntab.data(), g.ntab.size()))) return rc;
-    if ((rc = upload(c, c->d_ctab, g.ctab.data(), g.ctab.size()))) return rc;
-    // fastSigmoid table, 1001 entries (src/proNet.cpp:52-60; the reference
-    // sizes it 1000 and writes 1001 -- the build keeps all 1001)
-    std::vector<float> sig(1001);
-    for (int i = 0; i != 1000 + 1; i++) {
-        double x = i * 2.0 * 8.0 / 1000 - 8.0;
-        sig[i] = (float)(1.0 / (1.0 + std::exp(-x)));
-    }
-    if ((rc = upload(c, c->d_sig, sig.data(), sig.size()))) return rc;
-    c->has_graph = true;
-    return SMORE_OK;
-}
-
-DevGraph dev_graph(const smore_ctx* c) {
-    DevGraph d;
-    d.offsets = c->d_offsets;
-    d.targets = c->d_targets;
-    d.vtab = reinterpret_cast<const uint2*>(c->d_vtab);
-    d.ntab = reinterpret_cast<const uint2*>(c->d_ntab);
-    d.ctab = reinterpret_cast<const uint2*>(c->d_ctab);
-    d.vt32 = c->packed_ok ? c->d_vt32 : nullptr;
-    d.ct16 = c->packed_ok ? c->d_ct16 : nullptr;
-    d.V = (uint32_t)c->g.V;
-    return d;
-}
-
-float* table_ptr(smore_ctx* c, int which) {
-    if (which < 0 || which > 1) return nullptr;
-    return c->d_table[which];
-}
-
-}  // namespace
+using namespace smore_host;
 
 extern "C" {
 
@@ -198,6 +48,7 @@ int smore_create(int device, smore_ctx** out) {
 
 void smore_destroy(smore_ctx* c) {
     if (!c) return;
+    smore_exchange_release(c);
     if (c->device >= 0) {
         (void)hipSetDevice(c->device);
         (void)hipStreamSynchronize(c->stream);
@@ -240,10 +91,10 @@ int smore_set_graph_edges(smore_ctx* c, int64_t V, int64_t E, const int32_t* src
     if (!c) return SMORE_EINVAL;
     if ((E > 0 && (!src || !dst || !w)) || vm < 0 || vm > 2 || nm < 0 || nm > 2)
         return fail(c, SMORE_EINVAL, "bad arguments");
-    c->g = HostGraph();
+    c->g = std::make_shared<HostGraph>();
     c->hot_key.clear();
     c->semantics = SMORE_SEM_CPP;
-    if (!build_graph(V, E, src, dst, w, vm, nm, c->g, c->err)) return SMORE_EINVAL;
+    if (!build_graph(V, E, src, dst, w, vm, nm, *c->g, c->err)) return SMORE_EINVAL;
     return upload_graph(c);
 }
 
@@ -256,33 +107,33 @@ int smore_load_edgelist(smore_ctx* c, const char* path, int undirected, int vm, 
     if (names.empty()) return fail(c, SMORE_EIO, std::string("no edges in ") + path);
     int rc = smore_set_graph_edges(c, (int64_t)names.size(), (int64_t)src.size(), src.data(), dst.data(),
                                    w.data(), vm, nm);
-    if (rc == SMORE_OK) c->g.names = std::move(names);
+    if (rc == SMORE_OK) c->g->names = std::move(names);
     return rc;
 }
 
 int smore_graph_info(const smore_ctx* c, int64_t* V, int64_t* E) {
     if (!c) return SMORE_EINVAL;
-    if (V) *V = c->g.V;
-    if (E) *E = c->g.E;
+    if (V) *V = c->g->V;
+    if (E) *E = c->g->E;
     return c->has_graph ? SMORE_OK : SMORE_ESTATE;
 }
 
 const char* smore_vertex_name(const smore_ctx* c, int64_t vid) {
-    if (!c || vid < 0 || vid >= (int64_t)c->g.names.size()) return nullptr;
-    return c->g.names[vid].c_str();
+    if (!c || vid < 0 || vid >= (int64_t)c->g->names.size()) return nullptr;
+    return c->g->names[vid].c_str();
 }
 
 int smore_get_csr(const smore_ctx* c, int64_t* offsets, int32_t* targets) {
     if (!c || !c->has_graph) return SMORE_ESTATE;
-    if (offsets) memcpy(offsets, c->g.offsets.data(), c->g.offsets.size() * sizeof(int64_t));
-    if (targets) memcpy(targets, c->g.targets.data(), c->g.targets.size() * sizeof(int32_t));
+    if (offsets) memcpy(offsets, c->g->offsets.data(), c->g->offsets.size() * sizeof(int64_t));
+    if (targets) memcpy(targets, c->g->targets.data(), c->g->targets.size() * sizeof(int32_t));
     return SMORE_OK;
 }
 
 int smore_set_alias(smore_ctx* c, int which, const double* prob, const int64_t* alias, int64_t n) {
     if (!c || !prob || !alias) return SMORE_EINVAL;
     if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
-    HostGraph& g = c->g;
+    HostGraph& g = *c->g;
     int64_t want = which == SMORE_AT_CONTEXT ? g.E : g.V;
     if (which < 0 || which > 2 || n != want) return fail(c, SMORE_EINVAL, "alias table size mismatch");
     int64_t lim = g.V;
@@ -308,7 +159,7 @@ int smore_set_alias(smore_ctx* c, int which, const double* prob, const int64_t* 
 
 int smore_get_alias(const smore_ctx* c, int which, double* prob, int64_t* alias, int64_t n) {
     if (!c || !c->has_graph || which < 0 || which > 2) return SMORE_EINVAL;
-    const HostGraph& g = c->g;
+    const HostGraph& g = *c->g;
     const std::vector<double>& P = which == 0 ? g.vprob : which == 1 ? g.nprob : g.cprob;
     const std::vector<int64_t>& A = which == 0 ? g.valias : which == 1 ? g.nalias : g.calias;
     if (n != (int64_t)P.size()) return SMORE_EINVAL;
@@ -319,7 +170,7 @@ int smore_get_alias(const smore_ctx* c, int which, double* prob, int64_t* alias,
 
 int smore_get_alias_encoded(const smore_ctx* c, int which, uint32_t* thresh, int32_t* alias, int64_t n) {
     if (!c || !c->has_graph || which < 0 || which > 2) return SMORE_EINVAL;
-    const HostGraph& g = c->g;
+    const HostGraph& g = *c->g;
     const std::vector<AliasEntry>& T = which == 0 ? g.vtab : which == 1 ? g.ntab : g.ctab;
     if (n != (int64_t)T.size()) return SMORE_EINVAL;
     for (int64_t i = 0; i < n; ++i) {
@@ -341,7 +192,7 @@ int smore_alloc_tables(smore_ctx* c, int dim, int ntables) {
     c->dim = dim;
     c->dpad = (dim + 3) / 4 * 4;
     c->ntables = ntables;
-    size_t bytes = (size_t)c->g.V * c->dpad * sizeof(float);
+    size_t bytes = (size_t)c->g->V * c->dpad * sizeof(float);
     for (int t = 0; t < ntables; ++t) {
         HIPCHK(c, hipMalloc((void**)&c->d_table[t], bytes));
         HIPCHK(c, hipMemset(c->d_table[t], 0, bytes));
@@ -360,8 +211,8 @@ int smore_init_table_glibc(smore_ctx* c, int which, uint64_t skip) {
     if ((rc = check_table(c, which))) return rc;
     GlibcRand r;
     r.discard(skip);
-    std::vector<float> h((size_t)c->g.V * c->dpad, 0.0f);
-    for (int64_t v = 0; v < c->g.V; ++v)
+    std::vector<float> h((size_t)c->g->V * c->dpad, 0.0f);
+    for (int64_t v = 0; v < c->g->V; ++v)
         for (int d = 0; d < c->dim; ++d)
             h[(size_t)v * c->dpad + d] = (float)((r.next() / (double)2147483647 - 0.5) / c->dim);
     if ((rc = set_device(c))) return rc;
@@ -373,7 +224,7 @@ int smore_init_table_uniform(smore_ctx* c, int which, uint64_t seed) {
     int rc;
     if ((rc = check_table(c, which))) return rc;
     if ((rc = set_device(c))) return rc;
-    HIPCHK(c, launch_init_uniform(c->d_table[which], c->g.V, c->dim, c->dpad, seed, c->stream));
+    HIPCHK(c, launch_init_uniform(c->d_table[which], c->g->V, c->dim, c->dpad, seed, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return SMORE_OK;
 }
@@ -382,7 +233,7 @@ int smore_zero_table(smore_ctx* c, int which) {
     int rc;
     if ((rc = check_table(c, which))) return rc;
     if ((rc = set_device(c))) return rc;
-    HIPCHK(c, hipMemsetAsync(c->d_table[which], 0, (size_t)c->g.V * c->dpad * sizeof(float), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_table[which], 0, (size_t)c->g->V * c->dpad * sizeof(float), c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return SMORE_OK;
 }
@@ -390,7 +241,7 @@ int smore_zero_table(smore_ctx* c, int which) {
 int smore_set_table(smore_ctx* c, int which, const float* host, int64_t rows, int dim) {
     int rc;
     if ((rc = check_table(c, which))) return rc;
-    if (!host || rows != c->g.V || dim != c->dim) return fail(c, SMORE_EINVAL, "table shape mismatch");
+    if (!host || rows != c->g->V || dim != c->dim) return fail(c, SMORE_EINVAL, "table shape mismatch");
     if ((rc = set_device(c))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy2D(c->d_table[which], c->dpad * sizeof(float), host, dim * sizeof(float),
@@ -402,7 +253,7 @@ int smore_get_table(const smore_ctx* cc, int which, float* host, int64_t rows, i
     smore_ctx* c = const_cast<smore_ctx*>(cc);
     int rc;
     if ((rc = check_table(c, which))) return rc;
-    if (!host || rows != c->g.V || dim != c->dim) return fail(c, SMORE_EINVAL, "table shape mismatch");
+    if (!host || rows != c->g->V || dim != c->dim) return fail(c, SMORE_EINVAL, "table shape mismatch");
     if ((rc = set_device(c))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy2D(host, dim * sizeof(float), c->d_table[which], c->dpad * sizeof(float),
@@ -435,10 +286,10 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
     snprintf(key, sizeof key, "%d/%d/%lld/%.9g/%d/%d/%s", model, K, (long long)M, c->hot_tau, c->sh_max, c->sh_flush,
              stale_env ? stale_env : "");
     if (c->hot_key == key) return SMORE_OK;
-    if (c->g.V >= ((int64_t)1 << 30)) return fail(c, SMORE_EINVAL, "hybrid scatter needs V < 2^30");
+    if (c->g->V >= ((int64_t)1 << 30)) return fail(c, SMORE_EINVAL, "hybrid scatter needs V < 2^30");
     std::vector<double> ps, pn, pc;
-    draw_probabilities(c->g, ps, pn, pc);
-    const int64_t V = c->g.V, E = c->g.E;
+    draw_probabilities(*c->g, ps, pn, pc);
+    const int64_t V = c->g->V, E = c->g->E;
     std::vector<uint8_t> hw((size_t)V, 0), hc((size_t)V, 0);
     const int negs = model == SMORE_BPR ? 5 : K;
     c->hot_rows[0] = c->hot_rows[1] = 0;
@@ -482,7 +333,7 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
         if ((rc2 = upload(c, c->d_sh_ids, ids.data(), ids.size()))) return rc2;
         c->sh_rows = (int)n;
     }
-    const HostGraph& g = c->g;
+    const HostGraph& g = *c->g;
     auto tag_tab = [&](const std::vector<AliasEntry>& tab, const std::vector<uint8_t>& hot) {
         std::vector<AliasEntry> t(tab);
         for (int64_t i = 0; i < V; ++i) {
@@ -524,7 +375,7 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
 // current (tagged) tables; skipped when offsets do not fit 32 bits
 static int ensure_packed(smore_ctx* c) {
     if (c->packed_ok) return SMORE_OK;
-    const int64_t V = c->g.V, E = c->g.E;
+    const int64_t V = c->g->V, E = c->g->E;
     if (E >= ((int64_t)1 << 32)) return SMORE_OK;
     if (!c->d_vt32) HIPCHK(c, hipMalloc(&c->d_vt32, (size_t)std::max<int64_t>(V, 1) * 2 * sizeof(uint4)));
     if (!c->d_ct16) HIPCHK(c, hipMalloc(&c->d_ct16, (size_t)std::max<int64_t>(E, 1) * sizeof(uint4)));
@@ -560,7 +411,7 @@ static int edge_grid(smore_ctx* c, const EdgeArgs& a, bool leave_slot = false) {
     // two samples in flight), so that on small graphs the expected number of
     // in-flight updates per row stays O(1) as in the reference's few-thread
     // Hogwild; the benchmark graphs (V >= 1M) are far from the cap.
-    const int64_t cap_groups = std::max<int64_t>(1, c->g.V / 16);
+    const int64_t cap_groups = std::max<int64_t>(1, c->g->V / 16);
     const int64_t cap = (cap_groups + groups_per_block - 1) / groups_per_block;
     if (cap < grid) grid = cap;
     return (int)(grid < 1 ? 1 : grid);
@@ -724,15 +575,15 @@ int smore_set_semantics(smore_ctx* c, int semantics) {
     if (semantics == c->semantics) return SMORE_OK;
     c->packed_ok = false;
     std::vector<double> tcum;
-    if (semantics == SMORE_SEM_GO) build_go_tables(c->g, tcum);
-    else build_cpp_vn_tables(c->g);
+    if (semantics == SMORE_SEM_GO) build_go_tables(*c->g, tcum);
+    else build_cpp_vn_tables(*c->g);
     c->semantics = semantics;
     c->hot_key.clear();
     if (c->device < 0) return SMORE_OK;
     int rc;
     if ((rc = set_device(c))) return rc;
-    if ((rc = upload(c, c->d_vtab, c->g.vtab.data(), c->g.vtab.size()))) return rc;
-    if ((rc = upload(c, c->d_ntab, c->g.ntab.data(), c->g.ntab.size()))) return rc;
+    if ((rc = upload(c, c->d_vtab, c->g->vtab.data(), c->g->vtab.size()))) return rc;
+    if ((rc = upload(c, c->d_ntab, c->g->ntab.data(), c->g->ntab.size()))) return rc;
     if (semantics == SMORE_SEM_GO) {
         if ((rc = upload(c, c->d_tcum, tcum.data(), tcum.size()))) return rc;
     } else {
@@ -813,13 +664,13 @@ int smore_load_pretrain(smore_ctx* c, int which, const char* path) {
     int rc;
     if ((rc = check_table(c, which))) return rc;
     if (!path) return SMORE_EINVAL;
-    if (c->g.names.empty()) return fail(c, SMORE_ESTATE, "warm start needs vertex names (load an edge list)");
-    std::vector<float> h((size_t)c->g.V * c->dpad);
+    if (c->g->names.empty()) return fail(c, SMORE_ESTATE, "warm start needs vertex names (load an edge list)");
+    std::vector<float> h((size_t)c->g->V * c->dpad);
     if ((rc = set_device(c))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(h.data(), c->d_table[which], h.size() * sizeof(float), hipMemcpyDeviceToHost));
     int64_t loaded = 0;
-    if (!load_pretrain(path, c->g, h.data(), c->dim, c->dpad, &loaded, c->err)) return SMORE_EIO;
+    if (!load_pretrain(path, *c->g, h.data(), c->dim, c->dpad, &loaded, c->err)) return SMORE_EIO;
     c->last_loaded = loaded;
     HIPCHK(c, hipMemcpy(c->d_table[which], h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
     return SMORE_OK;
@@ -830,46 +681,62 @@ int smore_save_weights(const smore_ctx* cc, int which, const char* path, int fmt
     int rc;
     if ((rc = check_table(c, which))) return rc;
     if (!path) return SMORE_EINVAL;
-    std::vector<float> h((size_t)c->g.V * c->dpad);
+    std::vector<float> h((size_t)c->g->V * c->dpad);
     if ((rc = set_device(c))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(h.data(), c->d_table[which], h.size() * sizeof(float), hipMemcpyDeviceToHost));
-    if (!save_weights(path, c->g, h.data(), c->g.V, c->dim, c->dpad, fmt, c->err)) return SMORE_EIO;
+    if (!save_weights(path, *c->g, h.data(), c->g->V, c->dim, c->dpad, fmt, c->err)) return SMORE_EIO;
     return SMORE_OK;
 }
 
-int smore_train_deepwalk(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
-                         int window, int K, double alpha0, uint64_t seed, const int64_t* order, int mode) {
+int smore_train_deepwalk_async(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, int walk_times,
+                               int walk_steps, int window, int K, double alpha0, uint64_t seed, const int64_t* order,
+                               int mode) {
     if (!c) return SMORE_EINVAL;
     if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
     if (c->ntables < 2) return fail(c, SMORE_ESTATE, "DeepWalk needs W and C tables");
     if (!order || walk_times <= 0 || walk_steps < 0 || window <= 0 || K < 0 || K > 10 || mode < 0 || mode > 3)
         return fail(c, SMORE_EINVAL, "bad DeepWalk arguments");
-    const uint64_t total = (uint64_t)walk_times * (uint64_t)c->g.V;
+    const uint64_t total = (uint64_t)walk_times * (uint64_t)c->g->V;
     if (walk_end > total) walk_end = total;
     if (walk_begin >= walk_end) return SMORE_OK;
-    for (uint64_t i = 0; i < total; ++i)
-        if (order[i] < 0 || order[i] >= c->g.V) return fail(c, SMORE_EINVAL, "walk start out of range");
+    // only this call's walks [walk_begin, walk_end) are read: validate and
+    // upload that slice on every call (no caching by host pointer)
+    const uint64_t nw_call = walk_end - walk_begin;
+    for (uint64_t i = walk_begin; i < walk_end; ++i)
+        if (order[i] < 0 || order[i] >= c->g->V) return fail(c, SMORE_EINVAL, "walk start out of range");
     int rc;
     if ((rc = set_device(c))) return rc;
-    // device copy of the start order; re-uploaded when the caller passes a
-    // different array (the caller must not mutate one it has passed)
-    if (c->walk_order_n != total || c->walk_order_host != order) {
-        if ((rc = upload(c, c->d_order, order, total))) return rc;
-        c->walk_order_n = total;
-        c->walk_order_host = order;
+    if (c->order_cap < nw_call) {
+        dfree(c->d_order);
+        c->order_cap = 0;
+        HIPCHK(c, hipMalloc((void**)&c->d_order, nw_call * sizeof(int64_t)));
+        c->order_cap = nw_call;
     }
-    // C++ semantics: walks -> pair records -> update kernel, 2^18 walks per chunk
-    // (~61M pairs at walk_steps 40, window 5); Go semantics: fused walk kernel
+    HIPCHK(c, hipMemcpyAsync(c->d_order, order + walk_begin, nw_call * sizeof(int64_t), hipMemcpyHostToDevice,
+                             c->stream));
+    // C++ semantics: walks -> pair records -> update kernel; chunks of up to
+    // 2^18 walks whose pair records (sized by the per-walk upper bound, so no
+    // host read-back of the pair count) stay under 4 GiB.  Go semantics: fused
+    // walk kernel, 2^20 walks per chunk.
     const bool cpp = c->semantics != SMORE_SEM_GO;
-    const uint64_t chunk = std::min<uint64_t>(walk_end - walk_begin, (uint64_t)1 << (cpp ? 18 : 20));
+    const int RW = rec_width(kmax_of(K));
+    const uint64_t pb = std::max<uint64_t>(1, pair_bound(walk_steps, window));
+    uint64_t chunk_cap = (uint64_t)1 << (cpp ? 18 : 20);
+    if (cpp) chunk_cap = std::max<uint64_t>(1, std::min<uint64_t>(chunk_cap, ((uint64_t)1 << 30) / (pb * RW)));
+    const uint64_t chunk = std::min<uint64_t>(nw_call, chunk_cap);
     const size_t need = chunk * (size_t)(walk_steps + 1);
     if (c->walk_buf_n < need) {
         dfree(c->d_walks);
-        dfree(c->d_lens);
+        c->walk_buf_n = 0;
         HIPCHK(c, hipMalloc((void**)&c->d_walks, need * sizeof(int32_t)));
-        HIPCHK(c, hipMalloc((void**)&c->d_lens, chunk * sizeof(int32_t)));
         c->walk_buf_n = need;
+    }
+    if (c->walk_lens_n < chunk) {
+        dfree(c->d_lens);
+        c->walk_lens_n = 0;
+        HIPCHK(c, hipMalloc((void**)&c->d_lens, chunk * sizeof(int32_t)));
+        c->walk_lens_n = chunk;
     }
     EdgeArgs a{};
     a.g = dev_graph(c);
@@ -885,19 +752,25 @@ int smore_train_deepwalk(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, i
     EdgeArgs ar = a;   // the update kernel over pair records (C++ semantics)
     int ugrid = 1;
     if (cpp) {
-        if (c->pair_walks < chunk) {
+        if (c->pair_walks < chunk + 1) {
             dfree(c->d_pcount);
             dfree(c->d_poff);
             c->pair_walks = 0;
-            HIPCHK(c, hipMalloc((void**)&c->d_pcount, chunk * sizeof(uint32_t)));
-            HIPCHK(c, hipMalloc((void**)&c->d_poff, chunk * sizeof(uint64_t)));
-            c->pair_walks = chunk;
+            HIPCHK(c, hipMalloc((void**)&c->d_pcount, (chunk + 1) * sizeof(uint32_t)));
+            HIPCHK(c, hipMalloc((void**)&c->d_poff, (chunk + 1) * sizeof(uint64_t)));
+            c->pair_walks = chunk + 1;
+        }
+        if (c->rec_cap < chunk * pb * RW) {
+            dfree(c->d_rec);
+            c->rec_cap = 0;
+            HIPCHK(c, hipMalloc(&c->d_rec, chunk * pb * RW * sizeof(int32_t)));
+            c->rec_cap = chunk * pb * RW;
         }
         const bool combine = mode == SMORE_HYBRID;
         ar.sh_rows = combine ? std::min(c->sh_max, 8192 / std::max(1, c->dpad)) : 0;
         ar.alpha_rec = 1;
         ar.work = c->d_work;
-        ar.count = (uint64_t)1 << 40;   // grid for a full chunk of pairs (a launch never needs more)
+        ar.count = chunk * pb;   // grid for the most pairs a chunk can have
         ugrid = edge_grid(c, ar);
         if (mode == SMORE_HYBRID) {
             const int64_t M = (int64_t)ugrid * (256 / lanes_of(c->dpad));
@@ -913,6 +786,7 @@ int smore_train_deepwalk(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, i
     for (uint64_t b = walk_begin; b < walk_end; b += chunk) {
         WalkArgs w;
         w.order = c->d_order;
+        w.order_base = walk_begin;
         w.walks = c->d_walks;
         w.lens = c->d_lens;
         w.walk_begin = b;
@@ -927,30 +801,19 @@ int smore_train_deepwalk(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, i
         if (c->semantics == SMORE_SEM_GO) {
             HIPCHK(c, launch_go_walk(a, w, g2, c->stream));
         } else {
+            // counts of walks [0, n) plus a zero at n: the exclusive scan's entry
+            // n is the chunk's pair total, which the update kernel reads on the
+            // device (no host round trip between chunks)
             HIPCHK(c, launch_walk_gen(ar.g, w, seed, c->stream));
+            HIPCHK(c, hipMemsetAsync(c->d_pcount + w.nwalks, 0, sizeof(uint32_t), c->stream));
             HIPCHK(c, launch_pair_count(w, seed, c->d_pcount, c->stream));
-            HIPCHK(c, scan_pair_counts(c->d_pcount, c->d_poff, w.nwalks, &c->d_scan_tmp, &c->scan_tmp_bytes,
+            HIPCHK(c, scan_pair_counts(c->d_pcount, c->d_poff, w.nwalks + 1, &c->d_scan_tmp, &c->scan_tmp_bytes,
                                        c->stream));
-            uint64_t last_off = 0;
-            uint32_t last_cnt = 0;
-            HIPCHK(c, hipMemcpyAsync(&last_off, c->d_poff + (w.nwalks - 1), sizeof last_off, hipMemcpyDeviceToHost,
-                                     c->stream));
-            HIPCHK(c, hipMemcpyAsync(&last_cnt, c->d_pcount + (w.nwalks - 1), sizeof last_cnt,
-                                     hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(c, hipStreamSynchronize(c->stream));
-            const uint64_t npairs = last_off + last_cnt;
-            if (npairs == 0) continue;
-            const int RW = rec_width(kmax_of(K));
-            if (c->rec_cap < npairs * RW) {
-                dfree(c->d_rec);
-                c->rec_cap = 0;
-                HIPCHK(c, hipMalloc(&c->d_rec, npairs * RW * sizeof(int32_t)));
-                c->rec_cap = npairs * RW;
-            }
             HIPCHK(c, launch_pair_emit(ar.g, w, seed, K, alpha0, c->d_poff, c->d_rec, c->stream));
             EdgeArgs ak = ar;
             ak.begin = 0;
-            ak.count = npairs;
+            ak.count = w.nwalks * pb;
+            ak.count_dev = c->d_poff + w.nwalks;
             ak.rec = c->d_rec;
             HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
             HIPCHK(c, launch_edge_train(ak, mode == SMORE_SERIAL ? 1 : ugrid, c->stream));
@@ -959,6 +822,14 @@ int smore_train_deepwalk(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, i
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
     c->phase_n = 0;
+    return SMORE_OK;
+}
+
+int smore_train_deepwalk(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
+                         int window, int K, double alpha0, uint64_t seed, const int64_t* order, int mode) {
+    int rc = smore_train_deepwalk_async(c, walk_begin, walk_end, walk_times, walk_steps, window, K, alpha0, seed,
+                                        order, mode);
+    if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return SMORE_OK;
 }

@@ -10,12 +10,12 @@ int main(int argc, char** argv) {
         printf("[smore-mi355x] BPR\n\nOptions Description:\n");
         printf("\t-train <string>\n\t-save <string>\n\t-dimensions <int> (64)\n\t-sample_times <int> (10, x10^6)\n");
         printf("\t-alpha <float> (0.025)\n\t-threads <int>\n");
-        printf("\t-device <int> -mode hogwild|atomic|hybrid|serial -seed <int> -format cpp|go\n");
+        printf("\t-device <int> -gpus <int> -mode hogwild|atomic|hybrid|serial -seed <int> -format cpp|go\n");
         printf("Usage:\n./bpr -train net.txt -save rep.txt -dimensions 64 -sample_times 10 -alpha 0.025 -threads 1\n");
         return 0;
     }
     char network_file[4096] = "", rep_file[4096] = "";
-    int dimensions = 64, negative_samples = 5, sample_times = 10, threads = 1, device = 0, fmt = 0;
+    int dimensions = 64, negative_samples = 5, sample_times = 10, threads = 1, device = 0, gpus = 1, fmt = 0;
     int mode = SMORE_HYBRID;
     unsigned long long seed = 1;
     double init_alpha = 0.025, reg = 0.01;
@@ -28,23 +28,26 @@ int main(int argc, char** argv) {
     if ((i = ArgPos("-alpha", argc, argv)) > 0) init_alpha = atof(argv[i + 1]);
     if ((i = ArgPos("-threads", argc, argv)) > 0) threads = atoi(argv[i + 1]);
     if ((i = ArgPos("-device", argc, argv)) > 0) device = atoi(argv[i + 1]);
+    if ((i = ArgPos("-gpus", argc, argv)) > 0) gpus = atoi(argv[i + 1]);
     if ((i = ArgPos("-mode", argc, argv)) > 0) mode = mode_of(argv[i + 1]);
     if ((i = ArgPos("-seed", argc, argv)) > 0) seed = strtoull(argv[i + 1], 0, 10);
     if ((i = ArgPos("-format", argc, argv)) > 0) fmt = !strcmp(argv[i + 1], "go");
     (void)negative_samples; (void)reg;
 
-    smore_ctx* ctx = open_context(device);
+    Run run = open_run(device, gpus);
+    smore_ctx* ctx = run.ctx;
     // BPR() sets negative_method "no_degrees" (src/model/BPR.cpp:4-7); LoadEdgeList(file, 0)
-    SMORE_CLI_CHECK(ctx, smore_load_edgelist(ctx, network_file, 0, SMORE_VM_OUT_DEGREES, SMORE_NM_NO_DEGREES));
+    run_load(run, network_file, 0, SMORE_VM_OUT_DEGREES, SMORE_NM_NO_DEGREES);
     print_graph(ctx);
     printf("Model Setting:\n\tdimension:\t\t%d\n", dimensions);
-    SMORE_CLI_CHECK(ctx, smore_alloc_tables(ctx, dimensions, 1));
+    run_alloc(run, dimensions, 1);
     SMORE_CLI_CHECK(ctx, smore_init_table_glibc(ctx, SMORE_W, 0));
+    run_replicate(run);
     printf("Model:\n\t[BPR]\nLearning Parameters:\n\tsample_times:\t\t%d\n\talpha:\t\t\t%g\n\tworkers:\t\t%d\n"
            "Start Training:\n", sample_times, init_alpha, threads);
     const unsigned long long total = (unsigned long long)sample_times * 1000000ull;
-    train_chunks(ctx, SMORE_BPR, total, total, 5, init_alpha, 0.0, seed, mode);
+    train_chunks(run, SMORE_BPR, total, total, 5, init_alpha, 0.0, seed, mode);
     save(ctx, rep_file, fmt);
-    smore_destroy(ctx);
+    run_close(run);
     return 0;
 }

@@ -1,0 +1,178 @@
+// ctx.h -- the library context (one GPU's graph, tables and buffers) and the
+// host-side helpers shared by the C ABI translation units (capi.cpp,
+// exchange.cpp).  Internal: not part of the installed interface.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/smore_hip.h"
+#include "host_graph.h"
+#include "train_kernels.h"
+
+using namespace smore;
+
+struct smore_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipStream_t own_stream = nullptr;
+    hipStream_t draw_stream = nullptr;   // draw kernels overlapping the previous chunk's update
+    std::vector<hipEvent_t> sync_ev;     // draw-done / update-done hand-offs between the two streams
+    std::string err;
+    std::shared_ptr<HostGraph> g = std::make_shared<HostGraph>();   // shared by the replicas of a group
+    bool has_graph = false;
+    // device graph
+    int64_t* d_offsets = nullptr;
+    int32_t* d_targets = nullptr;
+    AliasEntry* d_vtab = nullptr;
+    AliasEntry* d_ntab = nullptr;
+    AliasEntry* d_ctab = nullptr;
+    float* d_sig = nullptr;
+    unsigned long long* d_skipped = nullptr;
+    unsigned long long* d_work = nullptr;   // chunk counter of the Hogwild edge kernels
+    // tables
+    float* d_table[2] = {nullptr, nullptr};
+    int dim = 0, dpad = 0, ntables = 0;
+    // hybrid scatter: hot-row bitmaps (1 bit per row), keyed by what built them
+    double hot_tau = 0.3;
+    std::string hot_key;
+    int64_t hot_rows[2] = {0, 0};
+    // DeepWalk buffers
+    int64_t* d_order = nullptr;         // the walk starts of the current call (a slice of the order)
+    size_t order_cap = 0;
+    int32_t* d_walks = nullptr;
+    int32_t* d_lens = nullptr;
+    size_t walk_buf_n = 0;              // int32 capacity of d_walks
+    size_t walk_lens_n = 0;             // walk capacity of d_lens
+    // timing
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    int cus = 0;
+    int64_t last_loaded = 0;
+    // semantics: SMORE_SEM_CPP (default) or SMORE_SEM_GO
+    int semantics = 0;
+    double* d_tcum = nullptr;
+    // hybrid write-combining: super-hot context rows (hash + slot ids)
+    int2* d_sh_hash = nullptr;
+    int32_t* d_sh_ids = nullptr;
+    int sh_rows = 0;
+    int sh_max = 128, sh_flush = 32;
+    // pre-drawn edge-sample records (train_draw.hip) and per-phase timing
+    int32_t* d_rec = nullptr;
+    // DeepWalk pair records: per-walk pair counts, their exclusive scan, scan scratch
+    uint32_t* d_pcount = nullptr;
+    uint64_t* d_poff = nullptr;
+    size_t pair_walks = 0;
+    void* d_scan_tmp = nullptr;
+    size_t scan_tmp_bytes = 0;
+    // packed draw tables (train_draw.hip), rebuilt when the graph tables change
+    uint4* d_vt32 = nullptr;
+    uint4* d_ct16 = nullptr;
+    bool packed_ok = false;
+    size_t rec_cap = 0;                 // int32 words
+    std::vector<hipEvent_t> phase_ev;   // {before draw 0, after draw 0, after update 0, after draw 1, ...}
+    int phase_n = 0;                    // chunks of the last edge launch
+    // replica exchange over RCCL (exchange.cpp): snapshot S, own delta D and
+    // the all-reduced deltas R per table, a communicator and its stream
+    void* comm = nullptr;               // ncclComm_t
+    bool own_comm = false;              // created by smore_comm_init (destroyed with the context)
+    int nranks = 1, rank = 0;
+    hipStream_t comm_stream = nullptr;
+    hipEvent_t ex_ready = nullptr, ex_done = nullptr;
+    float* ex_buf[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};   // [table][S, D, R]
+    size_t ex_n = 0;                    // floats per exchanged table
+    int ex_tables = 0;
+    bool ex_pending = false;            // an all-reduce is in flight
+    int ex_mean = 0;
+};
+
+// exchange.cpp: frees the exchange buffers and the communicator
+void smore_exchange_release(smore_ctx* c);
+
+namespace smore_host {
+
+inline int fail(smore_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+#define HIPCHK(c, expr)                                                                     \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return fail((c), SMORE_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+template <class T>
+inline void dfree(T*& p) {
+    if (p) (void)hipFree((void*)p);
+    p = nullptr;
+}
+
+template <class T>
+int upload(smore_ctx* c, T*& d, const T* h, size_t n) {
+    dfree(d);
+    if (n == 0) n = 1;
+    HIPCHK(c, hipMalloc((void**)&d, n * sizeof(T)));
+    if (h) HIPCHK(c, hipMemcpy(d, h, n * sizeof(T), hipMemcpyHostToDevice));
+    return SMORE_OK;
+}
+
+inline int set_device(smore_ctx* c) {
+    if (c->device < 0) return fail(c, SMORE_ESTATE, "host-only context (device < 0) has no GPU state");
+    HIPCHK(c, hipSetDevice(c->device));
+    return SMORE_OK;
+}
+
+inline int upload_graph(smore_ctx* c) {
+    int rc;
+    if (c->device < 0) {
+        c->has_graph = true;
+        return SMORE_OK;
+    }
+    if ((rc = set_device(c))) return rc;
+    HostGraph& g = *c->g;
+    c->packed_ok = false;
+    dfree(c->d_vt32);
+    dfree(c->d_ct16);
+    if ((rc = upload(c, c->d_offsets, g.offsets.data(), g.offsets.size()))) return rc;
+    if ((rc = upload(c, c->d_targets, g.targets.data(), g.targets.size()))) return rc;
+    if ((rc = upload(c, c->d_vtab, g.vtab.data(), g.vtab.size()))) return rc;
+    if ((rc = upload(c, c->d_ntab, g.ntab.data(), g.ntab.size()))) return rc;
+    if ((rc = upload(c, c->d_ctab, g.ctab.data(), g.ctab.size()))) return rc;
+    // fastSigmoid table, 1001 entries (src/proNet.cpp:52-60; the reference
+    // sizes it 1000 and writes 1001 -- the build keeps all 1001)
+    std::vector<float> sig(1001);
+    for (int i = 0; i != 1000 + 1; i++) {
+        double x = i * 2.0 * 8.0 / 1000 - 8.0;
+        sig[i] = (float)(1.0 / (1.0 + std::exp(-x)));
+    }
+    if ((rc = upload(c, c->d_sig, sig.data(), sig.size()))) return rc;
+    c->has_graph = true;
+    return SMORE_OK;
+}
+
+inline DevGraph dev_graph(const smore_ctx* c) {
+    DevGraph d;
+    d.offsets = c->d_offsets;
+    d.targets = c->d_targets;
+    d.vtab = reinterpret_cast<const uint2*>(c->d_vtab);
+    d.ntab = reinterpret_cast<const uint2*>(c->d_ntab);
+    d.ctab = reinterpret_cast<const uint2*>(c->d_ctab);
+    d.vt32 = c->packed_ok ? c->d_vt32 : nullptr;
+    d.ct16 = c->packed_ok ? c->d_ct16 : nullptr;
+    d.V = (uint32_t)c->g->V;
+    return d;
+}
+
+inline float* table_ptr(smore_ctx* c, int which) {
+    if (which < 0 || which > 1) return nullptr;
+    return c->d_table[which];
+}
+
+}  // namespace smore_host

@@ -469,6 +469,7 @@ edge_train_kernel(EdgeArgs a) {
     __syncthreads();
 
     const int lane = threadIdx.x & (G - 1);
+    const uint64_t count = a.count_dev ? *a.count_dev : a.count;   // records of this launch
     const uint64_t gpb = blockDim.x / G;                 // groups per block
     uint64_t r0 = (uint64_t)blockIdx.x * gpb;            // block-uniform round base
     const uint64_t gib = threadIdx.x / G;
@@ -552,7 +553,7 @@ edge_train_kernel(EdgeArgs a) {
     if (a.mode == 2) {
         // serial: records in order, gather after the previous sample's scatter
         constexpr int RW = rec_width(KMAX);
-        for (; r0 < a.count; ++r0) {
+        for (; r0 < count; ++r0) {
             const i32x4* p = reinterpret_cast<const i32x4*>(a.rec + r0 * RW);
             i32x4 r[RW / 4];
 #pragma unroll
@@ -616,8 +617,8 @@ edge_train_kernel(EdgeArgs a) {
             __syncthreads();
             return s_next;
         };
-        for (uint64_t c0 = grab(); c0 < a.count; c0 = grab()) {
-            const uint64_t lim = c0 + span < a.count ? c0 + span : a.count;
+        for (uint64_t c0 = grab(); c0 < count; c0 = grab()) {
+            const uint64_t lim = c0 + span < count ? c0 + span : count;
             if constexpr (SHARED == 2) {
                 // BPR: no row prefetch (a second set of 7 rows would halve the
                 // resident waves); the next record is still loaded one round ahead

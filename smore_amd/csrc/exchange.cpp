@@ -1,0 +1,475 @@
+// exchange.cpp -- multi-GPU replicas over RCCL in the C ABI.
+//
+// The reference scales one training run over CPU threads sharing the tables
+// (LINE::Train's `#pragma omp parallel for` over workers, src/model/LINE.cpp:162;
+// Go goroutines, internal/models/line/line.go:96-146).  Here every GPU holds a
+// replica of the graph and of the tables, trains a disjoint range of global
+// sample indices, and the replicas exchange table deltas over RCCL (xGMI):
+//
+//   begin  (after a step, context stream):  D = T - S;  R = D;  S = T
+//          all-reduce R (SUM) on the exchange stream, overlapping the next step
+//   end    (before the next begin):         X = scale*R - D;  T += X;  S += X
+//          (end fused with the next begin: delta_cycle, replica_sync.hip)
+//
+// so every sample's update lands on every replica one exchange late, and the
+// next D is again only this replica's own updates.  Two ways to drive it:
+//   * one process per GPU: smore_comm_unique_id / smore_comm_init, then
+//     smore_exchange_reset / _begin / _end around the training calls;
+//   * one process, N GPUs: smore_group_* (ncclCommInitAll, one host thread
+//     enqueues every replica's work; the collectives of all replicas go out in
+//     one ncclGroupStart/End).
+// RCCL is loaded on first use (dlopen librccl.so.1): single-GPU users and the
+// host-only context never load it.
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+#include <mutex>
+
+#include "ctx.h"
+
+using namespace smore_host;
+
+namespace {
+
+struct Rccl {
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) init_rank = nullptr;
+    decltype(&ncclCommInitAll) init_all = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclBroadcast) broadcast = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+    std::string err;
+};
+
+Rccl* rccl() {
+    static Rccl r;
+    static bool ok = false;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            r.err = std::string("cannot load RCCL: ") + dlerror();
+            return;
+        }
+#define SMORE_SYM(field, name)                                          \
+    r.field = reinterpret_cast<decltype(r.field)>(dlsym(h, #name));     \
+    if (!r.field) {                                                     \
+        r.err = "RCCL lacks " #name;                                    \
+        return;                                                         \
+    }
+        SMORE_SYM(get_unique_id, ncclGetUniqueId)
+        SMORE_SYM(init_rank, ncclCommInitRank)
+        SMORE_SYM(init_all, ncclCommInitAll)
+        SMORE_SYM(destroy, ncclCommDestroy)
+        SMORE_SYM(all_reduce, ncclAllReduce)
+        SMORE_SYM(broadcast, ncclBroadcast)
+        SMORE_SYM(group_start, ncclGroupStart)
+        SMORE_SYM(group_end, ncclGroupEnd)
+        SMORE_SYM(error_string, ncclGetErrorString)
+#undef SMORE_SYM
+        ok = true;
+    });
+    return ok ? &r : nullptr;
+}
+
+int nccl_fail(smore_ctx* c, const char* what, ncclResult_t r) {
+    Rccl* L = rccl();
+    return fail(c, SMORE_EHIP, std::string(what) + ": " + (L ? L->error_string(r) : "RCCL unavailable"));
+}
+
+#define NCCLCHK(c, what, expr)                                   \
+    do {                                                         \
+        ncclResult_t r_ = (expr);                                \
+        if (r_ != ncclSuccess) return nccl_fail((c), what, r_);  \
+    } while (0)
+
+size_t table_floats(const smore_ctx* c) { return (size_t)c->g->V * (size_t)c->dpad; }
+
+// exchange buffers S, D, R per table and the exchange stream / events
+int ensure_exchange(smore_ctx* c) {
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    if (!c->comm_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+    if (!c->ex_ready) HIPCHK(c, hipEventCreateWithFlags(&c->ex_ready, hipEventDisableTiming));
+    if (!c->ex_done) HIPCHK(c, hipEventCreateWithFlags(&c->ex_done, hipEventDisableTiming));
+    const size_t n = table_floats(c);
+    if (c->ex_n == n && c->ex_tables == c->ntables) return SMORE_OK;
+    for (auto& t : c->ex_buf)
+        for (float*& p : t) dfree(p);
+    c->ex_n = 0;
+    c->ex_tables = 0;
+    c->ex_pending = false;
+    for (int t = 0; t < c->ntables; ++t)
+        for (float*& p : c->ex_buf[t]) HIPCHK(c, hipMalloc((void**)&p, std::max<size_t>(n, 4) * sizeof(float)));
+    c->ex_n = n;
+    c->ex_tables = c->ntables;
+    return SMORE_OK;
+}
+
+int check_comm(smore_ctx* c) {
+    if (!c) return SMORE_EINVAL;
+    if (!c->comm) return fail(c, SMORE_ESTATE, "no communicator (smore_comm_init / smore_group_create)");
+    if (c->ntables < 1 || !c->d_table[0]) return fail(c, SMORE_ESTATE, "tables not allocated");
+    return ensure_exchange(c);
+}
+
+// S = T for every table: the replicas start from identical tables
+int exchange_reset(smore_ctx* c) {
+    int rc;
+    if ((rc = check_comm(c))) return rc;
+    if (c->ex_pending) {
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ex_done, 0));
+        c->ex_pending = false;
+    }
+    for (int t = 0; t < c->ntables; ++t)
+        HIPCHK(c, hipMemcpyAsync(c->ex_buf[t][0], c->d_table[t], c->ex_n * sizeof(float), hipMemcpyDeviceToDevice,
+                                 c->stream));
+    return SMORE_OK;
+}
+
+// the fused passes of an exchange's begin on the context stream (folding the
+// in-flight exchange in first), then the hand-off event for the collective
+int exchange_passes(smore_ctx* c, int mean) {
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    const float scale_prev = c->ex_mean ? 1.0f / (float)c->nranks : 1.0f;
+    if (c->ex_pending) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ex_done, 0));
+    for (int t = 0; t < c->ntables; ++t) {
+        float* T = c->d_table[t];
+        float* const* b = c->ex_buf[t];
+        if (c->ex_pending) HIPCHK(c, launch_delta_cycle(T, b[0], b[1], b[2], scale_prev, c->ex_n, c->cus, c->stream));
+        else HIPCHK(c, launch_delta_begin(T, b[0], b[1], b[2], c->ex_n, c->cus, c->stream));
+    }
+    HIPCHK(c, hipEventRecord(c->ex_ready, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->ex_ready, 0));
+    c->ex_mean = mean;
+    return SMORE_OK;
+}
+
+int exchange_collective(smore_ctx* c) {
+    Rccl* L = rccl();
+    for (int t = 0; t < c->ntables; ++t)
+        NCCLCHK(c, "ncclAllReduce",
+                L->all_reduce(c->ex_buf[t][2], c->ex_buf[t][2], c->ex_n, ncclFloat32, ncclSum, (ncclComm_t)c->comm,
+                              c->comm_stream));
+    return SMORE_OK;
+}
+
+int exchange_posted(smore_ctx* c) {
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    HIPCHK(c, hipEventRecord(c->ex_done, c->comm_stream));
+    c->ex_pending = true;
+    return SMORE_OK;
+}
+
+int exchange_end(smore_ctx* c) {
+    int rc;
+    if ((rc = check_comm(c))) return rc;
+    if (!c->ex_pending) return SMORE_OK;
+    const float scale = c->ex_mean ? 1.0f / (float)c->nranks : 1.0f;
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ex_done, 0));
+    for (int t = 0; t < c->ntables; ++t) {
+        float* const* b = c->ex_buf[t];
+        HIPCHK(c, launch_delta_end(c->d_table[t], b[0], b[1], b[2], scale, c->ex_n, c->cus, c->stream));
+    }
+    c->ex_pending = false;
+    return SMORE_OK;
+}
+
+}  // namespace
+
+void smore_exchange_release(smore_ctx* c) {
+    if (!c) return;
+    if (c->device >= 0) (void)hipSetDevice(c->device);
+    if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
+    for (auto& t : c->ex_buf)
+        for (float*& p : t) dfree(p);
+    if (c->comm && c->own_comm) {
+        if (Rccl* L = rccl()) (void)L->destroy((ncclComm_t)c->comm);
+    }
+    c->comm = nullptr;
+    if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
+    if (c->ex_ready) (void)hipEventDestroy(c->ex_ready);
+    if (c->ex_done) (void)hipEventDestroy(c->ex_done);
+    c->comm_stream = nullptr;
+    c->ex_ready = c->ex_done = nullptr;
+}
+
+struct smore_group {
+    std::vector<smore_ctx*> ctx;
+    std::vector<ncclComm_t> comms;
+    std::string err;
+};
+
+namespace {
+
+int gfail(smore_group* g, int rank, int rc) {
+    if (g && rc != SMORE_OK && rank >= 0) g->err = "replica " + std::to_string(rank) + ": " + g->ctx[rank]->err;
+    return rc;
+}
+
+// every replica adopts replica 0's (shared) host graph and uploads it
+int replicate_graph(smore_group* g) {
+    smore_ctx* c0 = g->ctx[0];
+    for (size_t r = 1; r < g->ctx.size(); ++r) {
+        smore_ctx* c = g->ctx[r];
+        c->g = c0->g;
+        c->hot_key.clear();
+        c->semantics = SMORE_SEM_CPP;
+        int rc = upload_graph(c);
+        if (rc) return gfail(g, (int)r, rc);
+    }
+    return SMORE_OK;
+}
+
+int group_exchange_begin(smore_group* g, int mean) {
+    int rc;
+    for (size_t r = 0; r < g->ctx.size(); ++r)
+        if ((rc = exchange_passes(g->ctx[r], mean))) return gfail(g, (int)r, rc);
+    Rccl* L = rccl();
+    ncclResult_t nr = L->group_start();
+    for (size_t r = 0; r < g->ctx.size() && nr == ncclSuccess; ++r) {
+        (void)hipSetDevice(g->ctx[r]->device);
+        if ((rc = exchange_collective(g->ctx[r]))) {
+            (void)L->group_end();
+            return gfail(g, (int)r, rc);
+        }
+    }
+    if (nr == ncclSuccess) nr = L->group_end();
+    if (nr != ncclSuccess) return gfail(g, 0, nccl_fail(g->ctx[0], "ncclGroupEnd", nr));
+    for (size_t r = 0; r < g->ctx.size(); ++r)
+        if ((rc = exchange_posted(g->ctx[r]))) return gfail(g, (int)r, rc);
+    return SMORE_OK;
+}
+
+int group_sync(smore_group* g) {
+    int rc;
+    for (size_t r = 0; r < g->ctx.size(); ++r)
+        if ((rc = smore_synchronize(g->ctx[r]))) return gfail(g, (int)r, rc);
+    return SMORE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int smore_comm_unique_id(unsigned char* id) {
+    if (!id) return SMORE_EINVAL;
+    Rccl* L = rccl();
+    if (!L) return SMORE_EHIP;
+    ncclUniqueId u;
+    if (L->get_unique_id(&u) != ncclSuccess) return SMORE_EHIP;
+    memcpy(id, u.internal, SMORE_COMM_ID_BYTES);
+    return SMORE_OK;
+}
+
+int smore_comm_init(smore_ctx* c, int nranks, int rank, const unsigned char* id) {
+    if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return SMORE_EINVAL;
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    Rccl* L = rccl();
+    if (!L) return fail(c, SMORE_EHIP, "RCCL unavailable");
+    if (c->comm) return fail(c, SMORE_ESTATE, "context already has a communicator");
+    ncclUniqueId u;
+    memcpy(u.internal, id, SMORE_COMM_ID_BYTES);
+    ncclComm_t comm = nullptr;
+    NCCLCHK(c, "ncclCommInitRank", L->init_rank(&comm, nranks, u, rank));
+    c->comm = comm;
+    c->own_comm = true;
+    c->nranks = nranks;
+    c->rank = rank;
+    return SMORE_OK;
+}
+
+int smore_exchange_reset(smore_ctx* c) { return exchange_reset(c); }
+
+int smore_exchange_begin(smore_ctx* c, int mean) {
+    int rc;
+    if ((rc = check_comm(c))) return rc;
+    if ((rc = exchange_passes(c, mean != 0))) return rc;
+    if ((rc = exchange_collective(c))) return rc;
+    return exchange_posted(c);
+}
+
+int smore_exchange_end(smore_ctx* c) { return exchange_end(c); }
+
+// ---------------------------------------------------------------- one process, N GPUs
+int smore_group_create(const int* devices, int n, smore_group** out) {
+    if (!out || !devices || n < 1 || n > 64) return SMORE_EINVAL;
+    *out = nullptr;
+    smore_group* g = new smore_group();
+    for (int r = 0; r < n; ++r) {
+        smore_ctx* c = nullptr;
+        const int rc = smore_create(devices[r], &c);
+        if (rc) {
+            smore_group_destroy(g);
+            return rc;
+        }
+        g->ctx.push_back(c);
+    }
+    if (n > 1) {
+        Rccl* L = rccl();
+        if (!L) {
+            smore_group_destroy(g);
+            return SMORE_EHIP;
+        }
+        g->comms.assign((size_t)n, nullptr);
+        if (L->init_all(g->comms.data(), n, devices) != ncclSuccess) {
+            g->comms.clear();
+            smore_group_destroy(g);
+            return SMORE_EHIP;
+        }
+        for (int r = 0; r < n; ++r) {
+            g->ctx[r]->comm = g->comms[r];
+            g->ctx[r]->own_comm = false;
+            g->ctx[r]->nranks = n;
+            g->ctx[r]->rank = r;
+        }
+    }
+    *out = g;
+    return SMORE_OK;
+}
+
+void smore_group_destroy(smore_group* g) {
+    if (!g) return;
+    for (smore_ctx* c : g->ctx) {
+        smore_exchange_release(c);
+        smore_destroy(c);
+    }
+    if (Rccl* L = g->comms.empty() ? nullptr : rccl())
+        for (ncclComm_t cm : g->comms)
+            if (cm) (void)L->destroy(cm);
+    delete g;
+}
+
+int smore_group_size(const smore_group* g) { return g ? (int)g->ctx.size() : 0; }
+
+smore_ctx* smore_group_ctx(smore_group* g, int rank) {
+    if (!g || rank < 0 || rank >= (int)g->ctx.size()) return nullptr;
+    return g->ctx[rank];
+}
+
+const char* smore_group_last_error(const smore_group* g) { return g ? g->err.c_str() : "null group"; }
+
+int smore_group_load_edgelist(smore_group* g, const char* path, int undirected, int vm, int nm) {
+    if (!g) return SMORE_EINVAL;
+    int rc = smore_load_edgelist(g->ctx[0], path, undirected, vm, nm);
+    if (rc) return gfail(g, 0, rc);
+    return replicate_graph(g);
+}
+
+int smore_group_set_graph_edges(smore_group* g, int64_t V, int64_t E, const int32_t* src, const int32_t* dst,
+                                const double* w, int vm, int nm) {
+    if (!g) return SMORE_EINVAL;
+    int rc = smore_set_graph_edges(g->ctx[0], V, E, src, dst, w, vm, nm);
+    if (rc) return gfail(g, 0, rc);
+    return replicate_graph(g);
+}
+
+int smore_group_set_semantics(smore_group* g, int semantics) {
+    if (!g) return SMORE_EINVAL;
+    for (size_t r = 0; r < g->ctx.size(); ++r) {
+        // the host tables are shared: replica 0 rebuilds them, the builders are
+        // idempotent, every replica uploads its own device copy
+        int rc = smore_set_semantics(g->ctx[r], semantics);
+        if (rc) return gfail(g, (int)r, rc);
+    }
+    return SMORE_OK;
+}
+
+int smore_group_alloc_tables(smore_group* g, int dim, int ntables) {
+    if (!g) return SMORE_EINVAL;
+    for (size_t r = 0; r < g->ctx.size(); ++r) {
+        int rc = smore_alloc_tables(g->ctx[r], dim, ntables);
+        if (rc) return gfail(g, (int)r, rc);
+    }
+    return SMORE_OK;
+}
+
+int smore_group_broadcast_tables(smore_group* g) {
+    if (!g) return SMORE_EINVAL;
+    if (g->ctx.size() == 1) return SMORE_OK;
+    int rc;
+    for (size_t r = 0; r < g->ctx.size(); ++r) {
+        smore_ctx* c = g->ctx[r];
+        if (c->ntables < 1 || !c->d_table[0]) return gfail(g, (int)r, fail(c, SMORE_ESTATE, "tables not allocated"));
+        if ((rc = smore_synchronize(c))) return gfail(g, (int)r, rc);
+    }
+    Rccl* L = rccl();
+    const size_t n = table_floats(g->ctx[0]);
+    for (int t = 0; t < g->ctx[0]->ntables; ++t) {
+        ncclResult_t nr = L->group_start();
+        for (size_t r = 0; r < g->ctx.size() && nr == ncclSuccess; ++r) {
+            smore_ctx* c = g->ctx[r];
+            (void)hipSetDevice(c->device);
+            nr = L->broadcast(c->d_table[t], c->d_table[t], n, ncclFloat32, 0, (ncclComm_t)c->comm, c->stream);
+        }
+        ncclResult_t ne = L->group_end();
+        if (nr == ncclSuccess) nr = ne;
+        if (nr != ncclSuccess) return gfail(g, 0, nccl_fail(g->ctx[0], "ncclBroadcast", nr));
+    }
+    return group_sync(g);
+}
+
+int smore_group_train_edges(smore_group* g, int model, uint64_t begin, uint64_t count, uint64_t total, int K,
+                            double alpha0, double reg, uint64_t seed, int mode, uint64_t sync_samples, int mean) {
+    if (!g) return SMORE_EINVAL;
+    const size_t n = g->ctx.size();
+    int rc;
+    if (n == 1) return gfail(g, 0, smore_train_edges(g->ctx[0], model, begin, count, total, K, alpha0, reg, seed, mode));
+    if (count == 0) return SMORE_OK;
+    const uint64_t per = sync_samples ? sync_samples : (uint64_t)1 << 27;
+    for (size_t r = 0; r < n; ++r)
+        if ((rc = exchange_reset(g->ctx[r]))) return gfail(g, (int)r, rc);
+    // round k: replica r runs [begin + (k n + r) per, + per) of the global range
+    for (uint64_t base = 0; base < count; base += per * n) {
+        for (size_t r = 0; r < n; ++r) {
+            const uint64_t b = base + r * per;
+            if (b >= count) break;
+            const uint64_t m = std::min<uint64_t>(per, count - b);
+            rc = smore_train_edges_async(g->ctx[r], model, begin + b, m, total, K, alpha0, reg, seed, mode);
+            if (rc) return gfail(g, (int)r, rc);
+        }
+        if ((rc = group_exchange_begin(g, mean))) return rc;
+    }
+    for (size_t r = 0; r < n; ++r)
+        if ((rc = exchange_end(g->ctx[r]))) return gfail(g, (int)r, rc);
+    return group_sync(g);
+}
+
+int smore_group_train_deepwalk(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
+                               int walk_steps, int window, int K, double alpha0, uint64_t seed, const int64_t* order,
+                               int mode, uint64_t sync_walks, int mean) {
+    if (!g) return SMORE_EINVAL;
+    const size_t n = g->ctx.size();
+    int rc;
+    if (n == 1)
+        return gfail(g, 0, smore_train_deepwalk(g->ctx[0], walk_begin, walk_end, walk_times, walk_steps, window, K,
+                                                alpha0, seed, order, mode));
+    if (walk_end <= walk_begin) return SMORE_OK;
+    const uint64_t per = sync_walks ? sync_walks : (uint64_t)1 << 18;
+    for (size_t r = 0; r < n; ++r)
+        if ((rc = exchange_reset(g->ctx[r]))) return gfail(g, (int)r, rc);
+    const uint64_t count = walk_end - walk_begin;
+    for (uint64_t base = 0; base < count; base += per * n) {
+        for (size_t r = 0; r < n; ++r) {
+            const uint64_t b = base + r * per;
+            if (b >= count) break;
+            const uint64_t m = std::min<uint64_t>(per, count - b);
+            rc = smore_train_deepwalk_async(g->ctx[r], walk_begin + b, walk_begin + b + m, walk_times, walk_steps,
+                                            window, K, alpha0, seed, order, mode);
+            if (rc) return gfail(g, (int)r, rc);
+        }
+        if ((rc = group_exchange_begin(g, mean))) return rc;
+    }
+    for (size_t r = 0; r < n; ++r)
+        if ((rc = exchange_end(g->ctx[r]))) return gfail(g, (int)r, rc);
+    return group_sync(g);
+}
+
+}  // extern "C"

@@ -278,7 +278,7 @@ __global__ void go_walk_gen_kernel(DevGraph g, const double* tcum, WalkArgs w, u
     const uint64_t unit = w.walk_begin + t;
     int32_t* out = w.walks + t * (uint64_t)(w.steps + 1);
     int L = 0;
-    int32_t cur = (int32_t)w.order[unit];
+    int32_t cur = (int32_t)w.order[unit - w.order_base];
     out[L++] = cur;
     uint4 b = make_uint4(0, 0, 0, 0);
     for (int s = 0; s < w.steps; ++s) {

@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "device_common.h"
 
 namespace smore {
@@ -22,6 +24,7 @@ struct EdgeArgs {
     // edge kernels: the pre-drawn sample records of samples [begin, begin+count)
     // (draw_kernel), rec_width(KMAX) int32 each
     const int32_t* rec;
+    const uint64_t* count_dev;     // non-null: the record count is read here (device-side pair totals)
     unsigned long long* work;      // Hogwild edge kernels: chunk counter, zeroed per launch
     int alpha_rec;                 // 1: learning rate in record word 2 + KMAX (DeepWalk pairs)
     uint64_t begin, count, total, seed;
@@ -32,8 +35,9 @@ struct EdgeArgs {
 
 // DeepWalk: a chunk of walks [walk_begin, walk_begin + nwalks)
 struct WalkArgs {
-    const int64_t* order;          // walk start vertices, all walk_times * V
-    int32_t* walks;                // nwalks x (steps + 1)
+    const int64_t* order;          // walk start vertices of walks [order_base, ...) (a slice of the full order)
+    uint64_t order_base;
+    int32_t* walks;                // nwalks x (steps + 1); C++ walks hold id | hc << 30 | hw << 31
     int32_t* lens;                 // nwalks
     uint64_t walk_begin, nwalks, total_walks;
     int steps, window;
@@ -60,6 +64,11 @@ hipError_t launch_delta_end(float* T, float* S, const float* D, const float* R, 
 hipError_t launch_delta_cycle(float* T, float* S, float* D, float* R, float scale, uint64_t n, int cus,
                               hipStream_t st);
 hipError_t launch_pair_count(const WalkArgs& w, uint64_t seed, uint32_t* count, hipStream_t st);
+// upper bound on the skip-gram pairs of one walk of `steps` steps (window shrink >= 1)
+inline uint64_t pair_bound(int steps, int window) {
+    const uint64_t L = (uint64_t)steps + 1, r = std::min<uint64_t>(2 * (uint64_t)window, L - 1);
+    return L * r;
+}
 hipError_t scan_pair_counts(const uint32_t* count, uint64_t* off, uint64_t n, void** temp, size_t* temp_bytes,
                             hipStream_t st);
 hipError_t launch_pair_emit(const DevGraph& g, const WalkArgs& w, uint64_t seed, int K, double alpha0,

@@ -68,8 +68,9 @@ __global__ void __launch_bounds__(256) pair_emit_kernel(DevGraph g, WalkArgs w, 
         for (int j = left; j <= right; ++j) {
             if (j == i) continue;
             int32_t x[RW];
-            x[0] = vi;
-            x[1] = walk[j];
+            // W row walk[i] with its W tag, C row walk[j] with its C tag
+            x[0] = (vi & ID_MASK) | (int32_t)((((uint32_t)vi >> 31) & 1u) << 30);
+            x[1] = walk[j] & (ID_MASK | (1 << 30));
 #pragma unroll
             for (int n = 0; n < RW - 2; ++n) x[2 + n] = -1;
 #pragma unroll

@@ -18,11 +18,15 @@ class ProNet:
 
     device=-1 gives a host-only context (graph and alias building, no GPU)."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, _ctx=None):
         self.ctx = C.c_void_p()
-        rc = lib.smore_create(int(device), C.byref(self.ctx))
-        if rc != _lib.OK:
-            raise _lib.SmoreError("smore_create(device=%d) failed with status %d" % (device, rc))
+        self._owned = _ctx is None
+        if _ctx is not None:          # a replica of a Group (owned by the group)
+            self.ctx = C.c_void_p(_ctx)
+        else:
+            rc = lib.smore_create(int(device), C.byref(self.ctx))
+            if rc != _lib.OK:
+                raise _lib.SmoreError("smore_create(device=%d) failed with status %d" % (device, rc))
         self.device = device
         self.vertex_method = "out_degrees"    # src/proNet.cpp:9
         self.negative_method = "degrees"      # src/proNet.cpp:11
@@ -30,9 +34,9 @@ class ProNet:
 
     # ---------------------------------------------------------------- lifecycle
     def close(self):
-        if self.ctx:
+        if self.ctx and self._owned:
             lib.smore_destroy(self.ctx)
-            self.ctx = C.c_void_p()
+        self.ctx = C.c_void_p()
 
     def __del__(self):
         try:
@@ -218,6 +222,24 @@ class ProNet:
         """delta_end then delta_begin in one pass."""
         self._chk(lib.smore_delta_cycle(self.ctx, T, S, D, R, float(scale), int(n)), "delta_cycle")
 
+    # ---------------------------------------------------------------- replica exchange (RCCL, in the library)
+    def comm_init(self, nranks, rank, uid):
+        """Join an RCCL communicator (uid: bytes of comm_unique_id() from rank 0)."""
+        buf = (C.c_ubyte * COMM_ID_BYTES).from_buffer_copy(bytes(uid))
+        self._chk(lib.smore_comm_init(self.ctx, int(nranks), int(rank), buf), "comm_init")
+
+    def exchange_reset(self):
+        """S = T: the replicas start from identical tables."""
+        self._chk(lib.smore_exchange_reset(self.ctx), "exchange_reset")
+
+    def exchange_begin(self, mean=False):
+        """After a step: fold the in-flight exchange in, snapshot this rank's
+        delta and start its all-reduce (overlaps the next step)."""
+        self._chk(lib.smore_exchange_begin(self.ctx, int(bool(mean))), "exchange_begin")
+
+    def exchange_end(self):
+        self._chk(lib.smore_exchange_end(self.ctx), "exchange_end")
+
     def last_phase_ms(self):
         """(exposed draw ms, update ms, update launches) of the last LINE/MF
         edge call, or None."""
@@ -233,6 +255,89 @@ class ProNet:
 
     def save_weights(self, which, path, fmt=0):
         self._chk(lib.smore_save_weights(self.ctx, which, path.encode(), int(fmt)), "save_weights")
+
+
+COMM_ID_BYTES = 128
+
+
+def comm_unique_id():
+    """An RCCL unique id (bytes) for ProNet.comm_init on every rank."""
+    buf = (C.c_ubyte * COMM_ID_BYTES)()
+    if lib.smore_comm_unique_id(buf) != _lib.OK:
+        raise _lib.SmoreError("comm_unique_id failed (RCCL unavailable?)")
+    return bytes(buf)
+
+
+class Group:
+    """One process driving N GPUs (smore_group_*): replica 0 (`primary`, a
+    ProNet view) loads, initialises and saves; broadcast_tables() copies its
+    tables to every replica; training calls split the global range over the
+    replicas and return with every replica holding every update."""
+
+    def __init__(self, devices):
+        devs = (C.c_int * len(devices))(*[int(d) for d in devices])
+        self.g = C.c_void_p()
+        rc = lib.smore_group_create(devs, len(devices), C.byref(self.g))
+        if rc != _lib.OK:
+            raise _lib.SmoreError("smore_group_create(%s) failed with status %d" % (list(devices), rc))
+        self.replicas = [ProNet(devices[r], _ctx=lib.smore_group_ctx(self.g, r)) for r in range(len(devices))]
+        self.primary = self.replicas[0]
+
+    def close(self):
+        if self.g:
+            for r in self.replicas:
+                r.ctx = C.c_void_p()
+            lib.smore_group_destroy(self.g)
+            self.g = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc, what):
+        if rc != _lib.OK:
+            raise _lib.SmoreError("%s failed (status %d): %s" % (what, rc, lib.smore_group_last_error(self.g).decode()))
+
+    def __len__(self):
+        return int(lib.smore_group_size(self.g))
+
+    def LoadEdgeList(self, filename, undirect, vertex_method="out_degrees", negative_method="degrees"):
+        self._chk(lib.smore_group_load_edgelist(self.g, filename.encode(), int(bool(undirect)),
+                                                _lib.VM[vertex_method], _lib.NM[negative_method]), "LoadEdgeList")
+
+    def set_graph_edges(self, V, src, dst, w, vertex_method="out_degrees", negative_method="degrees"):
+        src = np.ascontiguousarray(src, np.int32)
+        dst = np.ascontiguousarray(dst, np.int32)
+        w = np.ascontiguousarray(w, np.float64)
+        self._chk(lib.smore_group_set_graph_edges(self.g, int(V), len(src), ptr(src), ptr(dst), ptr(w),
+                                                  _lib.VM[vertex_method], _lib.NM[negative_method]),
+                  "set_graph_edges")
+
+    def set_semantics(self, semantics):
+        self._chk(lib.smore_group_set_semantics(self.g, _lib.SEM[semantics]), "set_semantics")
+
+    def alloc_tables(self, dim, ntables):
+        self._chk(lib.smore_group_alloc_tables(self.g, int(dim), int(ntables)), "alloc_tables")
+        for r in self.replicas:
+            r.dim = dim
+
+    def broadcast_tables(self):
+        self._chk(lib.smore_group_broadcast_tables(self.g), "broadcast_tables")
+
+    def train_edges(self, model, begin, count, total, K, alpha0, reg=0.0, seed=1, mode="hybrid", per=0, mean=False):
+        self._chk(lib.smore_group_train_edges(self.g, _lib.MODEL[model], int(begin), int(count), int(total), int(K),
+                                              float(alpha0), float(reg), int(seed), _lib.MODE[mode], int(per),
+                                              int(bool(mean))), "train_edges")
+
+    def train_deepwalk(self, walk_begin, walk_end, walk_times, walk_steps, window, K, alpha0, seed, order,
+                       mode="hybrid", per=0, mean=False):
+        order = np.ascontiguousarray(order, np.int64)
+        self._chk(lib.smore_group_train_deepwalk(self.g, int(walk_begin), int(walk_end), int(walk_times),
+                                                 int(walk_steps), int(window), int(K), float(alpha0), int(seed),
+                                                 ptr(order), _lib.MODE[mode], int(per), int(bool(mean))),
+                  "train_deepwalk")
 
 
 def deepwalk_order(V, walk_times, skip):

@@ -1,0 +1,49 @@
+"""One rank of the multi-process replica test (tests/test_gpu_multi.py): LINE-2
+on the 1k-vertex golden graph on cuda:0, the table deltas exchanged through
+smore_amd/dist.py ReplicaSync (the fused HIP passes of replica_sync.hip around a
+torch.distributed all-reduce; gloo here, since every rank shares one GPU).
+TEST INFRASTRUCTURE.
+
+    python tests/helpers/replica_worker.py RANK WORLD PORT TOTAL STEPS OUT.npz
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    rank, world, port, total, steps = (int(x) for x in sys.argv[1:6])
+    out = sys.argv[6]
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    if world > 1:
+        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    import smore_amd
+    from smore_amd.dist import ReplicaSync
+    pn = smore_amd.ProNet(0)
+    pn.LoadEdgeList(os.path.join(ROOT, "tests", "golden", "pl1k.txt"), 1)
+    pn.alloc_tables(32, 2)
+    pn.init_table_glibc(0, 0)
+    pn.zero_table(1)
+    sync = ReplicaSync(pn) if world > 1 else None
+    per = total // world // steps
+    for k in range(steps):
+        begin = (k * world + rank) * per
+        pn.train_edges("line2", begin, per, total, 5, 0.025, 0.0, 20251015, "atomic", sync=False)
+        if sync is not None:
+            sync.begin()
+    if sync is not None:
+        sync.end()
+    torch.cuda.synchronize()
+    np.savez(out, W=pn.get_table(0), C=pn.get_table(1))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,112 @@
+"""The Go drop-in's call sequence through the C ABI (go/pkg/pronet/hip.go,
+replayed by the C program tests/c/go_shape.c, since this image has no Go
+toolchain): adjacency of pn.Graph in vertex order -> smore_group_set_graph_edges,
+Go semantics, pn.NegativeAT injected, fp64 tables flattened to fp32, chunked
+training with total = sample_times * MaxLine, tables copied back.  In serial
+mode the result is bit-exact with the oracle's Go-rule fp32 spec
+(orc_go_*_f32; parity against Go itself is unpinned: no Go toolchain).
+Needs an MI355X."""
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from tests.conftest import GOLDEN, ROOT
+
+pytestmark = pytest.mark.gpu
+
+BIN = os.path.join(ROOT, "tests", "c", "go_shape")
+SEED = 4242
+SERIAL, ATOMIC = 2, 1
+MODEL = {"line2": 0, "line1": 1, "bpr": 3, "deepwalk": -1}
+
+
+def _shim_inputs(g):
+    """What NewHIP flattens: the directed slots of pn.Graph in vertex order."""
+    src = np.repeat(np.arange(g.V, dtype=np.int32), np.diff(g.offsets)).astype(np.int32)
+    dst = g.targets[:g.E].astype(np.int32)
+    w = g.weights[:g.E].astype(np.float64)
+    return src, dst, w
+
+
+def _run(tmp_path, g, model, dim, K, total, mode, alpha, lam, W0, C0, walk=None):
+    src, dst, w = _shim_inputs(g)
+    p_in, p_out = str(tmp_path / "in.bin"), str(tmp_path / "out.bin")
+    with open(p_in, "wb") as f:
+        f.write(struct.pack("<8q", g.V, g.E, dim, MODEL[model], K, total, 1, mode))
+        f.write(struct.pack("<2dQ", alpha, lam, SEED))
+        for a in (src, dst, w, g.nprob.astype(np.float64), g.nalias.astype(np.int64),
+                  W0.astype(np.float64), C0.astype(np.float64)):
+            f.write(np.ascontiguousarray(a).tobytes())
+        if walk is not None:
+            times, steps, window, order = walk
+            f.write(struct.pack("<4q", times, steps, window, len(order)))
+            f.write(np.ascontiguousarray(order, np.int64).tobytes())
+    r = subprocess.run([BIN, p_in, p_out], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = np.fromfile(p_out, np.float64).reshape(2, g.V, dim)
+    return out[0], out[1]
+
+
+def _tables(V, dim, seed):
+    rng = np.random.default_rng(seed)
+    return [(rng.random((V, dim), dtype=np.float32) - 0.5) for _ in range(2)]
+
+
+def _padded(T, dim):
+    out = np.zeros((T.shape[0], (dim + 3) // 4 * 4), np.float32)
+    out[:, :dim] = T
+    return out
+
+
+def test_go_shape_binary_built():
+    assert os.access(BIN, os.X_OK), "build it with `make goshape`"
+
+
+@pytest.mark.parametrize("model,fname,und,dim,K,lam", [("line2", "pl100w.txt", 1, 64, 5, 0.0),
+                                                       ("line1", "pl100w.txt", 1, 20, 5, 0.0),
+                                                       ("bpr", "bip.txt", 0, 16, 1, 0.001)])
+def test_go_shim_sequence_serial_bit_exact(tmp_path, model, fname, und, dim, K, lam):
+    g = orc.GoGraph.from_file(os.path.join(GOLDEN, fname), und)
+    max_line = g.E // 2 if und else g.E            # Go's MaxLine counts input lines
+    total = 3 * max_line                           # sample_times = 3
+    W0, C0 = _tables(g.V, dim, dim + K)
+    W, C = _run(tmp_path, g, model, dim, K, total, SERIAL, 0.025, lam, W0, C0)
+    Wr, Cr = _padded(W0, dim), _padded(C0, dim)
+    orc.go_train_f32(g, model, Wr, Cr, dim, K, 0.025, lam, total, 0, total, SEED)
+    np.testing.assert_array_equal(W.astype(np.float32), Wr[:, :dim])
+    if model != "line1":
+        np.testing.assert_array_equal(C.astype(np.float32), Cr[:, :dim])
+
+
+def test_go_shim_deepwalk_serial_bit_exact(tmp_path):
+    g = orc.GoGraph.from_file(os.path.join(GOLDEN, "pl100w.txt"), 1)
+    dim, K, times, steps, window = 32, 5, 2, 10, 3
+    order = np.concatenate([np.random.default_rng(t).permutation(g.V) for t in range(times)]).astype(np.int64)
+    W0, C0 = _tables(g.V, dim, 9)
+    W, C = _run(tmp_path, g, "deepwalk", dim, K, 0, SERIAL, 0.025, 0.0, W0, C0, (times, steps, window, order))
+    Wr, Cr = _padded(W0, dim), _padded(C0, dim)
+    orc.go_deepwalk_f32(g, Wr, Cr, dim, times, steps, window, K, 0.025, SEED, order)
+    np.testing.assert_array_equal(W.astype(np.float32), Wr[:, :dim])
+    np.testing.assert_array_equal(C.astype(np.float32), Cr[:, :dim])
+
+
+def test_go_shim_atomic_trains(tmp_path):
+    """The shim's default scatter (atomic) on the 1k-vertex graph: finite, and
+    positive edges score above random pairs."""
+    g = orc.GoGraph.from_file(os.path.join(GOLDEN, "pl1k.txt"), 1)
+    dim = 32
+    W0, C0 = _tables(g.V, dim, 3)
+    W0 /= dim
+    C0 /= dim
+    W, C = _run(tmp_path, g, "line2", dim, 5, 200 * (g.E // 2), ATOMIC, 0.025, 0.0, W0, C0)
+    assert np.isfinite(W).all() and np.isfinite(C).all()
+    rng = np.random.default_rng(0)
+    src = np.repeat(np.arange(g.V), np.diff(g.offsets))
+    pick = rng.integers(0, g.E, 5000)
+    pos = np.einsum("ij,ij->i", W[src[pick]], C[g.targets[pick]])
+    neg = np.einsum("ij,ij->i", W[rng.integers(0, g.V, 5000)], C[rng.integers(0, g.V, 5000)])
+    assert (pos[:, None] > neg[None, :1000]).mean() > 0.75

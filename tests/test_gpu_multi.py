@@ -1,0 +1,121 @@
+"""Multi-GPU replica exchange on one MI355X:
+  * the library's own RCCL path (smore_comm_init / smore_exchange_*,
+    exchange.cpp) at world size 1, where every exchange must add exactly zero;
+  * a 1-replica smore_group_* run equals the single-context run;
+  * two processes sharing the GPU, exchanging deltas through the fused HIP
+    passes (replica_sync.hip) around a gloo all-reduce: the replicas agree
+    within float rounding, and the held-out LINE-2 loss at equal total samples
+    is within 1 % of one process.
+The 2..8-GPU RCCL runs are the driver's (bench.py under torchrun)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from tests.conftest import GOLDEN, ROOT
+
+pytestmark = pytest.mark.gpu
+SEED = 20251015
+PL1K = os.path.join(GOLDEN, "pl1k.txt")
+
+
+@pytest.fixture(scope="module")
+def smore():
+    import smore_amd
+    return smore_amd
+
+
+def _fresh(smore):
+    pn = smore.ProNet(0)
+    pn.LoadEdgeList(PL1K, 1)
+    pn.alloc_tables(64, 2)
+    pn.init_table_glibc(0, 0)
+    pn.zero_table(1)
+    return pn
+
+
+def test_capi_rccl_world1_exchange_adds_zero(smore):
+    total, n = 10 ** 6, 20000
+    ref = _fresh(smore)
+    for k in range(3):
+        ref.train_edges("line2", k * n, n, total, 5, 0.025, 0.0, SEED, "serial")
+    pn = _fresh(smore)
+    pn.comm_init(1, 0, smore.comm_unique_id())
+    pn.exchange_reset()
+    before = pn.get_table(0)
+    pn.exchange_begin()
+    pn.exchange_end()
+    np.testing.assert_array_equal(pn.get_table(0), before)
+    for k in range(3):      # begin after every step: the 2nd and 3rd fold the previous one in (delta_cycle)
+        pn.train_edges("line2", k * n, n, total, 5, 0.025, 0.0, SEED, "serial", sync=False)
+        pn.exchange_begin()
+    pn.exchange_end()
+    pn.synchronize()
+    np.testing.assert_array_equal(pn.get_table(0), ref.get_table(0))
+    np.testing.assert_array_equal(pn.get_table(1), ref.get_table(1))
+
+
+def test_group_of_one_equals_single_context(smore):
+    total, n = 10 ** 6, 30000
+    ref = _fresh(smore)
+    ref.train_edges("line2", 100, n, total, 5, 0.025, 0.0, SEED, "serial")
+    g = smore.Group([0])
+    assert len(g) == 1
+    g.LoadEdgeList(PL1K, 1)
+    g.alloc_tables(64, 2)
+    g.primary.init_table_glibc(0, 0)
+    g.primary.zero_table(1)
+    g.broadcast_tables()
+    g.train_edges("line2", 100, n, total, 5, 0.025, 0.0, SEED, "serial")
+    np.testing.assert_array_equal(g.primary.get_table(0), ref.get_table(0))
+    np.testing.assert_array_equal(g.primary.get_table(1), ref.get_table(1))
+    order = smore.deepwalk_order(ref.MAX_vid, 1, 0)
+    ref.train_deepwalk(0, 300, 1, 10, 3, 2, 0.025, SEED, order, "serial")
+    g.train_deepwalk(0, 300, 1, 10, 3, 2, 0.025, SEED, order, "serial")
+    np.testing.assert_array_equal(g.primary.get_table(0), ref.get_table(0))
+    g.close()
+
+
+def _heldout_loss(W, C, draws):
+    v, c, negs = draws[:, 0], draws[:, 1], draws[:, 2:]
+    keep = c >= 0
+    v, c, negs = v[keep], c[keep], negs[keep]
+    Wv = W[v].astype(np.float64)
+    loss = np.logaddexp(0.0, -np.einsum("ij,ij->i", Wv, C[c].astype(np.float64)))
+    for k in range(negs.shape[1]):
+        loss += np.logaddexp(0.0, np.einsum("ij,ij->i", Wv, C[negs[:, k]].astype(np.float64)))
+    return float(loss.mean())
+
+
+def _run_ranks(tmp_path, world, total, steps):
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    worker = os.path.join(ROOT, "tests", "helpers", "replica_worker.py")
+    outs = [str(tmp_path / ("w%d_r%d.npz" % (world, r))) for r in range(world)]
+    procs = [subprocess.Popen([sys.executable, "-u", worker, str(r), str(world), str(port), str(total), str(steps),
+                               outs[r]], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+             for r in range(world)]
+    for p in procs:
+        out, _ = p.communicate(timeout=240)
+        assert p.returncode == 0, out[-3000:]
+    return [np.load(o) for o in outs]
+
+
+def test_two_ranks_hip_passes_agree_and_train_like_one(tmp_path):
+    total, steps = 4 * 10 ** 6, 8
+    one = _run_ranks(tmp_path, 1, total, steps)[0]
+    two = _run_ranks(tmp_path, 2, total, steps)
+    for key in ("W", "C"):
+        np.testing.assert_allclose(two[0][key], two[1][key], atol=2e-5, rtol=0)
+    g = orc.Graph.from_file(PL1K, 1)
+    heldout = orc.sample_line(g, SEED + 7, 0, 50_000, 5)
+    l1 = _heldout_loss(one["W"], one["C"], heldout)
+    l2 = _heldout_loss(two[0]["W"], two[0]["C"], heldout)
+    assert l1 < 0.9 * np.log(2.0) * 6, l1
+    assert abs(l2 - l1) <= 0.01 * l1, (l1, l2)
