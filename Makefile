@@ -22,7 +22,7 @@ all: lib cli goshape
 
 lib: $(LIB)
 
-HOST_SRCS := host_graph capi exchange graphgen
+HOST_SRCS := host_graph loader capi exchange graphgen
 $(OBJ)/%.o: $(SRC)/%.cpp $(HOST_HDRS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(CXXFLAGS) -c -o $@ $<

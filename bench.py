@@ -60,7 +60,7 @@ def parse():
                     help="scatter: hybrid (default), atomic (every row), hogwild (plain stores, loses updates)")
     ap.add_argument("--hot-tau", type=float, default=0.3, help="hybrid: hot-row threshold")
     ap.add_argument("--combine-rows", type=int, default=128, help="hybrid: LDS write-combined hottest rows")
-    ap.add_argument("--combine-flush", type=int, default=32, help="hybrid: rounds between LDS flushes")
+    ap.add_argument("--combine-flush", type=int, default=0, help="hybrid: rounds between LDS drains (0: automatic)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
     ap.add_argument("--sync-every", type=int, default=1)
     ap.add_argument("--sync", default="sum", choices=["sum", "mean"])

@@ -82,6 +82,15 @@ const char* smore_version(void);
  * add both directions.  Builds CSR + alias tables and uploads them. */
 int smore_load_edgelist(smore_ctx* ctx, const char* path, int undirected,
                         int vertex_method, int negative_method);
+/* loader options (new): the text is parsed by all host threads
+ * (ids still in order of first appearance).  With a cache directory (this call,
+ * or $SMORE_CACHE_DIR), the parsed names and edge slots are stored there under
+ * a hash of the input bytes and read back on later loads of the same input.
+ * dir NULL or "" = no cache. */
+int smore_set_load_cache(smore_ctx* ctx, const char* dir);
+/* the last smore_load_edgelist: wall seconds of the text/cache stage, parser
+ * threads, 1 if it was served from the cache */
+int smore_last_load_info(const smore_ctx* ctx, double* seconds, int* threads, int* cache_hit);
 /* replaces: the graph half of LoadEdgeList + BuildAliasMethod
  * (src/proNet.cpp:410-542) for callers that already hold ids: E directed
  * edge slots (src[e] -> dst[e], weight w[e]) in push order. */
@@ -167,11 +176,14 @@ int smore_set_hot_threshold(smore_ctx* ctx, double tau);
 /* rows marked hot in W and C by the last hybrid launch */
 /* hybrid scatter: the `rows` hottest hot context rows (default 128; 0 = off; at
  * most 8192/dim) are write-combined per workgroup in LDS and drained to HBM every
- * `flush_rounds` rounds of a wave's loop (default 32) -- bounded extra staleness on
- * those rows only (rows whose expected updates per flush window exceed 65536 stay
- * on atomics), in exchange for not serialising every sample's atomic adds on the
- * same few HBM lines. */
+ * `flush_rounds` rounds of a wave's loop -- bounded extra staleness on those rows
+ * only (rows whose expected updates per flush window exceed 65536 stay on
+ * atomics), in exchange for not serialising every sample's atomic adds on the
+ * same few HBM lines.  flush_rounds 0 (default) = automatic: 8..32 rounds, fewer
+ * the hotter the hottest combined row (same expected staleness as config 4 at 32). */
 int smore_set_write_combine(smore_ctx* ctx, int rows, int flush_rounds);
+/* the combined rows and the drain interval the last hybrid launch used */
+int smore_write_combine_info(const smore_ctx* ctx, int* rows, int* flush_rounds);
 int smore_hot_rows(const smore_ctx* ctx, int64_t* hot_w, int64_t* hot_c);
 /* samples whose source had no out-edge (reference: TargetSample -> -1) */
 int smore_skipped(smore_ctx* ctx, uint64_t* skipped);

@@ -142,7 +142,10 @@ def read_edgelist(path, undirected):
             if len(parts) < 3:
                 continue
             a, b = parts[0].decode(), parts[1].decode()
-            x = float(parts[2])
+            try:
+                x = float(parts[2])
+            except ValueError:       # unparsable weight: skipped (pkg/pronet/pronet.go:139-143)
+                continue
             for n in (a, b):
                 if n not in ids:
                     ids[n] = len(names)

@@ -36,6 +36,8 @@ def _load():
         "smore_synchronize": (i32, [P]),
         "smore_version": (C.c_char_p, []),
         "smore_load_edgelist": (i32, [P, C.c_char_p, i32, i32, i32]),
+        "smore_set_load_cache": (i32, [P, C.c_char_p]),
+        "smore_last_load_info": (i32, [P, C.POINTER(dbl), C.POINTER(i32), C.POINTER(i32)]),
         "smore_set_graph_edges": (i32, [P, i64, i64, P, P, P, i32, i32]),
         "smore_graph_info": (i32, [P, C.POINTER(i64), C.POINTER(i64)]),
         "smore_vertex_name": (C.c_char_p, [P, i64]),
@@ -56,6 +58,7 @@ def _load():
         "smore_set_hot_threshold": (i32, [P, dbl]),
         "smore_set_semantics": (i32, [P, i32]),
         "smore_set_write_combine": (i32, [P, i32, i32]),
+        "smore_write_combine_info": (i32, [P, C.POINTER(i32), C.POINTER(i32)]),
         "smore_gen_powerlaw": (i32, [i64, i64, i32, dbl, u64, P, P]),
         "smore_hot_rows": (i32, [P, C.POINTER(i64), C.POINTER(i64)]),
         "smore_last_kernel_ms": (C.c_float, [P]),

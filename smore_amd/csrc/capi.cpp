@@ -6,6 +6,7 @@
 #include "ctx.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -103,12 +104,29 @@ int smore_load_edgelist(smore_ctx* c, const char* path, int undirected, int vm, 
     std::vector<std::string> names;
     std::vector<int32_t> src, dst;
     std::vector<double> w;
-    if (!read_edgelist(path, undirected != 0, names, src, dst, w, c->err)) return SMORE_EIO;
+    const char* cache = !c->cache_dir.empty() ? c->cache_dir.c_str() : getenv("SMORE_CACHE_DIR");
+    const auto t0 = std::chrono::steady_clock::now();
+    if (!read_edgelist(path, undirected != 0, names, src, dst, w, c->err, cache, &c->load_stats)) return SMORE_EIO;
+    c->load_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (names.empty()) return fail(c, SMORE_EIO, std::string("no edges in ") + path);
     int rc = smore_set_graph_edges(c, (int64_t)names.size(), (int64_t)src.size(), src.data(), dst.data(),
                                    w.data(), vm, nm);
     if (rc == SMORE_OK) c->g->names = std::move(names);
     return rc;
+}
+
+int smore_set_load_cache(smore_ctx* c, const char* dir) {
+    if (!c) return SMORE_EINVAL;
+    c->cache_dir = dir ? dir : "";
+    return SMORE_OK;
+}
+
+int smore_last_load_info(const smore_ctx* c, double* seconds, int* threads, int* cache_hit) {
+    if (!c) return SMORE_EINVAL;
+    if (seconds) *seconds = c->load_seconds;
+    if (threads) *threads = c->load_stats.threads;
+    if (cache_hit) *cache_hit = c->load_stats.cache_hit;
+    return SMORE_OK;
 }
 
 int smore_graph_info(const smore_ctx* c, int64_t* V, int64_t* E) {
@@ -279,6 +297,11 @@ int smore_table_device(smore_ctx* c, int which, void** dptr, int64_t* stride) {
 // tables and the CSR targets (one union set for shared-table models).  Written
 // in place into the existing device arrays; the host graph stays untagged.
 constexpr double SH_STALE_MAX = 65536.0;
+// automatic drain interval (smore_set_write_combine flush_rounds 0, the
+// default): the hottest combined row gathers about M * p_top * flush updates
+// that other workgroups cannot see yet; flush = budget / (M * p_top) within
+// [8, 32] rounds keeps that at the config-4 level (flush 32) on hotter graphs
+constexpr double SH_AUTO_BUDGET = 6144.0;
 
 static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
     char key[128];
@@ -305,13 +328,14 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
         double stale_max = SH_STALE_MAX;   // SMORE_SH_STALE overrides (tuning)
         if (const char* e = getenv("SMORE_SH_STALE")) stale_max = atof(e);
         std::vector<std::pair<double, int32_t>> r;
+        const int flush_cap = c->sh_flush > 0 ? c->sh_flush : 32;
         for (int64_t v = 0; v < V; ++v) {
             const double p = model == SMORE_LINE2 ? pc[v] + negs * pn[v] : ps[v] + pc[v] + negs * pn[v];
             // bounded staleness: a combined row's pending deltas are invisible to
             // other workgroups for up to sh_flush rounds, i.e. about
             // M * p * sh_flush updates; rows above SH_STALE_MAX stay on atomics
             // (on small graphs that is every hot row)
-            if (hc[v] && (double)M * p * c->sh_flush <= stale_max) r.push_back({p, (int32_t)v});
+            if (hc[v] && (double)M * p * flush_cap <= stale_max) r.push_back({p, (int32_t)v});
         }
         const int64_t cap = std::max<int64_t>(0, std::min<int64_t>(c->sh_max, 8192 / std::max(1, c->dpad)));
         const int64_t n = std::min<int64_t>(cap, (int64_t)r.size());
@@ -332,6 +356,11 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
         if ((rc2 = upload(c, c->d_sh_hash, hash.data(), hash.size()))) return rc2;
         if ((rc2 = upload(c, c->d_sh_ids, ids.data(), ids.size()))) return rc2;
         c->sh_rows = (int)n;
+        c->sh_flush_eff = flush_cap;
+        if (c->sh_flush <= 0 && n > 0) {
+            const double f = SH_AUTO_BUDGET / ((double)M * r[0].first);
+            c->sh_flush_eff = (int)std::max(8.0, std::min((double)flush_cap, std::floor(f)));
+        }
     }
     const HostGraph& g = *c->g;
     auto tag_tab = [&](const std::vector<AliasEntry>& tab, const std::vector<uint8_t>& hot) {
@@ -476,7 +505,7 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
     a.sh_rows = combine ? c->sh_rows : 0;
     a.sh_hash = c->d_sh_hash;
     a.sh_ids = c->d_sh_ids;
-    a.sh_flush = std::max(1, c->sh_flush);
+    a.sh_flush = std::max(1, c->sh_flush_eff);
     // edge models: draw kernel -> update kernel per chunk of samples.  With
     // several chunks the draws of chunk k+1 run on a second stream while
     // chunk k updates (two record buffers; the update kernel leaves one block
@@ -599,10 +628,17 @@ int smore_set_hot_threshold(smore_ctx* c, double tau) {
 }
 
 int smore_set_write_combine(smore_ctx* c, int rows, int flush_rounds) {
-    if (!c || rows < 0 || rows > 1024 || flush_rounds < 1) return SMORE_EINVAL;
+    if (!c || rows < 0 || rows > 1024 || flush_rounds < 0) return SMORE_EINVAL;
     c->sh_max = rows;
     c->sh_flush = flush_rounds;
     c->hot_key.clear();
+    return SMORE_OK;
+}
+
+int smore_write_combine_info(const smore_ctx* c, int* rows, int* flush_rounds) {
+    if (!c) return SMORE_EINVAL;
+    if (rows) *rows = c->sh_rows;
+    if (flush_rounds) *flush_rounds = c->sh_flush_eff;
     return SMORE_OK;
 }
 
@@ -780,7 +816,7 @@ int smore_train_deepwalk_async(smore_ctx* c, uint64_t walk_begin, uint64_t walk_
         ar.sh_rows = combine ? c->sh_rows : 0;
         ar.sh_hash = c->d_sh_hash;
         ar.sh_ids = c->d_sh_ids;
-        ar.sh_flush = std::max(1, c->sh_flush);
+        ar.sh_flush = std::max(1, c->sh_flush_eff);
     }
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     for (uint64_t b = walk_begin; b < walk_end; b += chunk) {

@@ -54,6 +54,10 @@ struct smore_ctx {
     bool timed = false;
     int cus = 0;
     int64_t last_loaded = 0;
+    // edge-list loader: binary cache directory ("" = off) and the last load's figures
+    std::string cache_dir;
+    LoadStats load_stats;
+    double load_seconds = 0.0;
     // semantics: SMORE_SEM_CPP (default) or SMORE_SEM_GO
     int semantics = 0;
     double* d_tcum = nullptr;
@@ -61,7 +65,8 @@ struct smore_ctx {
     int2* d_sh_hash = nullptr;
     int32_t* d_sh_ids = nullptr;
     int sh_rows = 0;
-    int sh_max = 128, sh_flush = 32;
+    int sh_max = 128, sh_flush = 0;      // flush 0: automatic drain interval (capi build_hot_maps)
+    int sh_flush_eff = 32;               // the interval of the last hybrid launch
     // pre-drawn edge-sample records (train_draw.hip) and per-phase timing
     int32_t* d_rec = nullptr;
     // DeepWalk pair records: per-walk pair counts, their exclusive scan, scan scratch

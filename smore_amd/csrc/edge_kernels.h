@@ -163,9 +163,23 @@ __device__ __forceinline__ void gather_rows(const EdgeArgs& a, int lane, const b
     }
 }
 
+// the K+1 context rows only (W_v held by the caller)
+template <int G, int M, int KMAX>
+__device__ __forceinline__ void gather_ctx_rows(const EdgeArgs& a, int lane, const bool (&ev)[M],
+                                                const int32_t (&id)[KMAX + 1], float (&rows)[KMAX + 1][M]) {
+#pragma unroll
+    for (int k = 0; k <= KMAX; ++k) {
+        const float* cp = a.C + (int64_t)(id[k] < 0 ? 0 : id[k]) * a.dpad + lane;
+#pragma unroll
+        for (int m = 0; m < M; ++m) rows[k][m] = (ev[m] && id[k] >= 0) ? cp[m * G] : 0.0f;
+    }
+}
+
 // sgd_update on rows already gathered by gather_rows (wv, rows are consumed).
 // SHARED: -1 = runtime (a.model), 0 = two tables (LINE-2), 1 = one table.
-template <int G, int M, int KMAX, int MODE, int SHARED = -1>
+// WOUT false (two tables only): W_v is not scattered; wv returns its new value
+// (the caller keeps it in registers over a run of samples with the same v).
+template <int G, int M, int KMAX, int MODE, int SHARED = -1, bool WOUT = true>
 __device__ __forceinline__ void sgd_update_rows(const EdgeArgs& a, const float* s_sig, int lane,
                                                 const bool (&ev)[M], int32_t v, const int32_t (&id)[KMAX + 1],
                                                 bool hotw, const bool (&hot)[KMAX + 1], float alpha, bool shared_rt,
@@ -278,7 +292,8 @@ __device__ __forceinline__ void sgd_update_rows(const EdgeArgs& a, const float* 
     for (int m = 0; m < M; ++m) wv[m] = wv[m] + e[m];
 
     // ---- scatter
-    {
+    static_assert(WOUT || SHARED == 0, "W_v stays in registers only with two tables");
+    if constexpr (WOUT) {
         float* wq = Tw + (int64_t)v * dpad + lane;
 #pragma unroll
         for (int m = 0; m < M; ++m) {
@@ -619,6 +634,50 @@ edge_train_kernel(EdgeArgs a) {
         };
         for (uint64_t c0 = grab(); c0 < count; c0 = grab()) {
             const uint64_t lim = c0 + span < count ? c0 + span : count;
+            if constexpr (SHARED == 0) {
+                if (a.alpha_rec) {
+                    // DeepWalk pair records: a walk's pairs are consecutive and
+                    // share rows (walk[i] is the W row of up to 2*window pairs in
+                    // a row), so they must not be spread over concurrent groups.
+                    // Each group takes a contiguous slice of CH_ROUNDS records and
+                    // runs it in order (gather after the previous scatter), keeps
+                    // W_v in registers while v repeats and adds W_v's accumulated
+                    // delta atomically when v changes: no W update is lost, and W
+                    // moves once per run instead of once per pair.
+                    const uint64_t s0 = c0 + gib * CH_ROUNDS;
+                    const uint64_t s1 = s0 + CH_ROUNDS < lim ? s0 + CH_ROUNDS : lim;
+                    int32_t cv = -1;
+                    float wv[M], wv0[M], rows[KMAX + 1][M];
+#pragma unroll
+                    for (int m = 0; m < M; ++m) wv[m] = wv0[m] = 0.0f;
+                    auto flush_w = [&]() {
+                        if (cv < 0) return;
+                        float* wq = a.W + (int64_t)cv * a.dpad + lane;
+#pragma unroll
+                        for (int m = 0; m < M; ++m)
+                            if (ev[m]) unsafeAtomicAdd(wq + m * G, wv[m] - wv0[m]);
+                    };
+                    if (s0 < s1) load_rec(s0, s1, rr);
+                    for (uint64_t t = s0; t < s1; ++t) {
+                        decode(t, s1, rr, xa);
+                        load_rec(t + 1, s1, rr);
+                        if (!xa.live) continue;
+                        if (xa.v != cv) {
+                            flush_w();
+                            cv = xa.v;
+                            const float* wp = a.W + (int64_t)cv * a.dpad + lane;
+#pragma unroll
+                            for (int m = 0; m < M; ++m) wv[m] = wv0[m] = ev[m] ? wp[m * G] : 0.0f;
+                        }
+                        gather_ctx_rows<G, M, KMAX>(a, lane, ev, xa.id, rows);
+                        sgd_update_rows<G, M, KMAX, MODE, 0, false>(a, s_sig, lane, ev, xa.v, xa.id, false, xa.hot,
+                                                                    xa.alpha, false, false, sh, wv, rows);
+                        maybe_flush();
+                    }
+                    flush_w();
+                    continue;
+                }
+            }
             if constexpr (SHARED == 2) {
                 // BPR: no row prefetch (a second set of 7 rows would halve the
                 // resident waves); the next record is still loaded one round ahead

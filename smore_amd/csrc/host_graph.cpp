@@ -5,6 +5,8 @@
 #include <sys/stat.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <functional>
 #include <cmath>
 #include <cstdio>
@@ -14,17 +16,23 @@
 
 namespace smore {
 
+// d^0.75 as std::pow computes it; 1 and 0 (unit and missing weights, the
+// common cases) are exact without the call
+static inline double pow075(double x) { return x == 1.0 ? 1.0 : x == 0.0 ? 0.0 : std::pow(x, 0.75); }
+
 void alias_cpp(const double* dist, int64_t n, double* prob, int64_t* alias) {
     // sequential sum in index order, as src/proNet.cpp:556-559
     double sum = 0.0;
-    for (int64_t i = 0; i < n; ++i) sum += std::pow(dist[i], 0.75);
+    for (int64_t i = 0; i < n; ++i) sum += pow075(dist[i]);
     const double norm = (double)n / sum;
-    std::vector<double> q((size_t)n);
-    std::vector<int64_t> small, large;
-    small.reserve((size_t)n);
-    large.reserve((size_t)n);
+    // per-thread scratch: the context tables call this once per vertex
+    thread_local std::vector<double> q;
+    thread_local std::vector<int64_t> small, large;
+    q.resize((size_t)n);
+    small.clear();
+    large.clear();
     for (int64_t i = 0; i < n; ++i) {
-        q[i] = std::pow(dist[i], 0.75) * norm;
+        q[i] = pow075(dist[i]) * norm;
         prob[i] = 0.0;
         alias[i] = -1;
     }
@@ -39,6 +47,11 @@ void alias_cpp(const double* dist, int64_t n, double* prob, int64_t* alias) {
     }
     while (!large.empty()) { prob[large.back()] = 1.0; large.pop_back(); }
     while (!small.empty()) { prob[small.back()] = 1.0; small.pop_back(); }
+    if (q.capacity() > ((size_t)1 << 24)) {   // do not keep a hub's scratch per thread
+        std::vector<double>().swap(q);
+        std::vector<int64_t>().swap(small);
+        std::vector<int64_t>().swap(large);
+    }
 }
 
 void alias_encode(const double* prob, const int64_t* alias, int64_t n, const int32_t* self_ids,
@@ -161,6 +174,14 @@ static std::vector<uint64_t> sort_slots_by_source(int64_t V, int64_t E, const in
 
 bool build_graph(int64_t V, int64_t E, const int32_t* src, const int32_t* dst, const double* w,
                  int vertex_method, int negative_method, HostGraph& g, std::string& err) {
+    const bool verbose = getenv("SMORE_LOAD_VERBOSE") != nullptr;
+    auto tick = std::chrono::steady_clock::now();
+    auto phase = [&](const char* what) {
+        if (!verbose) return;
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[build] %-12s %.2f s\n", what, std::chrono::duration<double>(now - tick).count());
+        tick = now;
+    };
     if (V <= 0 || V >= (int64_t)1 << 30 || E < 0 || E >= (int64_t)1 << 32) {   // ids carry a tag in bit 30
         err = "bad graph size (V < 2^30, E < 2^32)";
         return false;
@@ -202,6 +223,7 @@ bool build_graph(int64_t V, int64_t E, const int32_t* src, const int32_t* dst, c
         for (int64_t v = 0; v < V; ++v)                // sources without edges
             if (g.offsets[v + 1] < g.offsets[v]) g.offsets[v + 1] = g.offsets[v];
     }
+    phase("csr");
     // degrees (src/proNet.cpp:431-443): out in adjacency order, in over the CSR
     g.out_deg.assign((size_t)V, 0.0);
     g.in_deg.assign((size_t)V, 0.0);
@@ -234,12 +256,14 @@ bool build_graph(int64_t V, int64_t E, const int32_t* src, const int32_t* dst, c
         });
     }
 
+    phase("degrees");
     g.vertex_method = vertex_method;
     g.negative_method = negative_method;
     g.vprob.resize((size_t)V); g.valias.resize((size_t)V);
     g.nprob.resize((size_t)V); g.nalias.resize((size_t)V);
     g.vtab.resize((size_t)V); g.ntab.resize((size_t)V);
     build_cpp_vn_tables(g);
+    phase("v/n tables");
     // per-vertex context tables, alias remapped to the target vid
     // (src/proNet.cpp:517-537); vertices are independent -> threads
     g.cprob.resize((size_t)E); g.calias.resize((size_t)E);
@@ -255,6 +279,7 @@ bool build_graph(int64_t V, int64_t E, const int32_t* src, const int32_t* dst, c
                          g.ctab.data() + off);
         }
     });
+    phase("ctx tables");
     return true;
 }
 
@@ -301,91 +326,6 @@ void draw_probabilities(const HostGraph& g, std::vector<double>& p_src, std::vec
         if (br == 0 || p_src[v] == 0) continue;
         alias_marginal(g.cprob, g.calias, off, br, g.targets.data(), p_src[v] / br, p_ctx);
     }
-}
-
-// ---------------------------------------------------------------- loader
-static bool is_dir(const std::string& p) {
-    struct stat st;
-    return stat(p.c_str(), &st) == 0 && S_ISDIR(st.st_mode);
-}
-
-bool read_edgelist(const std::string& path, bool undirected, std::vector<std::string>& names,
-                   std::vector<int32_t>& src, std::vector<int32_t>& dst, std::vector<double>& w,
-                   std::string& err) {
-    std::vector<std::string> files;
-    if (is_dir(path)) {  // directory input (src/proNet.cpp:124-134), readdir order
-        DIR* d = opendir(path.c_str());
-        if (!d) { err = "cannot open directory " + path; return false; }
-        while (struct dirent* ent = readdir(d)) {
-            std::string f = path + "/" + ent->d_name;
-            if (!is_dir(f)) files.push_back(f);
-        }
-        closedir(d);
-    } else {
-        files.push_back(path);
-    }
-    std::unordered_map<std::string, int32_t> ids;
-    auto intern = [&](const char* b, size_t n) -> int32_t {
-        std::string key(b, n);
-        auto it = ids.find(key);
-        if (it != ids.end()) return it->second;
-        int32_t id = (int32_t)names.size();
-        ids.emplace(std::move(key), id);
-        names.emplace_back(b, n);
-        return id;
-    };
-    std::vector<char> buf(1 << 22);
-    for (const auto& fn : files) {
-        FILE* f = fopen(fn.c_str(), "rb");
-        if (!f) { err = "cannot open " + fn; return false; }
-        std::string carry;
-        size_t got;
-        auto handle_line = [&](const char* s, const char* e) {
-            // first three whitespace-separated fields "v1 v2 w" (lines with
-            // fewer are skipped, as pkg/pronet/pronet.go:132-134)
-            const char* tok[3]; size_t len[3]; int nt = 0;
-            const char* p = s;
-            while (p < e && nt < 3) {
-                while (p < e && (*p == ' ' || *p == '\t' || *p == '\r')) ++p;
-                if (p >= e) break;
-                const char* q = p;
-                while (q < e && !(*q == ' ' || *q == '\t' || *q == '\r')) ++q;
-                tok[nt] = p; len[nt] = (size_t)(q - p); ++nt;
-                p = q;
-            }
-            if (nt < 3) return;
-            char wb[64];
-            size_t wl = std::min<size_t>(len[2], 63);
-            memcpy(wb, tok[2], wl); wb[wl] = 0;
-            char* endp;
-            double x = strtod(wb, &endp);
-            if (endp == wb) return;
-            int32_t a = intern(tok[0], len[0]);
-            int32_t b = intern(tok[1], len[1]);
-            src.push_back(a); dst.push_back(b); w.push_back(x);
-            if (undirected) { src.push_back(b); dst.push_back(a); w.push_back(x); }
-        };
-        while ((got = fread(buf.data(), 1, buf.size(), f)) > 0) {
-            const char* s = buf.data();
-            const char* end = s + got;
-            const char* nl;
-            while ((nl = (const char*)memchr(s, '\n', (size_t)(end - s)))) {
-                if (!carry.empty()) {
-                    carry.append(s, nl);
-                    handle_line(carry.data(), carry.data() + carry.size());
-                    carry.clear();
-                } else {
-                    handle_line(s, nl);
-                }
-                s = nl + 1;
-            }
-            carry.append(s, end);
-        }
-        if (!carry.empty()) handle_line(carry.data(), carry.data() + carry.size());
-        fclose(f);
-        if (names.size() >= ((size_t)1 << 31) - 1) { err = "too many vertices"; return false; }
-    }
-    return true;
 }
 
 // ---------------------------------------------------------------- glibc rand

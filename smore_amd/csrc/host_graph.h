@@ -60,10 +60,17 @@ bool build_graph(int64_t V, int64_t E, const int32_t* src, const int32_t* dst, c
 // stored methods (src/proNet.cpp:457-510).
 void build_cpp_vn_tables(HostGraph& g);
 
-// Text edge list(s) -> names + directed slots (src/proNet.cpp:115-236).
+// Text edge list(s) -> names + directed slots (src/proNet.cpp:115-236), parsed
+// in parallel (loader.cpp); with a cache directory, a binary copy keyed by the
+// input's content hash is written on the first load and read on later ones.
+struct LoadStats {
+    int threads = 0;
+    size_t bytes = 0;
+    int cache_hit = 0, cache_written = 0;
+};
 bool read_edgelist(const std::string& path, bool undirected, std::vector<std::string>& names,
                    std::vector<int32_t>& src, std::vector<int32_t>& dst, std::vector<double>& w,
-                   std::string& err);
+                   std::string& err, const char* cache_dir = nullptr, LoadStats* stats = nullptr);
 
 // glibc TYPE_3 rand() stream after srand(1) (the reference's Init).
 class GlibcRand {

@@ -159,5 +159,11 @@ class ReplicaSync(OverlapSync):
     passes, the training kernels and the collective are ordered on it."""
 
     def __init__(self, pn, mean=False, tables=(0, 1), group=None):
+        # the passes, the training kernels and the collective must be ordered
+        # on ONE stream.  The context runs on its own non-blocking stream when
+        # handed the null stream (handle 0), which the legacy null stream does
+        # not order against, so a dedicated torch stream is made current first.
+        if torch.cuda.current_stream().cuda_stream == 0:
+            torch.cuda.set_stream(torch.cuda.Stream())
         pn.set_stream(torch.cuda.current_stream().cuda_stream)
         super().__init__([table_tensor(pn, w) for w in tables], mean=mean, group=group, passes=HipPasses(pn))

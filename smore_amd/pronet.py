@@ -65,6 +65,16 @@ class ProNet:
                                           _lib.VM[self.vertex_method], _lib.NM[self.negative_method]),
                   "LoadEdgeList(%s)" % filename)
 
+    def set_load_cache(self, directory):
+        """Binary edge-list cache directory for LoadEdgeList (None: off)."""
+        self._chk(lib.smore_set_load_cache(self.ctx, directory.encode() if directory else None), "set_load_cache")
+
+    def last_load_info(self):
+        """(seconds, parser threads, served from cache) of the last LoadEdgeList."""
+        sec, th, hit = C.c_double(), C.c_int(), C.c_int()
+        self._chk(lib.smore_last_load_info(self.ctx, C.byref(sec), C.byref(th), C.byref(hit)), "last_load_info")
+        return sec.value, th.value, bool(hit.value)
+
     def set_graph_edges(self, V, src, dst, w):
         """Graph from ids: directed edge slots src->dst (weight w) in push order."""
         src = np.ascontiguousarray(src, np.int32)
@@ -187,9 +197,16 @@ class ProNet:
         self._chk(lib.smore_set_semantics(self.ctx, _lib.SEM[semantics]), "set_semantics")
         self.semantics = semantics
 
-    def set_write_combine(self, rows, flush_rounds=32):
-        """Hybrid scatter: LDS write-combining of the `rows` hottest context rows."""
+    def set_write_combine(self, rows, flush_rounds=0):
+        """Hybrid scatter: LDS write-combining of the `rows` hottest context rows,
+        drained every `flush_rounds` rounds (0: automatic)."""
         self._chk(lib.smore_set_write_combine(self.ctx, int(rows), int(flush_rounds)), "set_write_combine")
+
+    def write_combine_info(self):
+        """(combined rows, drain interval) of the last hybrid launch."""
+        r, f = C.c_int(), C.c_int()
+        self._chk(lib.smore_write_combine_info(self.ctx, C.byref(r), C.byref(f)), "write_combine_info")
+        return r.value, f.value
 
     def set_hot_threshold(self, tau):
         self._chk(lib.smore_set_hot_threshold(self.ctx, float(tau)), "set_hot_threshold")

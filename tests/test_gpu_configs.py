@@ -92,7 +92,7 @@ def test_c2_full_grid_hybrid_matches_atomic(c2):
         pn.init_table_uniform(0, 5)
         pn.zero_table(1)
         pn.set_hot_threshold(0.3)
-        pn.set_write_combine(128, 32)
+        pn.set_write_combine(128, 0)     # the defaults: 128 rows, automatic drain interval
         pn.train_edges("line2", 0, total, total, K, 0.025, 0.0, SEED, mode)
         W, C = pn.get_table(0), pn.get_table(1)
         assert np.isfinite(W).all() and np.isfinite(C).all()

@@ -108,7 +108,10 @@ def _run_ranks(tmp_path, world, total, steps):
 
 
 def test_two_ranks_hip_passes_agree_and_train_like_one(tmp_path):
-    total, steps = 4 * 10 ** 6, 8
+    """Exchange period: 8k samples per rank (~9 updates per row of the 920-row
+    tables per rank between exchanges -- the C4 bench's 2^27 samples per rank
+    give ~13 per row)."""
+    total, steps = 4 * 10 ** 6, 250
     one = _run_ranks(tmp_path, 1, total, steps)[0]
     two = _run_ranks(tmp_path, 2, total, steps)
     for key in ("W", "C"):

@@ -1,0 +1,130 @@
+"""The parallel edge-list loader and its binary cache (smore_amd/csrc/loader.cpp,
+SURVEY.md 8f-1) on a host-only context (no GPU): vertex ids in order of first
+appearance and directed slots in the reference's push order
+(src/proNet.cpp:115-236), checked against the oracle's sequential restatement
+(oracle/oracle.py read_edgelist) on the golden edge lists and on a generated
+file large enough to be cut into many chunks, with ragged lines."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from tests.conftest import GOLDEN
+
+
+def _load(path, und, cache=None, threads=None):
+    import smore_amd
+    if threads:
+        os.environ["SMORE_LOAD_THREADS"] = str(threads)
+    try:
+        pn = smore_amd.ProNet(-1)
+        if cache:
+            pn.set_load_cache(cache)
+        pn.LoadEdgeList(path, und)
+        info = pn.last_load_info()
+        off, tgt = pn.csr()
+        return pn.names, off, tgt, info
+    finally:
+        os.environ.pop("SMORE_LOAD_THREADS", None)
+
+
+def _expected(path, und):
+    names, s, d, w = orc.read_edgelist(path, und)
+    g = orc.Graph(len(names), s, d, w)
+    return names, g.offsets, g.targets[:g.E]
+
+
+@pytest.mark.parametrize("fname,und", [("toy.txt", 1), ("toy.txt", 0), ("pl1k.txt", 1), ("bip.txt", 0),
+                                       ("pl100w.txt", 1)])
+def test_golden_edge_lists(fname, und):
+    path = os.path.join(GOLDEN, fname)
+    names, off, tgt, _ = _load(path, und)
+    en, eo, et = _expected(path, und)
+    assert names == en
+    np.testing.assert_array_equal(off, eo)
+    np.testing.assert_array_equal(tgt, et)
+
+
+def _ragged_file(path, lines=1_000_000, seed=5):
+    """Zipf-ish ids, mixed separators, \\r\\n, short and malformed lines, no
+    trailing newline."""
+    rng = np.random.default_rng(seed)
+    a = (rng.zipf(1.6, lines) % 50_000).astype(np.int64)
+    b = (rng.zipf(1.6, lines) % 50_000).astype(np.int64)
+    w = rng.integers(1, 5, lines)
+    out = []
+    for i in range(lines):
+        r = i % 97
+        if r == 13:
+            out.append("lonely%d 7" % a[i])                       # 2 fields: skipped
+        elif r == 29:
+            out.append("u%d\tv%d\tnotanumber" % (a[i], b[i]))     # bad weight: skipped
+        elif r == 41:
+            out.append("")                                         # empty line
+        elif r == 53:
+            out.append("  u%d   v%d  %d.5 extra fields\r" % (a[i], b[i], w[i]))
+        else:
+            out.append("u%d v%d %d" % (a[i], b[i], w[i]))
+    with open(path, "w") as f:
+        f.write("\n".join(out))                                    # no newline at the end
+
+
+@pytest.mark.parametrize("und,threads", [(1, 8), (0, 3), (1, 1)])
+def test_parallel_loader_matches_sequential(tmp_path, und, threads):
+    path = str(tmp_path / "ragged.txt")
+    _ragged_file(path)
+    names, off, tgt, info = _load(path, und, threads=threads)
+    en, eo, et = _expected(path, und)
+    assert info[1] == min(threads, os.path.getsize(path) // (1 << 20) + 1)   # >= 1 MiB of text per thread
+    assert names == en
+    np.testing.assert_array_equal(off, eo)
+    np.testing.assert_array_equal(tgt, et)
+
+
+def test_directory_input(tmp_path):
+    d = tmp_path / "parts"
+    d.mkdir()
+    for k in range(3):
+        _ragged_file(str(d / ("p%d.txt" % k)), lines=20_000, seed=k)
+    names, off, tgt, _ = _load(str(d), 1, threads=4)
+    # readdir order (the reference's opendir/readdir loop, src/proNet.cpp:124-134)
+    files = [str(d / e) for e in os.listdir(str(d))]
+    en, s, dd, w = [], [], [], []
+    ids = {}
+    for fn in files:
+        nm, s1, d1, w1 = orc.read_edgelist(fn, 1)
+        remap = []
+        for n in nm:
+            if n not in ids:
+                ids[n] = len(en)
+                en.append(n)
+            remap.append(ids[n])
+        remap = np.array(remap, np.int32)
+        s.append(remap[s1]); dd.append(remap[d1]); w.append(w1)
+    g = orc.Graph(len(en), np.concatenate(s), np.concatenate(dd), np.concatenate(w))
+    assert names == en
+    np.testing.assert_array_equal(off, g.offsets)
+    np.testing.assert_array_equal(tgt, g.targets[:g.E])
+
+
+def test_binary_cache_roundtrip(tmp_path):
+    path = str(tmp_path / "g.txt")
+    _ragged_file(path, lines=100_000)
+    cache = str(tmp_path / "cache")
+    os.makedirs(cache)
+    n1, o1, t1, i1 = _load(path, 1, cache=cache)
+    assert not i1[2]
+    assert len([f for f in os.listdir(cache) if f.endswith(".smorelc")]) == 1
+    n2, o2, t2, i2 = _load(path, 1, cache=cache)
+    assert i2[2], "second load not served from the cache"
+    assert n1 == n2
+    np.testing.assert_array_equal(o1, o2)
+    np.testing.assert_array_equal(t1, t2)
+    # the undirected flag and the content are part of the key
+    _, _, _, i3 = _load(path, 0, cache=cache)
+    assert not i3[2]
+    with open(path, "a") as f:
+        f.write("\nnewa newb 1\n")
+    n4, _, _, i4 = _load(path, 1, cache=cache)
+    assert not i4[2] and n4[-2:] == ["newa", "newb"]
