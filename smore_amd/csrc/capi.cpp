@@ -211,8 +211,23 @@ int smore_alloc_tables(smore_ctx* c, int dim, int ntables) {
     c->dpad = (dim + 3) / 4 * 4;
     c->ntables = ntables;
     size_t bytes = (size_t)c->g->V * c->dpad * sizeof(float);
+    // The embedding tables live in UNCACHED device memory: every row access is
+    // served memory-side (Infinity Cache / HBM), which is coherent across the
+    // 8 XCDs.  In the default coarse-grained memory each XCD's L2 keeps its own
+    // copy of a row, so a plain-store (Hogwild) update made on one XCD is
+    // overwritten by a read-modify-write from another XCD that still holds the
+    // old line -- lost updates the reference's cache-coherent CPU Hogwild never
+    // has (DESIGN.md "Scatter modes": DeepWalk held-out AUC on 2 blocks 0.82 ->
+    // 0.87, the atomic level).  Measured on one box, C4 LINE-2 +2.5 %, C5
+    // DeepWalk +8.6 %, C3 BPR equal (rows are random and miss L2 anyway).
+    // SMORE_TABLE_MEM=coarse|finegrained|uncached overrides (experiments).
+    unsigned flags = hipDeviceMallocUncached;
+    if (const char* e = getenv("SMORE_TABLE_MEM")) {
+        if (!strcmp(e, "coarse")) flags = hipDeviceMallocDefault;
+        else if (!strcmp(e, "finegrained")) flags = hipDeviceMallocFinegrained;
+    }
     for (int t = 0; t < ntables; ++t) {
-        HIPCHK(c, hipMalloc((void**)&c->d_table[t], bytes));
+        HIPCHK(c, hipExtMallocWithFlags((void**)&c->d_table[t], bytes, flags));
         HIPCHK(c, hipMemset(c->d_table[t], 0, bytes));
     }
     return SMORE_OK;
@@ -432,6 +447,11 @@ static int edge_grid(smore_ctx* c, const EdgeArgs& a, bool leave_slot = false) {
         if (cap > 0 && cap < per_cu) per_cu = cap;
     }
     int64_t grid = (int64_t)c->cus * per_cu;
+    // tuning knob: SMORE_MAX_BLOCKS caps the whole grid
+    if (const char* e = getenv("SMORE_MAX_BLOCKS")) {
+        const int64_t cap = atoll(e);
+        if (cap > 0 && cap < grid) grid = cap;
+    }
     const int G = lanes_of(a.dpad);
     const int64_t groups_per_block = 256 / G;
     const int64_t need = ((int64_t)a.count + groups_per_block - 1) / groups_per_block;

@@ -46,7 +46,41 @@ struct EdgeInst {
     }
 };
 
+// DeepWalk pair records in the Hogwild modes (pair_train_kernel)
+template <int KMAX, int MODE>
+struct PairInst {
+    static hipError_t launch(const EdgeArgs& a, int grid, hipStream_t st) {
+        const int G = lanes_of(a.dpad), M = (a.dpad + G - 1) / G;
+        const size_t lds = MODE == MODE_HYBRID ? sh_lds_bytes(a.sh_rows, a.dpad) : 0;
+#define X(g, m)                                                                                      \
+    if (G == g && M == m) {                                                                          \
+        hipLaunchKernelGGL((pair_train_kernel<g, m, KMAX, MODE>), dim3(grid), dim3(256), lds, st, a); \
+        return hipGetLastError();                                                                    \
+    }
+        SMORE_FOR_EACH_GM(X)
+#undef X
+        return hipErrorInvalidValue;
+    }
+    static const void* symbol(const EdgeArgs& a) {
+        const int G = lanes_of(a.dpad), M = (a.dpad + G - 1) / G;
+#define X(g, m) \
+    if (G == g && M == m) return (const void*)pair_train_kernel<g, m, KMAX, MODE>;
+        SMORE_FOR_EACH_GM(X)
+#undef X
+        return nullptr;
+    }
+};
+
 }  // namespace smore
+
+// defines launch_pair_<name>(a, grid, st) and pair_symbol_<name>(a)
+#define SMORE_PAIR_INST(name, KMAX, MODE)                                                  \
+    namespace smore {                                                                      \
+    hipError_t launch_pair_##name(const EdgeArgs& a, int grid, hipStream_t st) {           \
+        return PairInst<KMAX, MODE>::launch(a, grid, st);                                  \
+    }                                                                                      \
+    const void* pair_symbol_##name(const EdgeArgs& a) { return PairInst<KMAX, MODE>::symbol(a); } \
+    }
 
 // defines launch_edge_<name>(a, grid, st) and edge_symbol_<name>(a)
 #define SMORE_EDGE_INST(name, KMAX, MODE)                                                  \

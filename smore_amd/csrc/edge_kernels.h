@@ -458,18 +458,15 @@ _Pragma("unroll") for (int k2 = 0; k2 < NS; ++k2) if (k2 != (K_) && id[k2] == id
     }
 }
 
-// ------------------------------------------------------------------ edge kernel
-// LINE-2 (W,C; SHARED 0), LINE-1 / MF (W,W; SHARED 1, Opt_SGD for MF at run
-// time) and BPR (W,W; SHARED 2, UpdateBPRPair); the scatter MODE is
-// compile-time.
-template <int G, int M, int KMAX, int MODE, int SHARED>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(waves_of(MODE, SHARED))))
-edge_train_kernel(EdgeArgs a) {
-    __shared__ float s_sig[1001];
-    extern __shared__ float s_dyn[];   // hybrid: int2 hash[SH_HASH], int ids[n], float pend[n][dpad]
+// ------------------------------------------------------------------ block setup
+// fastSigmoid table into LDS and, for the hybrid scatter, the write-combining
+// state (hash, slot ids, zeroed pending deltas) in the dynamic LDS; ends with
+// a workgroup barrier.
+template <int MODE>
+__device__ __forceinline__ ShState block_setup(const EdgeArgs& a, float* s_sig, float* s_dyn, int32_t*& sh_ids) {
     for (int i = threadIdx.x; i < 1001; i += blockDim.x) s_sig[i] = a.sig[i];
     ShState sh{nullptr, nullptr, 0};
-    int32_t* sh_ids = nullptr;
+    sh_ids = nullptr;
     if constexpr (MODE == MODE_HYBRID) {
         if (a.sh_rows > 0) {
             int2* h = reinterpret_cast<int2*>(s_dyn);
@@ -482,6 +479,39 @@ edge_train_kernel(EdgeArgs a) {
         }
     }
     __syncthreads();
+    return sh;
+}
+
+// Adds pending write-combined deltas to HBM (one row per wave-instruction).
+// Wave w of the block drains its share of the pending rows with an LDS
+// exchange (read-and-zero in one atomic), so there is no workgroup barrier:
+// an LDS add racing with the drain lands either in this drain or in the
+// wave's next one, never lost.
+__device__ __forceinline__ void sh_drain(const ShState& sh, const int32_t* sh_ids, float* Tc, int dpad) {
+    const int nwaves = blockDim.x / 64, wave = threadIdx.x / 64;
+    const int n = sh.n * dpad;
+    const int per = (n + nwaves - 1) / nwaves;
+    const int lo = wave * per, hi = n < lo + per ? n : lo + per;
+    for (int i = lo + (threadIdx.x & 63); i < hi; i += 64) {
+        const float x = atomicExch(&sh.pend[i], 0.0f);
+        if (x != 0.0f) {
+            const int s = i / dpad, e = i - s * dpad;
+            unsafeAtomicAdd(Tc + (int64_t)sh_ids[s] * dpad + e, x);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ edge kernel
+// LINE-2 (W,C; SHARED 0), LINE-1 / MF (W,W; SHARED 1, Opt_SGD for MF at run
+// time) and BPR (W,W; SHARED 2, UpdateBPRPair); the scatter MODE is
+// compile-time.
+template <int G, int M, int KMAX, int MODE, int SHARED>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(waves_of(MODE, SHARED))))
+edge_train_kernel(EdgeArgs a) {
+    __shared__ float s_sig[1001];
+    extern __shared__ float s_dyn[];   // hybrid: int2 hash[SH_HASH], int ids[n], float pend[n][dpad]
+    int32_t* sh_ids = nullptr;
+    const ShState sh = block_setup<MODE>(a, s_sig, s_dyn, sh_ids);
 
     const int lane = threadIdx.x & (G - 1);
     const uint64_t count = a.count_dev ? *a.count_dev : a.count;   // records of this launch
@@ -499,24 +529,8 @@ edge_train_kernel(EdgeArgs a) {
     const uint64_t base = (mf || SHARED == 2) ? 0 : 1;   // LINE counts from 1, MF and BPR from 0
     float* const Tc = a.C;
 
-    // adds pending super-hot deltas to HBM (one row per wave-instruction).
-    // Wave w of the block drains its share of the pending rows with an LDS
-    // exchange (read-and-zero in one atomic), so there is no workgroup barrier
-    // in the loop: an LDS add racing with the drain lands either in this
-    // flush or in the wave's next one, never lost.
-    const int nwaves = blockDim.x / 64, wave = threadIdx.x / 64;
-    auto drain = [&]() {
-        const int n = sh.n * a.dpad;
-        const int per = (n + nwaves - 1) / nwaves;
-        const int lo = wave * per, hi = n < lo + per ? n : lo + per;
-        for (int i = lo + (threadIdx.x & 63); i < hi; i += 64) {
-            const float x = atomicExch(&sh.pend[i], 0.0f);
-            if (x != 0.0f) {
-                const int s = i / a.dpad, e = i - s * a.dpad;
-                unsafeAtomicAdd(Tc + (int64_t)sh_ids[s] * a.dpad + e, x);
-            }
-        }
-    };
+    // pending super-hot deltas -> HBM (sh_drain)
+    auto drain = [&]() { sh_drain(sh, sh_ids, Tc, a.dpad); };
     auto flush = [&]() {   // end of the kernel: every wave is done adding
         __syncthreads();
         drain();
@@ -634,50 +648,6 @@ edge_train_kernel(EdgeArgs a) {
         };
         for (uint64_t c0 = grab(); c0 < count; c0 = grab()) {
             const uint64_t lim = c0 + span < count ? c0 + span : count;
-            if constexpr (SHARED == 0) {
-                if (a.alpha_rec) {
-                    // DeepWalk pair records: a walk's pairs are consecutive and
-                    // share rows (walk[i] is the W row of up to 2*window pairs in
-                    // a row), so they must not be spread over concurrent groups.
-                    // Each group takes a contiguous slice of CH_ROUNDS records and
-                    // runs it in order (gather after the previous scatter), keeps
-                    // W_v in registers while v repeats and adds W_v's accumulated
-                    // delta atomically when v changes: no W update is lost, and W
-                    // moves once per run instead of once per pair.
-                    const uint64_t s0 = c0 + gib * CH_ROUNDS;
-                    const uint64_t s1 = s0 + CH_ROUNDS < lim ? s0 + CH_ROUNDS : lim;
-                    int32_t cv = -1;
-                    float wv[M], wv0[M], rows[KMAX + 1][M];
-#pragma unroll
-                    for (int m = 0; m < M; ++m) wv[m] = wv0[m] = 0.0f;
-                    auto flush_w = [&]() {
-                        if (cv < 0) return;
-                        float* wq = a.W + (int64_t)cv * a.dpad + lane;
-#pragma unroll
-                        for (int m = 0; m < M; ++m)
-                            if (ev[m]) unsafeAtomicAdd(wq + m * G, wv[m] - wv0[m]);
-                    };
-                    if (s0 < s1) load_rec(s0, s1, rr);
-                    for (uint64_t t = s0; t < s1; ++t) {
-                        decode(t, s1, rr, xa);
-                        load_rec(t + 1, s1, rr);
-                        if (!xa.live) continue;
-                        if (xa.v != cv) {
-                            flush_w();
-                            cv = xa.v;
-                            const float* wp = a.W + (int64_t)cv * a.dpad + lane;
-#pragma unroll
-                            for (int m = 0; m < M; ++m) wv[m] = wv0[m] = ev[m] ? wp[m * G] : 0.0f;
-                        }
-                        gather_ctx_rows<G, M, KMAX>(a, lane, ev, xa.id, rows);
-                        sgd_update_rows<G, M, KMAX, MODE, 0, false>(a, s_sig, lane, ev, xa.v, xa.id, false, xa.hot,
-                                                                    xa.alpha, false, false, sh, wv, rows);
-                        maybe_flush();
-                    }
-                    flush_w();
-                    continue;
-                }
-            }
             if constexpr (SHARED == 2) {
                 // BPR: no row prefetch (a second set of 7 rows would halve the
                 // resident waves); the next record is still loaded one round ahead
@@ -725,6 +695,108 @@ edge_train_kernel(EdgeArgs a) {
     }
     if constexpr (MODE == MODE_HYBRID) {
         if (sh.n > 0) flush();
+    }
+}
+
+// ------------------------------------------------------------------ pair kernel
+// DeepWalk skip-gram pair records (train_pairs.hip: {walk[i], walk[j], K
+// negatives, .., alpha bits at word 2 + KMAX}, walk-major in the reference's
+// pair order) in the Hogwild modes; the serial mode runs them through
+// edge_train_kernel.  A walk's pairs are consecutive and share rows (walk[i]
+// is the W row of up to 2*window pairs in a row), so they are not spread over
+// concurrent groups: each group takes a contiguous slice of CH_ROUNDS records
+// and runs it in order (gather after the previous scatter), keeps W_v in
+// registers while v repeats and adds W_v's accumulated delta atomically when v
+// changes -- no W update is lost, and W moves once per run instead of once per
+// pair.  Context rows scatter as the MODE says (the tables are uncached
+// device memory, so a plain store is seen by every XCD: capi alloc_tables).
+template <int G, int M, int KMAX, int MODE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(waves_of(MODE))))
+pair_train_kernel(EdgeArgs a) {
+    __shared__ float s_sig[1001];
+    extern __shared__ float s_dyn[];
+    int32_t* sh_ids = nullptr;
+    const ShState sh = block_setup<MODE>(a, s_sig, s_dyn, sh_ids);
+    const int lane = threadIdx.x & (G - 1);
+    const uint64_t count = a.count_dev ? *a.count_dev : a.count;
+    const uint64_t gpb = blockDim.x / G, gib = threadIdx.x / G;
+    bool ev[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) ev[m] = lane + G * m < a.dpad;
+    constexpr int RW = rec_width(KMAX);
+    uint32_t round = 0;
+    __shared__ uint64_t s_next;
+    const uint64_t span = CH_ROUNDS * gpb;
+    for (;;) {
+        __syncthreads();   // every wave has read the previous s_next
+        if (threadIdx.x == 0) s_next = atomicAdd(a.work, 1ull) * span;
+        __syncthreads();
+        const uint64_t c0 = s_next;
+        if (c0 >= count) break;
+        const uint64_t lim = c0 + span < count ? c0 + span : count;
+        const uint64_t s0 = c0 + gib * CH_ROUNDS;
+        const uint64_t s1 = s0 + CH_ROUNDS < lim ? s0 + CH_ROUNDS : lim;
+        int32_t cv = -1;
+        float wv[M], wv0[M], rows[KMAX + 1][M];
+#pragma unroll
+        for (int m = 0; m < M; ++m) wv[m] = wv0[m] = 0.0f;
+        i32x4 r[RW / 4];
+        auto load_rec = [&](uint64_t t) {
+#pragma unroll
+            for (int q = 0; q < RW / 4; ++q) r[q] = i32x4{-1, -1, -1, -1};
+            if (t < s1) {
+                const i32x4* p = reinterpret_cast<const i32x4*>(a.rec + t * RW);
+#pragma unroll
+                for (int q = 0; q < RW / 4; ++q) r[q] = __builtin_nontemporal_load(p + q);
+            }
+        };
+        auto flush_w = [&]() {
+            if (cv < 0) return;
+            float* wq = a.W + (int64_t)cv * a.dpad + lane;
+#pragma unroll
+            for (int m = 0; m < M; ++m)
+                if (ev[m]) unsafeAtomicAdd(wq + m * G, wv[m] - wv0[m]);
+        };
+        load_rec(s0);
+        for (uint64_t t = s0; t < s1; ++t) {
+            // decode this record, then load the next one behind it
+            const int32_t tv = r[0][0], c = r[0][1];
+            const float alpha = __int_as_float(r[(2 + KMAX) / 4][(2 + KMAX) % 4]);
+            int32_t id[KMAX + 1];
+            bool hot[KMAX + 1];
+#pragma unroll
+            for (int k = 0; k <= KMAX; ++k) {
+                const int32_t w = (k == 0) ? c : (k - 1 < a.K ? r[(k + 1) / 4][(k + 1) % 4] : -1);
+                hot[k] = scatter_atomic<MODE>(w);
+                id[k] = w < 0 ? -1 : untag(w);
+            }
+            load_rec(t + 1);
+            if (c < 0) continue;
+            const int32_t v = untag(tv);
+            if (v != cv) {
+                flush_w();
+                cv = v;
+                const float* wp = a.W + (int64_t)cv * a.dpad + lane;
+#pragma unroll
+                for (int m = 0; m < M; ++m) wv[m] = wv0[m] = ev[m] ? wp[m * G] : 0.0f;
+            }
+            gather_ctx_rows<G, M, KMAX>(a, lane, ev, id, rows);
+            sgd_update_rows<G, M, KMAX, MODE, 0, false>(a, s_sig, lane, ev, v, id, false, hot, alpha, false, false, sh,
+                                                        wv, rows);
+            if constexpr (MODE == MODE_HYBRID) {
+                if (sh.n > 0 && ++round == (uint32_t)a.sh_flush) {
+                    sh_drain(sh, sh_ids, a.C, a.dpad);
+                    round = 0;
+                }
+            }
+        }
+        flush_w();
+    }
+    if constexpr (MODE == MODE_HYBRID) {
+        if (sh.n > 0) {
+            __syncthreads();
+            sh_drain(sh, sh_ids, a.C, a.dpad);
+        }
     }
 }
 

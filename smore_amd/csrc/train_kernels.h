@@ -94,7 +94,16 @@ hipError_t launch_walk_gen(const DevGraph& g, const WalkArgs& w, uint64_t seed, 
 SMORE_DECL_EDGE(s5) SMORE_DECL_EDGE(s10) SMORE_DECL_EDGE(s20)
 SMORE_DECL_EDGE(a5) SMORE_DECL_EDGE(a10) SMORE_DECL_EDGE(a20)
 SMORE_DECL_EDGE(h5) SMORE_DECL_EDGE(h10) SMORE_DECL_EDGE(h20)
+// DeepWalk pair-kernel instantiations (train_pair_*.hip; K <= 10)
+#define SMORE_DECL_PAIR(name)                                                   \
+    hipError_t launch_pair_##name(const EdgeArgs& a, int grid, hipStream_t st); \
+    const void* pair_symbol_##name(const EdgeArgs& a);
+SMORE_DECL_PAIR(s5) SMORE_DECL_PAIR(s10) SMORE_DECL_PAIR(a5) SMORE_DECL_PAIR(a10)
+SMORE_DECL_PAIR(h5) SMORE_DECL_PAIR(h10)
+#undef SMORE_DECL_PAIR
 #undef SMORE_DECL_EDGE
+// launch_edge_train / edge_kernel_symbol route DeepWalk pair records
+// (alpha_rec) in the Hogwild modes to pair_train_kernel
 hipError_t launch_edge_train(const EdgeArgs& a, int grid, hipStream_t st);
 const void* edge_kernel_symbol(const EdgeArgs& a);
 hipError_t launch_sample(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K,

@@ -68,14 +68,27 @@ int lanes_of(int dpad) {
         return k == 5 ? fn##s5(__VA_ARGS__) : k == 10 ? fn##s10(__VA_ARGS__) : fn##s20(__VA_ARGS__);                \
     }
 
+#define SMORE_PAIR_DISPATCH(fn, ...)                                           \
+    {                                                                          \
+        const bool k5 = kmax_of(a.K) == 5;                                     \
+        if (a.mode == 1) return k5 ? fn##a5(__VA_ARGS__) : fn##a10(__VA_ARGS__); \
+        if (a.mode == 3) return k5 ? fn##h5(__VA_ARGS__) : fn##h10(__VA_ARGS__); \
+        return k5 ? fn##s5(__VA_ARGS__) : fn##s10(__VA_ARGS__);                \
+    }
+
+static bool pair_path(const EdgeArgs& a) { return a.alpha_rec && a.mode != 2 && a.K <= 10; }
+
 hipError_t launch_edge_train(const EdgeArgs& a, int grid, hipStream_t st) {
+    if (pair_path(a)) SMORE_PAIR_DISPATCH(launch_pair_, a, grid, st)
     SMORE_EDGE_DISPATCH(launch_edge_, a, grid, st)
 }
 
 const void* edge_kernel_symbol(const EdgeArgs& a) {
+    if (pair_path(a)) SMORE_PAIR_DISPATCH(pair_symbol_, a)
     SMORE_EDGE_DISPATCH(edge_symbol_, a)
 }
 #undef SMORE_EDGE_DISPATCH
+#undef SMORE_PAIR_DISPATCH
 
 hipError_t launch_sample(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K,
                          int bpr, int32_t* out, hipStream_t st) {
