@@ -278,6 +278,26 @@ int smore_train_deepwalk_async(smore_ctx* ctx, uint64_t walk_begin, uint64_t wal
  * glibc rand() after `skip` Init draws (src/model/DeepWalk.cpp:122-131) */
 int smore_deepwalk_order(int64_t V, int walk_times, uint64_t skip, int64_t* order);
 
+/* replaces: Walklets::Train (src/model/Walklets.cpp:24-63): walks [walk_begin,
+ * walk_end) of walk_times*V, walk w starting at vertex w mod V (the reference
+ * walks from vid itself), pairs of ScaleSkipGrams(walk, window_min, window_max,
+ * 0) (src/proNet.cpp:928-987, its clamping included), UpdatePair per pair.
+ * Draws: stream 1, unit w: the walk's 2 per step, then 2K per pair. */
+int smore_train_walklets(smore_ctx* ctx, uint64_t walk_begin, uint64_t walk_end, int walk_times,
+                         int walk_steps, int window_min, int window_max, int K, double alpha0,
+                         uint64_t seed, int mode);
+/* replaces: APP::Train (src/model/APP.cpp:59-120): units [unit_begin, unit_end)
+ * of walk_times*V*sample_times; unit u = w*sample_times + s runs
+ * JumpingRandomWalk(order[w], jump) (src/proNet.cpp:685-701) and
+ * UpdatePair(order[w], walk end) with K negatives.  order[]: walk_times*V start
+ * vertices (host; APP shuffles like DeepWalk: smore_deepwalk_order).  Draws:
+ * stream 1, unit u: per step p, index, jump test, then 2K.  jump must be > 0
+ * (the reference never ends a walk with jump 0 on a graph without dead ends);
+ * a walk stops after 2^24 steps. */
+int smore_train_app(smore_ctx* ctx, uint64_t unit_begin, uint64_t unit_end, int walk_times,
+                    int sample_times, double jump, int K, double alpha0, uint64_t seed,
+                    const int64_t* order, int mode);
+
 /* ---- samplers (parity tests) -------------------------------------------------------- */
 /* replaces: SourceSample/TargetSample/NegativeSample (src/proNet.cpp:623-683):
  * draws of samples [begin, begin+count) as the training kernels draw them.

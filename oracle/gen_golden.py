@@ -203,6 +203,12 @@ def gen_e2e(graphs, seed, only):
         ("e2e_deepwalk_pl100w", ["deepwalk", graphs["pl100w"], 1, 8, 2, 10, 3, 2, 0.025, seed]),
         # config 5's model shape: d=128, walk_steps 40, window 5, K 5
         ("e2e_deepwalk_d128_pl100w", ["deepwalk", graphs["pl100w"], 1, 128, 1, 40, 5, 5, 0.025, seed]),
+        # Walklets (src/model/Walklets.cpp): window_min 2, window_max 4
+        ("e2e_walklets_pl100w", ["walklets", graphs["pl100w"], 1, 8, 2, 10, 2, 4, 2, 0.025, seed]),
+        # APP (src/model/APP.cpp): 3 jumping walks per start, jump 0.15
+        ("e2e_app_pl100w", ["app", graphs["pl100w"], 1, 8, 2, 3, 0.15, 2, 0.025, seed]),
+        # HPE (src/model/HPE.cpp): 10^6 samples, walk_steps 3, K 2, reg 0.01
+        ("e2e_hpe_pl100w", ["hpe", graphs["pl100w"], 1, 8, 1, 3, 2, 0.01, 0.025, seed]),
     ]
     for name, args in e2e:
         if only and name not in only:

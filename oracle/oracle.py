@@ -77,6 +77,21 @@ def _declare(L):
     L.orc_train_deepwalk_f32.argtypes = [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, dbl, u64, P, u64, u64]
     L.orc_lane_width.restype = C.c_int
     L.orc_lane_width.argtypes = [C.c_int]
+    L.orc_train_walklets_f64.restype = C.c_int
+    L.orc_train_walklets_f64.argtypes = [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, dbl, u64]
+    L.orc_train_walklets_f32.restype = C.c_int
+    L.orc_train_walklets_f32.argtypes = [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, dbl,
+                                         u64, u64, u64]
+    L.orc_train_app_f64.restype = C.c_int
+    L.orc_train_app_f64.argtypes = [P, P, P, C.c_int, C.c_int, C.c_int, dbl, C.c_int, dbl, u64, P]
+    L.orc_train_app_f32.restype = C.c_int
+    L.orc_train_app_f32.argtypes = [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, dbl, C.c_int, dbl, u64, P, u64, u64]
+    L.orc_train_hpe_f64.restype = C.c_int
+    L.orc_train_hpe_f64.argtypes = [P, P, P, C.c_int, C.c_int, C.c_int, dbl, dbl, u64, u64, u64, u64]
+    L.orc_train_hpe_f32.restype = C.c_int
+    L.orc_train_hpe_f32.argtypes = [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, dbl, dbl, u64, u64, u64, u64]
+    L.orc_app_pairs.restype = None
+    L.orc_app_pairs.argtypes = [P, C.c_int, C.c_int, dbl, u64, P, u64, u64, P]
 
 
 def ptr(a):
@@ -282,6 +297,53 @@ def train_deepwalk_f32(g, W, C_, dim, walk_times, walk_steps, window, K, alpha0,
         end = walk_times * g.V
     return lib().orc_train_deepwalk_f32(g.ref, ptr(W), ptr(C_), dim, W.shape[1], walk_times, walk_steps, window,
                                         K, alpha0, seed, ptr(order), begin, end)
+
+
+def train_walklets_f64(g, W, C_, walk_times, walk_steps, wmin, wmax, K, alpha0, seed):
+    """Walklets::Train (src/model/Walklets.cpp:24-63), 1 worker, fp64."""
+    return lib().orc_train_walklets_f64(g.ref, ptr(W), ptr(C_), W.shape[1], walk_times, walk_steps, wmin, wmax, K,
+                                        alpha0, seed)
+
+
+def train_walklets_f32(g, W, C_, dim, walk_times, walk_steps, wmin, wmax, K, alpha0, seed, begin=0, end=None):
+    if end is None:
+        end = walk_times * g.V
+    return lib().orc_train_walklets_f32(g.ref, ptr(W), ptr(C_), dim, W.shape[1], walk_times, walk_steps, wmin, wmax,
+                                        K, alpha0, seed, begin, end)
+
+
+def train_app_f64(g, W, C_, walk_times, sample_times, jump, K, alpha0, seed, order):
+    """APP::Train (src/model/APP.cpp:59-120), 1 worker, fp64."""
+    order = np.ascontiguousarray(order, np.int64)
+    return lib().orc_train_app_f64(g.ref, ptr(W), ptr(C_), W.shape[1], walk_times, sample_times, jump, K, alpha0,
+                                   seed, ptr(order))
+
+
+def train_app_f32(g, W, C_, dim, walk_times, sample_times, jump, K, alpha0, seed, order, begin=0, end=None):
+    order = np.ascontiguousarray(order, np.int64)
+    if end is None:
+        end = walk_times * g.V * sample_times
+    return lib().orc_train_app_f32(g.ref, ptr(W), ptr(C_), dim, W.shape[1], walk_times, sample_times, jump, K,
+                                   alpha0, seed, ptr(order), begin, end)
+
+
+def train_hpe_f64(g, W, C_, walk_steps, K, reg, alpha0, total, begin, end, seed):
+    """HPE::Train (src/model/HPE.cpp:94-150), 1 worker, fp64; returns skipped samples."""
+    return lib().orc_train_hpe_f64(g.ref, ptr(W), ptr(C_), W.shape[1], walk_steps, K, reg, alpha0, total, begin, end,
+                                   seed)
+
+
+def train_hpe_f32(g, W, C_, dim, walk_steps, K, reg, alpha0, total, begin, end, seed):
+    return lib().orc_train_hpe_f32(g.ref, ptr(W), ptr(C_), dim, W.shape[1], walk_steps, K, reg, alpha0, total, begin,
+                                   end, seed)
+
+
+def app_pairs(g, walk_times, sample_times, jump, seed, order, begin, end):
+    """(start, walk end) of APP units [begin, end)."""
+    order = np.ascontiguousarray(order, np.int64)
+    out = np.zeros((end - begin, 2), np.int32)
+    lib().orc_app_pairs(g.ref, walk_times, sample_times, jump, seed, ptr(order), begin, end, ptr(out))
+    return out
 
 
 # --------------------------------------------------------------------- Go semantics

@@ -10,7 +10,11 @@
 // the build's RNG spec (DESIGN.md "RNG spec"):
 //   edge models  : draw n of the run -> unit n / D, slot n % D, stream 0
 //   DeepWalk     : proNet::RandomWalk is wrapped (ld --wrap) so each walk
-//                  starts unit = walk index, slot 0, stream 1
+//                  starts unit = walk index, slot 0, stream 1 (Walklets too)
+//   APP          : proNet::JumpingRandomWalk is wrapped the same way: each
+//                  jumping walk (and its UpdatePair) is one unit
+//   HPE          : proNet::SourceSample is wrapped (HPE mode only): each
+//                  sample is one unit of stream 0, consecutive slots
 //   random_gen(0,1)   -> k * 2^-32
 //   random_gen(a,b)   -> a + floor(k * (b-a) / 2^32)
 // Weight init keeps the reference's own glibc rand() calls.
@@ -22,8 +26,11 @@
 #include <string>
 #include <vector>
 
+#include "model/APP.h"
 #include "model/BPR.h"
 #include "model/DeepWalk.h"
+#include "model/HPE.h"
+#include "model/Walklets.h"
 #include "model/LINE.h"
 #include "model/MF.h"
 
@@ -38,11 +45,13 @@ static uint64_t g_n = 0;            // draw counter (edge models)
 static int g_walk_mode = 0;
 static uint64_t g_walk_unit = 0, g_walk_counter = 0;
 static uint32_t g_walk_slot = 0;
+static uint32_t g_walk_stream = 1;     // walk models: stream 1; HPE: stream 0
+static int g_hpe_mode = 0;
 
 double random_gen(const int& min, const int& max) {
     uint32_t k;
     if (g_walk_mode) {
-        k = orc_word(g_seed, 1, g_walk_unit, g_walk_slot++);
+        k = orc_word(g_seed, g_walk_stream, g_walk_unit, g_walk_slot++);
     } else {
         uint64_t s = g_n / g_D, slot = g_n % g_D;
         g_n++;
@@ -59,6 +68,24 @@ extern "C" void* __wrap__ZN6proNet10RandomWalkEli(void* ret, void* self, long st
     g_walk_unit = g_walk_counter++;
     g_walk_slot = 0;
     return __real__ZN6proNet10RandomWalkEli(ret, self, start, steps);
+}
+
+// proNet::JumpingRandomWalk(long, double): same sret convention (jump in xmm0)
+extern "C" void* __real__ZN6proNet17JumpingRandomWalkEld(void* ret, void* self, long start, double jump);
+extern "C" void* __wrap__ZN6proNet17JumpingRandomWalkEld(void* ret, void* self, long start, double jump) {
+    g_walk_unit = g_walk_counter++;
+    g_walk_slot = 0;
+    return __real__ZN6proNet17JumpingRandomWalkEld(ret, self, start, jump);
+}
+
+// proNet::SourceSample(): HPE's sample starts here (a new unit)
+extern "C" long __real__ZN6proNet12SourceSampleEv(void* self);
+extern "C" long __wrap__ZN6proNet12SourceSampleEv(void* self) {
+    if (g_hpe_mode) {
+        g_walk_unit = g_walk_counter++;
+        g_walk_slot = 0;
+    }
+    return __real__ZN6proNet12SourceSampleEv(self);
 }
 
 // ---------------------------------------------------------------- tiny container
@@ -148,6 +175,9 @@ static void usage() {
             "ref_harness mf <edges> <dim> <sample_times> <K> <alpha> <reg> <seed> <out>\n"
             "ref_harness bpr <edges> <dim> <sample_times> <alpha> <reg> <seed> <out>\n"
             "ref_harness deepwalk <edges> <undirected> <dim> <walk_times> <walk_steps> <window> <K> <alpha> <seed> <out>\n"
+            "ref_harness walklets <edges> <undirected> <dim> <walk_times> <walk_steps> <wmin> <wmax> <K> <alpha> <seed> <out>\n"
+            "ref_harness app <edges> <undirected> <dim> <walk_times> <sample_times> <jump> <K> <alpha> <seed> <out>\n"
+            "ref_harness hpe <edges> <undirected> <dim> <sample_times> <walk_steps> <K> <reg> <alpha> <seed> <out>\n"
             "ref_harness updates <edges> <undirected> <model:line2|line1|mf|bpr> <dim> <K> <alpha> <reg> <seed> <first> <n> <out>\n");
     exit(1);
 }
@@ -240,6 +270,52 @@ int main(int argc, char** argv) {
         o.table("W0", m.w_vertex, dim); o.table("C0", m.w_context, dim);
         g_walk_mode = 1; g_walk_counter = 0;
         m.Train(wt, ws, win, K, alpha, 1);
+        o.table("W", m.w_vertex, dim); o.table("C", m.w_context, dim);
+        dump_graph(o, m.pnet);
+        return 0;
+    }
+    if (mode == "walklets" && argc == 13) {
+        int dim = atoi(argv[4]), wt = atoi(argv[5]), ws = atoi(argv[6]), wmin = atoi(argv[7]), wmax = atoi(argv[8]);
+        int K = atoi(argv[9]);
+        double alpha = atof(argv[10]);
+        g_seed = strtoull(argv[11], 0, 10);
+        Walklets m;
+        m.LoadEdgeList(argv[2], atoi(argv[3]) != 0);
+        m.Init(dim);
+        Out o(argv[12]);
+        o.table("W0", m.w_vertex, dim); o.table("C0", m.w_context, dim);
+        g_walk_mode = 1; g_walk_counter = 0;
+        m.Train(wt, ws, wmin, wmax, K, alpha, 1);
+        o.table("W", m.w_vertex, dim); o.table("C", m.w_context, dim);
+        dump_graph(o, m.pnet);
+        return 0;
+    }
+    if (mode == "app" && argc == 12) {
+        int dim = atoi(argv[4]), wt = atoi(argv[5]), st = atoi(argv[6]), K = atoi(argv[8]);
+        double jump = atof(argv[7]), alpha = atof(argv[9]);
+        g_seed = strtoull(argv[10], 0, 10);
+        APP m;
+        m.LoadEdgeList(argv[2], atoi(argv[3]) != 0);
+        m.Init(dim);
+        Out o(argv[11]);
+        o.table("W0", m.w_vertex, dim); o.table("C0", m.w_context, dim);
+        g_walk_mode = 1; g_walk_counter = 0;
+        m.Train(wt, st, jump, K, alpha, 1);
+        o.table("W", m.w_vertex, dim); o.table("C", m.w_context, dim);
+        dump_graph(o, m.pnet);
+        return 0;
+    }
+    if (mode == "hpe" && argc == 12) {
+        int dim = atoi(argv[4]), st = atoi(argv[5]), ws = atoi(argv[6]), K = atoi(argv[7]);
+        double reg = atof(argv[8]), alpha = atof(argv[9]);
+        g_seed = strtoull(argv[10], 0, 10);
+        HPE m;
+        m.LoadEdgeList(argv[2], atoi(argv[3]) != 0);
+        m.Init(dim);
+        Out o(argv[11]);
+        o.table("W0", m.w_vertex, dim); o.table("C0", m.w_context, dim);
+        g_walk_mode = 1; g_walk_stream = 0; g_hpe_mode = 1; g_walk_counter = 0;
+        m.Train(st, ws, K, reg, alpha, 1);
         o.table("W", m.w_vertex, dim); o.table("C", m.w_context, dim);
         dump_graph(o, m.pnet);
         return 0;

@@ -812,6 +812,255 @@ int orc_train_deepwalk_f32(const orc_graph* g, float* W, float* C, int dim, int 
     return 0;
 }
 
+/* ---- Walklets --------------------------------------------------------------
+ * ScaleSkipGrams(walk, window_min, window_max, 0), src/proNet.cpp:928-987, with
+ * its clamping exactly as written: the left range [max(0,i-wmax), max(0,i-wmin)]
+ * and the right range [min(i+wmin,L-1), min(i+wmax,L-1)], i itself skipped
+ * (a clamped range can pair vertices closer than window_min). No draws. */
+static int scale_skip_grams(const int32_t* walk, int L, int wmin, int wmax, int32_t* pv, int32_t* pc) {
+    int n = 0;
+    for (int i = 0; i < L; ++i) {
+        int left = i - wmax; if (left < 0) left = 0;
+        int right = i - wmin; if (right < 0) right = 0;
+        for (int j = left; j <= right; ++j) {
+            if (i == j) continue;
+            pv[n] = walk[i]; pc[n] = walk[j]; n++;
+        }
+        left = i + wmin; if (left >= L) left = L - 1;
+        right = i + wmax; if (right >= L) right = L - 1;
+        for (int j = left; j <= right; ++j) {
+            if (i == j) continue;
+            pv[n] = walk[i]; pc[n] = walk[j]; n++;
+        }
+    }
+    return n;
+}
+
+static int walklets(const orc_graph* g, double* W64, double* C64, float* W32, float* C32, int dim, int dpad,
+                    int walk_times, int walk_steps, int wmin, int wmax, int K, double alpha0, uint64_t seed,
+                    uint64_t walk_begin, uint64_t walk_end) {
+    sig_init();
+    int64_t V = g->V;
+    uint64_t total = (uint64_t)walk_times * (uint64_t)V;
+    if (walk_end > total) walk_end = total;
+    int32_t* walk = (int32_t*)malloc(sizeof(int32_t) * (walk_steps + 1));
+    int span = wmax - wmin + 1; if (span < 1) span = 1;
+    int maxp = 2 * (span + 1) * (walk_steps + 1) + 1;
+    int32_t* pv = (int32_t*)malloc(sizeof(int32_t) * maxp);
+    int32_t* pc = (int32_t*)malloc(sizeof(int32_t) * maxp);
+    int32_t negs[MAX_SLOTS];
+    double* e64 = (double*)malloc(sizeof(double) * (dim > dpad ? dim : dpad));
+    float* e32 = (float*)malloc(sizeof(float) * (dpad > 0 ? dpad : 1));
+    for (uint64_t w = walk_begin; w < walk_end; ++w) {
+        walk_rng r = {seed, w, 0, {0, 0, 0, 0}, 0xFFFFFFFFu};
+        double alpha = orc_alpha_walk(w, alpha0, total);
+        int L = random_walk(g, &r, (int32_t)(w % (uint64_t)V), walk_steps, walk);
+        int np = scale_skip_grams(walk, L, wmin, wmax, pv, pc);
+        for (int p = 0; p < np; ++p) {
+            for (int j = 0; j < K; ++j) {
+                uint32_t ki = walk_next(&r), kp = walk_next(&r);
+                negs[j] = negative_sample(g, ki, kp);
+            }
+            if (W64) update_edge_f64(0, W64, C64, dim, pv[p], pc[p], negs, K, alpha, 0.0, e64);
+            else update_edge_f32(0, W32, C32, dpad, pv[p], pc[p], negs, K, (float)alpha, 0.0f, e32);
+        }
+    }
+    free(walk); free(pv); free(pc); free(e64); free(e32);
+    return 0;
+}
+
+int orc_train_walklets_f64(const orc_graph* g, double* W, double* C, int dim, int walk_times, int walk_steps,
+                           int window_min, int window_max, int K, double alpha0, uint64_t seed) {
+    return walklets(g, W, C, NULL, NULL, dim, 0, walk_times, walk_steps, window_min, window_max, K, alpha0, seed, 0,
+                    (uint64_t)-1);
+}
+
+int orc_train_walklets_f32(const orc_graph* g, float* W, float* C, int dim, int dpad, int walk_times,
+                           int walk_steps, int window_min, int window_max, int K, double alpha0, uint64_t seed,
+                           uint64_t walk_begin, uint64_t walk_end) {
+    return walklets(g, NULL, NULL, W, C, dim, dpad, walk_times, walk_steps, window_min, window_max, K, alpha0, seed,
+                    walk_begin, walk_end);
+}
+
+/* ---- APP ----------------------------------------------------------------------
+ * JumpingRandomWalk(start, jump), src/proNet.cpp:685-701: from `start`, while
+ * the current vertex has out-edges: TargetSample (p, index), then stop when
+ * random_gen(0.0, 1.0) < jump (the double arguments bind to the int
+ * parameters: U[0,1)).  Returns the walk's last vertex (start for a dead
+ * start).  The reference has no step bound; this one stops after 2^24 steps
+ * (the GPU's bound, where a jump >= 1e-6 ends first with probability
+ * 1 - e^-16). */
+#define APP_MAX_STEPS (1 << 24)
+static int32_t jumping_walk_end(const orc_graph* g, walk_rng* r, int32_t start, double jump) {
+    int32_t next = start;
+    for (int s = 0; s < APP_MAX_STEPS; ++s) {
+        if (g->offsets[next + 1] - g->offsets[next] == 0) return next;
+        uint32_t kp = walk_next(r), ki = walk_next(r);
+        next = target_sample(g, next, kp, ki);
+        if (draw_unit(walk_next(r)) < jump) break;
+    }
+    return next;
+}
+
+void orc_app_pairs(const orc_graph* g, int walk_times, int sample_times, double jump, uint64_t seed,
+                   const int64_t* order, uint64_t unit_begin, uint64_t unit_end, int32_t* vc) {
+    (void)walk_times;
+    for (uint64_t u = unit_begin; u < unit_end; ++u) {
+        walk_rng r = {seed, u, 0, {0, 0, 0, 0}, 0xFFFFFFFFu};
+        int32_t start = (int32_t)order[u / (uint64_t)sample_times];
+        vc[2 * (u - unit_begin)] = start;
+        vc[2 * (u - unit_begin) + 1] = jumping_walk_end(g, &r, start, jump);
+    }
+}
+
+static int app(const orc_graph* g, double* W64, double* C64, float* W32, float* C32, int dim, int dpad,
+               int walk_times, int sample_times, double jump, int K, double alpha0, uint64_t seed,
+               const int64_t* order, uint64_t unit_begin, uint64_t unit_end) {
+    sig_init();
+    uint64_t total = (uint64_t)walk_times * (uint64_t)g->V;
+    uint64_t units = total * (uint64_t)sample_times;
+    if (unit_end > units) unit_end = units;
+    int32_t negs[MAX_SLOTS];
+    double* e64 = (double*)malloc(sizeof(double) * (dim > dpad ? dim : dpad));
+    float* e32 = (float*)malloc(sizeof(float) * (dpad > 0 ? dpad : 1));
+    for (uint64_t u = unit_begin; u < unit_end; ++u) {
+        uint64_t w = u / (uint64_t)sample_times;
+        walk_rng r = {seed, u, 0, {0, 0, 0, 0}, 0xFFFFFFFFu};
+        double alpha = orc_alpha_walk(w, alpha0, total);
+        int32_t v = (int32_t)order[w];
+        int32_t c = jumping_walk_end(g, &r, v, jump);
+        for (int j = 0; j < K; ++j) {
+            uint32_t ki = walk_next(&r), kp = walk_next(&r);
+            negs[j] = negative_sample(g, ki, kp);
+        }
+        if (W64) update_edge_f64(0, W64, C64, dim, v, c, negs, K, alpha, 0.0, e64);
+        else update_edge_f32(0, W32, C32, dpad, v, c, negs, K, (float)alpha, 0.0f, e32);
+    }
+    free(e64); free(e32);
+    return 0;
+}
+
+int orc_train_app_f64(const orc_graph* g, double* W, double* C, int dim, int walk_times, int sample_times,
+                      double jump, int K, double alpha0, uint64_t seed, const int64_t* order) {
+    return app(g, W, C, NULL, NULL, dim, 0, walk_times, sample_times, jump, K, alpha0, seed, order, 0,
+               (uint64_t)-1);
+}
+
+int orc_train_app_f32(const orc_graph* g, float* W, float* C, int dim, int dpad, int walk_times, int sample_times,
+                      double jump, int K, double alpha0, uint64_t seed, const int64_t* order,
+                      uint64_t unit_begin, uint64_t unit_end) {
+    return app(g, NULL, NULL, W, C, dim, dpad, walk_times, sample_times, jump, K, alpha0, seed, order, unit_begin,
+               unit_end);
+}
+
+/* ---- HPE ----------------------------------------------------------------------
+ * Opt_SigmoidRegSGD, src/proNet.cpp:1332-1351 (the caller passes C[c] as the
+ * context loss too): f = sig(W.C); g = label - f; first the whole
+ * err += alpha*(g*c - reg*w) loop, then c += alpha*(g*w - reg*c). */
+static void opt_sigmoid_reg_f64(const double* wv, double* wc, double label, double alpha, double reg, int dim,
+                                double* err) {
+    double f = 0.0;
+    for (int d = 0; d < dim; ++d) f += wv[d] * wc[d];
+    f = orc_fast_sigmoid(f);
+    double gg = label - f;
+    for (int d = 0; d < dim; ++d) err[d] += alpha * (gg * wc[d] - reg * wv[d]);
+    for (int d = 0; d < dim; ++d) wc[d] += alpha * (gg * wv[d] - reg * wc[d]);
+}
+
+/* fp32 spec of the same step (the MF rule's element form with the sigmoid
+ * gradient): e = fmaf(alpha, g*c - reg*w, e); c = fmaf(alpha, g*w - reg*c, c) */
+static void opt_sigmoid_reg_f32(const float* wv, float* wc, float label, float alpha, float reg, int dpad, float* e) {
+    float f = dot_spec(wv, wc, dpad);
+    float gg = label - fast_sigmoid_f32(f);
+    for (int d = 0; d < dpad; ++d) {
+        float ce = wc[d], we = wv[d];
+        float t1 = gg * ce - reg * we;
+        float t2 = gg * we - reg * ce;
+        e[d] = fmaf(alpha, t1, e[d]);
+        wc[d] = fmaf(alpha, t2, ce);
+    }
+}
+
+typedef struct { uint64_t seed, unit; uint32_t slot; uint32_t buf[4]; uint32_t bufblk; } unit_rng;
+static inline uint32_t unit_next(unit_rng* r) {   /* stream 0, consecutive slots of one unit */
+    uint32_t blk = r->slot >> 2;
+    if (blk != r->bufblk) {
+        uint32_t ctr[4] = {(uint32_t)r->unit, (uint32_t)(r->unit >> 32), blk, 0u};
+        uint32_t key[2] = {(uint32_t)r->seed, (uint32_t)(r->seed >> 32)};
+        orc_philox4x32_10(ctr, key, r->buf);
+        r->bufblk = blk;
+    }
+    return r->buf[r->slot++ & 3];
+}
+/* TargetSample: no draws on a vertex without out-edges */
+static inline int32_t unit_target(const orc_graph* g, unit_rng* r, int32_t v) {
+    if (g->offsets[v + 1] - g->offsets[v] == 0) return -1;
+    uint32_t kp = unit_next(r), ki = unit_next(r);
+    return target_sample(g, v, kp, ki);
+}
+
+static int hpe(const orc_graph* g, double* W64, double* C64, float* W32, float* C32, int dim, int dpad,
+               int walk_steps, int K, double reg, double alpha0, uint64_t total, uint64_t begin, uint64_t end,
+               uint64_t seed) {
+    sig_init();
+    int skipped = 0;
+    int32_t negs[MAX_SLOTS];
+    int n = dim > dpad ? dim : dpad;
+    double* e64 = (double*)malloc(sizeof(double) * (n > 0 ? n : 1));
+    float* e32 = (float*)malloc(sizeof(float) * (n > 0 ? n : 1));
+    for (uint64_t s = begin; s < end; ++s) {
+        unit_rng r = {seed, s, 0, {0, 0, 0, 0}, 0xFFFFFFFFu};
+        uint32_t kp = unit_next(&r), ki = unit_next(&r);
+        int32_t v1 = source_sample(g, kp, ki);
+        int32_t v2 = unit_target(g, &r, v1);
+        if (v2 < 0) { skipped++; continue; }
+        double alpha = orc_alpha_line(s, alpha0, total);
+        int32_t ctx = v2;
+        for (int st = 0; st < walk_steps; ++st) {
+            if (st != 0) {
+                ctx = unit_target(g, &r, ctx);
+                if (ctx == -1) break;
+            }
+            for (int j = 0; j < K; ++j) {
+                uint32_t a = unit_next(&r), b = unit_next(&r);
+                negs[j] = negative_sample(g, a, b);
+            }
+            if (W64) {
+                double* wv = W64 + (int64_t)v1 * dim;
+                for (int d = 0; d < dim; ++d) e64[d] = 0.0;
+                opt_sigmoid_reg_f64(wv, C64 + (int64_t)ctx * dim, 1.0, alpha, reg, dim, e64);
+                for (int j = 0; j < K; ++j) opt_sigmoid_reg_f64(wv, C64 + (int64_t)negs[j] * dim, 0.0, alpha, reg, dim, e64);
+                for (int d = 0; d < dim; ++d) wv[d] += e64[d];
+            } else {
+                float* wv = W32 + (int64_t)v1 * dpad;
+                for (int d = 0; d < dpad; ++d) e32[d] = 0.0f;
+                opt_sigmoid_reg_f32(wv, C32 + (int64_t)ctx * dpad, 1.0f, (float)alpha, (float)reg, dpad, e32);
+                for (int j = 0; j < K; ++j)
+                    opt_sigmoid_reg_f32(wv, C32 + (int64_t)negs[j] * dpad, 0.0f, (float)alpha, (float)reg, dpad, e32);
+                for (int d = 0; d < dpad; ++d) wv[d] = wv[d] + e32[d];
+            }
+        }
+        for (int j = 0; j < K; ++j) {
+            uint32_t a = unit_next(&r), b = unit_next(&r);
+            negs[j] = negative_sample(g, a, b);
+        }
+        if (W64) update_edge_f64(0, W64, C64, dim, v2, v1, negs, K, alpha, 0.0, e64);
+        else update_edge_f32(0, W32, C32, dpad, v2, v1, negs, K, (float)alpha, 0.0f, e32);
+    }
+    free(e64); free(e32);
+    return skipped;
+}
+
+int orc_train_hpe_f64(const orc_graph* g, double* W, double* C, int dim, int walk_steps, int K, double reg,
+                      double alpha0, uint64_t total, uint64_t begin, uint64_t end, uint64_t seed) {
+    return hpe(g, W, C, NULL, NULL, dim, 0, walk_steps, K, reg, alpha0, total, begin, end, seed);
+}
+
+int orc_train_hpe_f32(const orc_graph* g, float* W, float* C, int dim, int dpad, int walk_steps, int K, double reg,
+                      double alpha0, uint64_t total, uint64_t begin, uint64_t end, uint64_t seed) {
+    return hpe(g, NULL, NULL, W, C, dim, dpad, walk_steps, K, reg, alpha0, total, begin, end, seed);
+}
+
 /* ========================================================================== */
 /* Go semantics (pkg/pronet, internal/models/{line,bpr,deepwalk}).             */
 /* No Go toolchain exists here: these restate the Go source and are            */

@@ -745,20 +745,28 @@ int smore_save_weights(const smore_ctx* cc, int which, const char* path, int fmt
     return SMORE_OK;
 }
 
-int smore_train_deepwalk_async(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, int walk_times,
-                               int walk_steps, int window, int K, double alpha0, uint64_t seed, const int64_t* order,
-                               int mode) {
+// Walk models on the record path: DeepWalk (rule 0) and Walklets (rule 1)
+// walks -> skip-gram pair records -> update kernel.  `order` holds the walk
+// start of every walk index (DeepWalk's shuffled keys; Walklets: vid).
+static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
+                       int window, int window_min, int K, double alpha0, uint64_t seed, const int64_t* order,
+                       uint64_t order_base, int mode) {
     if (!c) return SMORE_EINVAL;
     if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
-    if (c->ntables < 2) return fail(c, SMORE_ESTATE, "DeepWalk needs W and C tables");
+    if (c->ntables < 2) return fail(c, SMORE_ESTATE, "walk models need W and C tables");
     if (!order || walk_times <= 0 || walk_steps < 0 || window <= 0 || K < 0 || K > 10 || mode < 0 || mode > 3)
-        return fail(c, SMORE_EINVAL, "bad DeepWalk arguments");
+        return fail(c, SMORE_EINVAL, "bad DeepWalk / Walklets arguments");
+    if (rule == 1 && (window_min < 0 || window_min > window))
+        return fail(c, SMORE_EINVAL, "Walklets: need 0 <= window_min <= window_max");
+    if (rule == 1 && c->semantics == SMORE_SEM_GO) return fail(c, SMORE_EINVAL, "Walklets has no Go semantics");
     const uint64_t total = (uint64_t)walk_times * (uint64_t)c->g->V;
     if (walk_end > total) walk_end = total;
     if (walk_begin >= walk_end) return SMORE_OK;
     // only this call's walks [walk_begin, walk_end) are read: validate and
     // upload that slice on every call (no caching by host pointer)
     const uint64_t nw_call = walk_end - walk_begin;
+    if (walk_begin < order_base) return fail(c, SMORE_EINVAL, "walk order slice does not cover the range");
+    order -= order_base;   // order[w] is walk w's start
     for (uint64_t i = walk_begin; i < walk_end; ++i)
         if (order[i] < 0 || order[i] >= c->g->V) return fail(c, SMORE_EINVAL, "walk start out of range");
     int rc;
@@ -777,7 +785,7 @@ int smore_train_deepwalk_async(smore_ctx* c, uint64_t walk_begin, uint64_t walk_
     // walk kernel, 2^20 walks per chunk.
     const bool cpp = c->semantics != SMORE_SEM_GO;
     const int RW = rec_width(kmax_of(K));
-    const uint64_t pb = std::max<uint64_t>(1, pair_bound(walk_steps, window));
+    const uint64_t pb = std::max<uint64_t>(1, pair_bound(walk_steps, window, rule, window_min));
     uint64_t chunk_cap = (uint64_t)1 << (cpp ? 18 : 20);
     if (cpp) chunk_cap = std::max<uint64_t>(1, std::min<uint64_t>(chunk_cap, ((uint64_t)1 << 30) / (pb * RW)));
     const uint64_t chunk = std::min<uint64_t>(nw_call, chunk_cap);
@@ -850,6 +858,8 @@ int smore_train_deepwalk_async(smore_ctx* c, uint64_t walk_begin, uint64_t walk_
         w.total_walks = total;
         w.steps = walk_steps;
         w.window = window;
+        w.rule = rule;
+        w.window_min = window_min;
         const int64_t groups_per_block = 256 / lanes_of(c->dpad);
         int g2 = grid;
         if ((int64_t)g2 * groups_per_block > (int64_t)w.nwalks && mode != SMORE_SERIAL)
@@ -878,6 +888,112 @@ int smore_train_deepwalk_async(smore_ctx* c, uint64_t walk_begin, uint64_t walk_
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
     c->phase_n = 0;
+    return SMORE_OK;
+}
+
+int smore_train_deepwalk_async(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, int walk_times,
+                               int walk_steps, int window, int K, double alpha0, uint64_t seed, const int64_t* order,
+                               int mode) {
+    return train_walks(c, 0, walk_begin, walk_end, walk_times, walk_steps, window, 0, K, alpha0, seed, order, 0,
+                       mode);
+}
+
+int smore_train_walklets(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
+                         int window_min, int window_max, int K, double alpha0, uint64_t seed, int mode) {
+    if (!c) return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    // Walklets::Train walks from vid itself (src/model/Walklets.cpp:45): start of walk w = w mod V
+    const uint64_t V = (uint64_t)c->g->V, total = (uint64_t)std::max(0, walk_times) * V;
+    const uint64_t e = std::min(walk_end, total);
+    if (walk_begin >= e) return SMORE_OK;
+    std::vector<int64_t> ord(e - walk_begin);   // starts of walks [walk_begin, e)
+    for (uint64_t w = walk_begin; w < e; ++w) ord[w - walk_begin] = (int64_t)(w % V);
+    int rc = train_walks(c, 1, walk_begin, e, walk_times, walk_steps, window_max, window_min, K, alpha0, seed,
+                         ord.data(), walk_begin, mode);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return SMORE_OK;
+}
+
+int smore_train_app(smore_ctx* c, uint64_t unit_begin, uint64_t unit_end, int walk_times, int sample_times,
+                    double jump, int K, double alpha0, uint64_t seed, const int64_t* order, int mode) {
+    if (!c) return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    if (c->ntables < 2) return fail(c, SMORE_ESTATE, "APP needs W and C tables");
+    if (c->semantics == SMORE_SEM_GO) return fail(c, SMORE_EINVAL, "APP has no Go semantics");
+    // jump <= 0 never ends a walk on a graph without dead ends (the reference
+    // loops forever); the device walk is bounded, but reject it up front
+    if (!order || walk_times <= 0 || sample_times <= 0 || !(jump > 0.0) || K < 0 || K > 10 || mode < 0 || mode > 3)
+        return fail(c, SMORE_EINVAL, "bad APP arguments");
+    const uint64_t total = (uint64_t)walk_times * (uint64_t)c->g->V;
+    const uint64_t units = total * (uint64_t)sample_times;
+    if (unit_end > units) unit_end = units;
+    if (unit_begin >= unit_end) return SMORE_OK;
+    const uint64_t w0 = unit_begin / (uint64_t)sample_times, w1 = (unit_end - 1) / (uint64_t)sample_times + 1;
+    for (uint64_t w = w0; w < w1; ++w)
+        if (order[w] < 0 || order[w] >= c->g->V) return fail(c, SMORE_EINVAL, "walk start out of range");
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    if (c->order_cap < w1 - w0) {
+        dfree(c->d_order);
+        c->order_cap = 0;
+        HIPCHK(c, hipMalloc((void**)&c->d_order, (w1 - w0) * sizeof(int64_t)));
+        c->order_cap = w1 - w0;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_order, order + w0, (w1 - w0) * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+    const int RW = rec_width(kmax_of(K));
+    const uint64_t chunk = std::min<uint64_t>(unit_end - unit_begin, (uint64_t)1 << 25);
+    if (c->rec_cap < chunk * RW) {
+        dfree(c->d_rec);
+        c->rec_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_rec, chunk * RW * sizeof(int32_t)));
+        c->rec_cap = chunk * RW;
+    }
+    EdgeArgs a{};
+    a.sig = c->d_sig;
+    a.W = c->d_table[0];
+    a.C = c->d_table[1];
+    a.skipped = c->d_skipped;
+    a.total = total; a.seed = seed; a.alpha0 = alpha0; a.reg = 0.0f;
+    a.dpad = c->dpad; a.K = K; a.model = SMORE_LINE2; a.mode = mode;
+    a.tcum = c->d_tcum;
+    a.alpha_rec = 1;
+    a.work = c->d_work;
+    a.count = chunk;
+    const int combine = mode == SMORE_HYBRID;
+    a.sh_rows = combine ? std::min(c->sh_max, 8192 / std::max(1, c->dpad)) : 0;
+    const int grid = edge_grid(c, a);
+    if (mode == SMORE_HYBRID) {
+        const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
+        if ((rc = build_hot_maps(c, SMORE_LINE2, K, M))) return rc;
+    }
+    a.g = dev_graph(c);
+    a.sh_rows = combine ? c->sh_rows : 0;
+    a.sh_hash = c->d_sh_hash;
+    a.sh_ids = c->d_sh_ids;
+    a.sh_flush = std::max(1, c->sh_flush_eff);
+    a.rec = c->d_rec;
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    for (uint64_t b = unit_begin; b < unit_end; b += chunk) {
+        AppArgs p;
+        p.order = c->d_order;
+        p.order_base = w0;
+        p.unit_begin = b;
+        p.n = std::min<uint64_t>(chunk, unit_end - b);
+        p.total_walks = total;
+        p.sample_times = sample_times;
+        p.jump = jump;
+        HIPCHK(c, launch_app_records(a.g, p, seed, K, alpha0, c->d_rec, c->stream));
+        EdgeArgs ak = a;
+        ak.begin = 0;
+        ak.count = p.n;
+        HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
+        HIPCHK(c, launch_edge_train(ak, mode == SMORE_SERIAL ? 1 : grid, c->stream));
+    }
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
+    c->phase_n = 0;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     return SMORE_OK;
 }
 

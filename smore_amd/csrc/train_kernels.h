@@ -41,6 +41,17 @@ struct WalkArgs {
     int32_t* lens;                 // nwalks
     uint64_t walk_begin, nwalks, total_walks;
     int steps, window;
+    int rule;                      // pair rule: 0 DeepWalk SkipGrams (random shrink), 1 Walklets ScaleSkipGrams
+    int window_min;                // Walklets: pairs at distance [window_min, window] (clamped as the reference)
+};
+
+// APP: units [unit_begin, unit_begin + n) of walk_times * V * sample_times; unit
+// u = w * sample_times + s jumps from order[w - order_base] (APP::Train)
+struct AppArgs {
+    const int64_t* order;
+    uint64_t order_base, unit_begin, n, total_walks;
+    int sample_times;
+    double jump;
 };
 
 // lanes per sample group: G = min(64, pow2ceil(dpad / SMORE_EPL)); lane l owns
@@ -64,9 +75,12 @@ hipError_t launch_delta_end(float* T, float* S, const float* D, const float* R, 
 hipError_t launch_delta_cycle(float* T, float* S, float* D, float* R, float scale, uint64_t n, int cus,
                               hipStream_t st);
 hipError_t launch_pair_count(const WalkArgs& w, uint64_t seed, uint32_t* count, hipStream_t st);
-// upper bound on the skip-gram pairs of one walk of `steps` steps (window shrink >= 1)
-inline uint64_t pair_bound(int steps, int window) {
-    const uint64_t L = (uint64_t)steps + 1, r = std::min<uint64_t>(2 * (uint64_t)window, L - 1);
+// upper bound on the skip-gram pairs of one walk of `steps` steps: DeepWalk
+// (window shrink >= 1) or Walklets (two clamped ranges of window - window_min + 1)
+inline uint64_t pair_bound(int steps, int window, int rule = 0, int window_min = 0) {
+    const uint64_t L = (uint64_t)steps + 1;
+    if (rule == 1) return L * 2 * (uint64_t)std::max(1, window - window_min + 1);
+    const uint64_t r = std::min<uint64_t>(2 * (uint64_t)window, L - 1);
     return L * r;
 }
 hipError_t scan_pair_counts(const uint32_t* count, uint64_t* off, uint64_t n, void** temp, size_t* temp_bytes,
@@ -87,6 +101,9 @@ hipError_t launch_go_walk(const EdgeArgs& a, const WalkArgs& w, int grid, hipStr
 hipError_t launch_go_sample(const DevGraph& g, const double* tcum, uint64_t seed, uint64_t begin, uint64_t count,
                             int K, int32_t* out, hipStream_t st);
 hipError_t launch_walk_gen(const DevGraph& g, const WalkArgs& w, uint64_t seed, hipStream_t st);
+hipError_t launch_app_records(const DevGraph& g, const AppArgs& p, uint64_t seed, int K, double alpha0, int32_t* rec,
+                              hipStream_t st);
+constexpr int APP_MAX_STEPS = 1 << 24;   // jumping-walk bound (oracle APP_MAX_STEPS)
 // edge kernel instantiations, one per (scatter mode s/a/h, KMAX) (train_edge_*.hip)
 #define SMORE_DECL_EDGE(name)                                                   \
     hipError_t launch_edge_##name(const EdgeArgs& a, int grid, hipStream_t st); \

@@ -1,6 +1,6 @@
-// train_pairs.hip -- DeepWalk skip-gram pairs as sample records for the update
-// kernel (edge_kernels.h), so DeepWalk gets the same row prefetch, chunked
-// scheduling and write-combining as LINE.
+// train_pairs.hip -- DeepWalk / Walklets skip-gram pairs as sample records for
+// the update kernel (edge_kernels.h: pair_train_kernel in the Hogwild modes,
+// edge_train_kernel's serial mode), and APP's jumping-walk pairs.
 //
 // DeepWalk::Train's per-walk body after RandomWalk (src/model/DeepWalk.cpp:
 // 133-139): SkipGrams with the random window shrink (src/proNet.cpp:769-809)
@@ -12,6 +12,9 @@
 //     {walk[i], walk[j], n_1 .. n_K, .., alpha bits at word 2 + KMAX}
 // walk-major in pair order, so a serial update over them is the reference's
 // order.  alpha is DeepWalk's per-walk rate (src/model/DeepWalk.cpp:141-147).
+// Walklets (rule 1, src/model/Walklets.cpp:46-48): walks start at vid in
+// order, pairs of ScaleSkipGrams (src/proNet.cpp:928-987), which draws
+// nothing: the negatives start right after the walk's 2(L-1) draws.
 #include <cstring>
 #include <rocprim/device/device_scan.hpp>
 
@@ -32,17 +35,39 @@ struct WalkWords {   // consecutive Philox words of one walk unit (stream 1)
     }
 };
 
+// Walklets' two ranges around position i (ScaleSkipGrams src/proNet.cpp:928-987,
+// clamped exactly as written: a clamped range may hold i itself, which is skipped)
+struct ScaleRanges {
+    int l0, r0, l1, r1;
+    __device__ ScaleRanges(int i, int L, int wmin, int wmax) {
+        l0 = i - wmax < 0 ? 0 : i - wmax;
+        r0 = i - wmin < 0 ? 0 : i - wmin;
+        l1 = i + wmin >= L ? L - 1 : i + wmin;
+        r1 = i + wmax >= L ? L - 1 : i + wmax;
+    }
+    __device__ static uint32_t span(int l, int r, int i) {
+        return r < l ? 0u : (uint32_t)(r - l + 1) - ((i >= l && i <= r) ? 1u : 0u);
+    }
+};
+
 __global__ void __launch_bounds__(256) pair_count_kernel(WalkArgs w, uint64_t seed, uint32_t* count) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= w.nwalks) return;
     const int L = w.lens[t];
-    WalkWords wd{seed, w.walk_begin + t};
-    const uint32_t win_base = 2u * (uint32_t)(L - 1);
     uint32_t n = 0;
-    for (int i = 0; i < L; ++i) {
-        const int r = (int)draw_index(wd(win_base + (uint32_t)i), (uint32_t)w.window) + 1;
-        const int left = i - r < 0 ? 0 : i - r, right = i + r >= L ? L - 1 : i + r;
-        n += (uint32_t)(right - left);   // [left, right] minus i itself
+    if (w.rule == 1) {
+        for (int i = 0; i < L; ++i) {
+            const ScaleRanges q(i, L, w.window_min, w.window);
+            n += ScaleRanges::span(q.l0, q.r0, i) + ScaleRanges::span(q.l1, q.r1, i);
+        }
+    } else {
+        WalkWords wd{seed, w.walk_begin + t};
+        const uint32_t win_base = 2u * (uint32_t)(L - 1);
+        for (int i = 0; i < L; ++i) {
+            const int r = (int)draw_index(wd(win_base + (uint32_t)i), (uint32_t)w.window) + 1;
+            const int left = i - r < 0 ? 0 : i - r, right = i + r >= L ? L - 1 : i + r;
+            n += (uint32_t)(right - left);   // [left, right] minus i itself
+        }
     }
     count[t] = n;
 }
@@ -59,13 +84,25 @@ __global__ void __launch_bounds__(256) pair_emit_kernel(DevGraph g, WalkArgs w, 
     const float alpha = alpha_walk(unit, alpha0, w.total_walks);
     WalkWords win{seed, unit}, neg{seed, unit};
     const uint32_t win_base = 2u * (uint32_t)(L - 1);
-    uint32_t slot = win_base + (uint32_t)L;
+    // negatives follow the walk's draws (and DeepWalk's L window draws)
+    uint32_t slot = win_base + (w.rule == 1 ? 0u : (uint32_t)L);
     int32_t* out = rec + off[t] * RW;
     for (int i = 0; i < L; ++i) {
-        const int r = (int)draw_index(win(win_base + (uint32_t)i), (uint32_t)w.window) + 1;
-        const int left = i - r < 0 ? 0 : i - r, right = i + r >= L ? L - 1 : i + r;
+        // DeepWalk: one range [i-r, i+r], r = shrunk window; Walklets: two ranges
+        int ranges[2][2];
+        int nr = 1;
+        if (w.rule == 1) {
+            const ScaleRanges q(i, L, w.window_min, w.window);
+            ranges[0][0] = q.l0; ranges[0][1] = q.r0; ranges[1][0] = q.l1; ranges[1][1] = q.r1;
+            nr = 2;
+        } else {
+            const int r = (int)draw_index(win(win_base + (uint32_t)i), (uint32_t)w.window) + 1;
+            ranges[0][0] = i - r < 0 ? 0 : i - r;
+            ranges[0][1] = i + r >= L ? L - 1 : i + r;
+        }
         const int32_t vi = walk[i];
-        for (int j = left; j <= right; ++j) {
+        for (int q = 0; q < nr; ++q)
+        for (int j = ranges[q][0]; j <= ranges[q][1]; ++j) {
             if (j == i) continue;
             int32_t x[RW];
             // W row walk[i] with its W tag, C row walk[j] with its C tag
@@ -128,6 +165,66 @@ hipError_t launch_pair_emit(const DevGraph& g, const WalkArgs& w, uint64_t seed,
         case 10: hipLaunchKernelGGL(pair_emit_kernel<10>, grid, dim3(block), 0, st, g, w, seed, K, alpha0, off, rec); break;
         default: hipLaunchKernelGGL(pair_emit_kernel<20>, grid, dim3(block), 0, st, g, w, seed, K, alpha0, off, rec); break;
     }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- APP
+// APP::Train's sample (src/model/APP.cpp:93-99): JumpingRandomWalk from the
+// start vertex (src/proNet.cpp:685-701: while the vertex has out-edges,
+// TargetSample -- p, then index -- then stop when random_gen(0,1) < jump),
+// then UpdatePair(start, walk.back()) with K negatives (index, then p).  One
+// thread per unit u = w * sample_times + s, all draws from stream 1, unit u,
+// consecutive slots (the oracle's orc_train_app).  One record per unit, so a
+// serial update over the records is the reference's order; consecutive
+// records share the start's W row (pair_train_kernel keeps it in registers).
+template <int KMAX>
+__global__ void __launch_bounds__(256) app_record_kernel(DevGraph g, AppArgs p, uint64_t seed, int K, double alpha0,
+                                                         int32_t* rec) {
+    constexpr int RW = rec_width(KMAX);
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= p.n) return;
+    const uint64_t u = p.unit_begin + t, w = u / (uint64_t)p.sample_times;
+    const int32_t start = (int32_t)p.order[w - p.order_base];
+    WalkWords wd{seed, u};
+    uint32_t slot = 0;
+    int32_t next = start;
+    for (int s = 0; s < APP_MAX_STEPS; ++s) {
+        if (g.offsets[next + 1] - g.offsets[next] == 0) break;
+        const uint32_t kp = wd(slot), ki = wd(slot + 1);
+        next = untag(target_sample(g, next, kp, ki));
+        const double jmp = (double)wd(slot + 2) * 0x1p-32;   // random_gen(0, 1)
+        slot += 3;
+        if (jmp < p.jump) break;
+    }
+    int32_t x[RW];
+    // W row start with its W tag, C row next with its C tag
+    x[0] = start | (int32_t)((g.vtab[start].y >> 31) << 30);
+    x[1] = next | (int32_t)((g.ntab[next].y >> 31) << 30);
+#pragma unroll
+    for (int n = 0; n < RW - 2; ++n) x[2 + n] = -1;
+#pragma unroll
+    for (int n = 0; n < KMAX; ++n) {
+        if (n < K) {
+            const uint32_t ki = wd(slot + 2u * (uint32_t)n), kp = wd(slot + 2u * (uint32_t)n + 1u);
+            const uint32_t ni = draw_index(ki, g.V);
+            x[2 + n] = alias_pick(ni, g.ntab[ni], kp);
+        }
+    }
+    x[2 + KMAX] = __float_as_int(alpha_walk(w, alpha0, p.total_walks));
+    i32x4* o = reinterpret_cast<i32x4*>(rec + t * RW);
+#pragma unroll
+    for (int q = 0; q < RW / 4; ++q) {
+        const i32x4 v = {x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]};
+        __builtin_nontemporal_store(v, o + q);
+    }
+}
+
+hipError_t launch_app_records(const DevGraph& g, const AppArgs& p, uint64_t seed, int K, double alpha0, int32_t* rec,
+                              hipStream_t st) {
+    const int block = 256;
+    const dim3 grid((unsigned)((p.n + block - 1) / block));
+    if (kmax_of(K) == 5) hipLaunchKernelGGL(app_record_kernel<5>, grid, dim3(block), 0, st, g, p, seed, K, alpha0, rec);
+    else hipLaunchKernelGGL(app_record_kernel<10>, grid, dim3(block), 0, st, g, p, seed, K, alpha0, rec);
     return hipGetLastError();
 }
 

@@ -1,5 +1,5 @@
 """Model drivers mirroring the reference's C++ model classes
-(src/model/{LINE,MF,BPR,DeepWalk}.h): LoadEdgeList / Init / Train / SaveWeights
+(src/model/{LINE,MF,BPR,DeepWalk,Walklets,APP}.h): LoadEdgeList / Init / Train / SaveWeights
 with the same argument meaning, banners and learning-rate schedule.  The hot
 loop is one HIP launch per chunk through the C ABI.
 
@@ -174,3 +174,55 @@ class DeepWalk(_EdgeModel):
     @property
     def w_context(self):
         return self.pnet.get_table(_lib.CTX)
+
+
+class Walklets(DeepWalk):
+    """Walklets (src/model/Walklets.{h,cpp}; a DeepWalk subclass there too):
+    walks from every vertex in id order, pairs at distances
+    [window_min, window_max] (ScaleSkipGrams, src/proNet.cpp:928-987)."""
+
+    def Train(self, walk_times, walk_steps, window_min, window_max, negative_samples, alpha, workers=1):
+        print("Model:\n\t[Walklets]\nParameters:")
+        print("\twalk_times:\t\t%d\n\twalk_steps:\t\t%d\n\twindow_min:\t\t%d\n\twindow_max:\t\t%d"
+              "\n\tnegative_samples:\t%d\n\talpha:\t\t\t%g\n\tworkers:\t\t%d"
+              % (walk_times, walk_steps, window_min, window_max, negative_samples, alpha, workers))
+        print("Start Training:")
+        V = self.pnet.MAX_vid
+        total = walk_times * V
+        step = max(1, CHUNK // (walk_steps * 2 * (window_max - window_min + 1) + 1))
+        done = 0
+        while done < total:
+            n = min(step, total - done)
+            self.pnet.train_walklets(done, done + n, walk_times, walk_steps, window_min, window_max,
+                                     negative_samples, alpha, self.seed, self.mode)
+            done += n
+            _progress(max(alpha * (1 - (done // MONITOR * MONITOR) / total), alpha * 1e-4), done / total)
+        print("\tProgress:\t\t100.00 %")
+
+
+class APP(DeepWalk):
+    """APP (src/model/APP.{h,cpp}): per start vertex, sample_times jumping
+    random walks (JumpingRandomWalk, src/proNet.cpp:685-701), UpdatePair of
+    (start, walk end) each; both tables random-initialised, starts shuffled
+    with glibc rand() as DeepWalk's."""
+
+    def Train(self, walk_times, sample_times, jump, negative_samples, alpha, workers=1):
+        print("Model:\n\t[APP]\nLearning Parameters:")
+        print("\twalk_times:\t\t%d\n\tsample_times:\t\t%d\n\tjumping factor:\t\t%g\n\tnegative_samples:\t%d"
+              "\n\talpha:\t\t\t%g\n\tworkers:\t\t%d"
+              % (walk_times, sample_times, jump, negative_samples, alpha, workers))
+        print("Start Training:")
+        V = self.pnet.MAX_vid
+        order = deepwalk_order(V, walk_times, self._rand_used)
+        total = walk_times * V
+        units = total * sample_times
+        step = max(sample_times, CHUNK // sample_times * sample_times)
+        done = 0
+        while done < units:
+            n = min(step, units - done)
+            self.pnet.train_app(done, done + n, walk_times, sample_times, jump, negative_samples, alpha, self.seed,
+                                order, self.mode)
+            done += n
+            w = done // sample_times
+            _progress(max(alpha * (1 - (w // MONITOR * MONITOR) / total), alpha * 1e-4), w / total)
+        print()

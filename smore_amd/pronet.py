@@ -192,6 +192,22 @@ class ProNet:
                                            int(walk_steps), int(window), int(K), float(alpha0), int(seed),
                                            ptr(order), _lib.MODE[mode]), "train_deepwalk")
 
+    def train_walklets(self, walk_begin, walk_end, walk_times, walk_steps, window_min, window_max, K, alpha0, seed,
+                       mode="hogwild"):
+        """Walklets::Train (src/model/Walklets.cpp:24-63) over walks [walk_begin, walk_end)."""
+        self._chk(lib.smore_train_walklets(self.ctx, int(walk_begin), int(walk_end), int(walk_times),
+                                           int(walk_steps), int(window_min), int(window_max), int(K), float(alpha0),
+                                           int(seed), _lib.MODE[mode]), "train_walklets")
+
+    def train_app(self, unit_begin, unit_end, walk_times, sample_times, jump, K, alpha0, seed, order,
+                  mode="hogwild"):
+        """APP::Train (src/model/APP.cpp:59-120) over units [unit_begin, unit_end) of
+        walk_times * V * sample_times; order = walk start vertices (walk_times * V)."""
+        order = np.ascontiguousarray(order, np.int64)
+        self._chk(lib.smore_train_app(self.ctx, int(unit_begin), int(unit_end), int(walk_times), int(sample_times),
+                                      float(jump), int(K), float(alpha0), int(seed), ptr(order), _lib.MODE[mode]),
+                  "train_app")
+
     def set_semantics(self, semantics):
         """"cpp" (src/proNet.cpp rules, default) or "go" (pkg/pronet rules)."""
         self._chk(lib.smore_set_semantics(self.ctx, _lib.SEM[semantics]), "set_semantics")
@@ -331,6 +347,22 @@ class Group:
         self._chk(lib.smore_group_set_graph_edges(self.g, int(V), len(src), ptr(src), ptr(dst), ptr(w),
                                                   _lib.VM[vertex_method], _lib.NM[negative_method]),
                   "set_graph_edges")
+
+    def train_walklets(self, walk_begin, walk_end, walk_times, walk_steps, window_min, window_max, K, alpha0, seed,
+                       mode="hogwild"):
+        """Walklets::Train (src/model/Walklets.cpp:24-63) over walks [walk_begin, walk_end)."""
+        self._chk(lib.smore_train_walklets(self.ctx, int(walk_begin), int(walk_end), int(walk_times),
+                                           int(walk_steps), int(window_min), int(window_max), int(K), float(alpha0),
+                                           int(seed), _lib.MODE[mode]), "train_walklets")
+
+    def train_app(self, unit_begin, unit_end, walk_times, sample_times, jump, K, alpha0, seed, order,
+                  mode="hogwild"):
+        """APP::Train (src/model/APP.cpp:59-120) over units [unit_begin, unit_end) of
+        walk_times * V * sample_times; order = walk start vertices (walk_times * V)."""
+        order = np.ascontiguousarray(order, np.int64)
+        self._chk(lib.smore_train_app(self.ctx, int(unit_begin), int(unit_end), int(walk_times), int(sample_times),
+                                      float(jump), int(K), float(alpha0), int(seed), ptr(order), _lib.MODE[mode]),
+                  "train_app")
 
     def set_semantics(self, semantics):
         self._chk(lib.smore_group_set_semantics(self.g, _lib.SEM[semantics]), "set_semantics")
