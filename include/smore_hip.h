@@ -297,6 +297,15 @@ int smore_train_walklets(smore_ctx* ctx, uint64_t walk_begin, uint64_t walk_end,
 int smore_train_app(smore_ctx* ctx, uint64_t unit_begin, uint64_t unit_end, int walk_times,
                     int sample_times, double jump, int K, double alpha0, uint64_t seed,
                     const int64_t* order, int mode);
+/* replaces: HPE::Train (src/model/HPE.cpp:94-150): samples [begin, begin+count)
+ * of total (= sample_times * 10^6): v1 = SourceSample, v2 = TargetSample(v1),
+ * UpdateCommunity(v1, v2, walk_steps) (src/proNet.cpp:3018-3054, the
+ * regularised Opt_SigmoidRegSGD, :1332-1351) then UpdatePair(v2, v1).  Draws:
+ * stream 0, unit = sample index, consecutive slots.  alpha: count from 0
+ * (src/model/HPE.cpp:133-137).  Sources without out-edges are skipped and
+ * counted (smore_skipped). */
+int smore_train_hpe(smore_ctx* ctx, uint64_t begin, uint64_t count, uint64_t total, int walk_steps,
+                    int K, double reg, double alpha0, uint64_t seed, int mode);
 
 /* ---- samplers (parity tests) -------------------------------------------------------- */
 /* replaces: SourceSample/TargetSample/NegativeSample (src/proNet.cpp:623-683):

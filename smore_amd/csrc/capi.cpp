@@ -997,6 +997,71 @@ int smore_train_app(smore_ctx* c, uint64_t unit_begin, uint64_t unit_end, int wa
     return SMORE_OK;
 }
 
+int smore_train_hpe(smore_ctx* c, uint64_t begin, uint64_t count, uint64_t total, int walk_steps, int K, double reg,
+                    double alpha0, uint64_t seed, int mode) {
+    if (!c) return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    if (c->ntables < 2) return fail(c, SMORE_ESTATE, "HPE needs W and C tables");
+    if (c->semantics == SMORE_SEM_GO) return fail(c, SMORE_EINVAL, "HPE has no Go semantics in this build");
+    if (walk_steps < 1 || walk_steps > 4096 || K < 0 || K > 10 || mode < 0 || mode > 3 || total == 0)
+        return fail(c, SMORE_EINVAL, "bad HPE arguments");
+    if (count == 0) return SMORE_OK;
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    const int RW = rec_width(kmax_of(K));
+    const uint64_t nrec = (uint64_t)walk_steps + 1;
+    const uint64_t chunk = std::min<uint64_t>(count, std::max<uint64_t>(1, ((uint64_t)1 << 27) / nrec));
+    if (c->rec_cap < chunk * nrec * RW) {
+        dfree(c->d_rec);
+        c->rec_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_rec, chunk * nrec * RW * sizeof(int32_t)));
+        c->rec_cap = chunk * nrec * RW;
+    }
+    EdgeArgs a{};
+    a.sig = c->d_sig;
+    a.W = c->d_table[0];
+    a.C = c->d_table[1];
+    a.skipped = c->d_skipped;
+    a.total = total; a.seed = seed; a.alpha0 = alpha0; a.reg = (float)reg;
+    a.dpad = c->dpad; a.K = K; a.model = SMORE_LINE2; a.mode = mode;
+    a.tcum = c->d_tcum;
+    a.alpha_rec = 1;
+    a.work = c->d_work;
+    a.count = chunk * nrec;
+    const int combine = mode == SMORE_HYBRID;
+    a.sh_rows = combine ? std::min(c->sh_max, 8192 / std::max(1, c->dpad)) : 0;
+    const int grid = edge_grid(c, a);
+    if (mode == SMORE_HYBRID) {
+        const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
+        if ((rc = build_hot_maps(c, SMORE_LINE2, K, M))) return rc;
+    }
+    a.g = dev_graph(c);
+    a.sh_rows = combine ? c->sh_rows : 0;
+    a.sh_hash = c->d_sh_hash;
+    a.sh_ids = c->d_sh_ids;
+    a.sh_flush = std::max(1, c->sh_flush_eff);
+    a.rec = c->d_rec;
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    for (uint64_t b = begin; b < begin + count; b += chunk) {
+        HpeArgs p;
+        p.begin = b;
+        p.n = std::min<uint64_t>(chunk, begin + count - b);
+        p.total = total;
+        p.walk_steps = walk_steps;
+        HIPCHK(c, launch_hpe_records(a.g, p, seed, K, alpha0, c->d_rec, c->d_skipped, c->stream));
+        EdgeArgs ak = a;
+        ak.begin = 0;
+        ak.count = p.n * nrec;
+        HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
+        HIPCHK(c, launch_edge_train(ak, mode == SMORE_SERIAL ? 1 : grid, c->stream));
+    }
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
+    c->phase_n = 0;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return SMORE_OK;
+}
+
 int smore_train_deepwalk(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
                          int window, int K, double alpha0, uint64_t seed, const int64_t* order, int mode) {
     int rc = smore_train_deepwalk_async(c, walk_begin, walk_end, walk_times, walk_steps, window, K, alpha0, seed,

@@ -179,15 +179,19 @@ __device__ __forceinline__ void gather_ctx_rows(const EdgeArgs& a, int lane, con
 // SHARED: -1 = runtime (a.model), 0 = two tables (LINE-2), 1 = one table.
 // WOUT false (two tables only): W_v is not scattered; wv returns its new value
 // (the caller keeps it in registers over a run of samples with the same v).
-template <int G, int M, int KMAX, int MODE, int SHARED = -1, bool WOUT = true>
+// REG (two tables only): reg_rt selects Opt_SigmoidRegSGD (src/proNet.cpp:
+// 1332-1351, HPE's UpdateCommunity) instead of Opt_SigmoidSGD at run time:
+// g = label - sig(f); e = fmaf(alpha, g*c - reg*w, e); c = fmaf(alpha, g*w - reg*c, c).
+template <int G, int M, int KMAX, int MODE, int SHARED = -1, bool WOUT = true, bool REG = false>
 __device__ __forceinline__ void sgd_update_rows(const EdgeArgs& a, const float* s_sig, int lane,
                                                 const bool (&ev)[M], int32_t v, const int32_t (&id)[KMAX + 1],
                                                 bool hotw, const bool (&hot)[KMAX + 1], float alpha, bool shared_rt,
                                                 bool mf_rt, const ShState& sh, float (&wv)[M],
-                                                float (&rows)[KMAX + 1][M]) {
+                                                float (&rows)[KMAX + 1][M], bool reg_rt = false) {
     constexpr bool DELTA = MODE == MODE_ATOMIC || MODE == MODE_HYBRID;
     const bool shared = SHARED < 0 ? shared_rt : SHARED == 1;
     const bool mf = SHARED == 0 ? false : mf_rt;
+    const bool regr = (REG && SHARED == 0) ? reg_rt : false;
     const int dpad = a.dpad;
     float* const Tw = a.W;
     float* const Tc = shared ? a.W : a.C;
@@ -256,6 +260,16 @@ __device__ __forceinline__ void sgd_update_rows(const EdgeArgs& a, const float* 
             float nk[M];
             if (mf) {
                 const float gg = (k == 0 ? 1.0f : -1.0f) - f;
+#pragma unroll
+                for (int m = 0; m < M; ++m) {
+                    const float ce = rows[k][m], we = wv[m];
+                    const float t1 = gg * ce - a.reg * we;
+                    const float t2 = gg * we - a.reg * ce;
+                    e[m] = __builtin_fmaf(alpha, t1, e[m]);
+                    nk[m] = __builtin_fmaf(alpha, t2, ce);
+                }
+            } else if (regr) {
+                const float gg = (k == 0 ? 1.0f : 0.0f) - fast_sigmoid(f, s_sig);
 #pragma unroll
                 for (int m = 0; m < M; ++m) {
                     const float ce = rows[k][m], we = wv[m];
@@ -539,12 +553,12 @@ edge_train_kernel(EdgeArgs a) {
     uint32_t round = 0;
     // the update rule on gathered rows
     auto update_rows = [&](int32_t v, const int32_t (&id)[KMAX + 1], bool hotw, const bool (&hot)[KMAX + 1],
-                           float alpha, float (&wv)[M], float (&rows)[KMAX + 1][M]) {
+                           float alpha, float (&wv)[M], float (&rows)[KMAX + 1][M], bool reg) {
         if constexpr (SHARED == 2) {
             if constexpr (KMAX == 5) bpr_update_rows<G, M, KMAX, MODE>(a, s_sig, lane, ev, v, id, hotw, hot, alpha, wv, rows);
         } else {
-            sgd_update_rows<G, M, KMAX, MODE, SHARED>(a, s_sig, lane, ev, v, id, hotw, hot, alpha, shared, mf, sh, wv,
-                                                      rows);
+            sgd_update_rows<G, M, KMAX, MODE, SHARED, true, true>(a, s_sig, lane, ev, v, id, hotw, hot, alpha, shared,
+                                                                  mf, sh, wv, rows, reg);
         }
     };
     // the update of one sample, ids tagged as drawn (c < 0: source without out-edges)
@@ -562,7 +576,8 @@ edge_train_kernel(EdgeArgs a) {
         }
         float wv[M], rows[KMAX + 1][M];
         gather_rows<G, M, KMAX>(a, lane, ev, v, id, shared, wv, rows);
-        update_rows(v, id, scatter_atomic<MODE>(tv), hot, alpha, wv, rows);
+        // word 0 bit 31: HPE community record (Opt_SigmoidRegSGD)
+        update_rows(v, id, scatter_atomic<MODE>(tv), hot, alpha, wv, rows, tv < 0);
     };
     auto maybe_flush = [&]() {
         if constexpr (MODE == MODE_HYBRID) {
@@ -781,8 +796,9 @@ pair_train_kernel(EdgeArgs a) {
                 for (int m = 0; m < M; ++m) wv[m] = wv0[m] = ev[m] ? wp[m * G] : 0.0f;
             }
             gather_ctx_rows<G, M, KMAX>(a, lane, ev, id, rows);
-            sgd_update_rows<G, M, KMAX, MODE, 0, false>(a, s_sig, lane, ev, v, id, false, hot, alpha, false, false, sh,
-                                                        wv, rows);
+            // word 0 bit 31: HPE community record (Opt_SigmoidRegSGD)
+            sgd_update_rows<G, M, KMAX, MODE, 0, false, true>(a, s_sig, lane, ev, v, id, false, hot, alpha, false,
+                                                              false, sh, wv, rows, tv < 0);
             if constexpr (MODE == MODE_HYBRID) {
                 if (sh.n > 0 && ++round == (uint32_t)a.sh_flush) {
                     sh_drain(sh, sh_ids, a.C, a.dpad);

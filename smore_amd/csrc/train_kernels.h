@@ -101,6 +101,14 @@ hipError_t launch_go_walk(const EdgeArgs& a, const WalkArgs& w, int grid, hipStr
 hipError_t launch_go_sample(const DevGraph& g, const double* tcum, uint64_t seed, uint64_t begin, uint64_t count,
                             int K, int32_t* out, hipStream_t st);
 hipError_t launch_walk_gen(const DevGraph& g, const WalkArgs& w, uint64_t seed, hipStream_t st);
+// HPE: samples [begin, begin + n) of total (HPE::Train), walk_steps community
+// steps each
+struct HpeArgs {
+    uint64_t begin, n, total;
+    int walk_steps;
+};
+hipError_t launch_hpe_records(const DevGraph& g, const HpeArgs& p, uint64_t seed, int K, double alpha0, int32_t* rec,
+                              unsigned long long* skipped, hipStream_t st);
 hipError_t launch_app_records(const DevGraph& g, const AppArgs& p, uint64_t seed, int K, double alpha0, int32_t* rec,
                               hipStream_t st);
 constexpr int APP_MAX_STEPS = 1 << 24;   // jumping-walk bound (oracle APP_MAX_STEPS)

@@ -22,14 +22,15 @@
 
 namespace smore {
 
-struct WalkWords {   // consecutive Philox words of one walk unit (stream 1)
+struct WalkWords {   // consecutive Philox words of one unit (walk models: stream 1)
     uint64_t seed, unit;
     uint32_t blk = 0xFFFFFFFFu;
     uint4 b;
+    uint32_t stream = 1;
     __device__ uint32_t operator()(uint32_t slot) {
         if ((slot >> 2) != blk) {
             blk = slot >> 2;
-            b = philox_block(seed, 1, unit, blk);
+            b = philox_block(seed, stream, unit, blk);
         }
         return comp(b, (int)(slot & 3));
     }
@@ -225,6 +226,105 @@ hipError_t launch_app_records(const DevGraph& g, const AppArgs& p, uint64_t seed
     const dim3 grid((unsigned)((p.n + block - 1) / block));
     if (kmax_of(K) == 5) hipLaunchKernelGGL(app_record_kernel<5>, grid, dim3(block), 0, st, g, p, seed, K, alpha0, rec);
     else hipLaunchKernelGGL(app_record_kernel<10>, grid, dim3(block), 0, st, g, p, seed, K, alpha0, rec);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- HPE
+// HPE::Train's sample (src/model/HPE.cpp:118-131): v1 = SourceSample, v2 =
+// TargetSample(v1), UpdateCommunity(v1, v2) (src/proNet.cpp:3018-3054: step j
+// > 0 walks on with TargetSample of the previous context, -1 ends it; each
+// step an Opt_SigmoidRegSGD of W[v1] against the context and K negatives),
+// then UpdatePair(v2, v1).  One thread per sample s, draws from stream 0, unit
+// s, consecutive slots (the oracle's orc_train_hpe); TargetSample on a vertex
+// without out-edges draws nothing.  Emits walk_steps + 1 records per sample:
+// the community steps (word 0 bit 31 set: the regularised rule; word 1 -1
+// after the walk ended) and the pair record {v2, v1}.  A source without
+// out-edges (v2 = -1, undefined in the reference) is skipped and counted.
+template <int KMAX>
+__global__ void __launch_bounds__(256) hpe_record_kernel(DevGraph g, HpeArgs p, uint64_t seed, int K, double alpha0,
+                                                         int32_t* rec, unsigned long long* skipped) {
+    constexpr int RW = rec_width(KMAX);
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= p.n) return;
+    const uint64_t s = p.begin + t;
+    WalkWords wd{seed, s};
+    wd.stream = 0;
+    uint32_t slot = 0;
+    const int nrec = p.walk_steps + 1;
+    i32x4* o = reinterpret_cast<i32x4*>(rec + t * (uint64_t)nrec * RW);
+    const float alpha = alpha_at(s, alpha0, p.total);   // MF/BPR-style count from 0
+    auto put = [&](int j, int32_t w0, int32_t w1, const int32_t (&negs)[KMAX]) {
+        int32_t x[RW];
+        x[0] = w0;
+        x[1] = w1;
+#pragma unroll
+        for (int n = 0; n < RW - 2; ++n) x[2 + n] = -1;
+#pragma unroll
+        for (int n = 0; n < KMAX; ++n) x[2 + n] = negs[n];
+        x[2 + KMAX] = __float_as_int(alpha);
+#pragma unroll
+        for (int q = 0; q < RW / 4; ++q) {
+            const i32x4 v = {x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]};
+            __builtin_nontemporal_store(v, o + (uint64_t)j * (RW / 4) + q);
+        }
+    };
+    auto draw_negs = [&](int32_t (&negs)[KMAX]) {
+#pragma unroll
+        for (int n = 0; n < KMAX; ++n) {
+            negs[n] = -1;
+            if (n < K) {
+                const uint32_t ki = wd(slot), kp = wd(slot + 1);
+                slot += 2;
+                const uint32_t ni = draw_index(ki, g.V);
+                negs[n] = alias_pick(ni, g.ntab[ni], kp);
+            }
+        }
+    };
+    int32_t none[KMAX];
+#pragma unroll
+    for (int n = 0; n < KMAX; ++n) none[n] = -1;
+    const uint32_t kp0 = wd(0), ki0 = wd(1);
+    slot = 2;
+    const int32_t v1 = untag(source_sample(g, kp0, ki0));
+    int32_t ctx = -1, ctxt = -1;
+    if (g.offsets[v1 + 1] - g.offsets[v1] != 0) {
+        ctxt = target_sample(g, v1, wd(slot), wd(slot + 1));
+        slot += 2;
+        ctx = untag(ctxt);
+    }
+    if (ctx < 0) {   // v1 without out-edges: the whole sample is skipped
+        for (int j = 0; j < nrec; ++j) put(j, -1, -1, none);
+        atomicAdd(skipped, 1ull);
+        return;
+    }
+    const int32_t v2 = ctx;
+    int j = 0;
+    for (; j < p.walk_steps; ++j) {
+        if (j != 0) {
+            if (g.offsets[ctx + 1] - g.offsets[ctx] == 0) break;
+            ctxt = target_sample(g, ctx, wd(slot), wd(slot + 1));
+            slot += 2;
+            ctx = untag(ctxt);
+        }
+        int32_t negs[KMAX];
+        draw_negs(negs);
+        put(j, (int32_t)((uint32_t)v1 | 0x80000000u), ctxt, negs);
+    }
+    for (int k = j; k < p.walk_steps; ++k) put(k, (int32_t)((uint32_t)v1 | 0x80000000u), -1, none);
+    int32_t negs[KMAX];
+    draw_negs(negs);
+    // UpdatePair(v2, v1): W row v2 (W tag), C row v1 (C tag)
+    put(p.walk_steps, v2 | (int32_t)((g.vtab[v2].y >> 31) << 30), v1 | (int32_t)((g.ntab[v1].y >> 31) << 30), negs);
+}
+
+hipError_t launch_hpe_records(const DevGraph& g, const HpeArgs& p, uint64_t seed, int K, double alpha0, int32_t* rec,
+                              unsigned long long* skipped, hipStream_t st) {
+    const int block = 256;
+    const dim3 grid((unsigned)((p.n + block - 1) / block));
+    if (kmax_of(K) == 5)
+        hipLaunchKernelGGL(hpe_record_kernel<5>, grid, dim3(block), 0, st, g, p, seed, K, alpha0, rec, skipped);
+    else
+        hipLaunchKernelGGL(hpe_record_kernel<10>, grid, dim3(block), 0, st, g, p, seed, K, alpha0, rec, skipped);
     return hipGetLastError();
 }
 

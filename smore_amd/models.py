@@ -1,5 +1,5 @@
 """Model drivers mirroring the reference's C++ model classes
-(src/model/{LINE,MF,BPR,DeepWalk,Walklets,APP}.h): LoadEdgeList / Init / Train / SaveWeights
+(src/model/{LINE,MF,BPR,DeepWalk,Walklets,APP,HPE}.h): LoadEdgeList / Init / Train / SaveWeights
 with the same argument meaning, banners and learning-rate schedule.  The hot
 loop is one HIP launch per chunk through the C ABI.
 
@@ -226,3 +226,34 @@ class APP(DeepWalk):
             w = done // sample_times
             _progress(max(alpha * (1 - (w // MONITOR * MONITOR) / total), alpha * 1e-4), w / total)
         print()
+
+
+class HPE(LINE):
+    """HPE (src/model/HPE.{h,cpp}; a LINE subclass there too): per sample
+    v1 = SourceSample, v2 = TargetSample(v1), UpdateCommunity(v1, v2) over
+    walk_steps steps (regularised sigmoid rule) then UpdatePair(v2, v1)."""
+
+    def Init(self, dim):
+        print("Model Setting:\n\tdimension:\t\t%d" % dim)
+        self.dim = dim
+        self.order = 2
+        V = self.pnet.MAX_vid
+        self.pnet.alloc_tables(dim, 2)
+        self.pnet.init_table_glibc(_lib.W, 0)           # src/model/HPE.cpp:38-45
+        self.pnet.init_table_glibc(_lib.CTX, V * dim)   # src/model/HPE.cpp:47-52
+
+    def Train(self, sample_times, walk_steps, negative_samples, reg, alpha, workers=1):
+        print("Model:\n\t[HPE]\nLearning Parameters:")
+        print("\tsample_times:\t\t%d\n\tnegative_samples:\t%d\n\twalk_steps:\t\t%d\n\tregularization:\t\t%g"
+              "\n\talpha:\t\t\t%g\n\tworkers:\t\t%d"
+              % (sample_times, negative_samples, walk_steps, reg, alpha, workers))
+        print("Start Training:")
+        total = int(sample_times) * 1000000
+        step = max(1, CHUNK // (walk_steps + 1))
+        done = 0
+        while done < total:
+            n = min(step, total - done)
+            self.pnet.train_hpe(done, n, total, walk_steps, negative_samples, reg, alpha, self.seed, self.mode)
+            done += n
+            _progress(_alpha_at(done, alpha, total), done / total)
+        _progress(_alpha_at(total, alpha, total), 1.0, "\n")

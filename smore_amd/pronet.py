@@ -208,6 +208,11 @@ class ProNet:
                                       float(jump), int(K), float(alpha0), int(seed), ptr(order), _lib.MODE[mode]),
                   "train_app")
 
+    def train_hpe(self, begin, count, total, walk_steps, K, reg, alpha0, seed, mode="hogwild"):
+        """HPE::Train (src/model/HPE.cpp:94-150) over samples [begin, begin + count) of total."""
+        self._chk(lib.smore_train_hpe(self.ctx, int(begin), int(count), int(total), int(walk_steps), int(K),
+                                      float(reg), float(alpha0), int(seed), _lib.MODE[mode]), "train_hpe")
+
     def set_semantics(self, semantics):
         """"cpp" (src/proNet.cpp rules, default) or "go" (pkg/pronet rules)."""
         self._chk(lib.smore_set_semantics(self.ctx, _lib.SEM[semantics]), "set_semantics")

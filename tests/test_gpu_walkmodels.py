@@ -1,13 +1,15 @@
-"""Walklets and APP on the GPU (other UpdatePair consumers on
-the pair-record path).  Needs an MI355X.
+"""Walklets, APP and HPE on the GPU (other UpdatePair consumers
+on the pair-record path).  Needs an MI355X.
 
 Tolerances:
   * serial mode vs the oracle's fp32 spec                 : bit-exact
   * serial mode vs the reference's 1-thread fp64 run      : 1e-5 absolute (north star)
   * Hogwild modes vs serial (held-out training loss)      : within 2 %
-The reference fixtures (tests/golden/e2e_{walklets,app}_pl100w.npz) come from
-oracle/_ref/ref_harness, the reference's Walklets.cpp / APP.cpp compiled
-unmodified (oracle/gen_golden.py).
+  * HPE 10^6-sample run vs the reference (fp64)          : 2e-3 max / 2e-4 median
+    (accumulated fp32 rounding, as DeepWalk's end-to-end test)
+The reference fixtures (tests/golden/e2e_{walklets,app,hpe}_pl100w.npz) come
+from oracle/_ref/ref_harness, the reference's Walklets.cpp / APP.cpp / HPE.cpp
+compiled unmodified (oracle/gen_golden.py).
 """
 import os
 import subprocess
@@ -115,6 +117,55 @@ def test_app_rejects_zero_jump(smore):
         pn.train_app(0, g.V, 1, 1, 0.0, 2, 0.025, SEED, order, "serial")
 
 
+# ---------------------------------------------------------------- HPE
+@pytest.mark.parametrize("dim,K,ws,reg", [(8, 2, 3, 0.01), (64, 5, 5, 0.01), (20, 1, 1, 0.0), (128, 5, 2, 0.1),
+                                          (32, 0, 4, 0.01)])
+def test_hpe_serial_bit_exact_vs_oracle(smore, dim, K, ws, reg):
+    g, pn = make_pair(smore, "pl100w.txt", 1)
+    V = g.V
+    W0, C0 = rand_tables(V, dim, 2, dim + K + ws)
+    pn.alloc_tables(dim, 2)
+    pn.set_table(0, W0)
+    pn.set_table(1, C0)
+    total = 10 ** 6
+    pn.train_hpe(1000, 20000, total, ws, K, reg, 0.025, SEED, "serial")
+    W, C = padded(W0, dim), padded(C0, dim)
+    orc.train_hpe_f32(g, W, C, dim, ws, K, reg, 0.025, total, 1000, 21000, SEED)
+    np.testing.assert_array_equal(pn.get_table(0), W[:, :dim])
+    np.testing.assert_array_equal(pn.get_table(1), C[:, :dim])
+
+
+def test_hpe_directed_bipartite_serial(smore):
+    """A directed bipartite graph (items are sinks: community walks end early);
+    serial bit-exact, skipped-sample count equal to the oracle's."""
+    g, pn = make_pair(smore, "bip.txt", 0)
+    dim = 8
+    pn.alloc_tables(dim, 2)
+    W0, C0 = rand_tables(g.V, dim, 2, 3)
+    pn.set_table(0, W0)
+    pn.set_table(1, C0)
+    before = pn.skipped()
+    pn.train_hpe(0, 30000, 10 ** 6, 3, 2, 0.01, 0.025, SEED, "serial")
+    W, C = padded(W0, dim), padded(C0, dim)
+    sk = orc.train_hpe_f32(g, W, C, dim, 3, 2, 0.01, 0.025, 10 ** 6, 0, 30000, SEED)
+    assert pn.skipped() - before == sk
+    np.testing.assert_array_equal(pn.get_table(0), W[:, :dim])
+    np.testing.assert_array_equal(pn.get_table(1), C[:, :dim])
+
+
+def test_hpe_end_to_end_vs_reference(smore):
+    z = gold("e2e_hpe_pl100w")
+    g, pn = make_pair(smore, "pl100w.txt", 1)
+    pn.alloc_tables(z["W0"].shape[1], 2)
+    pn.set_table(0, z["W0"].astype(np.float32))
+    pn.set_table(1, z["C0"].astype(np.float32))
+    total = 10 ** 6
+    pn.train_hpe(0, total, total, 3, 2, 0.01, 0.025, SEED, "serial")
+    for t, key in ((0, "W"), (1, "C")):
+        d = np.abs(pn.get_table(t) - z[key])
+        assert d.max() < 2e-3 and np.median(d) < 2e-4, (key, d.max(), np.median(d))
+
+
 # ---------------------------------------------------------------- Hogwild modes
 def _heldout(g, model, order, K):
     """Held-out training pairs of the model with K negatives from the negative
@@ -125,6 +176,9 @@ def _heldout(g, model, order, K):
     if model == "walklets":
         keep = draws[:, 1] >= 0
         return draws[keep, 0], draws[keep, 1], negs[keep]
+    if model == "hpe":   # UpdatePair(v2, v1): the reversed edges
+        keep = draws[:, 1] >= 0
+        return draws[keep, 1], draws[keep, 0], negs[keep]
     vc = orc.app_pairs(g, 4, 50, 0.15, SEED + 1, order, 0, 20000)
     return vc[:, 0], vc[:, 1], negs
 
@@ -138,7 +192,7 @@ def _loss(W, C, pv, pc, negs):
     return float(loss.mean())
 
 
-@pytest.mark.parametrize("model", ["walklets", "app"])
+@pytest.mark.parametrize("model", ["walklets", "app", "hpe"])
 def test_parallel_modes_train_like_serial(smore, model):
     """atomic and hybrid (tau 0.3: a mix of hot and cold rows) reach the serial
     order's held-out loss within 2 %; plain-store Hogwild runs and stays finite."""
@@ -154,6 +208,8 @@ def test_parallel_modes_train_like_serial(smore, model):
         pn.set_hot_threshold(0.3)
         if model == "walklets":
             pn.train_walklets(0, 4 * g.V, 4, 20, 1, 4, K, 0.025, SEED, mode)
+        elif model == "hpe":
+            pn.train_hpe(0, 10 ** 6, 10 ** 6, 3, K, 0.01, 0.025, SEED, mode)
         else:
             pn.train_app(0, 4 * g.V * 50, 4, 50, 0.15, K, 0.025, SEED, order, mode)
         W, C = pn.get_table(0), pn.get_table(1)
@@ -187,6 +243,7 @@ def _read_rep(path):
     ("walklets", ["-walk_times", 2, "-walk_steps", 10, "-window_min", 2, "-window_max", 4, "-negative_samples", 2],
      "e2e_walklets_pl100w"),
     ("app", ["-walk_times", 2, "-sample_times", 3, "-jump", 0.15, "-negative_samples", 2], "e2e_app_pl100w"),
+    ("hpe", ["-sample_times", 1, "-walk_steps", 3, "-negative_samples", 2, "-reg", 0.01], "e2e_hpe_pl100w"),
 ])
 def test_cli_vs_reference(tmp_path, tool, args, fixture):
     z = gold(fixture)
@@ -195,4 +252,7 @@ def test_cli_vs_reference(tmp_path, tool, args, fixture):
                "-dimensions", 8, "-alpha", 0.025, "-threads", 1, "-seed", SEED, "-mode", "serial", *args)
     assert "Start Training:" in log
     d = np.abs(_read_rep(out) - z["W"])
-    assert d.max() < 2e-5, d.max()   # 1e-5 arithmetic + the 6-significant-digit text format
+    if tool == "hpe":   # 10^6 samples: accumulated fp32 rounding (as DeepWalk's CLI test)
+        assert d.max() < 2e-3 and np.median(d) < 2e-4, (d.max(), np.median(d))
+    else:
+        assert d.max() < 2e-5, d.max()   # 1e-5 arithmetic + the 6-significant-digit text format
