@@ -216,12 +216,16 @@ def main():
     upd_s = upd_ms / 1e3 / args.steps if upd_ms > 0 else step_s       # update-kernel time per step
     launch_s = upd_ms / 1e3 / launches if launches else step_s         # per update launch (rocprof average)
     achieved = R_upd * S / upd_s / 1e9
-    traffic, traffic_src = None, None
+    # PMC traffic (FETCH_SIZE x 2 + WRITE_SIZE, tools/pmc_summary.py) of this
+    # config from a committed rocprofv3 --pmc run: per step (draw + update
+    # kernel, one launch each) and per update launch
+    traffic = traffic_upd = traffic_src = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         p = json.load(open(pmc))
         if p.get("config") == args.config and p.get("samples") == S and p.get("mode") == args.mode:
-            traffic = p.get("hbm_bytes_per_launch")   # FETCH_SIZE + WRITE_SIZE per update launch
+            traffic = p.get("hbm_bytes_per_step", p.get("hbm_bytes_per_launch"))
+            traffic_upd = p.get("hbm_bytes_per_launch")
             traffic_src = "profiles/pmc_traffic.json: rocprofv3 --pmc of this config (%s)" % p.get("round", "")
     copy_peak = measured_copy_peak(torch) if rank == 0 else 0.0
     Wt = pn.get_table(0)
@@ -258,9 +262,11 @@ def main():
                          "traffic_source": traffic_src,
                          "bytes_per_update_read": R, "bytes_per_update_write": Wb,
                          "ms_per_step": round(step_s * 1e3, 3),
+                         "traffic_per_algorithmic": (round(traffic / ((R + Wb) * S), 3) if traffic else None),
                          "measured_peak": {"copy_GBs": round(copy_peak, 1),
-                                           "frac": round(R * S / step_s / 1e9 / copy_peak, 4),
-                                           "note": "device-to-device copy, read+write bytes / time"},
+                                           "frac": round((R + Wb) * S / step_s / 1e9 / copy_peak, 4),
+                                           "note": "the path's algorithmic read+write bytes per second over a "
+                                                   "device-to-device copy's read+write bytes per second"},
                          "kernel": {"name": "edge_train_kernel (gather/update/scatter)",
                                     "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
                                     "bytes_per_update_read": R_upd, "bytes_per_update_write": Wb,
@@ -268,7 +274,8 @@ def main():
                                     "ms_per_launch": round(launch_s * 1e3, 3),
                                     "launches_per_step": round(launches / args.steps, 2),
                                     "update_ms_per_step": round(upd_s * 1e3, 3),
-                                    "exposed_draw_ms_per_step": round(draw_ms / args.steps, 3)}},
+                                    "exposed_draw_ms_per_step": round(draw_ms / args.steps, 3),
+                                    "traffic": traffic_upd}},
             "cpu_baseline": cpu,
             "skipped_samples": int(skipped),
         }

@@ -12,7 +12,12 @@ random 256-B rows from a 5-GB table, known byte counts): FETCH_SIZE reads
 float atomics).  Fetched bytes are therefore FETCH_SIZE x 2.
 
     python tools/pmc_summary.py --fetch F.csv --write W.csv --stats S.csv \
-        --config c4 --samples 134217728 --mode hybrid --out profiles/pmc_traffic.json
+        --config c4 --samples 134217728 --mode hybrid --out profiles/pmc_traffic.json \
+        [--kernel edge_train_kernel] [--step draw_kernel --round r02]
+
+With --step, the output holds the per-launch traffic of --kernel (the update
+kernel) and of each --step kernel, and hbm_bytes_per_step = their sum: one
+bench step launches each once (bench.py reads it as roofline.traffic).
 """
 import argparse
 import csv
@@ -39,16 +44,35 @@ def main():
     ap.add_argument("--samples", type=int, required=True)
     ap.add_argument("--mode", required=True)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--step", nargs="*", default=[])
+    ap.add_argument("--round", default="")
     a = ap.parse_args()
-    f, nf = per_dispatch(a.fetch, a.kernel)
+    one = summarize(a, a.kernel)
+    if not a.step:
+        json.dump(one, open(a.out, "w"), indent=1)
+        print(json.dumps(one))
+        return
+    parts = {a.kernel: one}
+    for k in a.step:
+        parts[k] = summarize(a, k)
+    out = {"round": a.round, "config": a.config, "samples": a.samples, "mode": a.mode,
+           "hbm_bytes_per_step": sum(p["hbm_bytes_per_launch"] for p in parts.values()),
+           "bytes_per_sample_step": sum(p["hbm_bytes_per_launch"] for p in parts.values()) / a.samples,
+           "hbm_bytes_per_launch": one["hbm_bytes_per_launch"], "kernels": parts}
+    json.dump(out, open(a.out, "w"), indent=1)
+    print(json.dumps(out))
+
+
+def summarize(a, kernel):
+    f, nf = per_dispatch(a.fetch, kernel)
     f_raw = f
     f = f * FETCH_CORRECTION
-    w, nw = per_dispatch(a.write, a.kernel)
-    stats = [r for r in csv.DictReader(open(a.stats)) if a.kernel in r["Name"]]
+    w, nw = per_dispatch(a.write, kernel)
+    stats = [r for r in csv.DictReader(open(a.stats)) if kernel in r["Name"]]
     avg_ns = float(stats[0]["AverageNs"]) if stats else None
     out = {
         "config": a.config, "samples": a.samples, "mode": a.mode,
-        "kernel": stats[0]["Name"] if stats else a.kernel,
+        "kernel": stats[0]["Name"] if stats else kernel,
         "dispatches_fetch": nf, "dispatches_write": nw,
         "fetch_size_kb_raw": f_raw, "fetch_kb_corrected": f, "write_size_kb": w,
         "hbm_bytes_per_launch": (f + w) * 1024.0,
@@ -59,8 +83,7 @@ def main():
                 "fetch = FETCH_SIZE x 2 (gfx950 half-count, calibrated in profiles/pmc_calibration.json); "
                 "includes Infinity-Cache hits",
     }
-    json.dump(out, open(a.out, "w"), indent=1)
-    print(json.dumps(out))
+    return out
 
 
 if __name__ == "__main__":
