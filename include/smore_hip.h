@@ -319,11 +319,16 @@ int smore_sample_edges(smore_ctx* ctx, int model, uint64_t begin, uint64_t count
 /* replaces: proNet::LoadPreTrain (src/proNet.cpp:238-286), DeepWalk -load_v /
  * -load_c (cli/deepwalk.cpp:61-62): rows of a SaveWeights-format file whose
  * names are vertices of the loaded graph overwrite those rows of the table;
- * a file whose dimension differs is skipped, as in the reference. */
+ * a file whose dimension differs is skipped, as in the reference.  A raw
+ * dump (smore_save_weights fmt 2) is read by vertex id. */
 int smore_load_pretrain(smore_ctx* ctx, int which, const char* path);
 /* replaces: SaveWeights (src/model/LINE.cpp:13-47; Go line.go:209-233):
  * "V dim" header then "name v1 ... vdim" per vertex.  fmt 0 = C++ ostream
- * default (%g, 6 significant digits), fmt 1 = Go "%.6f". */
+ * default (%g, 6 significant digits), fmt 1 = Go "%.6f"; rows are formatted by
+ * all host threads ($SMORE_SAVE_THREADS), byte-identical to a sequential loop.
+ * fmt 2 (new; checkpoint/resume): the raw fp32 table, "SMRAW1\0\0", int64 V,
+ * int32 dim, int32 0, then V x dim floats in vertex-id order;
+ * smore_load_pretrain reads it back (same V and dim, else skipped). */
 int smore_save_weights(const smore_ctx* ctx, int which, const char* path, int fmt);
 
 #ifdef __cplusplus

@@ -225,6 +225,7 @@ int smore_alloc_tables(smore_ctx* c, int dim, int ntables) {
     if (const char* e = getenv("SMORE_TABLE_MEM")) {
         if (!strcmp(e, "coarse")) flags = hipDeviceMallocDefault;
         else if (!strcmp(e, "finegrained")) flags = hipDeviceMallocFinegrained;
+        else if (!strcmp(e, "contiguous")) flags = hipDeviceMallocContiguous;
     }
     for (int t = 0; t < ntables; ++t) {
         HIPCHK(c, hipExtMallocWithFlags((void**)&c->d_table[t], bytes, flags));
@@ -736,7 +737,7 @@ int smore_save_weights(const smore_ctx* cc, int which, const char* path, int fmt
     smore_ctx* c = const_cast<smore_ctx*>(cc);
     int rc;
     if ((rc = check_table(c, which))) return rc;
-    if (!path) return SMORE_EINVAL;
+    if (!path || fmt < 0 || fmt > 2) return fail(c, SMORE_EINVAL, "save_weights: bad path or format");
     std::vector<float> h((size_t)c->g->V * c->dpad);
     if ((rc = set_device(c))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));

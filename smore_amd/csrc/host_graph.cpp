@@ -370,11 +370,32 @@ void deepwalk_order(int64_t V, int walk_times, uint64_t skip, int64_t* order) {
 }
 
 // ---------------------------------------------------------------- warm start
+// header of the raw fp32 table dump (save_weights fmt 2)
+static const char RAW_MAGIC[8] = {'S', 'M', 'R', 'A', 'W', '1', 0, 0};
+
 bool load_pretrain(const std::string& path, const HostGraph& g, float* table, int dim, int stride,
                    int64_t* loaded, std::string& err) {
     *loaded = 0;
     FILE* f = fopen(path.c_str(), "rb");
     if (!f) { err = "cannot open " + path; return false; }
+    {   // raw fp32 dump of save_weights fmt 2: rows are vertex ids
+        char magic[8];
+        if (fread(magic, 1, 8, f) == 8 && std::memcmp(magic, RAW_MAGIC, 8) == 0) {
+            int64_t n = 0;
+            int32_t hd[2] = {0, 0};
+            if (fread(&n, 8, 1, f) != 1 || fread(hd, 4, 2, f) != 2) { fclose(f); err = "truncated " + path; return false; }
+            if (hd[0] != dim || n != g.V) { fclose(f); *loaded = -1; return true; }
+            std::vector<float> row((size_t)dim);
+            for (int64_t v = 0; v < n; ++v) {
+                if (fread(row.data(), 4, (size_t)dim, f) != (size_t)dim) { fclose(f); err = "truncated " + path; return false; }
+                std::copy(row.begin(), row.end(), table + v * stride);
+            }
+            fclose(f);
+            *loaded = n;
+            return true;
+        }
+        rewind(f);
+    }
     std::string line;
     auto getline = [&](std::string& out) -> bool {
         out.clear();
@@ -423,24 +444,62 @@ bool load_pretrain(const std::string& path, const HostGraph& g, float* table, in
 }
 
 // ---------------------------------------------------------------- saver
+// Rows are formatted by all host threads in blocks (each thread snprintf's its
+// block into its own buffer: glibc's exact %g / %.6f), then written in order,
+// so the file is byte-identical to a sequential fprintf loop.  fmt 2 writes the
+// raw fp32 matrix (RAW_MAGIC, int64 rows, int32 dim, int32 0, rows x dim
+// floats) that load_pretrain reads back by vertex id.
 bool save_weights(const std::string& path, const HostGraph& g, const float* table, int64_t rows,
                   int dim, int stride, int fmt, std::string& err) {
     FILE* f = fopen(path.c_str(), "wb");
     if (!f) { err = "cannot open " + path; return false; }
-    std::vector<char> obuf(1 << 22);
-    setvbuf(f, obuf.data(), _IOFBF, obuf.size());
-    fprintf(f, "%lld %d\n", (long long)rows, dim);
-    for (int64_t v = 0; v < rows; ++v) {
-        if (!g.names.empty()) fputs(g.names[v].c_str(), f);
-        else fprintf(f, "%lld", (long long)v);
-        const float* r = table + v * stride;
-        for (int d = 0; d < dim; ++d) {
-            if (fmt == 1) fprintf(f, " %.6f", (double)r[d]);
-            else fprintf(f, " %g", (double)r[d]);
+    bool ok = true;
+    if (fmt == 2) {
+        const int64_t r64 = rows;
+        const int32_t hd[2] = {dim, 0};
+        ok = fwrite(RAW_MAGIC, 1, 8, f) == 8 && fwrite(&r64, 8, 1, f) == 1 && fwrite(hd, 4, 2, f) == 2;
+        std::vector<float> buf;
+        const int64_t blk = 1 << 16;
+        for (int64_t b = 0; ok && b < rows; b += blk) {
+            const int64_t n = std::min(blk, rows - b);
+            buf.resize((size_t)(n * dim));
+            for (int64_t v = 0; v < n; ++v) std::memcpy(&buf[(size_t)(v * dim)], table + (b + v) * stride, dim * 4);
+            ok = fwrite(buf.data(), 4, buf.size(), f) == buf.size();
         }
-        fputc('\n', f);
+    } else {
+        fprintf(f, "%lld %d\n", (long long)rows, dim);
+        int threads = (int)std::max(1u, std::thread::hardware_concurrency());
+        if (const char* e = getenv("SMORE_SAVE_THREADS")) threads = std::max(1, atoi(e));
+        threads = std::min(threads, 64);
+        const int64_t blk = 8192;
+        std::vector<std::string> out((size_t)threads);
+        auto format = [&](int t, int64_t b0) {
+            std::string& o = out[(size_t)t];
+            o.clear();
+            const int64_t lo = b0 + t * blk, hi = std::min(rows, lo + blk);
+            char num[64];
+            for (int64_t v = lo; v < hi; ++v) {
+                if (!g.names.empty()) o += g.names[(size_t)v];
+                else o += std::to_string((long long)v);
+                const float* r = table + v * stride;
+                for (int d = 0; d < dim; ++d) {
+                    const int k = snprintf(num, sizeof num, fmt == 1 ? " %.6f" : " %g", (double)r[d]);
+                    o.append(num, (size_t)k);
+                }
+                o.push_back('\n');
+            }
+        };
+        for (int64_t b0 = 0; ok && b0 < rows; b0 += blk * threads) {
+            std::vector<std::thread> pool;
+            for (int t = 1; t < threads; ++t) pool.emplace_back(format, t, b0);
+            format(0, b0);
+            for (auto& th : pool) th.join();
+            for (int t = 0; ok && t < threads; ++t)
+                ok = out[(size_t)t].empty() || fwrite(out[(size_t)t].data(), 1, out[(size_t)t].size(), f) ==
+                                                   out[(size_t)t].size();
+        }
     }
-    bool ok = fclose(f) == 0;
+    ok = (fclose(f) == 0) && ok;
     if (!ok) err = "write failed: " + path;
     return ok;
 }

@@ -446,3 +446,40 @@ def test_chunked_overlapped_draws(smore):
         assert ph is not None and ph[2] == (1 if chunk is None else -(-(total - 1) // int(chunk)))
         res[chunk] = _auc(W, C, g, np.random.default_rng(0))
     assert abs(res[None] - res["65536"]) < 0.02, res
+
+
+@pytest.mark.parametrize("fmt,spec", [(0, "%g"), (1, "%.6f")])
+def test_save_weights_parallel_text_is_exact(smore, tmp_path, fmt, spec):
+    """The multi-threaded saver writes exactly the sequential printf text
+    (C++ ostream default / Go %.6f), over more rows than one thread block."""
+    g, pn = make_pair(smore, "pl1k.txt", 1)
+    dim = 7
+    pn.alloc_tables(dim, 1)
+    W0 = (np.random.default_rng(4).standard_normal((g.V, dim)) * 10.0 ** np.random.default_rng(5).integers(
+        -6, 4, (g.V, dim))).astype(np.float32)
+    pn.set_table(0, W0)
+    p = str(tmp_path / "rep.txt")
+    os.environ["SMORE_SAVE_THREADS"] = "3"
+    try:
+        pn.save_weights(0, p, fmt)
+    finally:
+        del os.environ["SMORE_SAVE_THREADS"]
+    expect = ["%d %d" % (g.V, dim)]
+    for v in range(g.V):
+        expect.append(g.names[v] + "".join(" " + spec % float(x) for x in W0[v]))
+    assert open(p).read() == "\n".join(expect) + "\n"
+
+
+def test_save_weights_raw_roundtrip(smore, tmp_path):
+    """fmt 2: raw fp32 dump, read back bit-exactly by load_pretrain."""
+    _, pn = make_pair(smore, "pl100w.txt", 1)
+    dim = 13
+    pn.alloc_tables(dim, 2)
+    W0 = np.random.default_rng(9).standard_normal((pn.MAX_vid, dim)).astype(np.float32)
+    pn.set_table(0, W0)
+    p = str(tmp_path / "w.raw")
+    pn.save_weights(0, p, 2)
+    assert os.path.getsize(p) == 24 + 4 * W0.size
+    pn.zero_table(1)
+    pn.load_pretrain(1, p)
+    np.testing.assert_array_equal(pn.get_table(1), W0)
