@@ -227,10 +227,8 @@ int smore_alloc_tables(smore_ctx* c, int dim, int ntables) {
         else if (!strcmp(e, "finegrained")) flags = hipDeviceMallocFinegrained;
         else if (!strcmp(e, "contiguous")) flags = hipDeviceMallocContiguous;
     }
-    for (int t = 0; t < ntables; ++t) {
-        HIPCHK(c, hipExtMallocWithFlags((void**)&c->d_table[t], bytes, flags));
-        HIPCHK(c, hipMemset(c->d_table[t], 0, bytes));
-    }
+    for (int t = 0; t < ntables; ++t) HIPCHK(c, hipExtMallocWithFlags((void**)&c->d_table[t], bytes, flags));
+    for (int t = 0; t < ntables; ++t) HIPCHK(c, hipMemset(c->d_table[t], 0, bytes));
     return SMORE_OK;
 }
 
