@@ -85,11 +85,13 @@ int smore_load_edgelist(smore_ctx* ctx, const char* path, int undirected,
 /* loader options (new): the text is parsed by all host threads
  * (ids still in order of first appearance).  With a cache directory (this call,
  * or $SMORE_CACHE_DIR), the parsed names and edge slots are stored there under
- * a hash of the input bytes and read back on later loads of the same input.
+ * a hash of the input bytes, and the built graph (CSR, degrees, alias tables)
+ * under that hash and the sampling methods; later loads of the same input read
+ * the built graph back (or, for other methods, the edge slots).
  * dir NULL or "" = no cache. */
 int smore_set_load_cache(smore_ctx* ctx, const char* dir);
 /* the last smore_load_edgelist: wall seconds of the text/cache stage, parser
- * threads, 1 if it was served from the cache */
+ * threads, cache_hit 1 = edge slots from the cache, 2 = the built graph */
 int smore_last_load_info(const smore_ctx* ctx, double* seconds, int* threads, int* cache_hit);
 /* replaces: the graph half of LoadEdgeList + BuildAliasMethod
  * (src/proNet.cpp:410-542) for callers that already hold ids: E directed

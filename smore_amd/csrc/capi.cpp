@@ -101,17 +101,38 @@ int smore_set_graph_edges(smore_ctx* c, int64_t V, int64_t E, const int32_t* src
 
 int smore_load_edgelist(smore_ctx* c, const char* path, int undirected, int vm, int nm) {
     if (!c || !path) return SMORE_EINVAL;
+    if (vm < 0 || vm > 2 || nm < 0 || nm > 2) return fail(c, SMORE_EINVAL, "bad arguments");
     std::vector<std::string> names;
     std::vector<int32_t> src, dst;
     std::vector<double> w;
     const char* cache = !c->cache_dir.empty() ? c->cache_dir.c_str() : getenv("SMORE_CACHE_DIR");
     const auto t0 = std::chrono::steady_clock::now();
+    // with a cache directory: the built graph of this input and these methods,
+    // if an earlier load stored it (no parse, no CSR / alias build)
+    std::string gfile;
+    uint64_t key = 0;
+    if (cache && *cache && edgelist_key(path, undirected != 0, &key, c->err)) {
+        char name[96];
+        snprintf(name, sizeof name, "/%016llx-v%dn%d.smoregc", (unsigned long long)key, vm, nm);
+        gfile = std::string(cache) + name;
+        auto g = std::make_shared<HostGraph>();
+        if (load_graph_cache(gfile, key, vm, nm, *g)) {
+            c->g = g;
+            c->hot_key.clear();
+            c->semantics = SMORE_SEM_CPP;
+            c->load_stats = LoadStats();
+            c->load_stats.cache_hit = 2;
+            c->load_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            return upload_graph(c);
+        }
+    }
     if (!read_edgelist(path, undirected != 0, names, src, dst, w, c->err, cache, &c->load_stats)) return SMORE_EIO;
     c->load_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (names.empty()) return fail(c, SMORE_EIO, std::string("no edges in ") + path);
     int rc = smore_set_graph_edges(c, (int64_t)names.size(), (int64_t)src.size(), src.data(), dst.data(),
                                    w.data(), vm, nm);
     if (rc == SMORE_OK) c->g->names = std::move(names);
+    if (rc == SMORE_OK && !gfile.empty()) (void)save_graph_cache(gfile, key, *c->g);
     return rc;
 }
 
@@ -159,9 +180,9 @@ int smore_set_alias(smore_ctx* c, int which, const double* prob, const int64_t* 
         if (alias[i] >= lim || alias[i] < -1 || !(prob[i] >= 0)) return fail(c, SMORE_EINVAL, "alias entry out of range");
         if (which != SMORE_AT_CONTEXT && alias[i] >= g.V) return fail(c, SMORE_EINVAL, "alias out of range");
     }
-    std::vector<double>& P = which == 0 ? g.vprob : which == 1 ? g.nprob : g.cprob;
-    std::vector<int64_t>& A = which == 0 ? g.valias : which == 1 ? g.nalias : g.calias;
-    std::vector<AliasEntry>& T = which == 0 ? g.vtab : which == 1 ? g.ntab : g.ctab;
+    hvec<double>& P = which == 0 ? g.vprob : which == 1 ? g.nprob : g.cprob;
+    hvec<int64_t>& A = which == 0 ? g.valias : which == 1 ? g.nalias : g.calias;
+    hvec<AliasEntry>& T = which == 0 ? g.vtab : which == 1 ? g.ntab : g.ctab;
     P.assign(prob, prob + n);
     A.assign(alias, alias + n);
     c->hot_key.clear();
@@ -178,8 +199,8 @@ int smore_set_alias(smore_ctx* c, int which, const double* prob, const int64_t* 
 int smore_get_alias(const smore_ctx* c, int which, double* prob, int64_t* alias, int64_t n) {
     if (!c || !c->has_graph || which < 0 || which > 2) return SMORE_EINVAL;
     const HostGraph& g = *c->g;
-    const std::vector<double>& P = which == 0 ? g.vprob : which == 1 ? g.nprob : g.cprob;
-    const std::vector<int64_t>& A = which == 0 ? g.valias : which == 1 ? g.nalias : g.calias;
+    const hvec<double>& P = which == 0 ? g.vprob : which == 1 ? g.nprob : g.cprob;
+    const hvec<int64_t>& A = which == 0 ? g.valias : which == 1 ? g.nalias : g.calias;
     if (n != (int64_t)P.size()) return SMORE_EINVAL;
     if (prob) memcpy(prob, P.data(), n * sizeof(double));
     if (alias) memcpy(alias, A.data(), n * sizeof(int64_t));
@@ -189,7 +210,7 @@ int smore_get_alias(const smore_ctx* c, int which, double* prob, int64_t* alias,
 int smore_get_alias_encoded(const smore_ctx* c, int which, uint32_t* thresh, int32_t* alias, int64_t n) {
     if (!c || !c->has_graph || which < 0 || which > 2) return SMORE_EINVAL;
     const HostGraph& g = *c->g;
-    const std::vector<AliasEntry>& T = which == 0 ? g.vtab : which == 1 ? g.ntab : g.ctab;
+    const hvec<AliasEntry>& T = which == 0 ? g.vtab : which == 1 ? g.ntab : g.ctab;
     if (n != (int64_t)T.size()) return SMORE_EINVAL;
     for (int64_t i = 0; i < n; ++i) {
         if (thresh) thresh[i] = T[i].thresh;
@@ -377,8 +398,8 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
         }
     }
     const HostGraph& g = *c->g;
-    auto tag_tab = [&](const std::vector<AliasEntry>& tab, const std::vector<uint8_t>& hot) {
-        std::vector<AliasEntry> t(tab);
+    auto tag_tab = [&](const hvec<AliasEntry>& tab, const std::vector<uint8_t>& hot) {
+        std::vector<AliasEntry> t(tab.begin(), tab.end());
         for (int64_t i = 0; i < V; ++i) {
             const uint32_t al = (uint32_t)t[i].alias;
             t[i].alias = (int32_t)(al | ((uint32_t)hot[al] << 30) | ((uint32_t)hot[i] << 31));

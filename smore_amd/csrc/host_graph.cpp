@@ -304,7 +304,7 @@ void build_cpp_vn_tables(HostGraph& g) {
     alias_encode(g.nprob.data(), g.nalias.data(), V, nullptr, g.ntab.data());
 }
 
-static void alias_marginal(const std::vector<double>& prob, const std::vector<int64_t>& alias, int64_t off,
+static void alias_marginal(const hvec<double>& prob, const hvec<int64_t>& alias, int64_t off,
                            int64_t n, const int32_t* self_ids, double scale, std::vector<double>& p) {
     for (int64_t i = 0; i < n; ++i) {
         const double pr = prob[off + i];

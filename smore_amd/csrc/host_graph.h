@@ -6,7 +6,9 @@
 // reference code it replaces (RainBoltz/smore, C++ proNet-core).
 #pragma once
 #include <cstdint>
+#include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace smore {
@@ -16,19 +18,40 @@ struct AliasEntry {          // device encoding of one alias-table entry (8 B)
     int32_t alias;           // id returned otherwise (self when always accepted)
 };
 
+// std::allocator whose value-less construct() default-initialises: resize()
+// of a trivial element type leaves the memory untouched, so multi-GB graph
+// arrays are first touched (page-faulted) by the threads that fill them
+template <class T>
+struct UninitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = UninitAlloc<U>;
+    };
+    UninitAlloc() = default;
+    template <class U>
+    UninitAlloc(const UninitAlloc<U>&) {}
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        if constexpr (sizeof...(A) == 0) ::new ((void*)p) U;
+        else ::new ((void*)p) U(std::forward<A>(a)...);
+    }
+};
+template <class T>
+using hvec = std::vector<T, UninitAlloc<T>>;
+
 struct HostGraph {
     int64_t V = 0, E = 0;
     int vertex_method = 0, negative_method = 0;
     std::vector<std::string> names;          // empty when built from ids
-    std::vector<int64_t> offsets;            // V+1
-    std::vector<int32_t> targets;            // E, push order per source
-    std::vector<double> weights;             // E
-    std::vector<double> out_deg, in_deg;     // V
+    hvec<int64_t> offsets;                   // V+1
+    hvec<int32_t> targets;                   // E, push order per source
+    hvec<double> weights;                    // E
+    hvec<double> out_deg, in_deg;            // V
     // reference representation (prob, alias with -1 = none)
-    std::vector<double> vprob, nprob, cprob;
-    std::vector<int64_t> valias, nalias, calias;
+    hvec<double> vprob, nprob, cprob;
+    hvec<int64_t> valias, nalias, calias;
     // device encoding
-    std::vector<AliasEntry> vtab, ntab, ctab;
+    hvec<AliasEntry> vtab, ntab, ctab;
 };
 
 // Vose alias method, C++ rule (src/proNet.cpp:544-620): q = d^0.75 * n / sum
@@ -71,6 +94,11 @@ struct LoadStats {
 bool read_edgelist(const std::string& path, bool undirected, std::vector<std::string>& names,
                    std::vector<int32_t>& src, std::vector<int32_t>& dst, std::vector<double>& w,
                    std::string& err, const char* cache_dir = nullptr, LoadStats* stats = nullptr);
+// Built-graph cache (names, CSR, degrees, all alias tables) of one input and
+// sampling methods, keyed by the same content hash: <dir>/<key>-v<vm>n<nm>.smoregc.
+bool edgelist_key(const std::string& path, bool undirected, uint64_t* key, std::string& err);
+bool save_graph_cache(const std::string& file, uint64_t key, const HostGraph& g);
+bool load_graph_cache(const std::string& file, uint64_t key, int vm, int nm, HostGraph& g);
 
 // glibc TYPE_3 rand() stream after srand(1) (the reference's Init).
 class GlibcRand {

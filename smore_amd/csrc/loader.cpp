@@ -278,7 +278,187 @@ bool load_cache(const std::string& fn, uint64_t key, std::vector<std::string>& n
     return ok;
 }
 
+uint64_t content_key(const std::vector<std::unique_ptr<Mapped>>& maps, bool undirected, unsigned nt) {
+    uint64_t key = hash_bytes(undirected ? "u1" : "u0", 2);
+    for (const auto& m : maps) {
+        const size_t parts = std::max<size_t>(1, std::min<size_t>(nt, m->n / (1 << 22) + 1));
+        std::vector<uint64_t> ph(parts);
+        run_threads((unsigned)parts, [&](unsigned t) {
+            const size_t b = m->n * t / parts, e = m->n * (t + 1) / parts;
+            ph[t] = hash_bytes(m->p + b, e - b);
+        });
+        for (uint64_t h : ph) key = (key ^ h) * 0x9E3779B97F4A7C15ull + (uint64_t)m->n;
+    }
+    return key;
+}
+
+// ---------------------------------------------------------------- built-graph cache
+// The whole HostGraph of one (input, undirected, vertex method, negative
+// method): names, CSR, degrees, the three alias tables in both
+// representations.  Arrays are read back with parallel pread()s.
+constexpr char GRAPH_MAGIC[8] = {'S', 'M', 'O', 'R', 'E', 'G', 'C', '1'};
+
+struct Blk {   // one array of the file
+    void* p;
+    size_t bytes;
+};
+
+std::vector<Blk> graph_blocks(HostGraph& g, std::string& names_blob, bool weights_one) {
+    const size_t V = (size_t)g.V, E = (size_t)g.E;
+    std::vector<Blk> b = {{&names_blob[0], names_blob.size()},
+                          {g.offsets.data(), (V + 1) * 8}, {g.targets.data(), E * 4},
+                          {g.out_deg.data(), V * 8}, {g.in_deg.data(), V * 8},
+                          {g.vprob.data(), V * 8}, {g.valias.data(), V * 8},
+                          {g.nprob.data(), V * 8}, {g.nalias.data(), V * 8},
+                          {g.cprob.data(), E * 8}, {g.calias.data(), E * 8},
+                          {g.vtab.data(), V * 8}, {g.ntab.data(), V * 8}, {g.ctab.data(), E * 8}};
+    if (!weights_one) b.push_back({g.weights.data(), E * 8});
+    return b;
+}
+
 }  // namespace
+
+bool edgelist_key(const std::string& path, bool undirected, uint64_t* key, std::string& err) {
+    const std::vector<std::string> files = input_files(path, err);
+    if (files.empty()) return false;
+    std::vector<std::unique_ptr<Mapped>> maps;
+    size_t total = 0;
+    for (const auto& fn : files) {
+        maps.emplace_back(new Mapped());
+        if (!maps.back()->ok(err, fn)) return false;
+        total += maps.back()->n;
+    }
+    *key = content_key(maps, undirected, threads_for(total));
+    return true;
+}
+
+bool save_graph_cache(const std::string& fn, uint64_t key, const HostGraph& gc) {
+    HostGraph& g = const_cast<HostGraph&>(gc);
+    const std::string tmp = fn + ".tmp" + std::to_string((long)getpid());
+    const int fd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd < 0) return false;
+    std::string blob;
+    for (const auto& s : g.names) { blob += s; blob.push_back('\n'); }
+    bool one = true;
+    for (double x : g.weights) if (x != 1.0) { one = false; break; }
+    const uint64_t hdr[8] = {key, (uint64_t)g.V, (uint64_t)g.E, (uint64_t)g.vertex_method,
+                             (uint64_t)g.negative_method, (uint64_t)blob.size(), one ? 1ull : 0ull,
+                             (uint64_t)g.names.size()};
+    bool ok = pwrite(fd, GRAPH_MAGIC, 8, 0) == 8 && pwrite(fd, hdr, sizeof hdr, 8) == (ssize_t)sizeof hdr;
+    if (blob.empty()) blob.push_back('\0');   // graph_blocks takes &blob[0]; 0-byte blocks write nothing
+    std::vector<Blk> blks = graph_blocks(g, blob, one);
+    blks[0].bytes = (size_t)hdr[5];
+    // the arrays in <= 64-MiB pieces written by all host threads
+    struct Piece { size_t off; const char* src; size_t n; };
+    std::vector<Piece> pcs;
+    size_t off = 8 + sizeof hdr;
+    for (const Blk& b : blks) {
+        for (size_t o = 0; o < b.bytes; o += (size_t)1 << 26)
+            pcs.push_back({off + o, (const char*)b.p + o, std::min<size_t>((size_t)1 << 26, b.bytes - o)});
+        off += b.bytes;
+    }
+    std::atomic<size_t> next(0);
+    std::atomic<bool> good(ok);
+    run_threads(std::max(1u, std::min<unsigned>(threads_for(off), 16u)), [&](unsigned) {
+        for (size_t i; good && (i = next++) < pcs.size();) {
+            size_t done = 0;
+            while (done < pcs[i].n) {
+                const ssize_t r = pwrite(fd, pcs[i].src + done, pcs[i].n - done, (off_t)(pcs[i].off + done));
+                if (r <= 0) { good = false; return; }
+                done += (size_t)r;
+            }
+        }
+    });
+    ok = (close(fd) == 0) && good;
+    if (ok) ok = rename(tmp.c_str(), fn.c_str()) == 0;
+    if (!ok) unlink(tmp.c_str());
+    return ok;
+}
+
+bool load_graph_cache(const std::string& fn, uint64_t key, int vm, int nm, HostGraph& g) {
+    const bool verbose = getenv("SMORE_LOAD_VERBOSE") != nullptr;
+    auto tick = std::chrono::steady_clock::now();
+    auto phase = [&](const char* what) {
+        if (!verbose) return;
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[graph cache] %-10s %.2f s\n", what, std::chrono::duration<double>(now - tick).count());
+        tick = now;
+    };
+    const int fd = open(fn.c_str(), O_RDONLY);
+    if (fd < 0) return false;
+    char magic[8];
+    uint64_t hdr[8];
+    bool ok = pread(fd, magic, 8, 0) == 8 && memcmp(magic, GRAPH_MAGIC, 8) == 0 &&
+              pread(fd, hdr, sizeof hdr, 8) == (ssize_t)sizeof hdr && hdr[0] == key && hdr[3] == (uint64_t)vm &&
+              hdr[4] == (uint64_t)nm;
+    if (!ok) { close(fd); return false; }
+    const size_t V = hdr[1], E = hdr[2];
+    g.V = (int64_t)V; g.E = (int64_t)E; g.vertex_method = vm; g.negative_method = nm;
+    g.offsets.resize(V + 1); g.targets.resize(E); g.weights.resize(E);
+    g.out_deg.resize(V); g.in_deg.resize(V);
+    g.vprob.resize(V); g.valias.resize(V); g.nprob.resize(V); g.nalias.resize(V);
+    g.cprob.resize(E); g.calias.resize(E);
+    g.vtab.resize(V); g.ntab.resize(V); g.ctab.resize(E);
+    std::string blob(std::max<uint64_t>(hdr[5], 1), '\0');
+    phase("allocate");
+    std::vector<Blk> blks = graph_blocks(g, blob, hdr[6] != 0);
+    blks[0].bytes = (size_t)hdr[5];
+    // (file offset, destination, bytes) pieces of <= 64 MiB over all host threads
+    struct Piece { size_t off; char* dst; size_t n; };
+    std::vector<Piece> pcs;
+    size_t off = 8 + sizeof hdr;
+    for (const Blk& b : blks) {
+        for (size_t o = 0; o < b.bytes; o += (size_t)1 << 26)
+            pcs.push_back({off + o, (char*)b.p + o, std::min<size_t>((size_t)1 << 26, b.bytes - o)});
+        off += b.bytes;
+    }
+    std::atomic<size_t> next(0);
+    std::atomic<bool> good(true);
+    run_threads(std::max(1u, std::min<unsigned>(threads_for(off), 32u)), [&](unsigned) {
+        for (size_t i; (i = next++) < pcs.size();) {
+            size_t done = 0;
+            while (done < pcs[i].n) {
+                const ssize_t r = pread(fd, pcs[i].dst + done, pcs[i].n - done, (off_t)(pcs[i].off + done));
+                if (r <= 0) { good = false; return; }
+                done += (size_t)r;
+            }
+        }
+    });
+    close(fd);
+    phase("read");
+    if (!good) return false;
+    if (hdr[6]) {   // all-one weights are not stored: fill them on every thread
+        const unsigned nf = std::max(1u, std::min<unsigned>(threads_for(E * 8), 32u));
+        run_threads(nf, [&](unsigned t) {
+            std::fill(g.weights.begin() + (ptrdiff_t)(E * t / nf), g.weights.begin() + (ptrdiff_t)(E * (t + 1) / nf),
+                      1.0);
+        });
+    }
+    // names: newline-separated; threads take byte ranges, count their lines,
+    // then fill their slice of the pre-sized vector
+    const size_t nb = (size_t)hdr[5];
+    const unsigned nt = std::max(1u, std::min<unsigned>(threads_for(nb), 32u));
+    std::vector<size_t> lo(nt + 1), cnt(nt + 1, 0);
+    for (unsigned t = 0; t <= nt; ++t) {   // range starts just after a newline
+        size_t b = nb * t / nt;
+        while (b > 0 && b < nb && blob[b - 1] != '\n') ++b;
+        lo[t] = t == nt ? nb : b;
+    }
+    run_threads(nt, [&](unsigned t) {
+        for (size_t i = lo[t]; i < lo[t + 1]; ++i) cnt[t + 1] += blob[i] == '\n';
+    });
+    for (unsigned t = 0; t < nt; ++t) cnt[t + 1] += cnt[t];
+    if (cnt[nt] != hdr[7]) return false;
+    g.names.clear();
+    g.names.resize(hdr[7]);
+    run_threads(nt, [&](unsigned t) {
+        size_t k = cnt[t], st = lo[t];
+        for (size_t i = lo[t]; i < lo[t + 1]; ++i)
+            if (blob[i] == '\n') { g.names[k++].assign(blob, st, i - st); st = i + 1; }
+    });
+    phase("names");
+    return true;
+}
 
 bool read_edgelist(const std::string& path, bool undirected, std::vector<std::string>& names,
                    std::vector<int32_t>& src, std::vector<int32_t>& dst, std::vector<double>& w,
@@ -302,16 +482,7 @@ bool read_edgelist(const std::string& path, bool undirected, std::vector<std::st
     std::string cache_file;
     uint64_t key = 0;
     if (cache_dir && *cache_dir) {
-        key = hash_bytes(undirected ? "u1" : "u0", 2);
-        for (const auto& m : maps) {
-            const size_t parts = std::max<size_t>(1, std::min<size_t>(nt, m->n / (1 << 22) + 1));
-            std::vector<uint64_t> ph(parts);
-            run_threads((unsigned)parts, [&](unsigned t) {
-                const size_t b = m->n * t / parts, e = m->n * (t + 1) / parts;
-                ph[t] = hash_bytes(m->p + b, e - b);
-            });
-            for (uint64_t h : ph) key = (key ^ h) * 0x9E3779B97F4A7C15ull + (uint64_t)m->n;
-        }
+        key = content_key(maps, undirected, nt);
         char name[64];
         snprintf(name, sizeof name, "/%016llx.smorelc", (unsigned long long)key);
         cache_file = std::string(cache_dir) + name;

@@ -70,10 +70,11 @@ class ProNet:
         self._chk(lib.smore_set_load_cache(self.ctx, directory.encode() if directory else None), "set_load_cache")
 
     def last_load_info(self):
-        """(seconds, parser threads, served from cache) of the last LoadEdgeList."""
+        """(seconds, parser threads, cache hit: 0 none, 1 edge slots, 2 the built graph)
+        of the last LoadEdgeList."""
         sec, th, hit = C.c_double(), C.c_int(), C.c_int()
         self._chk(lib.smore_last_load_info(self.ctx, C.byref(sec), C.byref(th), C.byref(hit)), "last_load_info")
-        return sec.value, th.value, bool(hit.value)
+        return sec.value, th.value, hit.value
 
     def set_graph_edges(self, V, src, dst, w):
         """Graph from ids: directed edge slots src->dst (weight w) in push order."""

@@ -128,3 +128,38 @@ def test_binary_cache_roundtrip(tmp_path):
         f.write("\nnewa newb 1\n")
     n4, _, _, i4 = _load(path, 1, cache=cache)
     assert not i4[2] and n4[-2:] == ["newa", "newb"]
+
+
+def test_built_graph_cache(tmp_path):
+    """A second load of the same input with the same sampling methods reads the
+    built graph (CSR, degrees, every alias table) back: identical to a fresh
+    build; other methods fall back to the cached edge slots and build."""
+    import smore_amd
+    path = str(tmp_path / "g.txt")
+    _ragged_file(path, lines=50_000)
+    cache = str(tmp_path / "cache")
+    os.makedirs(cache)
+
+    def load(vm, nm):
+        pn = smore_amd.ProNet(-1)
+        pn.set_load_cache(cache)
+        pn.SetVertexMethod(vm)
+        pn.SetNegativeMethod(nm)
+        pn.LoadEdgeList(path, 1)
+        tabs = [pn.alias(w) + pn.alias_encoded(w) for w in range(3)]
+        return pn.last_load_info()[2], pn.names, pn.csr(), tabs
+
+    h1, n1, c1, t1 = load("out_degrees", "degrees")
+    assert h1 == 0 and len([f for f in os.listdir(cache) if f.endswith(".smoregc")]) == 1
+    h2, n2, c2, t2 = load("out_degrees", "degrees")
+    assert h2 == 2, "second load did not read the built graph"
+    h3, n3, c3, t3 = load("degrees", "in_degrees")
+    assert h3 == 1 and len([f for f in os.listdir(cache) if f.endswith(".smoregc")]) == 2
+    assert n1 == n2 == n3
+    for a, b in zip(c1 + c3, c2 + c3):
+        np.testing.assert_array_equal(a, b)
+    for x, y in zip(t1, t2):
+        for a, b in zip(x, y):
+            np.testing.assert_array_equal(a, b)
+    # the methods matter: the negative tables differ between the two builds
+    assert not np.array_equal(t1[1][0], t3[1][0])
