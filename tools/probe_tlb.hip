@@ -8,7 +8,7 @@
 //   alloc 2: VMM: 1-GiB-aligned VA, physical memory in 1-GiB hipMemCreate chunks
 //   alloc 3: VMM with the minimum granularity chunks (2 MiB)
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/probe_tlb tools/probe_tlb.hip
-// Run:   tools/probe_tlb [reps=5]
+// Run:   tools/probe_tlb [reps=5] [uniform ids=0|1] [kinds=3]
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 
@@ -105,6 +105,8 @@ struct Zipf {
 
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 5;
+    const bool uniform = argc > 2 && atoi(argv[2]) == 1;   // 1: uniform row ids instead of Zipf ranks
+    const int kinds = argc > 3 ? atoi(argv[3]) : 3;         // allocation kinds to run (0..kinds-1)
     const long V = 10000000, n = 1 << 24;
     const size_t bytes = (size_t)V * 64 * sizeof(float);
     int cus = 0;
@@ -114,7 +116,7 @@ int main(int argc, char** argv) {
     CHK(hipMalloc(&sink, 4));
     CHK(hipMalloc(&ids, n * 8 * sizeof(int)));
     {
-        Zipf z6(V, 0.6), z8(V, 0.8);
+        Zipf z6(V, uniform ? 0.0 : 0.6), z8(V, uniform ? 0.0 : 0.8);
         std::mt19937_64 rng(1);
         std::uniform_real_distribution<double> U(0, 1);
         std::vector<int> perm(V);
@@ -133,7 +135,7 @@ int main(int argc, char** argv) {
     CHK(hipEventCreate(&a));
     CHK(hipEventCreate(&b));
     const char* names[] = {"hipMalloc", "uncached", "vmm_1GiB_chunks", "vmm_min_chunks"};
-    for (int kind = 0; kind < 4; ++kind) {
+    for (int kind = 0; kind < kinds; ++kind) {
         for (int r = 0; r < reps; ++r) {
             float *W = nullptr, *C = nullptr;
             Vmm mw, mc;
@@ -159,8 +161,8 @@ int main(int argc, char** argv) {
                 CHK(hipEventElapsedTime(&ms, a, b));
                 best = std::min(best, ms);
             }
-            printf("{\"alloc\": \"%s\", \"rep\": %d, \"W\": \"%p\", \"C\": \"%p\", \"ms\": %.3f, "
-                   "\"Msamples_per_s\": %.1f}\n", names[kind], r, (void*)W, (void*)C, best, n / best / 1e3);
+            printf("{\"ids\": \"%s\", \"alloc\": \"%s\", \"rep\": %d, \"W\": \"%p\", \"C\": \"%p\", \"ms\": %.3f, "
+                   "\"Msamples_per_s\": %.1f}\n", uniform ? "uniform" : "zipf", names[kind], r, (void*)W, (void*)C, best, n / best / 1e3);
             fflush(stdout);
             if (kind <= 1) { CHK(hipFree(W)); CHK(hipFree(C)); }
             else { vmm_free(mw); vmm_free(mc); }
