@@ -1,5 +1,5 @@
 """Parity at the benchmark configurations' sizes and shapes:
-C2 (LINE-2, 1M vertices / 20M lines), C3 (BPR, 2M x 1M / 100M edges, d=128),
+C2 (LINE-2, 1M vertices / 20M lines; also Walklets, APP, HPE on that graph), C3 (BPR, 2M x 1M / 100M edges, d=128),
 C5 (DeepWalk d=128, 40 steps, window 5, K=5), the full-grid default hybrid
 scatter, the replica-exchange kernels with R != D, and DeepWalk context-buffer
 reuse.  Needs an MI355X.
@@ -77,6 +77,43 @@ def test_c2_serial_bit_exact(c2):
     orc.train_edge_f32(g, "line2", W0, C0, dim, K, 0.025, 0.0, total, begin, begin + 20_000, SEED)
     np.testing.assert_array_equal(pn.get_table(0), W0)
     np.testing.assert_array_equal(pn.get_table(1), C0)
+
+
+def test_c2_walklets_app_hpe_serial_bit_exact(c2):
+    """The other UpdatePair consumers (Walklets, APP, HPE) on the C2 graph
+    (1M vertices / 40M slots, d=64, K=5): serial mode bit-exact vs the oracle's
+    fp32 spec over ranges far from the start."""
+    import smore_amd
+    g, pn = c2
+    dim, K = 64, 5
+    W0, C0 = rand_tables(g.V, dim, 2, 77)
+    # Walklets: walks [500_000, 501_000) of walk_times 2, 40 steps, windows 1..5
+    pn.alloc_tables(dim, 2)
+    pn.set_table(0, W0)
+    pn.set_table(1, C0)
+    W, C = W0.copy(), C0.copy()
+    pn.train_walklets(500_000, 501_000, 2, 40, 1, 5, K, 0.025, SEED, "serial")
+    orc.train_walklets_f32(g, W, C, dim, 2, 40, 1, 5, K, 0.025, SEED, 500_000, 501_000)
+    np.testing.assert_array_equal(pn.get_table(0), W)
+    np.testing.assert_array_equal(pn.get_table(1), C)
+    # APP: units [3_000_000, 3_005_000) of walk_times 1, 10 samples per start
+    order = smore_amd.deepwalk_order(g.V, 1, 2 * g.V * dim)
+    pn.set_table(0, W0)
+    pn.set_table(1, C0)
+    W, C = W0.copy(), C0.copy()
+    pn.train_app(3_000_000, 3_005_000, 1, 10, 0.15, K, 0.025, SEED, order, "serial")
+    orc.train_app_f32(g, W, C, dim, 1, 10, 0.15, K, 0.025, SEED, order, 3_000_000, 3_005_000)
+    np.testing.assert_array_equal(pn.get_table(0), W)
+    np.testing.assert_array_equal(pn.get_table(1), C)
+    # HPE: samples [10^9, 10^9 + 5000) of 2 * 10^9, walk_steps 5
+    pn.set_table(0, W0)
+    pn.set_table(1, C0)
+    W, C = W0.copy(), C0.copy()
+    total = 2 * 10 ** 9
+    pn.train_hpe(10 ** 9, 5000, total, 5, K, 0.01, 0.025, SEED, "serial")
+    orc.train_hpe_f32(g, W, C, dim, 5, K, 0.01, 0.025, total, 10 ** 9, 10 ** 9 + 5000, SEED)
+    np.testing.assert_array_equal(pn.get_table(0), W)
+    np.testing.assert_array_equal(pn.get_table(1), C)
 
 
 def test_c2_full_grid_hybrid_matches_atomic(c2):
