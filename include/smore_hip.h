@@ -263,6 +263,15 @@ int smore_group_train_edges(smore_group* g, int model, uint64_t begin, uint64_t 
 int smore_group_train_deepwalk(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
                                int walk_steps, int window, int K, double alpha0, uint64_t seed,
                                const int64_t* order, int mode, uint64_t per, int mean);
+/* per = walks / APP units / HPE samples per replica per exchange (0: 2^18 / 2^24 / 2^24) */
+int smore_group_train_walklets(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
+                               int walk_steps, int window_min, int window_max, int K, double alpha0,
+                               uint64_t seed, int mode, uint64_t per, int mean);
+int smore_group_train_app(smore_group* g, uint64_t unit_begin, uint64_t unit_end, int walk_times,
+                          int sample_times, double jump, int K, double alpha0, uint64_t seed,
+                          const int64_t* order, int mode, uint64_t per, int mean);
+int smore_group_train_hpe(smore_group* g, uint64_t begin, uint64_t count, uint64_t total, int walk_steps,
+                          int K, double reg, double alpha0, uint64_t seed, int mode, uint64_t per, int mean);
 
 /* replaces: DeepWalk::Train (src/model/DeepWalk.cpp:98-155): walks
  * [walk_begin, walk_end) of walk_times*V, start vertices order[] (host,
@@ -308,6 +317,16 @@ int smore_train_app(smore_ctx* ctx, uint64_t unit_begin, uint64_t unit_end, int 
  * counted (smore_skipped). */
 int smore_train_hpe(smore_ctx* ctx, uint64_t begin, uint64_t count, uint64_t total, int walk_steps,
                     int K, double reg, double alpha0, uint64_t seed, int mode);
+/* the same three, returning once the work is queued on the context stream
+ * (order[] must stay valid until the context synchronizes) */
+int smore_train_walklets_async(smore_ctx* ctx, uint64_t walk_begin, uint64_t walk_end, int walk_times,
+                               int walk_steps, int window_min, int window_max, int K, double alpha0,
+                               uint64_t seed, int mode);
+int smore_train_app_async(smore_ctx* ctx, uint64_t unit_begin, uint64_t unit_end, int walk_times,
+                          int sample_times, double jump, int K, double alpha0, uint64_t seed,
+                          const int64_t* order, int mode);
+int smore_train_hpe_async(smore_ctx* ctx, uint64_t begin, uint64_t count, uint64_t total, int walk_steps,
+                          int K, double reg, double alpha0, uint64_t seed, int mode);
 
 /* ---- samplers (parity tests) -------------------------------------------------------- */
 /* replaces: SourceSample/TargetSample/NegativeSample (src/proNet.cpp:623-683):

@@ -89,6 +89,12 @@ def _load():
         "smore_train_walklets": (i32, [P, u64, u64, i32, i32, i32, i32, i32, dbl, u64, i32]),
         "smore_train_app": (i32, [P, u64, u64, i32, i32, dbl, i32, dbl, u64, P, i32]),
         "smore_train_hpe": (i32, [P, u64, u64, u64, i32, i32, dbl, dbl, u64, i32]),
+        "smore_train_walklets_async": (i32, [P, u64, u64, i32, i32, i32, i32, i32, dbl, u64, i32]),
+        "smore_train_app_async": (i32, [P, u64, u64, i32, i32, dbl, i32, dbl, u64, P, i32]),
+        "smore_train_hpe_async": (i32, [P, u64, u64, u64, i32, i32, dbl, dbl, u64, i32]),
+        "smore_group_train_walklets": (i32, [P, u64, u64, i32, i32, i32, i32, i32, dbl, u64, i32, u64, i32]),
+        "smore_group_train_app": (i32, [P, u64, u64, i32, i32, dbl, i32, dbl, u64, P, i32, u64, i32]),
+        "smore_group_train_hpe": (i32, [P, u64, u64, u64, i32, i32, dbl, dbl, u64, i32, u64, i32]),
         "smore_sample_edges": (i32, [P, i32, u64, u64, i32, u64, P]),
         "smore_save_weights": (i32, [P, i32, C.c_char_p, i32]),
         "smore_load_pretrain": (i32, [P, i32, C.c_char_p]),

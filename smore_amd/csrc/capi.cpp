@@ -774,7 +774,7 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
     if (!c) return SMORE_EINVAL;
     if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
     if (c->ntables < 2) return fail(c, SMORE_ESTATE, "walk models need W and C tables");
-    if (!order || walk_times <= 0 || walk_steps < 0 || window <= 0 || K < 0 || K > 10 || mode < 0 || mode > 3)
+    if ((!order && rule != 1) || walk_times <= 0 || walk_steps < 0 || window <= 0 || K < 0 || K > 10 || mode < 0 || mode > 3)
         return fail(c, SMORE_EINVAL, "bad DeepWalk / Walklets arguments");
     if (rule == 1 && (window_min < 0 || window_min > window))
         return fail(c, SMORE_EINVAL, "Walklets: need 0 <= window_min <= window_max");
@@ -785,20 +785,25 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
     // only this call's walks [walk_begin, walk_end) are read: validate and
     // upload that slice on every call (no caching by host pointer)
     const uint64_t nw_call = walk_end - walk_begin;
-    if (walk_begin < order_base) return fail(c, SMORE_EINVAL, "walk order slice does not cover the range");
-    order -= order_base;   // order[w] is walk w's start
-    for (uint64_t i = walk_begin; i < walk_end; ++i)
-        if (order[i] < 0 || order[i] >= c->g->V) return fail(c, SMORE_EINVAL, "walk start out of range");
     int rc;
+    if (order) {
+        if (walk_begin < order_base) return fail(c, SMORE_EINVAL, "walk order slice does not cover the range");
+        order -= order_base;   // order[w] is walk w's start
+        for (uint64_t i = walk_begin; i < walk_end; ++i)
+            if (order[i] < 0 || order[i] >= c->g->V) return fail(c, SMORE_EINVAL, "walk start out of range");
+    }
     if ((rc = set_device(c))) return rc;
-    if (c->order_cap < nw_call) {
+    if (!order) {
+        // starts computed on the device (walk mod V)
+    } else if (c->order_cap < nw_call) {
         dfree(c->d_order);
         c->order_cap = 0;
         HIPCHK(c, hipMalloc((void**)&c->d_order, nw_call * sizeof(int64_t)));
         c->order_cap = nw_call;
     }
-    HIPCHK(c, hipMemcpyAsync(c->d_order, order + walk_begin, nw_call * sizeof(int64_t), hipMemcpyHostToDevice,
-                             c->stream));
+    if (order)
+        HIPCHK(c, hipMemcpyAsync(c->d_order, order + walk_begin, nw_call * sizeof(int64_t), hipMemcpyHostToDevice,
+                                 c->stream));
     // C++ semantics: walks -> pair records -> update kernel; chunks of up to
     // 2^18 walks whose pair records (sized by the per-walk upper bound, so no
     // host read-back of the pair count) stay under 4 GiB.  Go semantics: fused
@@ -869,7 +874,7 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     for (uint64_t b = walk_begin; b < walk_end; b += chunk) {
         WalkArgs w;
-        w.order = c->d_order;
+        w.order = order ? c->d_order : nullptr;
         w.order_base = walk_begin;
         w.walks = c->d_walks;
         w.lens = c->d_lens;
@@ -918,25 +923,28 @@ int smore_train_deepwalk_async(smore_ctx* c, uint64_t walk_begin, uint64_t walk_
                        mode);
 }
 
-int smore_train_walklets(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
-                         int window_min, int window_max, int K, double alpha0, uint64_t seed, int mode) {
+int smore_train_walklets_async(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
+                               int window_min, int window_max, int K, double alpha0, uint64_t seed, int mode) {
     if (!c) return SMORE_EINVAL;
     if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
-    // Walklets::Train walks from vid itself (src/model/Walklets.cpp:45): start of walk w = w mod V
-    const uint64_t V = (uint64_t)c->g->V, total = (uint64_t)std::max(0, walk_times) * V;
-    const uint64_t e = std::min(walk_end, total);
-    if (walk_begin >= e) return SMORE_OK;
-    std::vector<int64_t> ord(e - walk_begin);   // starts of walks [walk_begin, e)
-    for (uint64_t w = walk_begin; w < e; ++w) ord[w - walk_begin] = (int64_t)(w % V);
-    int rc = train_walks(c, 1, walk_begin, e, walk_times, walk_steps, window_max, window_min, K, alpha0, seed,
-                         ord.data(), walk_begin, mode);
+    if (walk_times <= 0) return fail(c, SMORE_EINVAL, "bad DeepWalk / Walklets arguments");
+    // Walklets::Train walks from vid itself (src/model/Walklets.cpp:45): no
+    // order array, the walk kernel starts walk w at w mod V
+    return train_walks(c, 1, walk_begin, walk_end, walk_times, walk_steps, window_max, window_min, K, alpha0, seed,
+                       nullptr, 0, mode);
+}
+
+int smore_train_walklets(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
+                         int window_min, int window_max, int K, double alpha0, uint64_t seed, int mode) {
+    int rc = smore_train_walklets_async(c, walk_begin, walk_end, walk_times, walk_steps, window_min, window_max, K,
+                                        alpha0, seed, mode);
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return SMORE_OK;
 }
 
-int smore_train_app(smore_ctx* c, uint64_t unit_begin, uint64_t unit_end, int walk_times, int sample_times,
-                    double jump, int K, double alpha0, uint64_t seed, const int64_t* order, int mode) {
+int smore_train_app_async(smore_ctx* c, uint64_t unit_begin, uint64_t unit_end, int walk_times, int sample_times,
+                          double jump, int K, double alpha0, uint64_t seed, const int64_t* order, int mode) {
     if (!c) return SMORE_EINVAL;
     if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
     if (c->ntables < 2) return fail(c, SMORE_ESTATE, "APP needs W and C tables");
@@ -1013,12 +1021,20 @@ int smore_train_app(smore_ctx* c, uint64_t unit_begin, uint64_t unit_end, int wa
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
     c->phase_n = 0;
+    return SMORE_OK;
+}
+
+int smore_train_app(smore_ctx* c, uint64_t unit_begin, uint64_t unit_end, int walk_times, int sample_times,
+                    double jump, int K, double alpha0, uint64_t seed, const int64_t* order, int mode) {
+    int rc = smore_train_app_async(c, unit_begin, unit_end, walk_times, sample_times, jump, K, alpha0, seed, order,
+                                   mode);
+    if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return SMORE_OK;
 }
 
-int smore_train_hpe(smore_ctx* c, uint64_t begin, uint64_t count, uint64_t total, int walk_steps, int K, double reg,
-                    double alpha0, uint64_t seed, int mode) {
+int smore_train_hpe_async(smore_ctx* c, uint64_t begin, uint64_t count, uint64_t total, int walk_steps, int K,
+                          double reg, double alpha0, uint64_t seed, int mode) {
     if (!c) return SMORE_EINVAL;
     if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
     if (c->ntables < 2) return fail(c, SMORE_ESTATE, "HPE needs W and C tables");
@@ -1078,6 +1094,13 @@ int smore_train_hpe(smore_ctx* c, uint64_t begin, uint64_t count, uint64_t total
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
     c->phase_n = 0;
+    return SMORE_OK;
+}
+
+int smore_train_hpe(smore_ctx* c, uint64_t begin, uint64_t count, uint64_t total, int walk_steps, int K, double reg,
+                    double alpha0, uint64_t seed, int mode) {
+    int rc = smore_train_hpe_async(c, begin, count, total, walk_steps, K, reg, alpha0, seed, mode);
+    if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return SMORE_OK;
 }

@@ -1,5 +1,5 @@
-// app -- flag-compatible replacement of cli/app.cpp (APP) on one MI355X.
-// Extra flags: -device, -mode hogwild|atomic|hybrid|serial, -seed, -format cpp|go.
+// app -- flag-compatible replacement of cli/app.cpp (APP) on one MI355X
+// or -gpus N.  Extra flags: -device, -gpus, -mode hogwild|atomic|hybrid|serial, -seed, -format cpp|go.
 #include <vector>
 
 #include "cli_common.h"
@@ -11,7 +11,7 @@ int main(int argc, char** argv) {
         printf("\t-train <string>\n\t-save <string>\n\t-undirected <int> (1)\n\t-dimensions <int> (64)\n");
         printf("\t-walk_times <int> (10)\n\t-sample_times <int> (10)\n\t-jump <double> (0.15)\n");
         printf("\t-negative_samples <int> (5)\n\t-alpha <float> (0.025)\n\t-threads <int>\n");
-        printf("\t-device <int> -mode hogwild|atomic|hybrid|serial -seed <int> -format cpp|go\n");
+        printf("\t-device <int> -gpus <int> -mode hogwild|atomic|hybrid|serial -seed <int> -format cpp|go\n");
         printf("Usage:\n./app -train net.txt -save rep.txt -undirected 1 -dimensions 64 -walk_times 10 "
                "-sample_times 10 -jump 0.15 -negative_samples 5 -alpha 0.025 -threads 1\n");
         return 0;
@@ -19,7 +19,7 @@ int main(int argc, char** argv) {
     char network_file[4096] = "", rep_file[4096] = "";
     // defaults of cli/app.cpp:52-53
     int dimensions = 64, undirected = 1, negative_samples = 5, walk_times = 10, sample_times = 10, threads = 1;
-    int device = 0, fmt = 0, mode = SMORE_HYBRID;
+    int device = 0, gpus = 1, fmt = 0, mode = SMORE_HYBRID;
     unsigned long long seed = 1;
     double init_alpha = 0.025, jump = 0.15;
     if ((i = ArgPos("-train", argc, argv)) > 0) snprintf(network_file, sizeof network_file, "%s", argv[i + 1]);
@@ -33,18 +33,21 @@ int main(int argc, char** argv) {
     if ((i = ArgPos("-alpha", argc, argv)) > 0) init_alpha = atof(argv[i + 1]);
     if ((i = ArgPos("-threads", argc, argv)) > 0) threads = atoi(argv[i + 1]);
     if ((i = ArgPos("-device", argc, argv)) > 0) device = atoi(argv[i + 1]);
+    if ((i = ArgPos("-gpus", argc, argv)) > 0) gpus = atoi(argv[i + 1]);
     if ((i = ArgPos("-mode", argc, argv)) > 0) mode = mode_of(argv[i + 1]);
     if ((i = ArgPos("-seed", argc, argv)) > 0) seed = strtoull(argv[i + 1], 0, 10);
     if ((i = ArgPos("-format", argc, argv)) > 0) fmt = !strcmp(argv[i + 1], "go");
 
-    smore_ctx* ctx = open_context(device);
-    SMORE_CLI_CHECK(ctx, smore_load_edgelist(ctx, network_file, undirected, SMORE_VM_OUT_DEGREES, SMORE_NM_DEGREES));
+    Run run = open_run(device, gpus);
+    smore_ctx* ctx = run.ctx;
+    run_load(run, network_file, undirected, SMORE_VM_OUT_DEGREES, SMORE_NM_DEGREES);
     int64_t V = print_graph(ctx);
     printf("Model Setting:\n\tdimension:\t\t%d\n", dimensions);
-    SMORE_CLI_CHECK(ctx, smore_alloc_tables(ctx, dimensions, 2));
+    run_alloc(run, dimensions, 2);
     // APP::Init: W then C from one rand() stream (src/model/APP.cpp:35-58)
     SMORE_CLI_CHECK(ctx, smore_init_table_glibc(ctx, SMORE_W, 0));
     SMORE_CLI_CHECK(ctx, smore_init_table_glibc(ctx, SMORE_C, (uint64_t)V * dimensions));
+    run_replicate(run);
     printf("Model:\n\t[APP]\nLearning Parameters:\n\twalk_times:\t\t%d\n\tsample_times:\t\t%d\n"
            "\tjumping factor:\t\t%g\n\tnegative_samples:\t%d\n\talpha:\t\t\t%g\n\tworkers:\t\t%d\nStart Training:\n",
            walk_times, sample_times, jump, negative_samples, init_alpha, threads);
@@ -52,16 +55,20 @@ int main(int argc, char** argv) {
     std::vector<int64_t> order((size_t)V * walk_times);
     smore_deepwalk_order(V, walk_times, 2ull * V * dimensions, order.data());
     const uint64_t units = (uint64_t)V * walk_times * sample_times;
-    const uint64_t chunk = ((uint64_t)1 << 24) / sample_times * sample_times + sample_times;
+    const uint64_t chunk = (((uint64_t)1 << 24) / sample_times * sample_times + sample_times) * (gpus > 1 ? gpus : 1);
     for (uint64_t b = 0; b < units; b += chunk) {
         uint64_t e = b + chunk < units ? b + chunk : units;
-        SMORE_CLI_CHECK(ctx, smore_train_app(ctx, b, e, walk_times, sample_times, jump, negative_samples, init_alpha,
-                                             seed, order.data(), mode));
+        if (run.g)
+            SMORE_RUN_CHECK(run, smore_group_train_app(run.g, b, e, walk_times, sample_times, jump, negative_samples,
+                                                       init_alpha, seed, order.data(), mode, 0, 0));
+        else
+            SMORE_RUN_CHECK(run, smore_train_app(ctx, b, e, walk_times, sample_times, jump, negative_samples,
+                                                 init_alpha, seed, order.data(), mode));
         printf("\tProgress: %.3f %%%c", (double)e / units * 100, 13);
         fflush(stdout);
     }
     printf("\tProgress: 100.00 %%\n");
     save(ctx, rep_file, fmt);
-    smore_destroy(ctx);
+    run_close(run);
     return 0;
 }

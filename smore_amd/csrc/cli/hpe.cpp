@@ -1,6 +1,6 @@
 // hpe -- flag-compatible replacement of cli/hpe.cpp (HPE) on one MI355X,
 // including -load_v / -load_c warm starts (proNet::LoadPreTrain,
-// src/proNet.cpp:238-286).  Extra flags: -device, -mode
+// src/proNet.cpp:238-286), or on -gpus N.  Extra flags: -device, -gpus, -mode
 // hogwild|atomic|hybrid|serial, -seed, -format cpp|go.
 #include "cli_common.h"
 
@@ -12,7 +12,7 @@ int main(int argc, char** argv) {
         printf("\t-undirected <int> (1)\n\t-dimensions <int> (64)\n\t-negative_samples <int> (5)\n");
         printf("\t-walk_steps <int> (5)\n\t-sample_times <int> (10)\n\t-reg <float> (0.01)\n");
         printf("\t-alpha <float> (0.025)\n\t-threads <int>\n");
-        printf("\t-device <int> -mode hogwild|atomic|hybrid|serial -seed <int> -format cpp|go\n");
+        printf("\t-device <int> -gpus <int> -mode hogwild|atomic|hybrid|serial -seed <int> -format cpp|go\n");
         printf("Usage:\n./hpe -train net.txt -save rep.txt -undirected 1 -dimensions 64 -reg 0.01 -sample_times 5 "
                "-walk_steps 5 -negative_samples 5 -alpha 0.025 -threads 1\n");
         return 0;
@@ -20,7 +20,7 @@ int main(int argc, char** argv) {
     char network_file[4096] = "", rep_file[4096] = "", load_v[4096] = "", load_c[4096] = "";
     // defaults of cli/hpe.cpp:56-57
     int dimensions = 64, undirected = 1, negative_samples = 5, walk_steps = 5, sample_times = 10, threads = 1;
-    int device = 0, fmt = 0, mode = SMORE_HYBRID;
+    int device = 0, gpus = 1, fmt = 0, mode = SMORE_HYBRID;
     unsigned long long seed = 1;
     double init_alpha = 0.025, reg = 0.01;
     if ((i = ArgPos("-train", argc, argv)) > 0) snprintf(network_file, sizeof network_file, "%s", argv[i + 1]);
@@ -36,34 +36,41 @@ int main(int argc, char** argv) {
     if ((i = ArgPos("-alpha", argc, argv)) > 0) init_alpha = atof(argv[i + 1]);
     if ((i = ArgPos("-threads", argc, argv)) > 0) threads = atoi(argv[i + 1]);
     if ((i = ArgPos("-device", argc, argv)) > 0) device = atoi(argv[i + 1]);
+    if ((i = ArgPos("-gpus", argc, argv)) > 0) gpus = atoi(argv[i + 1]);
     if ((i = ArgPos("-mode", argc, argv)) > 0) mode = mode_of(argv[i + 1]);
     if ((i = ArgPos("-seed", argc, argv)) > 0) seed = strtoull(argv[i + 1], 0, 10);
     if ((i = ArgPos("-format", argc, argv)) > 0) fmt = !strcmp(argv[i + 1], "go");
 
-    smore_ctx* ctx = open_context(device);
-    SMORE_CLI_CHECK(ctx, smore_load_edgelist(ctx, network_file, undirected, SMORE_VM_OUT_DEGREES, SMORE_NM_DEGREES));
+    Run run = open_run(device, gpus);
+    smore_ctx* ctx = run.ctx;
+    run_load(run, network_file, undirected, SMORE_VM_OUT_DEGREES, SMORE_NM_DEGREES);
     int64_t V = print_graph(ctx);
     printf("Model Setting:\n\tdimension:\t\t%d\n", dimensions);
-    SMORE_CLI_CHECK(ctx, smore_alloc_tables(ctx, dimensions, 2));
+    run_alloc(run, dimensions, 2);
     // HPE::Init: W then C from one rand() stream (src/model/HPE.cpp:28-52)
     SMORE_CLI_CHECK(ctx, smore_init_table_glibc(ctx, SMORE_W, 0));
     SMORE_CLI_CHECK(ctx, smore_init_table_glibc(ctx, SMORE_C, (uint64_t)V * dimensions));
     if (load_v[0]) { printf("\tload pretrain:\t%s\n", load_v); SMORE_CLI_CHECK(ctx, smore_load_pretrain(ctx, SMORE_W, load_v)); }
     if (load_c[0]) { printf("\tload pretrain:\t%s\n", load_c); SMORE_CLI_CHECK(ctx, smore_load_pretrain(ctx, SMORE_C, load_c)); }
+    run_replicate(run);
     printf("Model:\n\t[HPE]\nLearning Parameters:\n\tsample_times:\t\t%d\n\tnegative_samples:\t%d\n"
            "\twalk_steps:\t\t%d\n\tregularization:\t\t%g\n\talpha:\t\t\t%g\n\tworkers:\t\t%d\nStart Training:\n",
            sample_times, negative_samples, walk_steps, reg, init_alpha, threads);
     const uint64_t total = (uint64_t)sample_times * 1000000ull;
-    const uint64_t chunk = ((uint64_t)1 << 24) / ((uint64_t)walk_steps + 1) + 1;
+    const uint64_t chunk = (((uint64_t)1 << 24) / ((uint64_t)walk_steps + 1) + 1) * (gpus > 1 ? gpus : 1);
     for (uint64_t b = 0; b < total; b += chunk) {
         uint64_t n = b + chunk < total ? chunk : total - b;
-        SMORE_CLI_CHECK(ctx, smore_train_hpe(ctx, b, n, total, walk_steps, negative_samples, reg, init_alpha, seed,
-                                             mode));
+        if (run.g)
+            SMORE_RUN_CHECK(run, smore_group_train_hpe(run.g, b, n, total, walk_steps, negative_samples, reg,
+                                                       init_alpha, seed, mode, 0, 0));
+        else
+            SMORE_RUN_CHECK(run, smore_train_hpe(ctx, b, n, total, walk_steps, negative_samples, reg, init_alpha,
+                                                 seed, mode));
         printf("\tProgress: %.3f %%%c", (double)(b + n) / total * 100, 13);
         fflush(stdout);
     }
     printf("\tProgress: 100.00 %%\n");
     save(ctx, rep_file, fmt);
-    smore_destroy(ctx);
+    run_close(run);
     return 0;
 }

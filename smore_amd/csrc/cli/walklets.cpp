@@ -1,5 +1,5 @@
 // walklets -- flag-compatible replacement of cli/walklets.cpp (Walklets) on one
-// MI355X.  Extra flags: -device, -mode hogwild|atomic|hybrid|serial, -seed,
+// MI355X or -gpus N.  Extra flags: -device, -gpus, -mode hogwild|atomic|hybrid|serial, -seed,
 // -format cpp|go.
 #include "cli_common.h"
 
@@ -10,7 +10,7 @@ int main(int argc, char** argv) {
         printf("\t-train <string>\n\t-save <string>\n\t-undirected <int> (1)\n\t-dimensions <int> (64)\n");
         printf("\t-window_min <int> (2)\n\t-window_max <int> (5)\n\t-negative_samples <int> (5)\n");
         printf("\t-walk_times <int> (10)\n\t-walk_steps <int> (40)\n\t-alpha <float> (0.025)\n\t-threads <int>\n");
-        printf("\t-device <int> -mode hogwild|atomic|hybrid|serial -seed <int> -format cpp|go\n");
+        printf("\t-device <int> -gpus <int> -mode hogwild|atomic|hybrid|serial -seed <int> -format cpp|go\n");
         printf("Usage:\n./walklets -train net.txt -save rep.txt -undirected 1 -dimensions 64 -walk_times 10 "
                "-walk_steps 40 -window_min 2 -window_max 5 -negative_samples 5 -alpha 0.025 -threads 1\n");
         return 0;
@@ -18,7 +18,7 @@ int main(int argc, char** argv) {
     char network_file[4096] = "", rep_file[4096] = "";
     // defaults of cli/walklets.cpp:54-55
     int dimensions = 64, undirected = 1, window_min = 2, window_max = 5, negative_samples = 5, walk_times = 10;
-    int walk_steps = 40, threads = 1, device = 0, fmt = 0, mode = SMORE_HYBRID;
+    int walk_steps = 40, threads = 1, device = 0, gpus = 1, fmt = 0, mode = SMORE_HYBRID;
     unsigned long long seed = 1;
     double init_alpha = 0.025;
     if ((i = ArgPos("-train", argc, argv)) > 0) snprintf(network_file, sizeof network_file, "%s", argv[i + 1]);
@@ -33,31 +33,38 @@ int main(int argc, char** argv) {
     if ((i = ArgPos("-alpha", argc, argv)) > 0) init_alpha = atof(argv[i + 1]);
     if ((i = ArgPos("-threads", argc, argv)) > 0) threads = atoi(argv[i + 1]);
     if ((i = ArgPos("-device", argc, argv)) > 0) device = atoi(argv[i + 1]);
+    if ((i = ArgPos("-gpus", argc, argv)) > 0) gpus = atoi(argv[i + 1]);
     if ((i = ArgPos("-mode", argc, argv)) > 0) mode = mode_of(argv[i + 1]);
     if ((i = ArgPos("-seed", argc, argv)) > 0) seed = strtoull(argv[i + 1], 0, 10);
     if ((i = ArgPos("-format", argc, argv)) > 0) fmt = !strcmp(argv[i + 1], "go");
 
-    smore_ctx* ctx = open_context(device);
-    SMORE_CLI_CHECK(ctx, smore_load_edgelist(ctx, network_file, undirected, SMORE_VM_OUT_DEGREES, SMORE_NM_DEGREES));
+    Run run = open_run(device, gpus);
+    smore_ctx* ctx = run.ctx;
+    run_load(run, network_file, undirected, SMORE_VM_OUT_DEGREES, SMORE_NM_DEGREES);
     int64_t V = print_graph(ctx);
     printf("Model Setting:\n\tdimension:\t\t%d\n", dimensions);
-    SMORE_CLI_CHECK(ctx, smore_alloc_tables(ctx, dimensions, 2));
+    run_alloc(run, dimensions, 2);
     // Walklets inherits DeepWalk::Init: W then C from one rand() stream
     SMORE_CLI_CHECK(ctx, smore_init_table_glibc(ctx, SMORE_W, 0));
     SMORE_CLI_CHECK(ctx, smore_init_table_glibc(ctx, SMORE_C, (uint64_t)V * dimensions));
+    run_replicate(run);
     printf("Model:\n\t[Walklets]\nParameters:\n\twalk_times:\t\t%d\n\twalk_steps:\t\t%d\n\twindow_min:\t\t%d\n"
            "\twindow_max:\t\t%d\n\tnegative_samples:\t%d\n\talpha:\t\t\t%g\n\tworkers:\t\t%d\nStart Training:\n",
            walk_times, walk_steps, window_min, window_max, negative_samples, init_alpha, threads);
-    const uint64_t total = (uint64_t)V * walk_times, chunk = (uint64_t)1 << 20;
+    const uint64_t total = (uint64_t)V * walk_times, chunk = (uint64_t)(1 << 20) * (gpus > 1 ? gpus : 1);
     for (uint64_t b = 0; b < total; b += chunk) {
         uint64_t e = b + chunk < total ? b + chunk : total;
-        SMORE_CLI_CHECK(ctx, smore_train_walklets(ctx, b, e, walk_times, walk_steps, window_min, window_max,
-                                                  negative_samples, init_alpha, seed, mode));
+        if (run.g)
+            SMORE_RUN_CHECK(run, smore_group_train_walklets(run.g, b, e, walk_times, walk_steps, window_min, window_max,
+                                                            negative_samples, init_alpha, seed, mode, 0, 0));
+        else
+            SMORE_RUN_CHECK(run, smore_train_walklets(ctx, b, e, walk_times, walk_steps, window_min, window_max,
+                                                      negative_samples, init_alpha, seed, mode));
         printf("\tProgress: %.3f %%%c", (double)e / total * 100, 13);
         fflush(stdout);
     }
     printf("\tProgress:\t\t100.00 %%\n");
     save(ctx, rep_file, fmt);
-    smore_destroy(ctx);
+    run_close(run);
     return 0;
 }

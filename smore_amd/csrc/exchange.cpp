@@ -256,6 +256,32 @@ int group_sync(smore_group* g) {
 
 }  // namespace
 
+// The group training round structure: round k, replica r queues units
+// [begin + (k n + r) per, + per) of the global range on its stream (run(ctx, b, e)
+// must not synchronize), then the group folds the previous exchange in and
+// starts this round's all-reduce, which overlaps round k+1
+template <class F>
+static int group_rounds(smore_group* g, uint64_t begin, uint64_t end, uint64_t per, int mean, F&& run) {
+    const size_t n = g->ctx.size();
+    int rc;
+    if (end <= begin) return SMORE_OK;
+    for (size_t r = 0; r < n; ++r)
+        if ((rc = exchange_reset(g->ctx[r]))) return gfail(g, (int)r, rc);
+    const uint64_t count = end - begin;
+    for (uint64_t base = 0; base < count; base += per * n) {
+        for (size_t r = 0; r < n; ++r) {
+            const uint64_t b = base + r * per;
+            if (b >= count) break;
+            const uint64_t m = std::min<uint64_t>(per, count - b);
+            if ((rc = run(g->ctx[r], begin + b, begin + b + m))) return gfail(g, (int)r, rc);
+        }
+        if ((rc = group_exchange_begin(g, mean))) return rc;
+    }
+    for (size_t r = 0; r < n; ++r)
+        if ((rc = exchange_end(g->ctx[r]))) return gfail(g, (int)r, rc);
+    return group_sync(g);
+}
+
 extern "C" {
 
 int smore_comm_unique_id(unsigned char* id) {
@@ -419,57 +445,65 @@ int smore_group_broadcast_tables(smore_group* g) {
 int smore_group_train_edges(smore_group* g, int model, uint64_t begin, uint64_t count, uint64_t total, int K,
                             double alpha0, double reg, uint64_t seed, int mode, uint64_t sync_samples, int mean) {
     if (!g) return SMORE_EINVAL;
-    const size_t n = g->ctx.size();
-    int rc;
-    if (n == 1) return gfail(g, 0, smore_train_edges(g->ctx[0], model, begin, count, total, K, alpha0, reg, seed, mode));
-    if (count == 0) return SMORE_OK;
-    const uint64_t per = sync_samples ? sync_samples : (uint64_t)1 << 27;
-    for (size_t r = 0; r < n; ++r)
-        if ((rc = exchange_reset(g->ctx[r]))) return gfail(g, (int)r, rc);
-    // round k: replica r runs [begin + (k n + r) per, + per) of the global range
-    for (uint64_t base = 0; base < count; base += per * n) {
-        for (size_t r = 0; r < n; ++r) {
-            const uint64_t b = base + r * per;
-            if (b >= count) break;
-            const uint64_t m = std::min<uint64_t>(per, count - b);
-            rc = smore_train_edges_async(g->ctx[r], model, begin + b, m, total, K, alpha0, reg, seed, mode);
-            if (rc) return gfail(g, (int)r, rc);
-        }
-        if ((rc = group_exchange_begin(g, mean))) return rc;
-    }
-    for (size_t r = 0; r < n; ++r)
-        if ((rc = exchange_end(g->ctx[r]))) return gfail(g, (int)r, rc);
-    return group_sync(g);
+    if (g->ctx.size() == 1)
+        return gfail(g, 0, smore_train_edges(g->ctx[0], model, begin, count, total, K, alpha0, reg, seed, mode));
+    return group_rounds(g, begin, begin + count, sync_samples ? sync_samples : (uint64_t)1 << 27, mean,
+                        [&](smore_ctx* c, uint64_t b, uint64_t e) {
+                            return smore_train_edges_async(c, model, b, e - b, total, K, alpha0, reg, seed, mode);
+                        });
 }
 
 int smore_group_train_deepwalk(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
                                int walk_steps, int window, int K, double alpha0, uint64_t seed, const int64_t* order,
                                int mode, uint64_t sync_walks, int mean) {
     if (!g) return SMORE_EINVAL;
-    const size_t n = g->ctx.size();
-    int rc;
-    if (n == 1)
+    if (g->ctx.size() == 1)
         return gfail(g, 0, smore_train_deepwalk(g->ctx[0], walk_begin, walk_end, walk_times, walk_steps, window, K,
                                                 alpha0, seed, order, mode));
-    if (walk_end <= walk_begin) return SMORE_OK;
-    const uint64_t per = sync_walks ? sync_walks : (uint64_t)1 << 18;
-    for (size_t r = 0; r < n; ++r)
-        if ((rc = exchange_reset(g->ctx[r]))) return gfail(g, (int)r, rc);
-    const uint64_t count = walk_end - walk_begin;
-    for (uint64_t base = 0; base < count; base += per * n) {
-        for (size_t r = 0; r < n; ++r) {
-            const uint64_t b = base + r * per;
-            if (b >= count) break;
-            const uint64_t m = std::min<uint64_t>(per, count - b);
-            rc = smore_train_deepwalk_async(g->ctx[r], walk_begin + b, walk_begin + b + m, walk_times, walk_steps,
-                                            window, K, alpha0, seed, order, mode);
-            if (rc) return gfail(g, (int)r, rc);
-        }
-        if ((rc = group_exchange_begin(g, mean))) return rc;
-    }
-    for (size_t r = 0; r < n; ++r)
-        if ((rc = exchange_end(g->ctx[r]))) return gfail(g, (int)r, rc);
-    return group_sync(g);
+    return group_rounds(g, walk_begin, walk_end, sync_walks ? sync_walks : (uint64_t)1 << 18, mean,
+                        [&](smore_ctx* c, uint64_t b, uint64_t e) {
+                            return smore_train_deepwalk_async(c, b, e, walk_times, walk_steps, window, K, alpha0,
+                                                              seed, order, mode);
+                        });
+}
+
+int smore_group_train_walklets(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
+                               int window_min, int window_max, int K, double alpha0, uint64_t seed, int mode,
+                               uint64_t sync_walks, int mean) {
+    if (!g) return SMORE_EINVAL;
+    if (g->ctx.size() == 1)
+        return gfail(g, 0, smore_train_walklets(g->ctx[0], walk_begin, walk_end, walk_times, walk_steps, window_min,
+                                                window_max, K, alpha0, seed, mode));
+    return group_rounds(g, walk_begin, walk_end, sync_walks ? sync_walks : (uint64_t)1 << 18, mean,
+                        [&](smore_ctx* c, uint64_t b, uint64_t e) {
+                            return smore_train_walklets_async(c, b, e, walk_times, walk_steps, window_min,
+                                                              window_max, K, alpha0, seed, mode);
+                        });
+}
+
+int smore_group_train_app(smore_group* g, uint64_t unit_begin, uint64_t unit_end, int walk_times, int sample_times,
+                          double jump, int K, double alpha0, uint64_t seed, const int64_t* order, int mode,
+                          uint64_t sync_units, int mean) {
+    if (!g) return SMORE_EINVAL;
+    if (g->ctx.size() == 1)
+        return gfail(g, 0, smore_train_app(g->ctx[0], unit_begin, unit_end, walk_times, sample_times, jump, K, alpha0,
+                                           seed, order, mode));
+    return group_rounds(g, unit_begin, unit_end, sync_units ? sync_units : (uint64_t)1 << 24, mean,
+                        [&](smore_ctx* c, uint64_t b, uint64_t e) {
+                            return smore_train_app_async(c, b, e, walk_times, sample_times, jump, K, alpha0, seed,
+                                                         order, mode);
+                        });
+}
+
+int smore_group_train_hpe(smore_group* g, uint64_t begin, uint64_t count, uint64_t total, int walk_steps, int K,
+                          double reg, double alpha0, uint64_t seed, int mode, uint64_t sync_samples, int mean) {
+    if (!g) return SMORE_EINVAL;
+    if (g->ctx.size() == 1)
+        return gfail(g, 0, smore_train_hpe(g->ctx[0], begin, count, total, walk_steps, K, reg, alpha0, seed, mode));
+    return group_rounds(g, begin, begin + count, sync_samples ? sync_samples : (uint64_t)1 << 24, mean,
+                        [&](smore_ctx* c, uint64_t b, uint64_t e) {
+                            return smore_train_hpe_async(c, b, e - b, total, walk_steps, K, reg, alpha0, seed, mode);
+                        });
 }
 
 }  // extern "C"

@@ -19,7 +19,8 @@ __global__ void walk_gen_kernel(DevGraph g, WalkArgs w, uint64_t seed) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= w.nwalks) return;
     const uint64_t unit = w.walk_begin + t;
-    const int32_t start = (int32_t)w.order[unit - w.order_base];
+    // no order: walk unit starts at unit mod V (Walklets::Train, src/model/Walklets.cpp:45)
+    const int32_t start = w.order ? (int32_t)w.order[unit - w.order_base] : (int32_t)(unit % g.V);
     int32_t* out = w.walks + t * (uint64_t)(w.steps + 1);
     int L = 0;
     int32_t next = start;

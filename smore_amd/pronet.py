@@ -354,22 +354,6 @@ class Group:
                                                   _lib.VM[vertex_method], _lib.NM[negative_method]),
                   "set_graph_edges")
 
-    def train_walklets(self, walk_begin, walk_end, walk_times, walk_steps, window_min, window_max, K, alpha0, seed,
-                       mode="hogwild"):
-        """Walklets::Train (src/model/Walklets.cpp:24-63) over walks [walk_begin, walk_end)."""
-        self._chk(lib.smore_train_walklets(self.ctx, int(walk_begin), int(walk_end), int(walk_times),
-                                           int(walk_steps), int(window_min), int(window_max), int(K), float(alpha0),
-                                           int(seed), _lib.MODE[mode]), "train_walklets")
-
-    def train_app(self, unit_begin, unit_end, walk_times, sample_times, jump, K, alpha0, seed, order,
-                  mode="hogwild"):
-        """APP::Train (src/model/APP.cpp:59-120) over units [unit_begin, unit_end) of
-        walk_times * V * sample_times; order = walk start vertices (walk_times * V)."""
-        order = np.ascontiguousarray(order, np.int64)
-        self._chk(lib.smore_train_app(self.ctx, int(unit_begin), int(unit_end), int(walk_times), int(sample_times),
-                                      float(jump), int(K), float(alpha0), int(seed), ptr(order), _lib.MODE[mode]),
-                  "train_app")
-
     def set_semantics(self, semantics):
         self._chk(lib.smore_group_set_semantics(self.g, _lib.SEM[semantics]), "set_semantics")
 
@@ -393,6 +377,28 @@ class Group:
                                                  int(walk_steps), int(window), int(K), float(alpha0), int(seed),
                                                  ptr(order), _lib.MODE[mode], int(per), int(bool(mean))),
                   "train_deepwalk")
+
+    def train_walklets(self, walk_begin, walk_end, walk_times, walk_steps, window_min, window_max, K, alpha0, seed,
+                       mode="hybrid", per=0, mean=False):
+        """Walklets::Train (src/model/Walklets.cpp:24-63) over the replicas."""
+        self._chk(lib.smore_group_train_walklets(self.g, int(walk_begin), int(walk_end), int(walk_times),
+                                                 int(walk_steps), int(window_min), int(window_max), int(K),
+                                                 float(alpha0), int(seed), _lib.MODE[mode], int(per), int(bool(mean))),
+                  "train_walklets")
+
+    def train_app(self, unit_begin, unit_end, walk_times, sample_times, jump, K, alpha0, seed, order,
+                  mode="hybrid", per=0, mean=False):
+        """APP::Train (src/model/APP.cpp:59-120) over the replicas."""
+        order = np.ascontiguousarray(order, np.int64)
+        self._chk(lib.smore_group_train_app(self.g, int(unit_begin), int(unit_end), int(walk_times),
+                                            int(sample_times), float(jump), int(K), float(alpha0), int(seed),
+                                            ptr(order), _lib.MODE[mode], int(per), int(bool(mean))), "train_app")
+
+    def train_hpe(self, begin, count, total, walk_steps, K, reg, alpha0, seed, mode="hybrid", per=0, mean=False):
+        """HPE::Train (src/model/HPE.cpp:94-150) over the replicas."""
+        self._chk(lib.smore_group_train_hpe(self.g, int(begin), int(count), int(total), int(walk_steps), int(K),
+                                            float(reg), float(alpha0), int(seed), _lib.MODE[mode], int(per),
+                                            int(bool(mean))), "train_hpe")
 
 
 def deepwalk_order(V, walk_times, skip):

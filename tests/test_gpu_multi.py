@@ -80,6 +80,29 @@ def test_group_of_one_equals_single_context(smore):
     g.close()
 
 
+def test_group_of_one_walk_models_equal_single_context(smore):
+    """smore_group_train_walklets / _app / _hpe (exchange.cpp) on one replica
+    are the single-context calls."""
+    ref = _fresh(smore)
+    g = smore.Group([0])
+    g.LoadEdgeList(PL1K, 1)
+    g.alloc_tables(64, 2)
+    g.primary.init_table_glibc(0, 0)
+    g.primary.zero_table(1)
+    g.broadcast_tables()
+    V = ref.MAX_vid
+    ref.train_walklets(0, 200, 2, 10, 2, 4, 3, 0.025, SEED, "serial")
+    g.train_walklets(0, 200, 2, 10, 2, 4, 3, 0.025, SEED, "serial")
+    order = smore.deepwalk_order(V, 1, 0)
+    ref.train_app(0, 500, 1, 3, 0.15, 3, 0.025, SEED, order, "serial")
+    g.train_app(0, 500, 1, 3, 0.15, 3, 0.025, SEED, order, "serial")
+    ref.train_hpe(0, 400, 10 ** 5, 3, 3, 0.01, 0.025, SEED, "serial")
+    g.train_hpe(0, 400, 10 ** 5, 3, 3, 0.01, 0.025, SEED, "serial")
+    np.testing.assert_array_equal(g.primary.get_table(0), ref.get_table(0))
+    np.testing.assert_array_equal(g.primary.get_table(1), ref.get_table(1))
+    g.close()
+
+
 def _heldout_loss(W, C, draws):
     v, c, negs = draws[:, 0], draws[:, 1], draws[:, 2:]
     keep = c >= 0
