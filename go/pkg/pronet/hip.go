@@ -308,3 +308,42 @@ func (h *HIP) TrainDeepWalk(w, c [][]float64, dim int, order []int64, walkTimes,
 	}
 	return h.transfer([][][]float64{w, c}, false)
 }
+
+// TrainNode2Vec is TrainDeepWalk with node2vec's biased second-order walk
+// (internal/models/node2vec/node2vec.go:82-175: 1/p back to the previous
+// vertex, 1 to its neighbours, 1/q otherwise) in place of RandomWalk.
+func (h *HIP) TrainNode2Vec(w, c [][]float64, dim int, order []int64, walkTimes, walkSteps, window, K int,
+	alpha, p, q float64, progress func(done uint64)) error {
+	if err := h.alloc(dim, 2); err != nil {
+		return err
+	}
+	if err := h.transfer([][][]float64{w, c}, true); err != nil {
+		return err
+	}
+	total := uint64(len(order))
+	if total == 0 {
+		return nil
+	}
+	ord := (*[1 << 40]C.int64_t)(C.malloc(C.size_t(8 * total)))[:total:total]
+	defer C.free(unsafe.Pointer(&ord[0]))
+	for i, v := range order {
+		ord[i] = C.int64_t(v)
+	}
+	step := uint64(1<<20) * uint64(h.cfg.GPUs)
+	for done := uint64(0); done < total; {
+		n := total - done
+		if n > step {
+			n = step
+		}
+		if rc := C.smore_group_train_node2vec(h.group, C.uint64_t(done), C.uint64_t(done+n), C.int(walkTimes),
+			C.int(walkSteps), C.int(window), C.int(K), C.double(alpha), C.double(p), C.double(q),
+			C.uint64_t(h.cfg.Seed), &ord[0], C.int(h.cfg.Mode), 0, 0); rc != C.SMORE_OK {
+			return h.err("smore_group_train_node2vec")
+		}
+		done += n
+		if progress != nil {
+			progress(done)
+		}
+	}
+	return h.transfer([][][]float64{w, c}, false)
+}

@@ -264,6 +264,9 @@ int smore_group_train_deepwalk(smore_group* g, uint64_t walk_begin, uint64_t wal
                                int walk_steps, int window, int K, double alpha0, uint64_t seed,
                                const int64_t* order, int mode, uint64_t per, int mean);
 /* per = walks / APP units / HPE samples per replica per exchange (0: 2^18 / 2^24 / 2^24) */
+int smore_group_train_node2vec(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
+                               int walk_steps, int window, int K, double alpha0, double p, double q,
+                               uint64_t seed, const int64_t* order, int mode, uint64_t per, int mean);
 int smore_group_train_walklets(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
                                int walk_steps, int window_min, int window_max, int K, double alpha0,
                                uint64_t seed, int mode, uint64_t per, int mean);
@@ -285,6 +288,41 @@ int smore_train_deepwalk(smore_ctx* ctx, uint64_t walk_begin, uint64_t walk_end,
 int smore_train_deepwalk_async(smore_ctx* ctx, uint64_t walk_begin, uint64_t walk_end,
                                int walk_times, int walk_steps, int window, int K, double alpha0,
                                uint64_t seed, const int64_t* order, int mode);
+/* replaces: (*Node2Vec).Train (Go, internal/models/node2vec/node2vec.go:178-258):
+ * walks [walk_begin, walk_end) of walk_times*V from order[] (as DeepWalk),
+ * biasedRandomWalk (:82-164: first step TargetSample, later steps weight *
+ * 1/p back to the previous vertex, * 1 to its neighbours, * 1/q otherwise),
+ * Go SkipGrams + UpdatePairs.  Go semantics only (smore_set_semantics(ctx,
+ * SMORE_SEM_GO) first; SMORE_EINVAL otherwise); p, q > 0; mode serial,
+ * atomic or hogwild.  Draws: stream 1, unit w: 1 slot per step, then 2K per
+ * pair (as Go DeepWalk). */
+int smore_train_node2vec(smore_ctx* ctx, uint64_t walk_begin, uint64_t walk_end, int walk_times,
+                         int walk_steps, int window, int K, double alpha0, double p, double q,
+                         uint64_t seed, const int64_t* order, int mode);
+int smore_train_node2vec_async(smore_ctx* ctx, uint64_t walk_begin, uint64_t walk_end, int walk_times,
+                               int walk_steps, int window, int K, double alpha0, double p, double q,
+                               uint64_t seed, const int64_t* order, int mode);
+/* replaces: pkg/hetero's typed neighbour index (hetero_graph.go:164-177
+ * buildTypeIndices / NodeTypes) for metapath2vec: node_type[V] in
+ * [0, ntypes) of the graph set by smore_set_graph_edges (the Go caller keeps
+ * its hetero loader and passes the ids it assigned). */
+int smore_set_node_types(smore_ctx* ctx, const int32_t* node_type, int ntypes);
+/* replaces: (*Metapath2Vec).Train (Go, internal/models/metapath2vec/
+ * metapath2vec.go:106-200): walks [walk_begin, walk_end) of walk_times*V from
+ * order[], each picks one of the npaths meta-paths (type ids, paths[] holds
+ * them back to back, path_lens[p] each), MetaPathWalk (pkg/hetero/
+ * hetero_graph.go:221-256), Go SkipGrams + UpdatePairs.  The negative table
+ * is the context's (set the Go model's uniform BuildAliasMethod(1, 0.75) with
+ * smore_set_alias).  Go semantics only; smore_set_node_types first.  Draws:
+ * stream 1, unit w: slot 0 the path, 1 slot per step, then 2K per pair. */
+int smore_train_metapath2vec(smore_ctx* ctx, uint64_t walk_begin, uint64_t walk_end, int walk_times,
+                             int walk_steps, int window, int K, double alpha0, const int32_t* paths,
+                             const int32_t* path_lens, int npaths, uint64_t seed, const int64_t* order,
+                             int mode);
+int smore_train_metapath2vec_async(smore_ctx* ctx, uint64_t walk_begin, uint64_t walk_end, int walk_times,
+                                   int walk_steps, int window, int K, double alpha0, const int32_t* paths,
+                                   const int32_t* path_lens, int npaths, uint64_t seed,
+                                   const int64_t* order, int mode);
 /* the reference's walk start order: per walk_time a Fisher-Yates shuffle with
  * glibc rand() after `skip` Init draws (src/model/DeepWalk.cpp:122-131) */
 int smore_deepwalk_order(int64_t V, int walk_times, uint64_t skip, int64_t* order);

@@ -398,6 +398,16 @@ def _declare_go(L):
     L.orc_go_deepwalk_f32.restype = C.c_int
     L.orc_go_deepwalk_f32.argtypes = [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, dbl, u64, P,
                                       u64, u64]
+    L.orc_go_metapath_walk.restype = C.c_int
+    L.orc_go_metapath_walk.argtypes = [P, P, P, P, C.c_int, u64, u64, C.c_int32, C.c_int, P]
+    L.orc_go_metapath_f32.restype = C.c_int
+    L.orc_go_metapath_f32.argtypes = [P, P, P, P, C.c_int, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                      C.c_int, dbl, u64, P, u64, u64]
+    L.orc_go_node2vec_walk.restype = C.c_int
+    L.orc_go_node2vec_walk.argtypes = [P, P, dbl, dbl, u64, u64, C.c_int32, C.c_int, P]
+    L.orc_go_node2vec_f32.restype = C.c_int
+    L.orc_go_node2vec_f32.argtypes = [P, P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, dbl, dbl,
+                                      dbl, u64, P, u64, u64]
     L.orc_go_deepwalk_f64.restype = C.c_int
     L.orc_go_deepwalk_f64.argtypes = [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, dbl, u64, P]
 
@@ -438,3 +448,55 @@ def go_deepwalk_f64(g, W, C_, walk_times, walk_steps, window, K, alpha0, seed, o
     order = np.ascontiguousarray(order, np.int64)
     return lib().orc_go_deepwalk_f64(g.ref, ptr(W), ptr(C_), W.shape[1], walk_times, walk_steps, window, K, alpha0,
                                      seed, ptr(order))
+
+
+def go_node2vec_walk(g, p, q, seed, unit, start, steps):
+    """internal/models/node2vec/node2vec.go:82-164 (one walk)."""
+    out = np.zeros(steps + 1, np.int32)
+    L = lib().orc_go_node2vec_walk(g.ref, ptr(g.weights), p, q, seed, unit, start, steps, ptr(out))
+    return out[:L].copy()
+
+
+def go_node2vec_f32(g, W, C_, dim, walk_times, walk_steps, window, K, alpha0, p, q, seed, order, begin=0, end=None):
+    order = np.ascontiguousarray(order, np.int64)
+    if end is None:
+        end = walk_times * g.V
+    return lib().orc_go_node2vec_f32(g.ref, ptr(g.weights), ptr(W), ptr(C_), dim, W.shape[1], walk_times,
+                                     walk_steps, window, K, alpha0, p, q, seed, ptr(order), begin, end)
+
+
+def _paths(paths):
+    flat = np.ascontiguousarray([t for p in paths for t in p] or [0], np.int32)
+    off = np.ascontiguousarray(np.concatenate([[0], np.cumsum([len(p) for p in paths])]), np.int32)
+    return flat, off
+
+
+def go_uniform_negatives(g):
+    """metapath2vec's NegativeAT = BuildAliasMethod(ones, 0.75) (metapath2vec.go:140-145),
+    written into the graph's negative table in place."""
+    prob, alias = alias_go(np.ones(g.V), 0.75)
+    thr, al = alias_encode(prob, alias)
+    g.nthr[:] = thr
+    g.nalias_enc[:] = al
+    return prob, alias
+
+
+def go_metapath_walk(g, ntype, paths, seed, unit, start, steps):
+    ntype = np.ascontiguousarray(ntype, np.int32)
+    flat, off = _paths(paths)
+    out = np.zeros(steps + 1, np.int32)
+    L = lib().orc_go_metapath_walk(g.ref, ptr(ntype), ptr(flat), ptr(off), len(paths), seed, unit, start, steps,
+                                   ptr(out))
+    return out[:L].copy()
+
+
+def go_metapath_f32(g, ntype, paths, W, C_, dim, walk_times, walk_steps, window, K, alpha0, seed, order, begin=0,
+                    end=None):
+    ntype = np.ascontiguousarray(ntype, np.int32)
+    flat, off = _paths(paths)
+    order = np.ascontiguousarray(order, np.int64)
+    if end is None:
+        end = walk_times * g.V
+    return lib().orc_go_metapath_f32(g.ref, ptr(ntype), ptr(flat), ptr(off), len(paths), ptr(W), ptr(C_), dim,
+                                     W.shape[1], walk_times, walk_steps, window, K, alpha0, seed, ptr(order),
+                                     begin, end)

@@ -1292,6 +1292,103 @@ static int go_random_walk(const orc_go_graph* g, walk_rng* r, int32_t start, int
     return L;
 }
 
+/* ---- Go node2vec (internal/models/node2vec/node2vec.go) ---------------------- */
+typedef struct { const double* w; double inv_p, inv_q; } n2v_params;
+
+/* areNeighbors (:167-175): linear scan of Graph[a] */
+static int n2v_adjacent(const orc_go_graph* g, int32_t a, int32_t b) {
+    for (int64_t e = g->base.offsets[a]; e < g->base.offsets[a + 1]; ++e)
+        if (g->base.targets[e] == b) return 1;
+    return 0;
+}
+
+/* biasedTargetSample (:114-164) with the draw k already taken */
+static int32_t n2v_biased_target(const orc_go_graph* g, const n2v_params* np_, int32_t prev, int32_t cur, uint32_t k) {
+    int64_t off = g->base.offsets[cur], deg = g->base.offsets[cur + 1] - off;
+    double total = 0.0;
+    double* bw = (double*)malloc(sizeof(double) * (size_t)deg);
+    for (int64_t i = 0; i < deg; ++i) {
+        int32_t nb = g->base.targets[off + i];
+        double bias = nb == prev ? np_->inv_p : (n2v_adjacent(g, prev, nb) ? 1.0 : np_->inv_q);
+        bw[i] = np_->w[off + i] * bias;
+        total += bw[i];
+    }
+    int32_t out = g->base.targets[off + deg - 1];
+    if (total == 0.0) {
+        out = g->base.targets[off + draw_index(k, (uint64_t)deg)];
+    } else {
+        double r = draw_unit(k) * total, cum = 0.0;
+        for (int64_t i = 0; i < deg; ++i) {
+            cum += bw[i];
+            if (r <= cum) { out = g->base.targets[off + i]; break; }
+        }
+    }
+    free(bw);
+    return out;
+}
+
+/* biasedRandomWalk (:82-110): first step TargetSample, later steps biased;
+ * a vertex without out-edges ends the walk before drawing */
+static int go_n2v_walk(const orc_go_graph* g, const n2v_params* np_, walk_rng* r, int32_t start, int steps,
+                       int32_t* walk) {
+    int L = 0;
+    walk[L++] = start;
+    for (int i = 0; i < steps; ++i) {
+        int32_t cur = walk[L - 1];
+        if (g->base.offsets[cur + 1] - g->base.offsets[cur] == 0) break;
+        uint32_t k = walk_next(r);
+        walk[L] = i == 0 ? go_target(g, cur, k) : n2v_biased_target(g, np_, walk[L - 2], cur, k);
+        L++;
+    }
+    return L;
+}
+
+int orc_go_node2vec_walk(const orc_go_graph* g, const double* weights, double p, double q, uint64_t seed,
+                         uint64_t unit, int32_t start, int steps, int32_t* walk) {
+    n2v_params np_ = {weights, 1.0 / p, 1.0 / q};
+    walk_rng r = {seed, unit, 0, {0, 0, 0, 0}, 0xFFFFFFFFu};
+    return go_n2v_walk(g, &np_, &r, start, steps, walk);
+}
+
+/* ---- Go metapath2vec (internal/models/metapath2vec, pkg/hetero) -------------- */
+typedef struct { const int32_t* ntype; const int32_t* paths; const int32_t* path_off; int npaths; } mp_params;
+
+/* Intn(len(metaPaths)) (metapath2vec.go:184), then MetaPathWalk
+ * (hetero_graph.go:221-256) with SampleNeighborByType (:206-214): the
+ * neighbours of the wanted type in Edges[cur] order, one picked by Intn */
+static int go_mp_walk(const orc_go_graph* g, const mp_params* mp, walk_rng* r, int32_t start, int steps,
+                      int32_t* walk) {
+    int L = 0;
+    walk[L++] = start;
+    int pi = (int)draw_index(walk_next(r), (uint64_t)mp->npaths);
+    const int32_t* path = mp->paths + mp->path_off[pi];
+    int plen = mp->path_off[pi + 1] - mp->path_off[pi];
+    if (plen < 2) return L;
+    int32_t cur = start;
+    for (int idx = 0; L < steps + 1; ++idx) {
+        if (mp->ntype[cur] != path[idx % plen]) break;
+        int nt = path[(idx + 1) % plen];
+        int64_t n = 0;
+        for (int64_t e = g->base.offsets[cur]; e < g->base.offsets[cur + 1]; ++e)
+            if (mp->ntype[g->base.targets[e]] == nt) n++;
+        if (n == 0) break;
+        int64_t pick = (int64_t)draw_index(walk_next(r), (uint64_t)n), seen = 0;
+        int32_t next = -1;
+        for (int64_t e = g->base.offsets[cur]; e < g->base.offsets[cur + 1]; ++e)
+            if (mp->ntype[g->base.targets[e]] == nt && seen++ == pick) { next = g->base.targets[e]; break; }
+        walk[L++] = next;
+        cur = next;
+    }
+    return L;
+}
+
+int orc_go_metapath_walk(const orc_go_graph* g, const int32_t* ntype, const int32_t* paths, const int32_t* path_off,
+                         int npaths, uint64_t seed, uint64_t unit, int32_t start, int steps, int32_t* walk) {
+    mp_params mp = {ntype, paths, path_off, npaths};
+    walk_rng r = {seed, unit, 0, {0, 0, 0, 0}, 0xFFFFFFFFu};
+    return go_mp_walk(g, &mp, &r, start, steps, walk);
+}
+
 static int go_skip_grams(const int32_t* walk, int L, int window, int32_t* pv, int32_t* pc) {
     int n = 0;
     for (int i = 0; i < L; ++i) {
@@ -1305,7 +1402,8 @@ static int go_skip_grams(const int32_t* walk, int L, int window, int32_t* pv, in
 
 static int go_deepwalk(const orc_go_graph* g, double* W64, double* C64, float* W32, float* C32, int dim, int dpad,
                        int walk_times, int walk_steps, int window, int K, double alpha0, uint64_t seed,
-                       const int64_t* order, uint64_t walk_begin, uint64_t walk_end) {
+                       const int64_t* order, uint64_t walk_begin, uint64_t walk_end, const n2v_params* n2v,
+                       const mp_params* mp) {
     sig_init();
     uint64_t total = (uint64_t)walk_times * (uint64_t)g->base.V;
     if (walk_end > total) walk_end = total;
@@ -1320,7 +1418,9 @@ static int go_deepwalk(const orc_go_graph* g, double* W64, double* C64, float* W
     for (uint64_t wk = walk_begin; wk < walk_end; ++wk) {
         walk_rng r = {seed, wk, 0, {0, 0, 0, 0}, 0xFFFFFFFFu};
         double alpha = orc_alpha_walk(wk, alpha0, total);
-        int L = go_random_walk(g, &r, (int32_t)order[wk], walk_steps, walk);
+        int L = mp    ? go_mp_walk(g, mp, &r, (int32_t)order[wk], walk_steps, walk)
+                : n2v ? go_n2v_walk(g, n2v, &r, (int32_t)order[wk], walk_steps, walk)
+                      : go_random_walk(g, &r, (int32_t)order[wk], walk_steps, walk);
         int np = go_skip_grams(walk, L, window, pv, pc);
         for (int p = 0; p < np; ++p) {
             for (int j = 0; j < K; ++j) {
@@ -1339,11 +1439,31 @@ int orc_go_deepwalk_f32(const orc_go_graph* g, float* W, float* C, int dim, int 
                         int walk_steps, int window, int K, double alpha0, uint64_t seed,
                         const int64_t* order, uint64_t walk_begin, uint64_t walk_end) {
     return go_deepwalk(g, NULL, NULL, W, C, dim, dpad, walk_times, walk_steps, window, K, alpha0, seed, order,
-                       walk_begin, walk_end);
+                       walk_begin, walk_end, NULL, NULL);
 }
 
 int orc_go_deepwalk_f64(const orc_go_graph* g, double* W, double* C, int dim, int walk_times, int walk_steps,
                         int window, int K, double alpha0, uint64_t seed, const int64_t* order) {
     return go_deepwalk(g, W, C, NULL, NULL, dim, dim, walk_times, walk_steps, window, K, alpha0, seed, order, 0,
-                       (uint64_t)-1);
+                       (uint64_t)-1, NULL, NULL);
+}
+
+/* Go node2vec = Go DeepWalk with biasedRandomWalk (node2vec.go:178-258) */
+int orc_go_node2vec_f32(const orc_go_graph* g, const double* weights, float* W, float* C, int dim, int dpad,
+                        int walk_times, int walk_steps, int window, int K, double alpha0, double p, double q,
+                        uint64_t seed, const int64_t* order, uint64_t walk_begin, uint64_t walk_end) {
+    n2v_params np_ = {weights, 1.0 / p, 1.0 / q};
+    return go_deepwalk(g, NULL, NULL, W, C, dim, dpad, walk_times, walk_steps, window, K, alpha0, seed, order,
+                       walk_begin, walk_end, &np_, NULL);
+}
+
+/* Go metapath2vec = Go DeepWalk's pairs over MetaPathWalk (metapath2vec.go:106-200);
+ * negatives from the graph's negative table (the caller sets the uniform one) */
+int orc_go_metapath_f32(const orc_go_graph* g, const int32_t* ntype, const int32_t* paths, const int32_t* path_off,
+                        int npaths, float* W, float* C, int dim, int dpad, int walk_times, int walk_steps, int window,
+                        int K, double alpha0, uint64_t seed, const int64_t* order, uint64_t walk_begin,
+                        uint64_t walk_end) {
+    mp_params mp = {ntype, paths, path_off, npaths};
+    return go_deepwalk(g, NULL, NULL, W, C, dim, dpad, walk_times, walk_steps, window, K, alpha0, seed, order,
+                       walk_begin, walk_end, NULL, &mp);
 }

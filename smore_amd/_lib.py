@@ -68,6 +68,11 @@ def _load():
         "smore_delta_cycle": (i32, [P, P, P, P, P, C.c_float, i64]),
         "smore_train_deepwalk": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, u64, P, i32]),
         "smore_train_deepwalk_async": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, u64, P, i32]),
+        "smore_set_node_types": (i32, [P, P, i32]),
+        "smore_train_metapath2vec": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, P, P, i32, u64, P, i32]),
+        "smore_train_metapath2vec_async": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, P, P, i32, u64, P, i32]),
+        "smore_train_node2vec": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, dbl, dbl, u64, P, i32]),
+        "smore_train_node2vec_async": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, dbl, dbl, u64, P, i32]),
         "smore_comm_unique_id": (i32, [P]),
         "smore_comm_init": (i32, [P, i32, i32, P]),
         "smore_exchange_reset": (i32, [P]),
@@ -85,6 +90,7 @@ def _load():
         "smore_group_broadcast_tables": (i32, [P]),
         "smore_group_train_edges": (i32, [P, i32, u64, u64, u64, i32, dbl, dbl, u64, i32, u64, i32]),
         "smore_group_train_deepwalk": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, u64, P, i32, u64, i32]),
+        "smore_group_train_node2vec": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, dbl, dbl, u64, P, i32, u64, i32]),
         "smore_deepwalk_order": (i32, [i64, i32, u64, P]),
         "smore_train_walklets": (i32, [P, u64, u64, i32, i32, i32, i32, i32, dbl, u64, i32]),
         "smore_train_app": (i32, [P, u64, u64, i32, i32, dbl, i32, dbl, u64, P, i32]),

@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 using namespace smore_host;
@@ -57,7 +58,7 @@ void smore_destroy(smore_ctx* c) {
     dfree(c->d_offsets); dfree(c->d_targets); dfree(c->d_vtab); dfree(c->d_ntab); dfree(c->d_ctab);
     dfree(c->d_sig); dfree(c->d_skipped); dfree(c->d_work); dfree(c->d_table[0]); dfree(c->d_table[1]);
 
-    dfree(c->d_order); dfree(c->d_walks); dfree(c->d_lens); dfree(c->d_tcum); dfree(c->d_sh_hash); dfree(c->d_sh_ids);
+    dfree(c->d_order); dfree(c->d_walks); dfree(c->d_lens); dfree(c->d_tcum); dfree(c->d_wts); dfree(c->d_nbr_sorted); dfree(c->d_ntype); dfree(c->d_ttargets); dfree(c->d_toff); dfree(c->d_paths); dfree(c->d_path_off); dfree(c->d_sh_hash); dfree(c->d_sh_ids);
     dfree(c->d_rec); dfree(c->d_vt32); dfree(c->d_ct16);
     dfree(c->d_pcount); dfree(c->d_poff);
     if (c->d_scan_tmp) (void)hipFree(c->d_scan_tmp);
@@ -768,9 +769,66 @@ int smore_save_weights(const smore_ctx* cc, int which, const char* path, int fmt
 // Walk models on the record path: DeepWalk (rule 0) and Walklets (rule 1)
 // walks -> skip-gram pair records -> update kernel.  `order` holds the walk
 // start of every walk index (DeepWalk's shuffled keys; Walklets: vid).
+// node2vec's device tables: the raw CSR edge weights (biasedTargetSample's
+// base weights) and every vertex's CSR targets sorted (areNeighbors), built
+// once per graph by all host threads.
+static int ensure_n2v_tables(smore_ctx* c) {
+    if (c->d_wts && c->d_nbr_sorted) return SMORE_OK;
+    const HostGraph& g = *c->g;
+    const int64_t V = g.V, E = g.E;
+    std::vector<int32_t> nbr(g.targets.data(), g.targets.data() + E);
+    const int nt = std::max(1, std::min(64, (int)std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            for (int64_t v = V * t / nt; v < V * (t + 1) / nt; ++v)
+                std::sort(nbr.begin() + g.offsets[v], nbr.begin() + g.offsets[v + 1]);
+        });
+    for (auto& x : th) x.join();
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    if ((rc = upload(c, c->d_nbr_sorted, nbr.data(), nbr.size()))) return rc;
+    return upload(c, c->d_wts, g.weights.data(), (size_t)E);
+}
+
+// metapath2vec's typed neighbour index: NeighborsByType (pkg/hetero/
+// hetero_graph.go:164-177) as every vertex's CSR targets stably grouped by the
+// neighbour's type, with per-(vertex, type) offsets.
+int smore_set_node_types(smore_ctx* c, const int32_t* node_type, int ntypes) {
+    if (!c || !node_type || ntypes <= 0) return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    const HostGraph& g = *c->g;
+    const int64_t V = g.V, T = ntypes;
+    for (int64_t v = 0; v < V; ++v)
+        if (node_type[v] < 0 || node_type[v] >= ntypes) return fail(c, SMORE_EINVAL, "node type out of range");
+    std::vector<int64_t> toff((size_t)(V * (T + 1)));
+    std::vector<int32_t> tt((size_t)std::max<int64_t>(1, g.E));
+    for (int64_t v = 0; v < V; ++v) {
+        int64_t* o = toff.data() + v * (T + 1);
+        const int64_t b = g.offsets[v], e = g.offsets[v + 1];
+        std::vector<int64_t> cnt((size_t)T, 0);
+        for (int64_t x = b; x < e; ++x) cnt[node_type[g.targets[x]]]++;
+        o[0] = b;
+        for (int64_t t = 0; t < T; ++t) o[t + 1] = o[t] + cnt[t];
+        std::vector<int64_t> pos(o, o + T);
+        for (int64_t x = b; x < e; ++x) {
+            const int32_t n = g.targets[x];
+            tt[pos[node_type[n]]++] = n;
+        }
+    }
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    if ((rc = upload(c, c->d_ntype, node_type, (size_t)V))) return rc;
+    if ((rc = upload(c, c->d_toff, toff.data(), toff.size()))) return rc;
+    if ((rc = upload(c, c->d_ttargets, tt.data(), tt.size()))) return rc;
+    c->ntypes = ntypes;
+    return SMORE_OK;
+}
+
 static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
                        int window, int window_min, int K, double alpha0, uint64_t seed, const int64_t* order,
-                       uint64_t order_base, int mode) {
+                       uint64_t order_base, int mode, double n2v_p = 1.0, double n2v_q = 1.0,
+                       int npaths = 0) {
     if (!c) return SMORE_EINVAL;
     if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
     if (c->ntables < 2) return fail(c, SMORE_ESTATE, "walk models need W and C tables");
@@ -779,6 +837,13 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
     if (rule == 1 && (window_min < 0 || window_min > window))
         return fail(c, SMORE_EINVAL, "Walklets: need 0 <= window_min <= window_max");
     if (rule == 1 && c->semantics == SMORE_SEM_GO) return fail(c, SMORE_EINVAL, "Walklets has no Go semantics");
+    if (rule == 2 && c->semantics != SMORE_SEM_GO)
+        return fail(c, SMORE_EINVAL, "node2vec is a Go model: smore_set_semantics(ctx, SMORE_SEM_GO) first");
+    if (rule == 2 && !(n2v_p > 0 && n2v_q > 0)) return fail(c, SMORE_EINVAL, "node2vec: need p > 0 and q > 0");
+    if (rule == 3 && c->semantics != SMORE_SEM_GO)
+        return fail(c, SMORE_EINVAL, "metapath2vec is a Go model: smore_set_semantics(ctx, SMORE_SEM_GO) first");
+    if (rule == 3 && (c->ntypes <= 0 || npaths <= 0 || !c->d_paths))
+        return fail(c, SMORE_ESTATE, "metapath2vec: node types and meta-paths not set");
     const uint64_t total = (uint64_t)walk_times * (uint64_t)c->g->V;
     if (walk_end > total) walk_end = total;
     if (walk_begin >= walk_end) return SMORE_OK;
@@ -793,6 +858,7 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
             if (order[i] < 0 || order[i] >= c->g->V) return fail(c, SMORE_EINVAL, "walk start out of range");
     }
     if ((rc = set_device(c))) return rc;
+    if (rule == 2 && (rc = ensure_n2v_tables(c))) return rc;
     if (!order) {
         // starts computed on the device (walk mod V)
     } else if (c->order_cap < nw_call) {
@@ -885,6 +951,18 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
         w.window = window;
         w.rule = rule;
         w.window_min = window_min;
+        w.inv_p = 1.0 / n2v_p;   // node2vec.go:136,142 (fp64 1.0 / p)
+        w.inv_q = 1.0 / n2v_q;
+        w.wts = c->d_wts;
+        w.nbr_sorted = c->d_nbr_sorted;
+        w.ntype = c->d_ntype;
+        w.ttargets = c->d_ttargets;
+        w.toff = c->d_toff;
+        w.paths = c->d_paths;
+        w.path_off = c->d_path_off;
+        w.ntypes = c->ntypes;
+        w.npaths = npaths;
+        w.slot_extra = rule == 3 ? 1 : 0;
         const int64_t groups_per_block = 256 / lanes_of(c->dpad);
         int g2 = grid;
         if ((int64_t)g2 * groups_per_block > (int64_t)w.nwalks && mode != SMORE_SERIAL)
@@ -921,6 +999,57 @@ int smore_train_deepwalk_async(smore_ctx* c, uint64_t walk_begin, uint64_t walk_
                                int mode) {
     return train_walks(c, 0, walk_begin, walk_end, walk_times, walk_steps, window, 0, K, alpha0, seed, order, 0,
                        mode);
+}
+
+int smore_train_node2vec_async(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, int walk_times,
+                               int walk_steps, int window, int K, double alpha0, double p, double q, uint64_t seed,
+                               const int64_t* order, int mode) {
+    return train_walks(c, 2, walk_begin, walk_end, walk_times, walk_steps, window, 0, K, alpha0, seed, order, 0, mode,
+                       p, q);
+}
+
+int smore_train_metapath2vec_async(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, int walk_times,
+                                   int walk_steps, int window, int K, double alpha0, const int32_t* paths,
+                                   const int32_t* path_lens, int npaths, uint64_t seed, const int64_t* order,
+                                   int mode) {
+    if (!c) return SMORE_EINVAL;
+    if (!paths || !path_lens || npaths <= 0) return fail(c, SMORE_EINVAL, "metapath2vec: no meta-paths");
+    std::vector<int32_t> off((size_t)npaths + 1, 0);
+    for (int p = 0; p < npaths; ++p) {
+        if (path_lens[p] < 0) return fail(c, SMORE_EINVAL, "metapath2vec: bad path length");
+        off[p + 1] = off[p] + path_lens[p];
+    }
+    for (int32_t i = 0; i < off[npaths]; ++i)
+        if (paths[i] < 0 || paths[i] >= c->ntypes) return fail(c, SMORE_EINVAL, "metapath2vec: unknown type in path");
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    // the previous call's kernels may still read the paths: reallocate only
+    // after the stream has drained
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if ((rc = upload(c, c->d_paths, paths, (size_t)off[npaths]))) return rc;
+    if ((rc = upload(c, c->d_path_off, off.data(), off.size()))) return rc;
+    return train_walks(c, 3, walk_begin, walk_end, walk_times, walk_steps, window, 0, K, alpha0, seed, order, 0, mode,
+                       1.0, 1.0, npaths);
+}
+
+int smore_train_metapath2vec(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
+                             int window, int K, double alpha0, const int32_t* paths, const int32_t* path_lens,
+                             int npaths, uint64_t seed, const int64_t* order, int mode) {
+    int rc = smore_train_metapath2vec_async(c, walk_begin, walk_end, walk_times, walk_steps, window, K, alpha0, paths,
+                                            path_lens, npaths, seed, order, mode);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return SMORE_OK;
+}
+
+int smore_train_node2vec(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
+                         int window, int K, double alpha0, double p, double q, uint64_t seed, const int64_t* order,
+                         int mode) {
+    int rc = smore_train_node2vec_async(c, walk_begin, walk_end, walk_times, walk_steps, window, K, alpha0, p, q,
+                                        seed, order, mode);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return SMORE_OK;
 }
 
 int smore_train_walklets_async(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,

@@ -61,6 +61,16 @@ struct smore_ctx {
     // semantics: SMORE_SEM_CPP (default) or SMORE_SEM_GO
     int semantics = 0;
     double* d_tcum = nullptr;
+    // node2vec (Go): raw CSR weights and per-vertex sorted CSR targets, built on first use
+    double* d_wts = nullptr;
+    int32_t* d_nbr_sorted = nullptr;
+    // metapath2vec (Go): node types and the per-type neighbour index (smore_set_node_types)
+    int32_t* d_ntype = nullptr;
+    int32_t* d_ttargets = nullptr;
+    int64_t* d_toff = nullptr;
+    int ntypes = 0;
+    int32_t* d_paths = nullptr;
+    int32_t* d_path_off = nullptr;
     // hybrid write-combining: super-hot context rows (hash + slot ids)
     int2* d_sh_hash = nullptr;
     int32_t* d_sh_ids = nullptr;
@@ -136,6 +146,12 @@ inline int set_device(smore_ctx* c) {
 
 inline int upload_graph(smore_ctx* c) {
     int rc;
+    dfree(c->d_wts);
+    dfree(c->d_nbr_sorted);
+    dfree(c->d_ntype);
+    dfree(c->d_ttargets);
+    dfree(c->d_toff);
+    c->ntypes = 0;
     if (c->device < 0) {
         c->has_graph = true;
         return SMORE_OK;

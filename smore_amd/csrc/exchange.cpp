@@ -467,6 +467,20 @@ int smore_group_train_deepwalk(smore_group* g, uint64_t walk_begin, uint64_t wal
                         });
 }
 
+int smore_group_train_node2vec(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
+                               int walk_steps, int window, int K, double alpha0, double p, double q, uint64_t seed,
+                               const int64_t* order, int mode, uint64_t sync_walks, int mean) {
+    if (!g) return SMORE_EINVAL;
+    if (g->ctx.size() == 1)
+        return gfail(g, 0, smore_train_node2vec(g->ctx[0], walk_begin, walk_end, walk_times, walk_steps, window, K,
+                                                alpha0, p, q, seed, order, mode));
+    return group_rounds(g, walk_begin, walk_end, sync_walks ? sync_walks : (uint64_t)1 << 18, mean,
+                        [&](smore_ctx* c, uint64_t b, uint64_t e) {
+                            return smore_train_node2vec_async(c, b, e, walk_times, walk_steps, window, K, alpha0, p,
+                                                              q, seed, order, mode);
+                        });
+}
+
 int smore_group_train_walklets(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
                                int window_min, int window_max, int K, double alpha0, uint64_t seed, int mode,
                                uint64_t sync_walks, int mean) {

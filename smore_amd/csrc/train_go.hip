@@ -8,7 +8,11 @@
 //     context's gradient and W_v's are applied at the end;
 //   * LINE order 1: updateFirstOrder (internal/models/line/line.go:153-200);
 //   * BPR: UpdateBPRPair with W (users) and C (items), lambda (optimizer.go:87-117);
-//   * DeepWalk: walks stop at a dead end, fixed window (pronet.go:292-333).
+//   * DeepWalk: walks stop at a dead end, fixed window (pronet.go:292-333);
+//   * node2vec: the biased second-order walk (internal/models/node2vec), then
+//     the DeepWalk pairs;
+//   * metapath2vec: meta-path-typed uniform walks (internal/models/metapath2vec,
+//     pkg/hetero), then the DeepWalk pairs.
 // fp32 arithmetic without fused multiply-adds (amd64 Go does not fuse); the
 // oracle's orc_go_*_f32 is the bit-exact spec.  Same lane layout as
 // edge_kernels.h.
@@ -290,7 +294,111 @@ __global__ void go_walk_gen_kernel(DevGraph g, const double* tcum, WalkArgs w, u
     w.lens[t] = L;
 }
 
-// Go SkipGrams (fixed window) + Go UpdatePair per pair; negatives from slot L-1.
+// areNeighbors(a, b) (internal/models/node2vec/node2vec.go:167-175): a linear
+// scan of Graph[a] there; membership does not depend on the order, so here a
+// binary search in a's sorted copy of its CSR targets.
+__device__ __forceinline__ bool n2v_adjacent(const DevGraph& g, const int32_t* nbr, int32_t a, int32_t b) {
+    int64_t lo = g.offsets[a], hi = g.offsets[a + 1];
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        const int32_t x = nbr[mid];
+        if (x == b) return true;
+        if (x < b) lo = mid + 1;
+        else hi = mid;
+    }
+    return false;
+}
+
+// node2vec biased weight of Graph[cur][i] after prev (node2vec.go:126-146)
+__device__ __forceinline__ double n2v_weight(const DevGraph& g, const WalkArgs& w, int32_t prev, int64_t e) {
+    const int32_t nb = untag(g.targets[e]);
+    const double bias = nb == prev ? w.inv_p : (n2v_adjacent(g, w.nbr_sorted, prev, nb) ? 1.0 : w.inv_q);
+    return w.wts[e] * bias;
+}
+
+// biasedRandomWalk (node2vec.go:82-110): the first step is Go's TargetSample,
+// every later step biasedTargetSample (:114-164) -- total of the biased weights
+// in the Go loop's order, r = Float64() * total, first i with r <= cum_i (the
+// last neighbour if rounding leaves none; Intn(deg) when total == 0).  Step s
+// draws slot s of stream 1 (as the Go RandomWalk); a dead end stops the walk
+// before drawing.
+__global__ void go_n2v_walk_gen_kernel(DevGraph g, const double* tcum, WalkArgs w, uint64_t seed) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= w.nwalks) return;
+    const uint64_t unit = w.walk_begin + t;
+    int32_t* out = w.walks + t * (uint64_t)(w.steps + 1);
+    int L = 0;
+    int32_t prev = -1, cur = (int32_t)w.order[unit - w.order_base];
+    out[L++] = cur;
+    uint4 b = make_uint4(0, 0, 0, 0);
+    for (int s = 0; s < w.steps; ++s) {
+        const int64_t off = g.offsets[cur], deg = g.offsets[cur + 1] - off;
+        if (deg == 0) break;
+        if ((s & 3) == 0) b = philox_block(seed, 1, unit, (uint32_t)s >> 2);
+        const uint32_t k = comp(b, s & 3);
+        int32_t next;
+        if (s == 0) {
+            next = go_target(g, tcum, cur, k);
+        } else {
+            double total = 0.0;
+            for (int64_t e = off; e < off + deg; ++e) total += n2v_weight(g, w, prev, e);
+            if (total == 0.0) {
+                next = untag(g.targets[off + draw_index(k, (uint32_t)deg)]);
+            } else {
+                const double r = ldexp((double)k, -32) * total;
+                double cum = 0.0;
+                int64_t e = off;
+                for (; e < off + deg - 1; ++e) {
+                    cum += n2v_weight(g, w, prev, e);
+                    if (r <= cum) break;
+                }
+                next = untag(g.targets[e]);
+            }
+        }
+        prev = cur;
+        cur = next;
+        out[L++] = cur;
+    }
+    w.lens[t] = L;
+}
+
+// metapath2vec walk (internal/models/metapath2vec/metapath2vec.go:184-188,
+// pkg/hetero/hetero_graph.go:206-256): slot 0 picks the meta-path
+// (Intn(len(metaPaths))); while the walk is shorter than steps + 1 the
+// current vertex must have the path's current type, and the next vertex is a
+// uniform pick (Intn, the next slot) among its neighbours of the next type, in
+// push order.  A type mismatch or no such neighbour ends the walk before
+// drawing.
+__global__ void go_mp_walk_gen_kernel(WalkArgs w, uint64_t seed) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= w.nwalks) return;
+    const uint64_t unit = w.walk_begin + t;
+    int32_t* out = w.walks + t * (uint64_t)(w.steps + 1);
+    int32_t cur = (int32_t)w.order[unit - w.order_base];
+    out[0] = cur;
+    uint4 b = philox_block(seed, 1, unit, 0);
+    const int pi = (int)draw_index(comp(b, 0), (uint32_t)w.npaths);
+    const int32_t* path = w.paths + w.path_off[pi];
+    const int plen = w.path_off[pi + 1] - w.path_off[pi];
+    int L = 1;
+    if (plen >= 2) {
+        for (int idx = 0; L < w.steps + 1; ++idx) {
+            if (w.ntype[cur] != path[idx % plen]) break;
+            const int nt = path[(idx + 1) % plen];
+            const int64_t* to = w.toff + (int64_t)cur * (w.ntypes + 1);
+            const int64_t lo = to[nt], n = to[nt + 1] - lo;
+            if (n == 0) break;
+            const uint32_t s = (uint32_t)L;   // slot L: the step's Intn
+            if ((s & 3) == 0) b = philox_block(seed, 1, unit, s >> 2);
+            cur = w.ttargets[lo + draw_index(comp(b, s & 3), (uint32_t)n)];
+            out[L++] = cur;
+        }
+    }
+    w.lens[t] = L;
+}
+
+// Go SkipGrams (fixed window) + Go UpdatePair per pair; negatives from slot
+// L-1 (+ slot_extra).
 template <int G, int M, int KMAX, int MODE>
 __global__ void __launch_bounds__(256) go_walk_pairs_kernel(EdgeArgs a, WalkArgs w) {
     __shared__ float s_sig[1001];
@@ -312,7 +420,7 @@ __global__ void __launch_bounds__(256) go_walk_pairs_kernel(EdgeArgs a, WalkArgs
         const int32_t* walk = w.walks + t * stride;
         const int L = w.lens[t];
         const float alpha = alpha_walk(unit, a.alpha0, w.total_walks);
-        uint32_t slot = (uint32_t)(L - 1);
+        uint32_t slot = (uint32_t)(L - 1 + w.slot_extra);
         for (int i = 0; i < L; ++i) {
             const int lo = i - w.window < 0 ? 0 : i - w.window;
             const int hi = i + w.window + 1 > L ? L : i + w.window + 1;
@@ -393,8 +501,15 @@ hipError_t launch_go_edge(const EdgeArgs& a, int grid, hipStream_t st) {
 
 hipError_t launch_go_walk(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st) {
     const int block = 256;
-    hipLaunchKernelGGL(go_walk_gen_kernel, dim3((unsigned)((w.nwalks + block - 1) / block)), dim3(block), 0, st, a.g,
-                       a.tcum, w, a.seed);
+    if (w.rule == 3)
+        hipLaunchKernelGGL(go_mp_walk_gen_kernel, dim3((unsigned)((w.nwalks + block - 1) / block)), dim3(block), 0, st,
+                           w, a.seed);
+    else if (w.rule == 2)
+        hipLaunchKernelGGL(go_n2v_walk_gen_kernel, dim3((unsigned)((w.nwalks + block - 1) / block)), dim3(block), 0, st,
+                           a.g, a.tcum, w, a.seed);
+    else
+        hipLaunchKernelGGL(go_walk_gen_kernel, dim3((unsigned)((w.nwalks + block - 1) / block)), dim3(block), 0, st,
+                           a.g, a.tcum, w, a.seed);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int G = lanes_of(a.dpad), M = (a.dpad + G - 1) / G;

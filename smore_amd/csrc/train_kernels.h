@@ -43,6 +43,21 @@ struct WalkArgs {
     int steps, window;
     int rule;                      // pair rule: 0 DeepWalk SkipGrams (random shrink), 1 Walklets ScaleSkipGrams
     int window_min;                // Walklets: pairs at distance [window_min, window] (clamped as the reference)
+    // node2vec (Go, rule 2): 1/p, 1/q, raw CSR edge weights and a per-vertex
+    // sorted copy of the CSR targets (areNeighbors by binary search)
+    double inv_p, inv_q;
+    const double* wts;
+    const int32_t* nbr_sorted;
+    // metapath2vec (Go, rule 3): node types, every vertex's CSR targets grouped
+    // by type (push order kept) with offsets toff[v * (ntypes + 1) + t], the
+    // meta-paths (type ids, path p = paths[path_off[p] .. path_off[p + 1]))
+    const int32_t* ntype;
+    const int32_t* ttargets;
+    const int64_t* toff;
+    const int32_t* paths;
+    const int32_t* path_off;
+    int ntypes, npaths;
+    int slot_extra;                // draws before the step draws (metapath2vec: the path choice)
 };
 
 // APP: units [unit_begin, unit_begin + n) of walk_times * V * sample_times; unit

@@ -8,7 +8,11 @@ Go semantics):
   * BPR    internal/models/bpr/bpr.go:61-136: total = sample_times * MaxLine,
            UpdateBPRPair(W users, C items, lambda), one negative per sample;
   * DeepWalk internal/models/deepwalk/deepwalk.go:61-142: walk_times * MaxVid
-           walks, dead-end stop, fixed window, UpdatePair per skip-gram pair.
+           walks, dead-end stop, fixed window, UpdatePair per skip-gram pair;
+  * Node2Vec internal/models/node2vec/node2vec.go:43-258: DeepWalk's loop over
+           the biased second-order walk (p return, q in-out);
+  * Metapath2Vec internal/models/metapath2vec/metapath2vec.go:30-200 over a
+           pkg/hetero graph: meta-path-typed walks, uniform negatives.
 
 Differences from the Go code, documented in DESIGN.md: draws come from the
 seeded Philox spec (not time-seeded math/rand); the learning rate of a sample
@@ -16,6 +20,9 @@ follows its global index (Go's shared counter skips dead-end samples); tables
 are fp32; Init uses the on-device uniform (u - 0.5) / dim generator.
 """
 from . import _lib
+import numpy as np
+
+from . import _lib as _l
 from .models import CHUNK, MONITOR, _progress
 from .pronet import ProNet, deepwalk_order
 
@@ -127,6 +134,144 @@ class DeepWalk(_GoModel):
             done += n
             _progress(_alpha(done, alpha, total), done / total)
         print()
+
+    @property
+    def w_context(self):
+        return self.pnet.get_table(_lib.CTX)
+
+
+class Node2Vec(DeepWalk):
+    """internal/models/node2vec/node2vec.go: Init(dim, p, q), Train as DeepWalk's
+    over biasedRandomWalk (on the GPU: smore_train_node2vec)."""
+
+    def Init(self, dim, p=1.0, q=1.0):
+        if not (p > 0 and q > 0):
+            raise ValueError("node2vec: p and q must be > 0")
+        self.p, self.q = float(p), float(q)
+        self._alloc(dim, 2)
+        print("\tp (return param):\t%.2f\n\tq (in-out param):\t%.2f" % (self.p, self.q))
+
+    def Train(self, walk_times, walk_steps, window_size, negative_samples, alpha, workers=1):
+        print("Model:\n\t[Node2Vec]\nLearning Parameters:")
+        print("\twalk_times:\t\t%d\n\twalk_steps:\t\t%d\n\twindow_size:\t\t%d\n\tnegative_samples:\t%d"
+              "\n\talpha:\t\t\t%.6f\n\tworkers:\t\t%d"
+              % (walk_times, walk_steps, window_size, negative_samples, alpha, workers))
+        print("Start Training:")
+        V = self.pnet.MAX_vid
+        order = deepwalk_order(V, walk_times, 0)
+        total = walk_times * V
+        step = max(1, CHUNK // (walk_steps * 2 * window_size + 1))
+        done = 0
+        while done < total:
+            n = min(step, total - done)
+            self.pnet.train_node2vec(done, done + n, walk_times, walk_steps, window_size, negative_samples,
+                                     alpha, self.p, self.q, self.seed, order, self.mode)
+            done += n
+            _progress(_alpha(done, alpha, total), done / total)
+        print()
+
+
+def load_hetero(filename, undirected):
+    """pkg/hetero (*HeteroGraph).LoadEdgeList (hetero_graph.go:60-160): lines
+    "src srcType dst dstType edgeType [weight]" (fewer than 5 fields skipped,
+    an unparsable weight is 1), node ids and type ids in first-appearance
+    order (a node keeps its first type), edges appended per source in input
+    order, the reverse edge right after when undirected.  Host-side input
+    parsing; a Go caller keeps its own loader and passes the same arrays."""
+    ids, names, ntype, tids, tkeys = {}, [], [], {}, []
+    src, dst, w = [], [], []
+
+    def node(name, typ):
+        if name in ids:
+            return ids[name]
+        ids[name] = len(names)
+        names.append(name)
+        if typ not in tids:
+            tids[typ] = len(tkeys)
+            tkeys.append(typ)
+        ntype.append(tids[typ])
+        return ids[name]
+
+    with open(filename) as f:
+        for line in f:
+            parts = line.split()
+            if len(parts) < 5:
+                continue
+            x = 1.0
+            if len(parts) >= 6:
+                try:
+                    x = float(parts[5])
+                except ValueError:
+                    x = 1.0
+            a, b = node(parts[0], parts[1]), node(parts[2], parts[3])
+            src.append(a), dst.append(b), w.append(x)
+            if undirected:
+                src.append(b), dst.append(a), w.append(x)
+    return names, np.array(ntype, np.int32), tkeys, np.array(src, np.int32), np.array(dst, np.int32), \
+        np.array(w, np.float64)
+
+
+class Metapath2Vec(_GoModel):
+    """internal/models/metapath2vec/metapath2vec.go: LoadEdgeList (pkg/hetero),
+    AddMetaPath, Init, Train (on the GPU: smore_train_metapath2vec),
+    SaveEmbeddings.  NegativeAT = BuildAliasMethod(ones, 0.75) (:140-145): every
+    normalised entry is exactly 1.0, so the table is {prob 1, alias i}."""
+
+    def LoadEdgeList(self, filename, undirected):
+        names, self.ntype, self.type_keys, s, d, w = load_hetero(filename, undirected)
+        self.names = names
+        self.pnet.set_graph_edges(len(names), s, d, w)
+        self.pnet.set_semantics("go")
+        self.pnet.set_node_types(self.ntype, len(self.type_keys))
+        V = len(names)
+        self.pnet.set_alias(_l.AT_NEGATIVE, np.ones(V), np.arange(V, dtype=np.int64))
+        self.meta_paths = []
+        self.undirected = bool(undirected)
+
+    def AddMetaPath(self, meta_path):
+        types = meta_path.split()
+        if len(types) < 2:
+            raise ValueError("meta-path must have at least 2 types, got: %s" % meta_path)
+        for t in types:
+            if t not in self.type_keys:
+                raise ValueError("invalid meta-path: unknown node type in meta-path: %s" % t)
+        self.meta_paths.append([self.type_keys.index(t) for t in types])
+        print("Added meta-path: %s" % meta_path)
+
+    def Init(self, dim):
+        self._alloc(dim, 2)
+
+    def Train(self, walk_times, walk_steps, window_size, negative_samples, alpha, workers=1):
+        if not self.meta_paths:
+            print("Error: No meta-paths defined. Use AddMetaPath() before training.")
+            return
+        print("Model:\n\t[Metapath2Vec - Heterogeneous Graph Embedding]\nLearning Parameters:")
+        print("\twalk_times:\t\t%d\n\twalk_steps:\t\t%d\n\twindow_size:\t\t%d\n\tnegative_samples:\t%d"
+              "\n\talpha:\t\t\t%.6f\n\tworkers:\t\t%d"
+              % (walk_times, walk_steps, window_size, negative_samples, alpha, workers))
+        print("Start Training:")
+        V = self.pnet.MAX_vid
+        order = deepwalk_order(V, walk_times, 0)
+        total = walk_times * V
+        step = max(1, CHUNK // (walk_steps * 2 * window_size + 1))
+        done = 0
+        while done < total:
+            n = min(step, total - done)
+            self.pnet.train_metapath2vec(done, done + n, walk_times, walk_steps, window_size, negative_samples,
+                                         alpha, self.meta_paths, self.seed, order, self.mode)
+            done += n
+            _progress(_alpha(done, alpha, total), done / total)
+        print()
+
+    def SaveEmbeddings(self, filename):
+        """metapath2vec.go:218-245: "V dim" header, rows "name[type] %.6f ..."."""
+        print("Save Model:")
+        W = self.pnet.get_table(_lib.W)
+        with open(filename, "w") as f:
+            f.write("%d %d\n" % (len(self.names), self.dim))
+            for i, name in enumerate(self.names):
+                f.write("%s[%s]%s\n" % (name, self.type_keys[self.ntype[i]], "".join(" %.6f" % x for x in W[i])))
+        print("\tSave to <%s>" % filename)
 
     @property
     def w_context(self):

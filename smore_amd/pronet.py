@@ -193,6 +193,32 @@ class ProNet:
                                            int(walk_steps), int(window), int(K), float(alpha0), int(seed),
                                            ptr(order), _lib.MODE[mode]), "train_deepwalk")
 
+    def set_node_types(self, node_type, ntypes):
+        """Node types of a heterogeneous graph (pkg/hetero NodeTypes) for metapath2vec."""
+        node_type = np.ascontiguousarray(node_type, np.int32)
+        self._chk(lib.smore_set_node_types(self.ctx, ptr(node_type), int(ntypes)), "set_node_types")
+
+    def train_metapath2vec(self, walk_begin, walk_end, walk_times, walk_steps, window, K, alpha0, paths, seed,
+                           order, mode="hogwild"):
+        """(*Metapath2Vec).Train (Go, internal/models/metapath2vec/metapath2vec.go:106-200)
+        over walks [walk_begin, walk_end); paths = list of meta-paths (lists of type ids)."""
+        order = np.ascontiguousarray(order, np.int64)
+        flat = np.ascontiguousarray([t for p in paths for t in p] or [0], np.int32)
+        lens = np.ascontiguousarray([len(p) for p in paths], np.int32)
+        self._chk(lib.smore_train_metapath2vec(self.ctx, int(walk_begin), int(walk_end), int(walk_times),
+                                               int(walk_steps), int(window), int(K), float(alpha0), ptr(flat),
+                                               ptr(lens), len(paths), int(seed), ptr(order), _lib.MODE[mode]),
+                  "train_metapath2vec")
+
+    def train_node2vec(self, walk_begin, walk_end, walk_times, walk_steps, window, K, alpha0, p, q, seed, order,
+                       mode="hogwild"):
+        """(*Node2Vec).Train (Go, internal/models/node2vec/node2vec.go:178-258) over walks
+        [walk_begin, walk_end); needs set_semantics("go")."""
+        order = np.ascontiguousarray(order, np.int64)
+        self._chk(lib.smore_train_node2vec(self.ctx, int(walk_begin), int(walk_end), int(walk_times),
+                                           int(walk_steps), int(window), int(K), float(alpha0), float(p), float(q),
+                                           int(seed), ptr(order), _lib.MODE[mode]), "train_node2vec")
+
     def train_walklets(self, walk_begin, walk_end, walk_times, walk_steps, window_min, window_max, K, alpha0, seed,
                        mode="hogwild"):
         """Walklets::Train (src/model/Walklets.cpp:24-63) over walks [walk_begin, walk_end)."""
@@ -377,6 +403,15 @@ class Group:
                                                  int(walk_steps), int(window), int(K), float(alpha0), int(seed),
                                                  ptr(order), _lib.MODE[mode], int(per), int(bool(mean))),
                   "train_deepwalk")
+
+    def train_node2vec(self, walk_begin, walk_end, walk_times, walk_steps, window, K, alpha0, p, q, seed, order,
+                       mode="atomic", per=0, mean=False):
+        """(*Node2Vec).Train (Go, internal/models/node2vec/node2vec.go:178-258) over the replicas."""
+        order = np.ascontiguousarray(order, np.int64)
+        self._chk(lib.smore_group_train_node2vec(self.g, int(walk_begin), int(walk_end), int(walk_times),
+                                                 int(walk_steps), int(window), int(K), float(alpha0), float(p),
+                                                 float(q), int(seed), ptr(order), _lib.MODE[mode], int(per),
+                                                 int(bool(mean))), "train_node2vec")
 
     def train_walklets(self, walk_begin, walk_end, walk_times, walk_steps, window_min, window_max, K, alpha0, seed,
                        mode="hybrid", per=0, mean=False):

@@ -220,3 +220,62 @@ def deepwalk(pn, W, C, walk_times, steps, window, K, alpha0, seed, order):
             for j in range(max(0, i - window), min(len(walk), i + window + 1)):
                 if i != j:
                     pn.update_pair(W, C, walk[i], walk[j], K, a, rng)
+
+
+def node2vec_walk(pn, start, steps, p, q, rng):
+    """biasedRandomWalk / biasedTargetSample / areNeighbors
+    (internal/models/node2vec/node2vec.go:82-175), literally."""
+    walk = [start]
+    if steps == 0:
+        return walk
+    first = pn.target(start, rng)
+    if first == -1:
+        return walk
+    walk.append(first)
+    for _ in range(1, steps):
+        cur, prev = walk[-1], walk[-2]
+        nb = pn.graph[cur]
+        if not nb:
+            break
+        bw, total = [], 0.0
+        for i, n in enumerate(nb):
+            if n == prev:
+                bias = 1.0 / p
+            elif n in pn.graph[prev]:
+                bias = 1.0
+            else:
+                bias = 1.0 / q
+            bw.append(pn.weights[cur][i] * bias)
+            total += bw[-1]
+        if total == 0:
+            walk.append(nb[rng.intn(len(nb))])
+            continue
+        r = rng.float64() * total
+        cum, nxt = 0.0, nb[-1]
+        for i, x in enumerate(bw):
+            cum += x
+            if r <= cum:
+                nxt = nb[i]
+                break
+        walk.append(nxt)
+    return walk
+
+
+def metapath_walk(graph, ntype, start, meta_path, steps, rng):
+    """MetaPathWalk + SampleNeighborByType (pkg/hetero/hetero_graph.go:206-256),
+    literally: graph[v] = Edges[v] in push order, ntype[v] = the node's type."""
+    if len(meta_path) < 2:
+        return [start]
+    walk, cur, idx = [start], start, 0
+    while len(walk) < steps + 1:
+        if ntype[cur] != meta_path[idx % len(meta_path)]:
+            break
+        nt = meta_path[(idx + 1) % len(meta_path)]
+        indices = [i for i, n in enumerate(graph[cur]) if ntype[n] == nt]
+        if not indices:
+            break
+        nxt = graph[cur][indices[rng.intn(len(indices))]]
+        walk.append(nxt)
+        cur = nxt
+        idx += 1
+    return walk

@@ -98,3 +98,76 @@ def test_go_semantics_differ_from_cpp():
     c, d = W0.copy(), C0.copy()
     orc.train_edge_f64(gc, "line2", c, d, 5, 0.025, 0.0, 10 ** 6, 0, 2000, SEED)
     assert not np.allclose(a, c)
+
+
+@pytest.mark.parametrize("name,und,p,q", [("pl100w.txt", 1, 0.25, 4.0), ("pl100w.txt", 1, 2.0, 0.5),
+                                          ("bip.txt", 0, 1.0, 1.0), ("pl1k.txt", 1, 0.5, 2.0)])
+def test_go_node2vec_walk_equals_restatement(name, und, p, q):
+    """The C oracle's node2vec walk vs the literal Python restatement of
+    internal/models/node2vec/node2vec.go:82-175 (parity unpinned vs Go itself)."""
+    g, pn = graphs(name, und)
+    for unit in range(0, 400):
+        start = unit % g.V
+        got = orc.go_node2vec_walk(g, p, q, SEED, unit, start, 12)
+        want = ref.node2vec_walk(pn, start, 12, p, q, ref.Rng(SEED, 1, unit, 64))
+        assert list(got) == want, (unit, list(got), want)
+
+
+def test_go_node2vec_unbiased_equals_deepwalk_walks():
+    """p = q = 1: every bias is 1, so the biased scan is
+    the plain TargetSample scan and node2vec trains exactly as Go DeepWalk."""
+    g, _ = graphs("pl100w.txt", 1)
+    W0, C0 = _tables(g.V, 8, 5)
+    order = orc.deepwalk_order(g.V, 1, 0)
+    Wa, Ca = W0.astype(np.float32), C0.astype(np.float32)
+    Wb, Cb = Wa.copy(), Ca.copy()
+    orc.go_deepwalk_f32(g, Wa, Ca, 8, 1, 6, 2, 3, 0.025, SEED, order)
+    orc.go_node2vec_f32(g, Wb, Cb, 8, 1, 6, 2, 3, 0.025, 1.0, 1.0, SEED, order)
+    np.testing.assert_array_equal(Wa, Wb)
+    np.testing.assert_array_equal(Ca, Cb)
+
+
+def _hetero(und):
+    from smore_amd.go_models import load_hetero   # host-side parser (no GPU call)
+    names, ntype, tkeys, s, d, w = load_hetero(os.path.join(GOLDEN, "hetero.txt"), und)
+    return names, ntype, tkeys, s, d, w
+
+
+def test_hetero_loader_first_appearance():
+    names, ntype, tkeys, s, d, w = _hetero(True)
+    assert tkeys[:2] == ["User", "Item"] and set(tkeys) == {"User", "Item", "Category"}
+    first = {}
+    with open(os.path.join(GOLDEN, "hetero.txt")) as f:
+        for line in f:
+            p = line.split()
+            for nm, ty in ((p[0], p[1]), (p[2], p[3])):
+                first.setdefault(nm, ty)
+    assert names == list(first)
+    assert [tkeys[t] for t in ntype] == [first[n] for n in names]
+    assert len(s) == 2 * 214 and s[0] == d[1] and d[0] == s[1]
+
+
+@pytest.mark.parametrize("und", [1, 0])
+def test_go_metapath_walk_equals_restatement(und):
+    names, ntype, tkeys, s, d, w = _hetero(und)
+    g = orc.GoGraph(len(names), s, d, w, names)
+    graph = {v: [] for v in range(g.V)}
+    for a, b in zip(s, d):
+        graph[int(a)].append(int(b))
+    U, I, C_ = (tkeys.index(x) for x in ("User", "Item", "Category"))
+    paths = [[U, I, U], [I, C_, I], [U, I, C_, I, U], [C_]]
+    for unit in range(600):
+        start = unit % g.V
+        got = orc.go_metapath_walk(g, ntype, paths, SEED, unit, start, 9)
+        rng = ref.Rng(SEED, 1, unit, 64)
+        mp = paths[rng.intn(len(paths))]
+        want = ref.metapath_walk(graph, ntype, start, mp, 9, rng)
+        assert list(got) == want, unit
+
+
+def test_go_uniform_negative_table():
+    """metapath2vec.go:140-145: BuildAliasMethod(ones, 0.75) is {prob 1, alias i}
+    exactly (what smore_amd.go_models.Metapath2Vec injects)."""
+    p, a = orc.alias_go(np.ones(101), 0.75)
+    np.testing.assert_array_equal(p, np.ones(101))
+    np.testing.assert_array_equal(a, np.arange(101))

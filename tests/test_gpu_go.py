@@ -165,7 +165,7 @@ def test_go_rejects_mf(smore):
 
 
 def test_go_model_drivers(smore, tmp_path):
-    """internal/models/{line,bpr,deepwalk} mirrors: Go totals and Go save format."""
+    """internal/models/{line,bpr,deepwalk,node2vec} mirrors: Go totals and Go save format."""
     from smore_amd import go_models
     path = os.path.join(GOLDEN, "pl1k.txt")
     m = go_models.LINE.New()
@@ -188,3 +188,96 @@ def test_go_model_drivers(smore, tmp_path):
     d.Init(8)
     d.Train(1, 10, 2, 3, 0.025, 1)
     assert np.isfinite(d.w_context).all()
+    n = go_models.Node2Vec.New()
+    n.LoadEdgeList(path, True)
+    n.Init(8, 0.5, 2.0)
+    n.Train(1, 10, 2, 3, 0.025, 1)
+    assert np.isfinite(n.w_context).all() and np.abs(n.w_vertex).max() > 0
+
+
+@pytest.mark.parametrize("fname,und,p,q,dim,K,window,steps",
+                         [("pl100w.txt", 1, 0.25, 4.0, 16, 5, 2, 10), ("pl1k.txt", 1, 2.0, 0.5, 64, 5, 5, 40),
+                          ("toy.txt", 0, 0.5, 2.0, 8, 3, 2, 8), ("pl100w.txt", 1, 1.0, 1.0, 100, 10, 3, 20)])
+def test_go_node2vec_serial_bit_exact(smore, fname, und, p, q, dim, K, window, steps):
+    """(*Node2Vec).Train (internal/models/node2vec/node2vec.go:178-258) on the GPU
+    vs the oracle's fp32 spec of it (parity unpinned vs Go: no Go toolchain)."""
+    g, pn = pair(smore, fname, und)
+    W0, C0 = tables(g.V, dim, dim + 1)
+    pn.alloc_tables(dim, 2)
+    pn.set_table(0, W0)
+    pn.set_table(1, C0)
+    order = orc.deepwalk_order(g.V, 2, 3)
+    half = g.V   # two calls: the second starts mid-order
+    pn.train_node2vec(0, half, 2, steps, window, K, 0.025, p, q, SEED, order, "serial")
+    pn.train_node2vec(half, 2 * g.V, 2, steps, window, K, 0.025, p, q, SEED, order, "serial")
+    W, C = padded(W0, dim), padded(C0, dim)
+    orc.go_node2vec_f32(g, W, C, dim, 2, steps, window, K, 0.025, p, q, SEED, order)
+    np.testing.assert_array_equal(pn.get_table(0), W[:, :dim])
+    np.testing.assert_array_equal(pn.get_table(1), C[:, :dim])
+
+
+def test_go_node2vec_parallel_and_rejects(smore):
+    g, pn = pair(smore, "pl1k.txt", 1)
+    W0, C0 = tables(g.V, 32, 7)
+    pn.alloc_tables(32, 2)
+    pn.set_table(0, W0)
+    pn.set_table(1, C0)
+    order = orc.deepwalk_order(g.V, 4, 0)
+    with pytest.raises(smore._lib.SmoreError):
+        pn.train_node2vec(0, 4 * g.V, 4, 20, 3, 5, 0.025, 0.0, 1.0, SEED, order, "atomic")   # p <= 0
+    pn.train_node2vec(0, 4 * g.V, 4, 20, 3, 5, 0.025, 0.5, 2.0, SEED, order, "atomic")
+    W = pn.get_table(0)
+    assert np.isfinite(W).all() and np.abs(W - W0).max() > 1e-3
+    pn.set_semantics("cpp")
+    with pytest.raises(smore._lib.SmoreError):
+        pn.train_node2vec(0, g.V, 1, 20, 3, 5, 0.025, 0.5, 2.0, SEED, order, "atomic")   # Go model only
+
+
+def _hetero_pair(smore, und):
+    from smore_amd.go_models import load_hetero
+    names, ntype, tkeys, s, d, w = load_hetero(os.path.join(GOLDEN, "hetero.txt"), und)
+    g = orc.GoGraph(len(names), s, d, w, names)
+    prob, alias = orc.go_uniform_negatives(g)
+    pn = smore.ProNet(0)
+    pn.set_graph_edges(len(names), s, d, w)
+    pn.set_semantics("go")
+    pn.set_node_types(ntype, len(tkeys))
+    pn.set_alias(smore._lib.AT_NEGATIVE, prob, alias)
+    U, I, C_ = (tkeys.index(x) for x in ("User", "Item", "Category"))
+    return g, pn, ntype, [[U, I, U], [I, C_, I], [U, I, C_, I, U]]
+
+
+@pytest.mark.parametrize("und,dim,K,window,steps", [(1, 16, 5, 2, 10), (1, 64, 5, 5, 40), (0, 8, 3, 2, 8)])
+def test_go_metapath2vec_serial_bit_exact(smore, und, dim, K, window, steps):
+    """(*Metapath2Vec).Train (internal/models/metapath2vec/metapath2vec.go:106-200)
+    on the GPU vs the oracle's fp32 spec (parity unpinned vs Go: no Go toolchain)."""
+    g, pn, ntype, paths = _hetero_pair(smore, und)
+    W0, C0 = tables(g.V, dim, dim + 3)
+    pn.alloc_tables(dim, 2)
+    pn.set_table(0, W0)
+    pn.set_table(1, C0)
+    order = orc.deepwalk_order(g.V, 2, 1)
+    pn.train_metapath2vec(0, g.V + 7, 2, steps, window, K, 0.025, paths, SEED, order, "serial")
+    pn.train_metapath2vec(g.V + 7, 2 * g.V, 2, steps, window, K, 0.025, paths, SEED, order, "serial")
+    W, C = padded(W0, dim), padded(C0, dim)
+    orc.go_metapath_f32(g, ntype, paths, W, C, dim, 2, steps, window, K, 0.025, SEED, order)
+    np.testing.assert_array_equal(pn.get_table(0), W[:, :dim])
+    np.testing.assert_array_equal(pn.get_table(1), C[:, :dim])
+
+
+def test_go_metapath2vec_model_driver(smore, tmp_path):
+    from smore_amd import go_models
+    m = go_models.Metapath2Vec.New(mode="atomic")
+    m.LoadEdgeList(os.path.join(GOLDEN, "hetero.txt"), True)
+    with pytest.raises(ValueError):
+        m.AddMetaPath("User Nope")
+    m.AddMetaPath("User Item User")
+    m.AddMetaPath("Item Category Item")
+    m.Init(16)
+    m.Train(3, 10, 2, 5, 0.025, 4)
+    W = m.w_vertex
+    assert np.isfinite(W).all() and np.abs(W).max() > 0
+    out = tmp_path / "mp.txt"
+    m.SaveEmbeddings(str(out))
+    lines = out.read_text().splitlines()
+    assert lines[0] == "%d 16" % len(m.names) and lines[1].split()[0].endswith("]")
