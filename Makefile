@@ -15,7 +15,7 @@ LIB      ?= smore_amd/lib/libsmore_hip.so
 BIN      := smore_amd/bin
 # kernels depend on the device headers only; host objects on the host headers
 DEV_HDRS := $(SRC)/device_common.h $(SRC)/train_kernels.h $(SRC)/edge_kernels.h $(SRC)/edge_inst.h
-HOST_HDRS := $(SRC)/host_graph.h $(SRC)/ctx.h $(SRC)/train_kernels.h $(SRC)/device_common.h include/smore_hip.h
+HOST_HDRS := $(SRC)/host_graph.h $(SRC)/ctx.h $(SRC)/train_kernels.h $(SRC)/device_common.h $(SRC)/go_walks.h include/smore_hip.h
 
 .PHONY: all lib cli goshape oracle ref clean
 all: lib cli goshape
@@ -30,6 +30,9 @@ $(OBJ)/%.o: $(SRC)/%.cpp $(HOST_HDRS)
 $(OBJ)/%.o: $(SRC)/%.hip $(DEV_HDRS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+# the Go walk kernels also depend on the CTDNE declarations
+$(OBJ)/train_go.o: $(SRC)/go_walks.h
 
 LIB_OBJS := $(patsubst %,$(OBJ)/%.o,$(HOST_SRCS)) $(patsubst $(SRC)/%.hip,$(OBJ)/%.o,$(wildcard $(SRC)/*.hip))
 

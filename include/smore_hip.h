@@ -323,6 +323,27 @@ int smore_train_metapath2vec_async(smore_ctx* ctx, uint64_t walk_begin, uint64_t
                                    int walk_steps, int window, int K, double alpha0, const int32_t* paths,
                                    const int32_t* path_lens, int npaths, uint64_t seed,
                                    const int64_t* order, int mode);
+/* replaces: pkg/temporal's OutEdges / GetActiveTimeRange (temporal_graph.go:
+ * 60-170, 254-288) for CTDNE: E timestamped directed edges src->dst (ids of
+ * the graph set by smore_set_graph_edges; the Go caller keeps its temporal
+ * loader).  Out-edges are sorted by timestamp per source (stable). */
+int smore_set_temporal_edges(smore_ctx* ctx, int64_t E, const int32_t* src, const int32_t* dst,
+                             const double* ts);
+/* replaces: (*CTDNE).Train (Go, internal/models/ctdne/ctdne.go:80-200): walks
+ * [walk_begin, walk_end) of walk_times*V from order[]; a start without edges
+ * trains nothing; startTime = min + Float64()*(max - min, or time_window when
+ * 0); TemporalRandomWalk (temporal_graph.go:225-252, incl. its timestamp of
+ * OutEdges[cur][idx]); Go SkipGrams + UpdatePairs with the context's
+ * negative table (CTDNE's BuildAliasMethod(activity, 0.75) is the Go table of
+ * the temporal edges given unit weights).  time_window <= 0: 0.1 x the time
+ * span (ctdne.go:45-49).  Go semantics only.  Draws: stream 1, unit w: slot 0
+ * the start time, 1 slot per step, then 2K per pair. */
+int smore_train_ctdne(smore_ctx* ctx, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
+                      int window, int K, double alpha0, double time_window, uint64_t seed,
+                      const int64_t* order, int mode);
+int smore_train_ctdne_async(smore_ctx* ctx, uint64_t walk_begin, uint64_t walk_end, int walk_times,
+                            int walk_steps, int window, int K, double alpha0, double time_window,
+                            uint64_t seed, const int64_t* order, int mode);
 /* the reference's walk start order: per walk_time a Fisher-Yates shuffle with
  * glibc rand() after `skip` Init draws (src/model/DeepWalk.cpp:122-131) */
 int smore_deepwalk_order(int64_t V, int walk_times, uint64_t skip, int64_t* order);

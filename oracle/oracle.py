@@ -398,6 +398,11 @@ def _declare_go(L):
     L.orc_go_deepwalk_f32.restype = C.c_int
     L.orc_go_deepwalk_f32.argtypes = [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, dbl, u64, P,
                                       u64, u64]
+    L.orc_go_ctdne_walk.restype = C.c_int
+    L.orc_go_ctdne_walk.argtypes = [i64, i64, P, P, P, dbl, u64, u64, C.c_int32, C.c_int, P]
+    L.orc_go_ctdne_f32.restype = C.c_int
+    L.orc_go_ctdne_f32.argtypes = [P, i64, P, P, P, dbl, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                   C.c_int, dbl, u64, P, u64, u64]
     L.orc_go_metapath_walk.restype = C.c_int
     L.orc_go_metapath_walk.argtypes = [P, P, P, P, C.c_int, u64, u64, C.c_int32, C.c_int, P]
     L.orc_go_metapath_f32.restype = C.c_int
@@ -500,3 +505,24 @@ def go_metapath_f32(g, ntype, paths, W, C_, dim, walk_times, walk_steps, window,
     return lib().orc_go_metapath_f32(g.ref, ptr(ntype), ptr(flat), ptr(off), len(paths), ptr(W), ptr(C_), dim,
                                      W.shape[1], walk_times, walk_steps, window, K, alpha0, seed, ptr(order),
                                      begin, end)
+
+
+def go_ctdne_walk(V, src, dst, ts, window, seed, unit, start, steps):
+    src = np.ascontiguousarray(src, np.int32)
+    dst = np.ascontiguousarray(dst, np.int32)
+    ts = np.ascontiguousarray(ts, np.float64)
+    out = np.zeros(steps + 1, np.int32)
+    L = lib().orc_go_ctdne_walk(V, len(src), ptr(src), ptr(dst), ptr(ts), window, seed, unit, start, steps, ptr(out))
+    return out[:L].copy()
+
+
+def go_ctdne_f32(g, src, dst, ts, window, W, C_, dim, walk_times, walk_steps, win, K, alpha0, seed, order, begin=0,
+                 end=None):
+    src = np.ascontiguousarray(src, np.int32)
+    dst = np.ascontiguousarray(dst, np.int32)
+    ts = np.ascontiguousarray(ts, np.float64)
+    order = np.ascontiguousarray(order, np.int64)
+    if end is None:
+        end = walk_times * g.V
+    return lib().orc_go_ctdne_f32(g.ref, len(src), ptr(src), ptr(dst), ptr(ts), window, ptr(W), ptr(C_), dim,
+                                  W.shape[1], walk_times, walk_steps, win, K, alpha0, seed, ptr(order), begin, end)

@@ -1,3 +1,4 @@
+#include <float.h>
 /*
  * smore_oracle.c -- CPU restatement of SMORe's sampled negative-sampling SGD hot
  * path (proNet alias samplers + Opt_SigmoidSGD / Opt_SGD / Opt_BPRSGD updates).
@@ -1389,6 +1390,90 @@ int orc_go_metapath_walk(const orc_go_graph* g, const int32_t* ntype, const int3
     return go_mp_walk(g, &mp, &r, start, steps, walk);
 }
 
+/* ---- Go CTDNE (internal/models/ctdne, pkg/temporal) ------------------------- */
+typedef struct {
+    int64_t V, E;
+    int64_t* off;      /* OutEdges per source, time-sorted (stable insertion sort) */
+    int32_t* tgt;
+    double* ts;
+    double* tmin;      /* GetActiveTimeRange */
+    double* tmax;
+    double max_time, window;
+} ct_graph;
+
+static void ct_build(ct_graph* t, int64_t V, int64_t E, const int32_t* src, const int32_t* dst, const double* ts) {
+    t->V = V; t->E = E;
+    t->off = (int64_t*)calloc((size_t)V + 1, sizeof(int64_t));
+    t->tgt = (int32_t*)malloc(sizeof(int32_t) * (size_t)(E + 1));
+    t->ts = (double*)malloc(sizeof(double) * (size_t)(E + 1));
+    t->tmin = (double*)malloc(sizeof(double) * (size_t)V);
+    t->tmax = (double*)malloc(sizeof(double) * (size_t)V);
+    for (int64_t i = 0; i < E; ++i) t->off[src[i] + 1]++;
+    for (int64_t v = 0; v < V; ++v) t->off[v + 1] += t->off[v];
+    int64_t* fill = (int64_t*)malloc(sizeof(int64_t) * (size_t)(V + 1));
+    memcpy(fill, t->off, sizeof(int64_t) * (size_t)V);
+    for (int64_t i = 0; i < E; ++i) {   /* append in input order, then insertion-sort by time (stable) */
+        int64_t x = fill[src[i]]++;
+        int64_t b = t->off[src[i]];
+        while (x > b && t->ts[x - 1] > ts[i]) { t->ts[x] = t->ts[x - 1]; t->tgt[x] = t->tgt[x - 1]; x--; }
+        t->ts[x] = ts[i]; t->tgt[x] = dst[i];
+    }
+    free(fill);
+    t->max_time = -DBL_MAX;
+    for (int64_t v = 0; v < V; ++v) { t->tmin[v] = DBL_MAX; t->tmax[v] = -DBL_MAX; }
+    for (int64_t i = 0; i < E; ++i) {
+        int32_t ends[2] = {src[i], dst[i]};
+        for (int k = 0; k < 2; ++k) {
+            if (ts[i] < t->tmin[ends[k]]) t->tmin[ends[k]] = ts[i];
+            if (ts[i] > t->tmax[ends[k]]) t->tmax[ends[k]] = ts[i];
+        }
+        if (ts[i] > t->max_time) t->max_time = ts[i];
+    }
+    for (int64_t v = 0; v < V; ++v) if (t->tmin[v] == DBL_MAX) t->tmin[v] = t->tmax[v] = 0.0;
+}
+
+static void ct_free(ct_graph* t) { free(t->off); free(t->tgt); free(t->ts); free(t->tmin); free(t->tmax); }
+
+/* ctdne.go:159-170 start time + TemporalRandomWalk (temporal_graph.go:225-252)
+ * with GetTemporalNeighbors' scan (:181-196) and SampleTemporalNeighbor's
+ * timestamp of OutEdges[cur][idx] (:198-208) */
+static int go_ct_walk(const ct_graph* t, walk_rng* r, int32_t start, int steps, int32_t* walk) {
+    int L = 0;
+    walk[L++] = start;
+    double lo = t->tmin[start], hi = t->tmax[start];
+    if (lo == 0.0 && hi == 0.0) return L;
+    double range = hi - lo;
+    if (range == 0.0) range = t->window;
+    double now = lo + draw_unit(walk_next(r)) * range;
+    int32_t cur = start;
+    while (L < steps + 1) {
+        double end = now + t->window;
+        if (end > t->max_time) end = t->max_time;
+        int64_t b = t->off[cur], e = t->off[cur + 1], n = 0, first = -1;
+        for (int64_t x = b; x < e; ++x) {
+            if (t->ts[x] >= now && t->ts[x] <= end) { if (first < 0) first = x; n++; }
+            if (t->ts[x] > end) break;
+        }
+        if (n == 0) break;
+        int64_t idx = (int64_t)draw_index(walk_next(r), (uint64_t)n);
+        cur = t->tgt[first + idx];
+        now = t->ts[b + idx];
+        walk[L++] = cur;
+    }
+    return L;
+}
+
+int orc_go_ctdne_walk(int64_t V, int64_t E, const int32_t* src, const int32_t* dst, const double* ts, double window,
+                      uint64_t seed, uint64_t unit, int32_t start, int steps, int32_t* walk) {
+    ct_graph t;
+    ct_build(&t, V, E, src, dst, ts);
+    t.window = window;
+    walk_rng r = {seed, unit, 0, {0, 0, 0, 0}, 0xFFFFFFFFu};
+    int L = go_ct_walk(&t, &r, start, steps, walk);
+    ct_free(&t);
+    return L;
+}
+
 static int go_skip_grams(const int32_t* walk, int L, int window, int32_t* pv, int32_t* pc) {
     int n = 0;
     for (int i = 0; i < L; ++i) {
@@ -1403,7 +1488,7 @@ static int go_skip_grams(const int32_t* walk, int L, int window, int32_t* pv, in
 static int go_deepwalk(const orc_go_graph* g, double* W64, double* C64, float* W32, float* C32, int dim, int dpad,
                        int walk_times, int walk_steps, int window, int K, double alpha0, uint64_t seed,
                        const int64_t* order, uint64_t walk_begin, uint64_t walk_end, const n2v_params* n2v,
-                       const mp_params* mp) {
+                       const mp_params* mp, const ct_graph* ct) {
     sig_init();
     uint64_t total = (uint64_t)walk_times * (uint64_t)g->base.V;
     if (walk_end > total) walk_end = total;
@@ -1418,7 +1503,8 @@ static int go_deepwalk(const orc_go_graph* g, double* W64, double* C64, float* W
     for (uint64_t wk = walk_begin; wk < walk_end; ++wk) {
         walk_rng r = {seed, wk, 0, {0, 0, 0, 0}, 0xFFFFFFFFu};
         double alpha = orc_alpha_walk(wk, alpha0, total);
-        int L = mp    ? go_mp_walk(g, mp, &r, (int32_t)order[wk], walk_steps, walk)
+        int L = ct    ? go_ct_walk(ct, &r, (int32_t)order[wk], walk_steps, walk)
+                : mp  ? go_mp_walk(g, mp, &r, (int32_t)order[wk], walk_steps, walk)
                 : n2v ? go_n2v_walk(g, n2v, &r, (int32_t)order[wk], walk_steps, walk)
                       : go_random_walk(g, &r, (int32_t)order[wk], walk_steps, walk);
         int np = go_skip_grams(walk, L, window, pv, pc);
@@ -1439,13 +1525,13 @@ int orc_go_deepwalk_f32(const orc_go_graph* g, float* W, float* C, int dim, int 
                         int walk_steps, int window, int K, double alpha0, uint64_t seed,
                         const int64_t* order, uint64_t walk_begin, uint64_t walk_end) {
     return go_deepwalk(g, NULL, NULL, W, C, dim, dpad, walk_times, walk_steps, window, K, alpha0, seed, order,
-                       walk_begin, walk_end, NULL, NULL);
+                       walk_begin, walk_end, NULL, NULL, NULL);
 }
 
 int orc_go_deepwalk_f64(const orc_go_graph* g, double* W, double* C, int dim, int walk_times, int walk_steps,
                         int window, int K, double alpha0, uint64_t seed, const int64_t* order) {
     return go_deepwalk(g, W, C, NULL, NULL, dim, dim, walk_times, walk_steps, window, K, alpha0, seed, order, 0,
-                       (uint64_t)-1, NULL, NULL);
+                       (uint64_t)-1, NULL, NULL, NULL);
 }
 
 /* Go node2vec = Go DeepWalk with biasedRandomWalk (node2vec.go:178-258) */
@@ -1454,7 +1540,7 @@ int orc_go_node2vec_f32(const orc_go_graph* g, const double* weights, float* W, 
                         uint64_t seed, const int64_t* order, uint64_t walk_begin, uint64_t walk_end) {
     n2v_params np_ = {weights, 1.0 / p, 1.0 / q};
     return go_deepwalk(g, NULL, NULL, W, C, dim, dpad, walk_times, walk_steps, window, K, alpha0, seed, order,
-                       walk_begin, walk_end, &np_, NULL);
+                       walk_begin, walk_end, &np_, NULL, NULL);
 }
 
 /* Go metapath2vec = Go DeepWalk's pairs over MetaPathWalk (metapath2vec.go:106-200);
@@ -1465,5 +1551,20 @@ int orc_go_metapath_f32(const orc_go_graph* g, const int32_t* ntype, const int32
                         uint64_t walk_end) {
     mp_params mp = {ntype, paths, path_off, npaths};
     return go_deepwalk(g, NULL, NULL, W, C, dim, dpad, walk_times, walk_steps, window, K, alpha0, seed, order,
-                       walk_begin, walk_end, NULL, &mp);
+                       walk_begin, walk_end, NULL, &mp, NULL);
+}
+
+/* Go CTDNE = Go DeepWalk's pairs over the temporal walks (ctdne.go:80-200);
+ * negatives from g's negative table (the Go table of the edges, unit weights) */
+int orc_go_ctdne_f32(const orc_go_graph* g, int64_t E, const int32_t* src, const int32_t* dst, const double* ts,
+                     double window, float* W, float* C, int dim, int dpad, int walk_times, int walk_steps,
+                     int win, int K, double alpha0, uint64_t seed, const int64_t* order, uint64_t walk_begin,
+                     uint64_t walk_end) {
+    ct_graph t;
+    ct_build(&t, g->base.V, E, src, dst, ts);
+    t.window = window;
+    int rc = go_deepwalk(g, NULL, NULL, W, C, dim, dpad, walk_times, walk_steps, win, K, alpha0, seed, order,
+                         walk_begin, walk_end, NULL, NULL, &t);
+    ct_free(&t);
+    return rc;
 }

@@ -68,6 +68,9 @@ def _load():
         "smore_delta_cycle": (i32, [P, P, P, P, P, C.c_float, i64]),
         "smore_train_deepwalk": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, u64, P, i32]),
         "smore_train_deepwalk_async": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, u64, P, i32]),
+        "smore_set_temporal_edges": (i32, [P, i64, P, P, P]),
+        "smore_train_ctdne": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, dbl, u64, P, i32]),
+        "smore_train_ctdne_async": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, dbl, u64, P, i32]),
         "smore_set_node_types": (i32, [P, P, i32]),
         "smore_train_metapath2vec": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, P, P, i32, u64, P, i32]),
         "smore_train_metapath2vec_async": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, P, P, i32, u64, P, i32]),

@@ -4,6 +4,7 @@
 // fastSigmoid table) and the embedding tables.  Everything on the device is
 // uploaded once; training calls only launch kernels on the context stream.
 #include "ctx.h"
+#include "go_walks.h"
 
 #include <algorithm>
 #include <chrono>
@@ -11,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <string>
 #include <thread>
 #include <vector>
@@ -58,7 +60,7 @@ void smore_destroy(smore_ctx* c) {
     dfree(c->d_offsets); dfree(c->d_targets); dfree(c->d_vtab); dfree(c->d_ntab); dfree(c->d_ctab);
     dfree(c->d_sig); dfree(c->d_skipped); dfree(c->d_work); dfree(c->d_table[0]); dfree(c->d_table[1]);
 
-    dfree(c->d_order); dfree(c->d_walks); dfree(c->d_lens); dfree(c->d_tcum); dfree(c->d_wts); dfree(c->d_nbr_sorted); dfree(c->d_ntype); dfree(c->d_ttargets); dfree(c->d_toff); dfree(c->d_paths); dfree(c->d_path_off); dfree(c->d_sh_hash); dfree(c->d_sh_ids);
+    dfree(c->d_order); dfree(c->d_walks); dfree(c->d_lens); dfree(c->d_tcum); dfree(c->d_wts); dfree(c->d_nbr_sorted); dfree(c->d_ntype); dfree(c->d_ttargets); dfree(c->d_toff); dfree(c->d_paths); dfree(c->d_path_off); dfree(c->d_t_off); dfree(c->d_t_tgt); dfree(c->d_t_ts); dfree(c->d_t_min); dfree(c->d_t_max); dfree(c->d_sh_hash); dfree(c->d_sh_ids);
     dfree(c->d_rec); dfree(c->d_vt32); dfree(c->d_ct16);
     dfree(c->d_pcount); dfree(c->d_poff);
     if (c->d_scan_tmp) (void)hipFree(c->d_scan_tmp);
@@ -825,10 +827,62 @@ int smore_set_node_types(smore_ctx* c, const int32_t* node_type, int ntypes) {
     return SMORE_OK;
 }
 
+// CTDNE's temporal graph (pkg/temporal/temporal_graph.go:60-170, 254-288):
+// OutEdges per source sorted by timestamp (stable: Go's sort.Slice leaves the
+// order of equal timestamps unspecified), the active time range of every
+// vertex over its out- and in-edges ({0, 0} without edges), Min/MaxTime.
+int smore_set_temporal_edges(smore_ctx* c, int64_t E, const int32_t* src, const int32_t* dst, const double* ts) {
+    if (!c || E < 0 || (E > 0 && (!src || !dst || !ts))) return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    const int64_t V = c->g->V;
+    for (int64_t i = 0; i < E; ++i)
+        if (src[i] < 0 || src[i] >= V || dst[i] < 0 || dst[i] >= V)
+            return fail(c, SMORE_EINVAL, "temporal edge id out of range");
+    std::vector<int64_t> off((size_t)V + 1, 0);
+    for (int64_t i = 0; i < E; ++i) off[(size_t)src[i] + 1]++;
+    for (int64_t v = 0; v < V; ++v) off[v + 1] += off[v];
+    std::vector<int64_t> slot(off.begin(), off.end() - 1), perm((size_t)std::max<int64_t>(1, E));
+    for (int64_t i = 0; i < E; ++i) perm[slot[src[i]]++] = i;
+    std::vector<int32_t> tgt((size_t)std::max<int64_t>(1, E));
+    std::vector<double> tts((size_t)std::max<int64_t>(1, E));
+    std::vector<double> tmin((size_t)V, std::numeric_limits<double>::max());
+    std::vector<double> tmax((size_t)V, -std::numeric_limits<double>::max());
+    double lo = std::numeric_limits<double>::max(), hi = -std::numeric_limits<double>::max();
+    for (int64_t v = 0; v < V; ++v) {
+        std::stable_sort(perm.begin() + off[v], perm.begin() + off[v + 1],
+                         [&](int64_t a, int64_t b) { return ts[a] < ts[b]; });
+        for (int64_t x = off[v]; x < off[v + 1]; ++x) {
+            tgt[x] = dst[perm[x]];
+            tts[x] = ts[perm[x]];
+        }
+    }
+    for (int64_t i = 0; i < E; ++i) {
+        for (int32_t v : {src[i], dst[i]}) {
+            tmin[v] = std::min(tmin[v], ts[i]);
+            tmax[v] = std::max(tmax[v], ts[i]);
+        }
+        lo = std::min(lo, ts[i]);
+        hi = std::max(hi, ts[i]);
+    }
+    for (int64_t v = 0; v < V; ++v)
+        if (tmin[v] == std::numeric_limits<double>::max()) tmin[v] = tmax[v] = 0.0;
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    if ((rc = upload(c, c->d_t_off, off.data(), off.size()))) return rc;
+    if ((rc = upload(c, c->d_t_tgt, tgt.data(), tgt.size()))) return rc;
+    if ((rc = upload(c, c->d_t_ts, tts.data(), tts.size()))) return rc;
+    if ((rc = upload(c, c->d_t_min, tmin.data(), tmin.size()))) return rc;
+    if ((rc = upload(c, c->d_t_max, tmax.data(), tmax.size()))) return rc;
+    c->t_min_time = lo;
+    c->t_max_time = hi;
+    c->has_temporal = true;
+    return SMORE_OK;
+}
+
 static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
                        int window, int window_min, int K, double alpha0, uint64_t seed, const int64_t* order,
                        uint64_t order_base, int mode, double n2v_p = 1.0, double n2v_q = 1.0,
-                       int npaths = 0) {
+                       int npaths = 0, double time_window = 0.0) {
     if (!c) return SMORE_EINVAL;
     if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
     if (c->ntables < 2) return fail(c, SMORE_ESTATE, "walk models need W and C tables");
@@ -840,6 +894,10 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
     if (rule == 2 && c->semantics != SMORE_SEM_GO)
         return fail(c, SMORE_EINVAL, "node2vec is a Go model: smore_set_semantics(ctx, SMORE_SEM_GO) first");
     if (rule == 2 && !(n2v_p > 0 && n2v_q > 0)) return fail(c, SMORE_EINVAL, "node2vec: need p > 0 and q > 0");
+    if (rule == 4 && c->semantics != SMORE_SEM_GO)
+        return fail(c, SMORE_EINVAL, "CTDNE is a Go model: smore_set_semantics(ctx, SMORE_SEM_GO) first");
+    if (rule == 4 && !c->has_temporal) return fail(c, SMORE_ESTATE, "CTDNE: no temporal edges");
+    if (rule == 4 && time_window <= 0) time_window = (c->t_max_time - c->t_min_time) * 0.1;   // ctdne.go:45-49
     if (rule == 3 && c->semantics != SMORE_SEM_GO)
         return fail(c, SMORE_EINVAL, "metapath2vec is a Go model: smore_set_semantics(ctx, SMORE_SEM_GO) first");
     if (rule == 3 && (c->ntypes <= 0 || npaths <= 0 || !c->d_paths))
@@ -962,12 +1020,16 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
         w.path_off = c->d_path_off;
         w.ntypes = c->ntypes;
         w.npaths = npaths;
-        w.slot_extra = rule == 3 ? 1 : 0;
+        w.slot_extra = rule >= 3 ? 1 : 0;   // metapath2vec: the path pick; CTDNE: the start time
         const int64_t groups_per_block = 256 / lanes_of(c->dpad);
         int g2 = grid;
         if ((int64_t)g2 * groups_per_block > (int64_t)w.nwalks && mode != SMORE_SERIAL)
             g2 = (int)std::max<int64_t>(1, ((int64_t)w.nwalks + groups_per_block - 1) / groups_per_block);
-        if (c->semantics == SMORE_SEM_GO) {
+        if (rule == 4) {
+            TemporalArgs tg{c->d_t_off, c->d_t_tgt, c->d_t_ts, c->d_t_min, c->d_t_max, c->t_max_time, time_window};
+            HIPCHK(c, launch_go_ctdne_walk(tg, w, seed, c->stream));
+            HIPCHK(c, launch_go_pairs(a, w, g2, c->stream));
+        } else if (c->semantics == SMORE_SEM_GO) {
             HIPCHK(c, launch_go_walk(a, w, g2, c->stream));
         } else {
             // counts of walks [0, n) plus a zero at n: the exclusive scan's entry
@@ -1037,6 +1099,22 @@ int smore_train_metapath2vec(smore_ctx* c, uint64_t walk_begin, uint64_t walk_en
                              int npaths, uint64_t seed, const int64_t* order, int mode) {
     int rc = smore_train_metapath2vec_async(c, walk_begin, walk_end, walk_times, walk_steps, window, K, alpha0, paths,
                                             path_lens, npaths, seed, order, mode);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return SMORE_OK;
+}
+
+int smore_train_ctdne_async(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
+                            int window, int K, double alpha0, double time_window, uint64_t seed, const int64_t* order,
+                            int mode) {
+    return train_walks(c, 4, walk_begin, walk_end, walk_times, walk_steps, window, 0, K, alpha0, seed, order, 0, mode,
+                       1.0, 1.0, 0, time_window);
+}
+
+int smore_train_ctdne(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps, int window,
+                      int K, double alpha0, double time_window, uint64_t seed, const int64_t* order, int mode) {
+    int rc = smore_train_ctdne_async(c, walk_begin, walk_end, walk_times, walk_steps, window, K, alpha0, time_window,
+                                     seed, order, mode);
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return SMORE_OK;

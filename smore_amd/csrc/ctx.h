@@ -71,6 +71,14 @@ struct smore_ctx {
     int ntypes = 0;
     int32_t* d_paths = nullptr;
     int32_t* d_path_off = nullptr;
+    // CTDNE (Go): time-sorted out-edges and active time ranges (smore_set_temporal_edges)
+    int64_t* d_t_off = nullptr;
+    int32_t* d_t_tgt = nullptr;
+    double* d_t_ts = nullptr;
+    double* d_t_min = nullptr;
+    double* d_t_max = nullptr;
+    double t_min_time = 0.0, t_max_time = 0.0;
+    bool has_temporal = false;
     // hybrid write-combining: super-hot context rows (hash + slot ids)
     int2* d_sh_hash = nullptr;
     int32_t* d_sh_ids = nullptr;
@@ -152,6 +160,12 @@ inline int upload_graph(smore_ctx* c) {
     dfree(c->d_ttargets);
     dfree(c->d_toff);
     c->ntypes = 0;
+    dfree(c->d_t_off);
+    dfree(c->d_t_tgt);
+    dfree(c->d_t_ts);
+    dfree(c->d_t_min);
+    dfree(c->d_t_max);
+    c->has_temporal = false;
     if (c->device < 0) {
         c->has_graph = true;
         return SMORE_OK;

@@ -17,6 +17,7 @@
 // oracle's orc_go_*_f32 is the bit-exact spec.  Same lane layout as
 // edge_kernels.h.
 #include "edge_kernels.h"
+#include "go_walks.h"
 
 namespace smore {
 
@@ -397,6 +398,64 @@ __global__ void go_mp_walk_gen_kernel(WalkArgs w, uint64_t seed) {
     w.lens[t] = L;
 }
 
+// CTDNE walk (internal/models/ctdne/ctdne.go:159-188, pkg/temporal/
+// temporal_graph.go:181-252).  A start vertex without edges (active range
+// {0, 0}) trains nothing and draws nothing.  Slot 0: startTime = min +
+// Float64() * (max - min, or timeWindow when 0).  Each step: the out-edges of
+// cur with timestamp in [t, min(t + timeWindow, MaxTime)] -- contiguous in the
+// time-sorted list, found by binary search -- one picked by Intn (the next
+// slot); the walk moves to its target and, as the Go code does, to the
+// timestamp of the idx-th out-edge of cur overall (OutEdges[cur][idx]).
+__global__ void go_ctdne_walk_gen_kernel(TemporalArgs tg, WalkArgs w, uint64_t seed) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= w.nwalks) return;
+    const uint64_t unit = w.walk_begin + t;
+    int32_t* out = w.walks + t * (uint64_t)(w.steps + 1);
+    int32_t cur = (int32_t)w.order[unit - w.order_base];
+    out[0] = cur;
+    int L = 1;
+    const double lo_t = tg.tmin[cur], hi_t = tg.tmax[cur];
+    if (!(lo_t == 0.0 && hi_t == 0.0)) {
+        uint4 b = philox_block(seed, 1, unit, 0);
+        double range = hi_t - lo_t;
+        if (range == 0.0) range = tg.window;
+        double now = lo_t + ldexp((double)comp(b, 0), -32) * range;
+        while (L < w.steps + 1) {
+            double end = now + tg.window;
+            if (end > tg.max_time) end = tg.max_time;
+            const int64_t off = tg.off[cur], deg = tg.off[cur + 1] - off;
+            int64_t a = 0, z = deg;   // first edge with ts >= now
+            while (a < z) {
+                const int64_t m = (a + z) >> 1;
+                if (tg.ts[off + m] >= now) z = m;
+                else a = m + 1;
+            }
+            int64_t e = a, y = deg;   // first edge with ts > end (from a)
+            while (e < y) {
+                const int64_t m = (e + y) >> 1;
+                if (tg.ts[off + m] > end) y = m;
+                else e = m + 1;
+            }
+            const int64_t n = e - a;
+            if (n <= 0) break;
+            const uint32_t s = (uint32_t)L;
+            if ((s & 3) == 0) b = philox_block(seed, 1, unit, s >> 2);
+            const int64_t idx = (int64_t)draw_index(comp(b, s & 3), (uint32_t)n);
+            cur = tg.tgt[off + a + idx];
+            now = tg.ts[off + idx];
+            out[L++] = cur;
+        }
+    }
+    w.lens[t] = L;
+}
+
+hipError_t launch_go_ctdne_walk(const TemporalArgs& tg, const WalkArgs& w, uint64_t seed, hipStream_t st) {
+    const int block = 256;
+    hipLaunchKernelGGL(go_ctdne_walk_gen_kernel, dim3((unsigned)((w.nwalks + block - 1) / block)), dim3(block), 0, st,
+                       tg, w, seed);
+    return hipGetLastError();
+}
+
 // Go SkipGrams (fixed window) + Go UpdatePair per pair; negatives from slot
 // L-1 (+ slot_extra).
 template <int G, int M, int KMAX, int MODE>
@@ -499,6 +558,18 @@ hipError_t launch_go_edge(const EdgeArgs& a, int grid, hipStream_t st) {
     return hipErrorInvalidValue;
 }
 
+hipError_t launch_go_pairs(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st) {
+    const int G = lanes_of(a.dpad), M = (a.dpad + G - 1) / G;
+#define X(g, m)                                                  \
+    if (G == g && M == m) {                                      \
+        if (a.K <= 5) return go_pairs<g, m, 5>(a, w, grid, st);  \
+        return go_pairs<g, m, 10>(a, w, grid, st);               \
+    }
+    SMORE_FOR_EACH_GM(X)
+#undef X
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_go_walk(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st) {
     const int block = 256;
     if (w.rule == 3)
@@ -512,15 +583,7 @@ hipError_t launch_go_walk(const EdgeArgs& a, const WalkArgs& w, int grid, hipStr
                            a.g, a.tcum, w, a.seed);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const int G = lanes_of(a.dpad), M = (a.dpad + G - 1) / G;
-#define X(g, m)                                                  \
-    if (G == g && M == m) {                                      \
-        if (a.K <= 5) return go_pairs<g, m, 5>(a, w, grid, st);  \
-        return go_pairs<g, m, 10>(a, w, grid, st);               \
-    }
-    SMORE_FOR_EACH_GM(X)
-#undef X
-    return hipErrorInvalidValue;
+    return launch_go_pairs(a, w, grid, st);
 }
 
 }  // namespace smore

@@ -12,7 +12,9 @@ Go semantics):
   * Node2Vec internal/models/node2vec/node2vec.go:43-258: DeepWalk's loop over
            the biased second-order walk (p return, q in-out);
   * Metapath2Vec internal/models/metapath2vec/metapath2vec.go:30-200 over a
-           pkg/hetero graph: meta-path-typed walks, uniform negatives.
+           pkg/hetero graph: meta-path-typed walks, uniform negatives;
+  * CTDNE  internal/models/ctdne/ctdne.go:29-200 over a pkg/temporal graph:
+           time-respecting walks, activity^0.75 negatives.
 
 Differences from the Go code, documented in DESIGN.md: draws come from the
 seeded Philox spec (not time-seeded math/rand); the learning rate of a sample
@@ -271,6 +273,86 @@ class Metapath2Vec(_GoModel):
             f.write("%d %d\n" % (len(self.names), self.dim))
             for i, name in enumerate(self.names):
                 f.write("%s[%s]%s\n" % (name, self.type_keys[self.ntype[i]], "".join(" %.6f" % x for x in W[i])))
+        print("\tSave to <%s>" % filename)
+
+    @property
+    def w_context(self):
+        return self.pnet.get_table(_lib.CTX)
+
+
+def load_temporal(filename):
+    """pkg/temporal (*TemporalGraph).LoadEdgeList (temporal_graph.go:60-130):
+    lines "src dst timestamp" (fewer than 3 fields or an unparsable timestamp:
+    skipped), ids in first-appearance order, directed edges."""
+    ids, names, src, dst, ts = {}, [], [], [], []
+
+    def node(name):
+        if name not in ids:
+            ids[name] = len(names)
+            names.append(name)
+        return ids[name]
+
+    with open(filename) as f:
+        for line in f:
+            parts = line.split()
+            if len(parts) < 3:
+                continue
+            try:
+                t = float(parts[2])
+            except ValueError:
+                continue
+            a, b = node(parts[0]), node(parts[1])
+            src.append(a), dst.append(b), ts.append(t)
+    return names, np.array(src, np.int32), np.array(dst, np.int32), np.array(ts, np.float64)
+
+
+class CTDNE(_GoModel):
+    """internal/models/ctdne/ctdne.go: LoadEdgeList (pkg/temporal), Init(dim,
+    timeWindow), Train (on the GPU: smore_train_ctdne), SaveWeights.  The
+    negative table BuildAliasMethod(activity, 0.75) (:119-131) is the Go
+    negative table of the temporal edges with unit weights (in + out counts;
+    every loaded vertex has an edge)."""
+
+    def LoadEdgeList(self, filename):
+        self.names, s, d, ts = load_temporal(filename)
+        self.pnet.set_graph_edges(len(self.names), s, d, np.ones(len(s)))
+        self.pnet.set_semantics("go")
+        self.pnet.set_temporal_edges(s, d, ts)
+        self.span = (float(ts.max()) - float(ts.min())) if len(ts) else 0.0
+        self.undirected = False
+
+    def Init(self, dim, time_window=0.0):
+        self.time_window = time_window if time_window > 0 else self.span * 0.1
+        self._alloc(dim, 2)
+        print("\ttime window:\t\t%.2f" % self.time_window)
+
+    def Train(self, walk_times, walk_steps, window_size, negative_samples, alpha, workers=1):
+        print("Model:\n\t[CTDNE - Continuous-Time Dynamic Network Embeddings]\nLearning Parameters:")
+        print("\twalk_times:\t\t%d\n\twalk_steps:\t\t%d\n\twindow_size:\t\t%d\n\tnegative_samples:\t%d"
+              "\n\talpha:\t\t\t%.6f\n\tworkers:\t\t%d"
+              % (walk_times, walk_steps, window_size, negative_samples, alpha, workers))
+        print("Start Training:")
+        V = self.pnet.MAX_vid
+        order = deepwalk_order(V, walk_times, 0)
+        total = walk_times * V
+        step = max(1, CHUNK // (walk_steps * 2 * window_size + 1))
+        done = 0
+        while done < total:
+            n = min(step, total - done)
+            self.pnet.train_ctdne(done, done + n, walk_times, walk_steps, window_size, negative_samples, alpha,
+                                  self.time_window, self.seed, order, self.mode)
+            done += n
+            _progress(_alpha(done, alpha, total), done / total)
+        print()
+
+    def SaveEmbeddings(self, filename):
+        """ctdne.go:212-238: "V dim" header, rows "name %.6f ..."."""
+        print("Save Model:")
+        W = self.pnet.get_table(_lib.W)
+        with open(filename, "w") as f:
+            f.write("%d %d\n" % (len(self.names), self.dim))
+            for i, name in enumerate(self.names):
+                f.write("%s%s\n" % (name, "".join(" %.6f" % x for x in W[i])))
         print("\tSave to <%s>" % filename)
 
     @property

@@ -193,6 +193,21 @@ class ProNet:
                                            int(walk_steps), int(window), int(K), float(alpha0), int(seed),
                                            ptr(order), _lib.MODE[mode]), "train_deepwalk")
 
+    def set_temporal_edges(self, src, dst, ts):
+        """Timestamped edges (pkg/temporal OutEdges) for CTDNE."""
+        src = np.ascontiguousarray(src, np.int32)
+        dst = np.ascontiguousarray(dst, np.int32)
+        ts = np.ascontiguousarray(ts, np.float64)
+        self._chk(lib.smore_set_temporal_edges(self.ctx, len(src), ptr(src), ptr(dst), ptr(ts)), "set_temporal_edges")
+
+    def train_ctdne(self, walk_begin, walk_end, walk_times, walk_steps, window, K, alpha0, time_window, seed, order,
+                    mode="hogwild"):
+        """(*CTDNE).Train (Go, internal/models/ctdne/ctdne.go:80-200) over walks [walk_begin, walk_end)."""
+        order = np.ascontiguousarray(order, np.int64)
+        self._chk(lib.smore_train_ctdne(self.ctx, int(walk_begin), int(walk_end), int(walk_times), int(walk_steps),
+                                        int(window), int(K), float(alpha0), float(time_window), int(seed),
+                                        ptr(order), _lib.MODE[mode]), "train_ctdne")
+
     def set_node_types(self, node_type, ntypes):
         """Node types of a heterogeneous graph (pkg/hetero NodeTypes) for metapath2vec."""
         node_type = np.ascontiguousarray(node_type, np.int32)

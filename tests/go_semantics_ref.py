@@ -279,3 +279,33 @@ def metapath_walk(graph, ntype, start, meta_path, steps, rng):
         cur = nxt
         idx += 1
     return walk
+
+
+def ctdne_walk(out_edges, tmin, tmax, max_time, window, start, steps, rng):
+    """CTDNE's start time (internal/models/ctdne/ctdne.go:159-170) and
+    TemporalRandomWalk / GetTemporalNeighbors / SampleTemporalNeighbor
+    (pkg/temporal/temporal_graph.go:181-252), literally; out_edges[v] = list of
+    (to, ts) sorted by ts."""
+    lo, hi = tmin[start], tmax[start]
+    if lo == 0 and hi == 0:
+        return [start]
+    rng_ = hi - lo
+    if rng_ == 0:
+        rng_ = window
+    now = lo + rng.float64() * rng_
+    walk, cur = [start], start
+    while len(walk) < steps + 1:
+        end = min(now + window, max_time)
+        nb = []
+        for to, t in out_edges[cur]:
+            if now <= t <= end:
+                nb.append(to)
+            if t > end:
+                break
+        if not nb:
+            break
+        idx = rng.intn(len(nb))
+        walk.append(nb[idx])
+        now = out_edges[cur][idx][1]
+        cur = nb[idx]
+    return walk

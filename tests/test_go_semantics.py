@@ -171,3 +171,48 @@ def test_go_uniform_negative_table():
     p, a = orc.alias_go(np.ones(101), 0.75)
     np.testing.assert_array_equal(p, np.ones(101))
     np.testing.assert_array_equal(a, np.arange(101))
+
+
+def _temporal():
+    from smore_amd.go_models import load_temporal   # host-side parser (no GPU call)
+    return load_temporal(os.path.join(GOLDEN, "temporal.txt"))
+
+
+def test_temporal_loader_skips_malformed():
+    names, s, d, ts = _temporal()
+    assert len(s) == 600 and len(names) <= 80 and np.isfinite(ts).all()
+
+
+@pytest.mark.parametrize("window", [5.0, 40.0, 0.5])
+def test_go_ctdne_walk_equals_restatement(window):
+    names, s, d, ts = _temporal()
+    V = len(names)
+    out = {v: [] for v in range(V)}
+    for a, b, t in zip(s, d, ts):
+        out[int(a)].append((int(b), float(t)))
+    for v in out:
+        out[v].sort(key=lambda e: e[1])
+    tmin, tmax = {}, {}
+    for a, b, t in zip(s, d, ts):
+        for v in (int(a), int(b)):
+            tmin[v] = min(tmin.get(v, np.inf), t)
+            tmax[v] = max(tmax.get(v, -np.inf), t)
+    tmin = [tmin.get(v, 0.0) for v in range(V)]
+    tmax = [tmax.get(v, 0.0) for v in range(V)]
+    for unit in range(400):
+        start = unit % V
+        got = orc.go_ctdne_walk(V, s, d, ts, window, SEED, unit, start, 15)
+        want = ref.ctdne_walk(out, tmin, tmax, float(ts.max()), window, start, 15, ref.Rng(SEED, 1, unit, 64))
+        assert list(got) == want, unit
+
+
+def test_go_ctdne_negative_table_is_activity():
+    """ctdne.go:119-131: BuildAliasMethod(out+in edge counts, 0.75) equals the Go
+    negative table of the temporal edges with unit weights."""
+    names, s, d, ts = _temporal()
+    V = len(names)
+    g = orc.GoGraph(V, s, d, np.ones(len(s)), names)
+    act = np.bincount(s, minlength=V) + np.bincount(d, minlength=V)
+    p, a = orc.alias_go(np.where(act > 0, act, 1).astype(np.float64), 0.75)
+    np.testing.assert_array_equal(g.nprob, p)
+    np.testing.assert_array_equal(g.nalias, a)

@@ -281,3 +281,48 @@ def test_go_metapath2vec_model_driver(smore, tmp_path):
     m.SaveEmbeddings(str(out))
     lines = out.read_text().splitlines()
     assert lines[0] == "%d 16" % len(m.names) and lines[1].split()[0].endswith("]")
+
+
+def _ctdne_pair(smore):
+    from smore_amd.go_models import load_temporal
+    names, s, d, ts = load_temporal(os.path.join(GOLDEN, "temporal.txt"))
+    g = orc.GoGraph(len(names), s, d, np.ones(len(s)), names)
+    pn = smore.ProNet(0)
+    pn.set_graph_edges(len(names), s, d, np.ones(len(s)))
+    pn.set_semantics("go")
+    pn.set_temporal_edges(s, d, ts)
+    return g, pn, s, d, ts
+
+
+@pytest.mark.parametrize("window,dim,K,win,steps", [(30.0, 16, 5, 2, 10), (8.0, 64, 5, 5, 40), (0.0, 8, 3, 2, 8)])
+def test_go_ctdne_serial_bit_exact(smore, window, dim, K, win, steps):
+    """(*CTDNE).Train (internal/models/ctdne/ctdne.go:80-200) on the GPU vs the
+    oracle's fp32 spec (parity unpinned vs Go: no Go toolchain).  window 0:
+    the library's default, 0.1 x the time span."""
+    g, pn, s, d, ts = _ctdne_pair(smore)
+    W0, C0 = tables(g.V, dim, dim + 5)
+    pn.alloc_tables(dim, 2)
+    pn.set_table(0, W0)
+    pn.set_table(1, C0)
+    order = orc.deepwalk_order(g.V, 2, 2)
+    pn.train_ctdne(0, g.V - 3, 2, steps, win, K, 0.025, window, SEED, order, "serial")
+    pn.train_ctdne(g.V - 3, 2 * g.V, 2, steps, win, K, 0.025, window, SEED, order, "serial")
+    W, C = padded(W0, dim), padded(C0, dim)
+    eff = window if window > 0 else (ts.max() - ts.min()) * 0.1
+    orc.go_ctdne_f32(g, s, d, ts, eff, W, C, dim, 2, steps, win, K, 0.025, SEED, order)
+    np.testing.assert_array_equal(pn.get_table(0), W[:, :dim])
+    np.testing.assert_array_equal(pn.get_table(1), C[:, :dim])
+
+
+def test_go_ctdne_model_driver(smore, tmp_path):
+    from smore_amd import go_models
+    m = go_models.CTDNE.New(mode="atomic")
+    m.LoadEdgeList(os.path.join(GOLDEN, "temporal.txt"))
+    m.Init(16, 0.0)
+    m.Train(3, 10, 2, 5, 0.025, 4)
+    W = m.w_vertex
+    assert np.isfinite(W).all() and np.abs(W).max() > 0
+    out = tmp_path / "ct.txt"
+    m.SaveEmbeddings(str(out))
+    lines = out.read_text().splitlines()
+    assert lines[0] == "%d 16" % len(m.names) and len(lines) == len(m.names) + 1
