@@ -254,6 +254,11 @@ int smore_group_load_edgelist(smore_group* g, const char* path, int undirected, 
 int smore_group_set_graph_edges(smore_group* g, int64_t V, int64_t E, const int32_t* src, const int32_t* dst,
                                 const double* w, int vertex_method, int negative_method);
 int smore_group_set_semantics(smore_group* g, int semantics);
+/* per-replica copies of smore_set_alias / smore_set_node_types / smore_set_temporal_edges */
+int smore_group_set_alias(smore_group* g, int which, const double* prob, const int64_t* alias, int64_t n);
+int smore_group_set_node_types(smore_group* g, const int32_t* node_type, int ntypes);
+int smore_group_set_temporal_edges(smore_group* g, int64_t E, const int32_t* src, const int32_t* dst,
+                                   const double* ts);
 int smore_group_alloc_tables(smore_group* g, int dim, int ntables);
 int smore_group_broadcast_tables(smore_group* g);
 /* per = samples per replica per exchange (0: 2^27) */
@@ -267,6 +272,13 @@ int smore_group_train_deepwalk(smore_group* g, uint64_t walk_begin, uint64_t wal
 int smore_group_train_node2vec(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
                                int walk_steps, int window, int K, double alpha0, double p, double q,
                                uint64_t seed, const int64_t* order, int mode, uint64_t per, int mean);
+int smore_group_train_metapath2vec(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
+                                   int walk_steps, int window, int K, double alpha0, const int32_t* paths,
+                                   const int32_t* path_lens, int npaths, uint64_t seed, const int64_t* order,
+                                   int mode, uint64_t per, int mean);
+int smore_group_train_ctdne(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
+                            int window, int K, double alpha0, double time_window, uint64_t seed,
+                            const int64_t* order, int mode, uint64_t per, int mean);
 int smore_group_train_walklets(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
                                int walk_steps, int window_min, int window_max, int K, double alpha0,
                                uint64_t seed, int mode, uint64_t per, int mean);

@@ -93,6 +93,12 @@ def _load():
         "smore_group_broadcast_tables": (i32, [P]),
         "smore_group_train_edges": (i32, [P, i32, u64, u64, u64, i32, dbl, dbl, u64, i32, u64, i32]),
         "smore_group_train_deepwalk": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, u64, P, i32, u64, i32]),
+        "smore_group_set_alias": (i32, [P, i32, P, P, i64]),
+        "smore_group_set_node_types": (i32, [P, P, i32]),
+        "smore_group_set_temporal_edges": (i32, [P, i64, P, P, P]),
+        "smore_group_train_metapath2vec": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, P, P, i32, u64, P, i32, u64,
+                                                 i32]),
+        "smore_group_train_ctdne": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, dbl, u64, P, i32, u64, i32]),
         "smore_group_train_node2vec": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, dbl, dbl, u64, P, i32, u64, i32]),
         "smore_deepwalk_order": (i32, [i64, i32, u64, P]),
         "smore_train_walklets": (i32, [P, u64, u64, i32, i32, i32, i32, i32, dbl, u64, i32]),

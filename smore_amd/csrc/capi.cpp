@@ -1085,11 +1085,16 @@ int smore_train_metapath2vec_async(smore_ctx* c, uint64_t walk_begin, uint64_t w
         if (paths[i] < 0 || paths[i] >= c->ntypes) return fail(c, SMORE_EINVAL, "metapath2vec: unknown type in path");
     int rc;
     if ((rc = set_device(c))) return rc;
-    // the previous call's kernels may still read the paths: reallocate only
-    // after the stream has drained
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if ((rc = upload(c, c->d_paths, paths, (size_t)off[npaths]))) return rc;
-    if ((rc = upload(c, c->d_path_off, off.data(), off.size()))) return rc;
+    std::vector<int32_t> key(path_lens, path_lens + npaths);
+    key.insert(key.end(), paths, paths + off[npaths]);
+    if (key != c->path_host || !c->d_paths) {
+        // the previous call's kernels may still read the paths: reallocate
+        // only after the stream has drained
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if ((rc = upload(c, c->d_paths, paths, (size_t)off[npaths]))) return rc;
+        if ((rc = upload(c, c->d_path_off, off.data(), off.size()))) return rc;
+        c->path_host.swap(key);
+    }
     return train_walks(c, 3, walk_begin, walk_end, walk_times, walk_steps, window, 0, K, alpha0, seed, order, 0, mode,
                        1.0, 1.0, npaths);
 }

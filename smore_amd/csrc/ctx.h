@@ -71,6 +71,7 @@ struct smore_ctx {
     int ntypes = 0;
     int32_t* d_paths = nullptr;
     int32_t* d_path_off = nullptr;
+    std::vector<int32_t> path_host;     // the uploaded meta-paths (lens then types): re-upload only on change
     // CTDNE (Go): time-sorted out-edges and active time ranges (smore_set_temporal_edges)
     int64_t* d_t_off = nullptr;
     int32_t* d_t_tgt = nullptr;

@@ -408,6 +408,34 @@ int smore_group_set_semantics(smore_group* g, int semantics) {
     return SMORE_OK;
 }
 
+int smore_group_set_alias(smore_group* g, int which, const double* prob, const int64_t* alias, int64_t n) {
+    if (!g) return SMORE_EINVAL;
+    for (size_t r = 0; r < g->ctx.size(); ++r) {
+        int rc = smore_set_alias(g->ctx[r], which, prob, alias, n);
+        if (rc) return gfail(g, (int)r, rc);
+    }
+    return SMORE_OK;
+}
+
+int smore_group_set_node_types(smore_group* g, const int32_t* node_type, int ntypes) {
+    if (!g) return SMORE_EINVAL;
+    for (size_t r = 0; r < g->ctx.size(); ++r) {
+        int rc = smore_set_node_types(g->ctx[r], node_type, ntypes);
+        if (rc) return gfail(g, (int)r, rc);
+    }
+    return SMORE_OK;
+}
+
+int smore_group_set_temporal_edges(smore_group* g, int64_t E, const int32_t* src, const int32_t* dst,
+                                   const double* ts) {
+    if (!g) return SMORE_EINVAL;
+    for (size_t r = 0; r < g->ctx.size(); ++r) {
+        int rc = smore_set_temporal_edges(g->ctx[r], E, src, dst, ts);
+        if (rc) return gfail(g, (int)r, rc);
+    }
+    return SMORE_OK;
+}
+
 int smore_group_alloc_tables(smore_group* g, int dim, int ntables) {
     if (!g) return SMORE_EINVAL;
     for (size_t r = 0; r < g->ctx.size(); ++r) {
@@ -478,6 +506,36 @@ int smore_group_train_node2vec(smore_group* g, uint64_t walk_begin, uint64_t wal
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_node2vec_async(c, b, e, walk_times, walk_steps, window, K, alpha0, p,
                                                               q, seed, order, mode);
+                        });
+}
+
+int smore_group_train_metapath2vec(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
+                                   int walk_steps, int window, int K, double alpha0, const int32_t* paths,
+                                   const int32_t* path_lens, int npaths, uint64_t seed, const int64_t* order,
+                                   int mode, uint64_t sync_walks, int mean) {
+    if (!g) return SMORE_EINVAL;
+    if (g->ctx.size() == 1)
+        return gfail(g, 0, smore_train_metapath2vec(g->ctx[0], walk_begin, walk_end, walk_times, walk_steps, window,
+                                                    K, alpha0, paths, path_lens, npaths, seed, order, mode));
+    return group_rounds(g, walk_begin, walk_end, sync_walks ? sync_walks : (uint64_t)1 << 18, mean,
+                        [&](smore_ctx* c, uint64_t b, uint64_t e) {
+                            return smore_train_metapath2vec_async(c, b, e, walk_times, walk_steps, window, K,
+                                                                  alpha0, paths, path_lens, npaths, seed, order,
+                                                                  mode);
+                        });
+}
+
+int smore_group_train_ctdne(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
+                            int window, int K, double alpha0, double time_window, uint64_t seed,
+                            const int64_t* order, int mode, uint64_t sync_walks, int mean) {
+    if (!g) return SMORE_EINVAL;
+    if (g->ctx.size() == 1)
+        return gfail(g, 0, smore_train_ctdne(g->ctx[0], walk_begin, walk_end, walk_times, walk_steps, window, K,
+                                             alpha0, time_window, seed, order, mode));
+    return group_rounds(g, walk_begin, walk_end, sync_walks ? sync_walks : (uint64_t)1 << 18, mean,
+                        [&](smore_ctx* c, uint64_t b, uint64_t e) {
+                            return smore_train_ctdne_async(c, b, e, walk_times, walk_steps, window, K, alpha0,
+                                                           time_window, seed, order, mode);
                         });
 }
 

@@ -398,6 +398,42 @@ class Group:
     def set_semantics(self, semantics):
         self._chk(lib.smore_group_set_semantics(self.g, _lib.SEM[semantics]), "set_semantics")
 
+    def set_alias(self, which, prob, alias):
+        prob = np.ascontiguousarray(prob, np.float64)
+        alias = np.ascontiguousarray(alias, np.int64)
+        self._chk(lib.smore_group_set_alias(self.g, which, ptr(prob), ptr(alias), len(prob)), "set_alias")
+
+    def set_node_types(self, node_type, ntypes):
+        node_type = np.ascontiguousarray(node_type, np.int32)
+        self._chk(lib.smore_group_set_node_types(self.g, ptr(node_type), int(ntypes)), "set_node_types")
+
+    def set_temporal_edges(self, src, dst, ts):
+        src = np.ascontiguousarray(src, np.int32)
+        dst = np.ascontiguousarray(dst, np.int32)
+        ts = np.ascontiguousarray(ts, np.float64)
+        self._chk(lib.smore_group_set_temporal_edges(self.g, len(src), ptr(src), ptr(dst), ptr(ts)),
+                  "set_temporal_edges")
+
+    def train_metapath2vec(self, walk_begin, walk_end, walk_times, walk_steps, window, K, alpha0, paths, seed, order,
+                           mode="atomic", per=0, mean=False):
+        """(*Metapath2Vec).Train (Go, internal/models/metapath2vec/metapath2vec.go:106-200) over the replicas."""
+        order = np.ascontiguousarray(order, np.int64)
+        flat = np.ascontiguousarray([t for p in paths for t in p] or [0], np.int32)
+        lens = np.ascontiguousarray([len(p) for p in paths], np.int32)
+        self._chk(lib.smore_group_train_metapath2vec(self.g, int(walk_begin), int(walk_end), int(walk_times),
+                                                     int(walk_steps), int(window), int(K), float(alpha0), ptr(flat),
+                                                     ptr(lens), len(paths), int(seed), ptr(order), _lib.MODE[mode],
+                                                     int(per), int(bool(mean))), "train_metapath2vec")
+
+    def train_ctdne(self, walk_begin, walk_end, walk_times, walk_steps, window, K, alpha0, time_window, seed, order,
+                    mode="atomic", per=0, mean=False):
+        """(*CTDNE).Train (Go, internal/models/ctdne/ctdne.go:80-200) over the replicas."""
+        order = np.ascontiguousarray(order, np.int64)
+        self._chk(lib.smore_group_train_ctdne(self.g, int(walk_begin), int(walk_end), int(walk_times),
+                                              int(walk_steps), int(window), int(K), float(alpha0),
+                                              float(time_window), int(seed), ptr(order), _lib.MODE[mode], int(per),
+                                              int(bool(mean))), "train_ctdne")
+
     def alloc_tables(self, dim, ntables):
         self._chk(lib.smore_group_alloc_tables(self.g, int(dim), int(ntables)), "alloc_tables")
         for r in self.replicas:

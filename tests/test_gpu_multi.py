@@ -147,3 +147,45 @@ def test_two_ranks_hip_passes_agree_and_train_like_one(tmp_path):
     l2 = _heldout_loss(two[0]["W"], two[0]["C"], heldout)
     assert l1 < 0.9 * np.log(2.0) * 6, l1
     assert abs(l2 - l1) <= 0.02 * l1, (l1, l2)
+
+
+def test_group_of_one_go_walk_models_equal_single_context(smore):
+    """smore_group_train_node2vec / _metapath2vec / _ctdne (exchange.cpp) and the
+    group setters on one replica are the single-context calls."""
+    from smore_amd.go_models import load_hetero, load_temporal
+    golden = os.path.join(ROOT, "tests", "golden")
+    names, ntype, tkeys, s, d, w = load_hetero(os.path.join(golden, "hetero.txt"), 1)
+    tn, ts_, td, tt = load_temporal(os.path.join(golden, "temporal.txt"))
+    for kind in ("node2vec", "metapath2vec", "ctdne"):
+        ref, g = smore.ProNet(0), smore.Group([0])
+        for x in (ref, g):
+            if kind == "ctdne":
+                x.set_graph_edges(len(tn), ts_, td, np.ones(len(ts_)))
+                x.set_semantics("go")
+                x.set_temporal_edges(ts_, td, tt)
+            else:
+                x.set_graph_edges(len(names), s, d, w)
+                x.set_semantics("go")
+                x.set_node_types(ntype, len(tkeys))
+                x.set_alias(smore._lib.AT_NEGATIVE, np.ones(len(names)), np.arange(len(names)))
+        V = ref.MAX_vid
+        ref.alloc_tables(32, 2)
+        g.alloc_tables(32, 2)
+        ref.init_table_glibc(0, 0)
+        g.primary.init_table_glibc(0, 0)
+        ref.zero_table(1)
+        g.primary.zero_table(1)
+        g.broadcast_tables()
+        order = smore.deepwalk_order(V, 2, 0)
+        paths = [[0, 1, 0], [1, 2, 1]]
+        for x in (ref, g):
+            if kind == "node2vec":
+                x.train_node2vec(0, 2 * V, 2, 10, 2, 3, 0.025, 0.5, 2.0, SEED, order, "serial")
+            elif kind == "metapath2vec":
+                x.train_metapath2vec(0, 2 * V, 2, 10, 2, 3, 0.025, paths, SEED, order, "serial")
+            else:
+                x.train_ctdne(0, 2 * V, 2, 10, 2, 3, 0.025, 20.0, SEED, order, "serial")
+        np.testing.assert_array_equal(g.primary.get_table(0), ref.get_table(0))
+        np.testing.assert_array_equal(g.primary.get_table(1), ref.get_table(1))
+        assert np.abs(ref.get_table(1)).max() > 0, kind
+        g.close()
