@@ -323,14 +323,24 @@ __device__ __forceinline__ double n2v_weight(const DevGraph& g, const WalkArgs& 
 // last neighbour if rounding leaves none; Intn(deg) when total == 0).  Step s
 // draws slot s of stream 1 (as the Go RandomWalk); a dead end stops the walk
 // before drawing.
-__global__ void go_n2v_walk_gen_kernel(DevGraph g, const double* tcum, WalkArgs w, uint64_t seed) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= w.nwalks) return;
+//
+// One wavefront per walk: hub vertices make a step cost O(deg) membership
+// tests, so the 64 lanes compute the biased weights of 64 edges at a time and
+// every lane then adds the 64 values in edge order through lane shuffles --
+// the sums keep the Go loop's sequential fp64 order (bit-exact), only the
+// membership tests run in parallel.  All control flow is wave-uniform.
+constexpr int N2V_WAVES = 4;   // walks per 256-thread block
+__global__ void __launch_bounds__(256) go_n2v_walk_gen_kernel(DevGraph g, const double* tcum, WalkArgs w,
+                                                              uint64_t seed) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t t = (uint64_t)blockIdx.x * N2V_WAVES + (threadIdx.x >> 6);
+    if (t >= w.nwalks) return;   // whole waves leave together
     const uint64_t unit = w.walk_begin + t;
     int32_t* out = w.walks + t * (uint64_t)(w.steps + 1);
     int L = 0;
     int32_t prev = -1, cur = (int32_t)w.order[unit - w.order_base];
-    out[L++] = cur;
+    if (lane == 0) out[L] = cur;
+    ++L;
     uint4 b = make_uint4(0, 0, 0, 0);
     for (int s = 0; s < w.steps; ++s) {
         const int64_t off = g.offsets[cur], deg = g.offsets[cur + 1] - off;
@@ -342,25 +352,41 @@ __global__ void go_n2v_walk_gen_kernel(DevGraph g, const double* tcum, WalkArgs 
             next = go_target(g, tcum, cur, k);
         } else {
             double total = 0.0;
-            for (int64_t e = off; e < off + deg; ++e) total += n2v_weight(g, w, prev, e);
+            for (int64_t base = 0; base < deg; base += 64) {
+                const int64_t e = base + lane;
+                const double bw = e < deg ? n2v_weight(g, w, prev, off + e) : 0.0;
+                const int cnt = (int)(deg - base < 64 ? deg - base : 64);
+                for (int i = 0; i < cnt; ++i) total += __shfl(bw, i, 64);
+            }
+            int64_t pick = deg - 1;
             if (total == 0.0) {
-                next = untag(g.targets[off + draw_index(k, (uint32_t)deg)]);
+                pick = draw_index(k, (uint32_t)deg);
             } else {
                 const double r = ldexp((double)k, -32) * total;
                 double cum = 0.0;
-                int64_t e = off;
-                for (; e < off + deg - 1; ++e) {
-                    cum += n2v_weight(g, w, prev, e);
-                    if (r <= cum) break;
+                bool found = false;
+                for (int64_t base = 0; base < deg && !found; base += 64) {
+                    const int64_t e = base + lane;
+                    const double bw = e < deg ? n2v_weight(g, w, prev, off + e) : 0.0;
+                    const int cnt = (int)(deg - base < 64 ? deg - base : 64);
+                    for (int i = 0; i < cnt; ++i) {
+                        cum += __shfl(bw, i, 64);
+                        if (r <= cum) {
+                            pick = base + i;
+                            found = true;
+                            break;
+                        }
+                    }
                 }
-                next = untag(g.targets[e]);
             }
+            next = untag(g.targets[off + pick]);
         }
         prev = cur;
         cur = next;
-        out[L++] = cur;
+        if (lane == 0) out[L] = cur;
+        ++L;
     }
-    w.lens[t] = L;
+    if (lane == 0) w.lens[t] = L;
 }
 
 // metapath2vec walk (internal/models/metapath2vec/metapath2vec.go:184-188,
@@ -576,8 +602,8 @@ hipError_t launch_go_walk(const EdgeArgs& a, const WalkArgs& w, int grid, hipStr
         hipLaunchKernelGGL(go_mp_walk_gen_kernel, dim3((unsigned)((w.nwalks + block - 1) / block)), dim3(block), 0, st,
                            w, a.seed);
     else if (w.rule == 2)
-        hipLaunchKernelGGL(go_n2v_walk_gen_kernel, dim3((unsigned)((w.nwalks + block - 1) / block)), dim3(block), 0, st,
-                           a.g, a.tcum, w, a.seed);
+        hipLaunchKernelGGL(go_n2v_walk_gen_kernel, dim3((unsigned)((w.nwalks + N2V_WAVES - 1) / N2V_WAVES)), dim3(256),
+                           0, st, a.g, a.tcum, w, a.seed);
     else
         hipLaunchKernelGGL(go_walk_gen_kernel, dim3((unsigned)((w.nwalks + block - 1) / block)), dim3(block), 0, st,
                            a.g, a.tcum, w, a.seed);

@@ -13,6 +13,7 @@ Timing: HIP events of the library (smore_last_kernel_ms) over `--steps`
 calls after one warmup call, inputs resident in HBM.
 
     python tools/bench_models.py --configs c2 c3 c5 [--mode hybrid]
+  c5go / c5n2v  Go DeepWalk / Go node2vec (p 0.5, q 2) on c5's graph (atomic)
 """
 import argparse
 import json
@@ -56,7 +57,7 @@ def main():
     import smore_amd
     from smore_amd import graphgen
     for cfg in args.configs:
-        V, (src, dst, w) = graphgen.config_edges(cfg)
+        V, (src, dst, w) = graphgen.config_edges("c5" if cfg.startswith("c5") else cfg)
         pn = smore_amd.ProNet(0)
         t0 = time.perf_counter()
         if cfg == "c3":
@@ -95,6 +96,29 @@ def main():
             ppw = pairs_per_walk(steps_ + 1, window)
             out.update(model="deepwalk", dim=128, K=K, walk_steps=steps_, window=window, walks_per_call=V,
                        ms_per_call=round(ms, 3), pairs_per_walk=round(ppw, 1),
+                       value=round(V * ppw / ms / 1e3, 1), unit="M pair-updates/s",
+                       walks_per_s=round(V / ms * 1e3, 1))
+        elif cfg in ("c5go", "c5n2v"):
+            # Go DeepWalk / Go node2vec (p=0.5, q=2) on C5's graph, atomic scatter
+            steps_, window, K = 40, 5, 5
+            pn.set_semantics("go")
+            pn.alloc_tables(128, 2)
+            pn.init_table_uniform(0, 1)
+            pn.init_table_uniform(1, 2)
+            order = smore_amd.deepwalk_order(V, 2, 0)
+            ms = []
+            for k in range(args.steps + 1):
+                if cfg == "c5go":
+                    pn.train_deepwalk(0, V, 2, steps_, window, K, 0.025, 7 + k, order, "atomic")
+                else:
+                    pn.train_node2vec(0, V, 2, steps_, window, K, 0.025, 0.5, 2.0, 7 + k, order, "atomic")
+                if k:
+                    ms.append(pn.last_kernel_ms())
+            ms = float(np.mean(ms))
+            L = steps_ + 1
+            ppw = sum(min(i + window, L - 1) - max(i - window, 0) for i in range(L))   # Go fixed window
+            out.update(model="go_deepwalk" if cfg == "c5go" else "go_node2vec", dim=128, K=K, walk_steps=steps_,
+                       window=window, walks_per_call=V, ms_per_call=round(ms, 3), pairs_per_walk=ppw,
                        value=round(V * ppw / ms / 1e3, 1), unit="M pair-updates/s",
                        walks_per_s=round(V / ms * 1e3, 1))
         print(json.dumps(out), flush=True)
