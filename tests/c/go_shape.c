@@ -66,6 +66,8 @@ int main(int argc, char** argv) {
         n_order = rd64(f);
         order = rd(f, 8 * n_order);
     }
+    double pq[2] = {1.0, 1.0};   /* node2vec (model -2): p, q */
+    if (model == -2 && fread(pq, 8, 2, f) != 2) return 3;
     fclose(f);
 
     /* NewHIP */
@@ -100,8 +102,14 @@ int main(int argc, char** argv) {
         for (uint64_t done = 0; done < (uint64_t)n_order;) {
             uint64_t n = (uint64_t)n_order - done;
             if (n > step) n = step;
-            CHECK("train_deepwalk", smore_group_train_deepwalk(G, done, done + n, (int)walk_times, (int)walk_steps,
-                                                               (int)window, (int)K, ad[0], seed, order, (int)mode, 0, 0));
+            if (model == -2)   /* TrainNode2Vec */
+                CHECK("train_node2vec", smore_group_train_node2vec(G, done, done + n, (int)walk_times, (int)walk_steps,
+                                                                   (int)window, (int)K, ad[0], pq[0], pq[1], seed,
+                                                                   order, (int)mode, 0, 0));
+            else
+                CHECK("train_deepwalk", smore_group_train_deepwalk(G, done, done + n, (int)walk_times,
+                                                                   (int)walk_steps, (int)window, (int)K, ad[0], seed,
+                                                                   order, (int)mode, 0, 0));
             done += n;
         }
     }

@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 BIN = os.path.join(ROOT, "tests", "c", "go_shape")
 SEED = 4242
 SERIAL, ATOMIC = 2, 1
-MODEL = {"line2": 0, "line1": 1, "bpr": 3, "deepwalk": -1}
+MODEL = {"line2": 0, "line1": 1, "bpr": 3, "deepwalk": -1, "node2vec": -2}
 
 
 def _shim_inputs(g):
@@ -42,9 +42,11 @@ def _run(tmp_path, g, model, dim, K, total, mode, alpha, lam, W0, C0, walk=None)
                   W0.astype(np.float64), C0.astype(np.float64)):
             f.write(np.ascontiguousarray(a).tobytes())
         if walk is not None:
-            times, steps, window, order = walk
+            times, steps, window, order = walk[:4]
             f.write(struct.pack("<4q", times, steps, window, len(order)))
             f.write(np.ascontiguousarray(order, np.int64).tobytes())
+            if model == "node2vec":
+                f.write(struct.pack("<2d", *walk[4]))
     r = subprocess.run([BIN, p_in, p_out], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     out = np.fromfile(p_out, np.float64).reshape(2, g.V, dim)
@@ -110,3 +112,17 @@ def test_go_shim_atomic_trains(tmp_path):
     pos = np.einsum("ij,ij->i", W[src[pick]], C[g.targets[pick]])
     neg = np.einsum("ij,ij->i", W[rng.integers(0, g.V, 5000)], C[rng.integers(0, g.V, 5000)])
     assert (pos[:, None] > neg[None, :1000]).mean() > 0.75
+
+
+def test_go_shim_node2vec_serial_bit_exact(tmp_path):
+    """(*HIP).TrainNode2Vec's call sequence (go/pkg/pronet/hip.go) vs the oracle."""
+    g = orc.GoGraph.from_file(os.path.join(GOLDEN, "pl1k.txt"), 1)
+    dim, K, times, steps, window = 16, 5, 2, 12, 3
+    order = np.concatenate([np.random.default_rng(t + 3).permutation(g.V) for t in range(times)]).astype(np.int64)
+    W0, C0 = _tables(g.V, dim, 10)
+    W, C = _run(tmp_path, g, "node2vec", dim, K, 0, SERIAL, 0.025, 0.0, W0, C0,
+                (times, steps, window, order, (0.25, 4.0)))
+    Wr, Cr = _padded(W0, dim), _padded(C0, dim)
+    orc.go_node2vec_f32(g, Wr, Cr, dim, times, steps, window, K, 0.025, 0.25, 4.0, SEED, order)
+    np.testing.assert_array_equal(W.astype(np.float32), Wr[:, :dim])
+    np.testing.assert_array_equal(C.astype(np.float32), Cr[:, :dim])
