@@ -70,13 +70,15 @@ __device__ __forceinline__ float dotg(const float (&a)[M], const float (&b)[M]) 
     return group_sum<G>(p);
 }
 
-// Go UpdatePair on W (vertex) and C (context); negs[] already drawn.
+// Go UpdatePair's context side (optimizer.go:21-58): given W_v in wv, updates
+// the negatives and C_c in memory and returns W_v's gradient in vg (the caller
+// applies it).  negs[] already drawn.
 template <int G, int M, int KMAX, int MODE>
-__device__ __forceinline__ void go_update_pair(const EdgeArgs& a, const float* s_sig, int lane, const bool (&ev)[M],
-                                               int32_t v, int32_t c, const int32_t (&negs)[KMAX], float alpha) {
+__device__ __forceinline__ void go_pair_ctx(const EdgeArgs& a, const float* s_sig, int lane, const bool (&ev)[M],
+                                            const float (&wv)[M], float (&vg)[M], int32_t c,
+                                            const int32_t (&negs)[KMAX], float alpha) {
     const int dpad = a.dpad;
-    float wv[M], cc[M], vg[M], cg[M];
-    load_row<G, M>(wv, a.W, v, dpad, lane, ev);
+    float cc[M], cg[M];
     load_row<G, M>(cc, a.C, c, dpad, lane, ev);
     float rows[KMAX][M];
 #pragma unroll
@@ -121,11 +123,23 @@ __device__ __forceinline__ void go_update_pair(const EdgeArgs& a, const float* s
         for (int j2 = j + 1; j2 < KMAX; ++j2) last = last && negs[j2] != negs[j];
         if (MODE == MODE_ATOMIC || last) put_row<G, M, MODE>(a.C, negs[j], dpad, lane, ev, nk, dk);
     }
-    float nw[M], nc[M];
+    float nc[M];
 #pragma unroll
-    for (int m = 0; m < M; ++m) { nw[m] = wv[m] + vg[m]; nc[m] = cc[m] + cg[m]; }
-    put_row<G, M, MODE>(a.W, v, dpad, lane, ev, nw, vg);
+    for (int m = 0; m < M; ++m) nc[m] = cc[m] + cg[m];
     put_row<G, M, MODE>(a.C, c, dpad, lane, ev, nc, cg);
+}
+
+// Go UpdatePair on W (vertex) and C (context); negs[] already drawn.
+template <int G, int M, int KMAX, int MODE>
+__device__ __forceinline__ void go_update_pair(const EdgeArgs& a, const float* s_sig, int lane, const bool (&ev)[M],
+                                               int32_t v, int32_t c, const int32_t (&negs)[KMAX], float alpha) {
+    float wv[M], vg[M];
+    load_row<G, M>(wv, a.W, v, a.dpad, lane, ev);
+    go_pair_ctx<G, M, KMAX, MODE>(a, s_sig, lane, ev, wv, vg, c, negs, alpha);
+    float nw[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) nw[m] = wv[m] + vg[m];
+    put_row<G, M, MODE>(a.W, v, a.dpad, lane, ev, nw, vg);
 }
 
 // Go updateFirstOrder on one table W (source s, target t).
@@ -509,6 +523,14 @@ __global__ void __launch_bounds__(256) go_walk_pairs_kernel(EdgeArgs a, WalkArgs
         for (int i = 0; i < L; ++i) {
             const int lo = i - w.window < 0 ? 0 : i - w.window;
             const int hi = i + w.window + 1 > L ? L : i + w.window + 1;
+            // the pairs of position i share W_v = W[walk[i]], which only they
+            // change (contexts and negatives are C rows): it stays in registers
+            // over the run and goes back once -- the sequential values exactly;
+            // in the atomic mode the run's summed gradient is added once
+            float wv[M], wsum[M];
+            load_row<G, M>(wv, a.W, walk[i], a.dpad, lane, ev);
+#pragma unroll
+            for (int m = 0; m < M; ++m) wsum[m] = 0.0f;
             for (int j = lo; j < hi; ++j) {
                 if (j == i) continue;
                 SlotWords<G, 2 * KMAX> nw;
@@ -518,8 +540,15 @@ __global__ void __launch_bounds__(256) go_walk_pairs_kernel(EdgeArgs a, WalkArgs
                 for (int n = 0; n < KMAX; ++n)
                     negs[n] = n < a.K ? go_alias(a.g.ntab, a.g.V, nw.w[2 * n], nw.w[2 * n + 1]) : -1;
                 slot += 2 * a.K;
-                go_update_pair<G, M, KMAX, MODE>(a, s_sig, lane, ev, walk[i], walk[j], negs, alpha);
+                float vg[M];
+                go_pair_ctx<G, M, KMAX, MODE>(a, s_sig, lane, ev, wv, vg, walk[j], negs, alpha);
+#pragma unroll
+                for (int m = 0; m < M; ++m) {
+                    wv[m] = wv[m] + vg[m];
+                    wsum[m] = wsum[m] + vg[m];
+                }
             }
+            if (hi - lo > 1) put_row<G, M, MODE>(a.W, walk[i], a.dpad, lane, ev, wv, wsum);
         }
     }
 }
