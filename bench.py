@@ -64,7 +64,7 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
     ap.add_argument("--sync-every", type=int, default=1)
     ap.add_argument("--sync", default="sum", choices=["sum", "mean"])
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=20251015)
     return ap.parse_args()
@@ -79,47 +79,37 @@ def host_cores():
     return mine, os.cpu_count() or mine
 
 
+def _cpu_rate(orc, g, W, C, K, seconds, threads):
+    """LINE-2 samples/s of the oracle's fp64 OpenMP Hogwild loop on `threads`
+    host threads, over >= `seconds` of training in 1M-sample chunks per thread."""
+    total = 1 << 40
+    chunk = 1_000_000 * threads
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        orc.train_edge_f64(g, "line2", W, C, K, 0.025, 0.0, total, done, done + chunk, 7, threads)
+        done += chunk
+    return done, time.perf_counter() - t0
+
+
 def cpu_baseline(V, src, dst, w, dim, K, seconds, config):
     """The reference's arithmetic and CPU structure -- fp64 rows, OpenMP Hogwild
     threads over contiguous sample blocks (src/model/LINE.cpp:160-191) -- as
     restated by the oracle (the reference sources do not travel to the GPU box),
-    on this host's cores, bounded in time."""
+    on the same graph, bounded in time: on every host CPU this process may run
+    on (SURVEY.md 8d "threads = nproc") and on 1 thread."""
     from oracle import oracle as orc
     mine, machine = host_cores()
-    threads = max(1, min(16, mine))
     g = orc.Graph(V, src, dst, w)
     W = (np.random.default_rng(1).random((V, dim)) - 0.5) / dim
     C = np.zeros_like(W)
-    total = 1 << 40
-    chunk, done, t0 = 2_000_000, 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        orc.train_edge_f64(g, "line2", W, C, K, 0.025, 0.0, total, done, done + chunk, 7, threads)
-        done += chunk
-    el = time.perf_counter() - t0
-    return {"value": round(done / el / 1e6, 4), "unit": "M edge-updates/s", "cores": threads, "kind": "port",
+    n_all, t_all = _cpu_rate(orc, g, W, C, K, seconds, mine)
+    n_one, t_one = _cpu_rate(orc, g, W, C, K, max(2.0, seconds / 2), 1)
+    return {"value": round(n_all / t_all / 1e6, 4), "unit": "M edge-updates/s", "cores": mine, "kind": "port",
             "arithmetic": "f64 (the reference's)", "host_cpus_available": mine, "host_cpus_machine": machine,
-            "sample": "%d LINE-2 samples (d=%d, K=%d) on the same %s graph, fp64 rows, %d OpenMP Hogwild threads "
-                      "(%d CPUs available to this process, %d on the machine), %.1f s"
-                      % (done, dim, K, config, threads, mine, machine, el)}
-
-
-def measured_copy_peak(torch, gib=4, reps=5):
-    """Device-to-device copy bandwidth on this GPU (read + write bytes / time)."""
-    n = (gib << 30) // 4
-    x = torch.empty(n, dtype=torch.float32, device="cuda").fill_(1.0)
-    y = torch.empty_like(x)
-    y.copy_(x)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    e0.record()
-    for _ in range(reps):
-        y.copy_(x)
-    e1.record()
-    torch.cuda.synchronize()
-    gbs = 2 * 4 * n * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
-    del x, y
-    torch.cuda.empty_cache()
-    return gbs
+            "value_1thread": round(n_one / t_one / 1e6, 4),
+            "sample": "LINE-2 (d=%d, K=%d) on the same %s graph, fp64 rows: %d samples on %d OpenMP Hogwild threads "
+                      "(every CPU available to this process; %d on the machine) in %.1f s, and %d samples on 1 "
+                      "thread in %.1f s" % (dim, K, config, n_all, mine, machine, t_all, n_one, t_one)}
 
 
 def main():
@@ -227,7 +217,7 @@ def main():
             traffic = p.get("hbm_bytes_per_step", p.get("hbm_bytes_per_launch"))
             traffic_upd = p.get("hbm_bytes_per_launch")
             traffic_src = "profiles/pmc_traffic.json: rocprofv3 --pmc of this config (%s)" % p.get("round", "")
-    copy_peak = measured_copy_peak(torch) if rank == 0 else 0.0
+    copy_peak = pn.copy_bandwidth(4 << 30, 5) if rank == 0 else 0.0   # membw.hip float4 copy
     Wt = pn.get_table(0)
     assert np.isfinite(Wt).all(), "non-finite embeddings"
 
@@ -265,8 +255,9 @@ def main():
                          "traffic_per_algorithmic": (round(traffic / ((R + Wb) * S), 3) if traffic else None),
                          "measured_peak": {"copy_GBs": round(copy_peak, 1),
                                            "frac": round((R + Wb) * S / step_s / 1e9 / copy_peak, 4),
-                                           "note": "the path's algorithmic read+write bytes per second over a "
-                                                   "device-to-device copy's read+write bytes per second"},
+                                           "note": "the path's algorithmic read+write bytes per second over the "
+                                                   "library's float4 device copy (membw.hip, 4 GiB, best of "
+                                                   "default / non-temporal policy and 4 / 8 blocks per CU)"},
                          "kernel": {"name": "edge_train_kernel (gather/update/scatter)",
                                     "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
                                     "bytes_per_update_read": R_upd, "bytes_per_update_write": Wb,

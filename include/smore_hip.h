@@ -191,6 +191,11 @@ int smore_hot_rows(const smore_ctx* ctx, int64_t* hot_w, int64_t* hot_c);
 int smore_skipped(smore_ctx* ctx, uint64_t* skipped);
 /* milliseconds of the last training launch (HIP events on the launch stream) */
 float smore_last_kernel_ms(const smore_ctx* ctx);
+/* measurement (SURVEY.md 8d "the measured copy bandwidth on the box"): the
+ * best (read + written bytes) / time of `reps` float4 device-to-device copies of
+ * `bytes` over a few cache policies and grid sizes, in GB/s.  Allocates and
+ * frees its own buffers; the context's tables and graph are untouched. */
+int smore_copy_bandwidth(smore_ctx* ctx, uint64_t bytes, int reps, double* gbs);
 /* the last LINE/MF edge call split by phase (HIP events on the context stream):
  * update_ms = total time of its `launches` update-kernel launches (gather/update/
  * scatter), draw_ms = time the context stream waited for draw kernels

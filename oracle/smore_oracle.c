@@ -229,6 +229,7 @@ int orc_build_graph(int64_t V, int64_t E, const int32_t* src, const int32_t* dst
     /* degrees: out_degree summed in adjacency order (:431-436), in_degree by a
      * pass over the context array in CSR order (:439-443) */
     for (int64_t v = 0; v < V; ++v) { out_deg[v] = 0.0; in_deg[v] = 0.0; }
+    #pragma omp parallel for schedule(static)
     for (int64_t v = 0; v < V; ++v)
         for (int64_t p = offsets[v]; p < offsets[v + 1]; ++p) out_deg[v] += ew[p];
     for (int64_t p = 0; p < E; ++p) in_deg[targets[p]] += ew[p];
@@ -249,7 +250,10 @@ int orc_build_graph(int64_t V, int64_t E, const int32_t* src, const int32_t* dst
     }
     orc_alias_cpp(dist, V, nprob, nalias);
     free(dist);
-    /* per-vertex context tables, alias remapped to the target vid (:517-537) */
+    /* per-vertex context tables, alias remapped to the target vid (:517-537);
+     * the vertices are independent, so they are built by all threads (same
+     * result as the sequential loop) */
+    #pragma omp parallel for schedule(dynamic, 4096)
     for (int64_t v = 0; v < V; ++v) {
         int64_t off = offsets[v], br = offsets[v + 1] - offsets[v];
         if (br == 0) continue;

@@ -62,6 +62,7 @@ def _load():
         "smore_gen_powerlaw": (i32, [i64, i64, i32, dbl, u64, P, P]),
         "smore_hot_rows": (i32, [P, C.POINTER(i64), C.POINTER(i64)]),
         "smore_last_kernel_ms": (C.c_float, [P]),
+        "smore_copy_bandwidth": (i32, [P, u64, i32, C.POINTER(C.c_double)]),
         "smore_last_phase_ms": (i32, [P, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(i32)]),
         "smore_delta_begin": (i32, [P, P, P, P, P, i64]),
         "smore_delta_end": (i32, [P, P, P, P, P, C.c_float, i64]),

@@ -703,6 +703,44 @@ int smore_skipped(smore_ctx* c, uint64_t* skipped) {
     return SMORE_OK;
 }
 
+// streaming-copy bandwidth of this GPU (membw.hip): two fresh buffers of
+// `bytes`, one warm-up copy, then `reps` timed copies per variant (default
+// policy, non-temporal) at 4 and 8 blocks per CU; the best variant's (read +
+// written bytes) / time.  Measurement only: nothing of the context changes.
+int smore_copy_bandwidth(smore_ctx* c, uint64_t bytes, int reps, double* gbs) {
+    if (!c || !gbs || reps < 1 || bytes < 4096) return SMORE_EINVAL;
+    if (c->device < 0) return fail(c, SMORE_ESTATE, "host-only context");
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    const uint64_t n16 = bytes / 16;
+    void *src = nullptr, *dst = nullptr;
+    HIPCHK(c, hipMalloc(&src, n16 * 16));
+    if (hipMalloc(&dst, n16 * 16) != hipSuccess) {
+        (void)hipFree(src);
+        return fail(c, SMORE_EHIP, "copy buffer allocation");
+    }
+    double best = 0.0;
+    hipError_t e = hipMemsetAsync(src, 0x3c, n16 * 16, c->stream);
+    for (int variant = 0; variant < 2 && e == hipSuccess; ++variant)
+        for (int per_cu = 4; per_cu <= 8 && e == hipSuccess; per_cu *= 2) {
+            const int blocks = c->cus * per_cu;
+            e = launch_copy(src, dst, n16, blocks, variant, c->stream);
+            if (e == hipSuccess) e = hipEventRecord(c->ev0, c->stream);
+            for (int r = 0; r < reps && e == hipSuccess; ++r) e = launch_copy(src, dst, n16, blocks, variant, c->stream);
+            if (e == hipSuccess) e = hipEventRecord(c->ev1, c->stream);
+            if (e == hipSuccess) e = hipEventSynchronize(c->ev1);
+            float ms = 0.0f;
+            if (e == hipSuccess) e = hipEventElapsedTime(&ms, c->ev0, c->ev1);
+            if (e == hipSuccess && ms > 0) best = std::max(best, 2.0 * (double)n16 * 16 * reps / (ms * 1e-3) / 1e9);
+        }
+    (void)hipFree(src);
+    (void)hipFree(dst);
+    c->timed = false;
+    if (e != hipSuccess) return fail(c, SMORE_EHIP, hipGetErrorString(e));
+    *gbs = best;
+    return SMORE_OK;
+}
+
 float smore_last_kernel_ms(const smore_ctx* c) {
     if (!c || !c->timed) return -1.0f;
     float ms = -1.0f;

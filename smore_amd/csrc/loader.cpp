@@ -278,14 +278,22 @@ bool load_cache(const std::string& fn, uint64_t key, std::vector<std::string>& n
     return ok;
 }
 
+// The key is a pure function of the bytes, the file sizes and the undirected
+// flag: every file is hashed in fixed 64-MiB pieces (the host's thread count
+// only decides how many pieces are hashed at once) and the piece hashes are
+// folded in file order.
+constexpr size_t KEY_PIECE = (size_t)1 << 26;
 uint64_t content_key(const std::vector<std::unique_ptr<Mapped>>& maps, bool undirected, unsigned nt) {
     uint64_t key = hash_bytes(undirected ? "u1" : "u0", 2);
     for (const auto& m : maps) {
-        const size_t parts = std::max<size_t>(1, std::min<size_t>(nt, m->n / (1 << 22) + 1));
+        const size_t parts = std::max<size_t>(1, (m->n + KEY_PIECE - 1) / KEY_PIECE);
         std::vector<uint64_t> ph(parts);
-        run_threads((unsigned)parts, [&](unsigned t) {
-            const size_t b = m->n * t / parts, e = m->n * (t + 1) / parts;
-            ph[t] = hash_bytes(m->p + b, e - b);
+        std::atomic<size_t> next(0);
+        run_threads((unsigned)std::max<size_t>(1, std::min<size_t>(nt, parts)), [&](unsigned) {
+            for (size_t i; (i = next++) < parts;) {
+                const size_t b = i * KEY_PIECE, e = std::min(m->n, b + KEY_PIECE);
+                ph[i] = hash_bytes(m->p + b, e - b);
+            }
         });
         for (uint64_t h : ph) key = (key ^ h) * 0x9E3779B97F4A7C15ull + (uint64_t)m->n;
     }
@@ -296,7 +304,31 @@ uint64_t content_key(const std::vector<std::unique_ptr<Mapped>>& maps, bool undi
 // The whole HostGraph of one (input, undirected, vertex method, negative
 // method): names, CSR, degrees, the three alias tables in both
 // representations.  Arrays are read back with parallel pread()s.
-constexpr char GRAPH_MAGIC[8] = {'S', 'M', 'O', 'R', 'E', 'G', 'C', '1'};
+constexpr char GRAPH_MAGIC[8] = {'S', 'M', 'O', 'R', 'E', 'G', 'C', '2'};
+// Version of the rules that produce a HostGraph (build_graph's CSR order, the
+// degree methods, alias_cpp, alias_encode).  Bump it whenever one of them
+// changes: a cache written under other rules is then rebuilt, never reused.
+constexpr uint64_t GRAPH_BUILDER_VERSION = 3;
+
+// cheap consistency checks of a graph read back from a cache file (a truncated
+// or corrupted file must not drive out-of-bounds device reads)
+bool graph_sane(const HostGraph& g) {
+    const int64_t V = g.V, E = g.E;
+    if (g.offsets[0] != 0 || g.offsets[V] != E) return false;
+    std::atomic<bool> ok(true);
+    const unsigned nt = std::max(1u, std::min<unsigned>(threads_for((size_t)E * 4), 32u));
+    run_threads(nt, [&](unsigned t) {
+        const int64_t vb = V * t / nt, ve = V * (t + 1) / nt;
+        for (int64_t v = vb; v < ve && ok; ++v)
+            if (g.offsets[v + 1] < g.offsets[v]) ok = false;
+        for (int64_t v = vb; v < ve && ok; ++v)
+            if (g.valias[v] < -1 || g.valias[v] >= V || g.nalias[v] < -1 || g.nalias[v] >= V) ok = false;
+        const int64_t eb = E * t / nt, ee = E * (t + 1) / nt;
+        for (int64_t e = eb; e < ee && ok; ++e)
+            if (g.targets[e] < 0 || g.targets[e] >= V || g.calias[e] < -1 || g.calias[e] >= V) ok = false;
+    });
+    return ok;
+}
 
 struct Blk {   // one array of the file
     void* p;
@@ -341,9 +373,9 @@ bool save_graph_cache(const std::string& fn, uint64_t key, const HostGraph& gc) 
     for (const auto& s : g.names) { blob += s; blob.push_back('\n'); }
     bool one = true;
     for (double x : g.weights) if (x != 1.0) { one = false; break; }
-    const uint64_t hdr[8] = {key, (uint64_t)g.V, (uint64_t)g.E, (uint64_t)g.vertex_method,
+    const uint64_t hdr[9] = {key, (uint64_t)g.V, (uint64_t)g.E, (uint64_t)g.vertex_method,
                              (uint64_t)g.negative_method, (uint64_t)blob.size(), one ? 1ull : 0ull,
-                             (uint64_t)g.names.size()};
+                             (uint64_t)g.names.size(), GRAPH_BUILDER_VERSION};
     bool ok = pwrite(fd, GRAPH_MAGIC, 8, 0) == 8 && pwrite(fd, hdr, sizeof hdr, 8) == (ssize_t)sizeof hdr;
     if (blob.empty()) blob.push_back('\0');   // graph_blocks takes &blob[0]; 0-byte blocks write nothing
     std::vector<Blk> blks = graph_blocks(g, blob, one);
@@ -387,10 +419,11 @@ bool load_graph_cache(const std::string& fn, uint64_t key, int vm, int nm, HostG
     const int fd = open(fn.c_str(), O_RDONLY);
     if (fd < 0) return false;
     char magic[8];
-    uint64_t hdr[8];
+    uint64_t hdr[9];
     bool ok = pread(fd, magic, 8, 0) == 8 && memcmp(magic, GRAPH_MAGIC, 8) == 0 &&
               pread(fd, hdr, sizeof hdr, 8) == (ssize_t)sizeof hdr && hdr[0] == key && hdr[3] == (uint64_t)vm &&
-              hdr[4] == (uint64_t)nm;
+              hdr[4] == (uint64_t)nm && hdr[8] == GRAPH_BUILDER_VERSION && hdr[1] < ((uint64_t)1 << 31) &&
+              hdr[2] < ((uint64_t)1 << 40);
     if (!ok) { close(fd); return false; }
     const size_t V = hdr[1], E = hdr[2];
     g.V = (int64_t)V; g.E = (int64_t)E; g.vertex_method = vm; g.negative_method = nm;
@@ -426,7 +459,7 @@ bool load_graph_cache(const std::string& fn, uint64_t key, int vm, int nm, HostG
     });
     close(fd);
     phase("read");
-    if (!good) return false;
+    if (!good || !graph_sane(g)) return false;
     if (hdr[6]) {   // all-one weights are not stored: fill them on every thread
         const unsigned nf = std::max(1u, std::min<unsigned>(threads_for(E * 8), 32u));
         run_threads(nf, [&](unsigned t) {

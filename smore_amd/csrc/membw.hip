@@ -1,0 +1,40 @@
+// membw.hip -- the box's streaming-copy bandwidth, the `measured_peak` the
+// benchmark prices the path against (SURVEY.md 8d "plus the measured copy
+// bandwidth on the box").  A grid-stride float4 copy: every lane moves 16 B per
+// load/store (global_load_dwordx4 / global_store_dwordx4), UNROLL independent
+// loads in flight per lane before the stores, one full 1-KiB segment per
+// wave-instruction; a few blocks per CU over the whole chip.
+#include "train_kernels.h"
+
+namespace smore {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int UNROLL, bool NT>
+__global__ void __launch_bounds__(256) copy_kernel(const f32x4* __restrict__ src, f32x4* __restrict__ dst,
+                                                   uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + (UNROLL - 1) * stride < n; i += UNROLL * stride) {
+        f32x4 v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) v[u] = NT ? __builtin_nontemporal_load(src + i + u * stride) : src[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            if (NT) __builtin_nontemporal_store(v[u], dst + i + u * stride);
+            else dst[i + u * stride] = v[u];
+        }
+    }
+    for (; i < n; i += stride) dst[i] = src[i];
+}
+
+// variant 0: default cache policy, 1: non-temporal loads and stores
+hipError_t launch_copy(const void* src, void* dst, uint64_t n16, int blocks, int variant, hipStream_t st) {
+    const f32x4* s = reinterpret_cast<const f32x4*>(src);
+    f32x4* d = reinterpret_cast<f32x4*>(dst);
+    if (variant == 1) hipLaunchKernelGGL((copy_kernel<4, true>), dim3(blocks), dim3(256), 0, st, s, d, n16);
+    else hipLaunchKernelGGL((copy_kernel<4, false>), dim3(blocks), dim3(256), 0, st, s, d, n16);
+    return hipGetLastError();
+}
+
+}  // namespace smore

@@ -525,8 +525,7 @@ __global__ void __launch_bounds__(256) go_walk_pairs_kernel(EdgeArgs a, WalkArgs
             const int hi = i + w.window + 1 > L ? L : i + w.window + 1;
             // the pairs of position i share W_v = W[walk[i]], which only they
             // change (contexts and negatives are C rows): it stays in registers
-            // over the run and goes back once -- the sequential values exactly;
-            // in the atomic mode the run's summed gradient is added once
+            // over the run and goes back once -- the sequential values exactly
             float wv[M], wsum[M];
             load_row<G, M>(wv, a.W, walk[i], a.dpad, lane, ev);
 #pragma unroll
@@ -548,7 +547,14 @@ __global__ void __launch_bounds__(256) go_walk_pairs_kernel(EdgeArgs a, WalkArgs
                     wsum[m] = wsum[m] + vg[m];
                 }
             }
-            if (hi - lo > 1) put_row<G, M, MODE>(a.W, walk[i], a.dpad, lane, ev, wv, wsum);
+            // serial: the sequential value is stored; Hogwild (plain-store mode
+            // included): the run's summed gradient is ADDED, so updates other
+            // walks made to this row while the run held it are not overwritten
+            // (a run lasts up to 2 * window pairs, hub rows see many of them)
+            if (hi - lo > 1) {
+                if (a.mode == 2) put_row<G, M, MODE_STORE>(a.W, walk[i], a.dpad, lane, ev, wv, wsum);
+                else put_row<G, M, MODE_ATOMIC>(a.W, walk[i], a.dpad, lane, ev, wv, wsum);
+            }
         }
     }
 }

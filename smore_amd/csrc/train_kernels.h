@@ -148,6 +148,8 @@ hipError_t launch_edge_train(const EdgeArgs& a, int grid, hipStream_t st);
 const void* edge_kernel_symbol(const EdgeArgs& a);
 hipError_t launch_sample(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K,
                          int bpr, int32_t* out, hipStream_t st);
+// streaming copy of n16 16-B words (membw.hip); variant 1 = non-temporal
+hipError_t launch_copy(const void* src, void* dst, uint64_t n16, int blocks, int variant, hipStream_t st);
 hipError_t launch_init_uniform(float* T, int64_t rows, int dim, int dpad, uint64_t seed,
                                hipStream_t st);
 

@@ -329,6 +329,14 @@ class ProNet:
             return None
         return float(d.value), float(u.value), int(n.value)
 
+    def copy_bandwidth(self, nbytes=4 << 30, reps=5):
+        """Streaming device-to-device copy rate of this GPU in GB/s (read +
+        written bytes; the library's float4 copy kernel, membw.hip)."""
+        import ctypes
+        g = ctypes.c_double()
+        self._chk(lib.smore_copy_bandwidth(self.ctx, int(nbytes), int(reps), ctypes.byref(g)), "copy_bandwidth")
+        return float(g.value)
+
     def load_pretrain(self, which, path):
         """proNet::LoadPreTrain (src/proNet.cpp:238-286)."""
         self._chk(lib.smore_load_pretrain(self.ctx, which, path.encode()), "load_pretrain")

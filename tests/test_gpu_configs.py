@@ -142,6 +142,75 @@ def test_c2_full_grid_hybrid_matches_atomic(c2):
     assert abs(res["hybrid"] - res["atomic"]) <= 0.01 * res["atomic"], res
 
 
+# ---------------------------------------------------------------- C4: the north-star graph
+# 10M vertices / 200M undirected lines = 400M directed slots: E above 2^28, the
+# 6.4-GB packed context table (ct16, u32 offsets), 33-bit sample indices and
+# the hybrid scatter's hot tags at V = 10M (src/model/LINE.cpp:160-191).  The
+# oracle graph build is the slow part (about a minute), so one fixture serves
+# every C4 test.
+@pytest.fixture(scope="module")
+def c4(smore):
+    return _config_pair(smore, "c4")
+
+
+@pytest.mark.timeout(600)
+def test_c4_draws_bit_exact(c4):
+    g, pn = c4
+    assert g.V == 10_000_000 and g.E == 400_000_000
+    for begin in (0, (1 << 33) + 4321):
+        np.testing.assert_array_equal(pn.sample_edges("line2", begin, 100_000, 5, SEED),
+                                      orc.sample_line(g, SEED, begin, 100_000, 5))
+
+
+@pytest.mark.timeout(600)
+def test_c4_serial_bit_exact(c4):
+    g, pn = c4
+    dim, K, total = 64, 5, 40 * 10 ** 9
+    W0, C0 = rand_tables(g.V, dim, 2, 44)
+    pn.alloc_tables(dim, 2)
+    pn.set_table(0, W0)
+    pn.set_table(1, C0)
+    begin = (1 << 34) + 77
+    pn.train_edges("line2", begin, 20_000, total, K, 0.025, 0.0, SEED, "serial")
+    orc.train_edge_f32(g, "line2", W0, C0, dim, K, 0.025, 0.0, total, begin, begin + 20_000, SEED)
+    np.testing.assert_array_equal(pn.get_table(0), W0)
+    np.testing.assert_array_equal(pn.get_table(1), C0)
+
+
+@pytest.mark.timeout(600)
+def test_c4_full_grid_hybrid_matches_atomic(c4):
+    """The bench's workload and default scatter: one full-grid hybrid launch of
+    2^27 samples is finite and tags hot rows at V = 10M; after 2^28 samples the
+    held-out LINE-2 loss of the hybrid scatter is within 1 % of the lossless
+    atomic scatter's."""
+    g, pn = c4
+    dim, K, total = 64, 5, 1 << 28
+    heldout = orc.sample_line(g, SEED + 1, 0, 100_000, K)
+    res = {}
+    for mode in ("atomic", "hybrid"):
+        pn.alloc_tables(dim, 2)
+        pn.init_table_uniform(0, 5)
+        pn.zero_table(1)
+        pn.set_hot_threshold(0.3)
+        pn.set_write_combine(128, 0)
+        pn.train_edges("line2", 0, 1 << 27, total, K, 0.025, 0.0, SEED, mode)
+        if mode == "hybrid":
+            W = pn.get_table(0)
+            assert np.isfinite(W).all()
+            hw, hc = pn.hot_rows()
+            assert hw > 0 and hc > 0, (hw, hc)
+            del W
+        pn.train_edges("line2", 1 << 27, 1 << 27, total, K, 0.025, 0.0, SEED, mode)
+        W, C = pn.get_table(0), pn.get_table(1)
+        assert np.isfinite(W).all() and np.isfinite(C).all()
+        res[mode] = _heldout_loss(W, C, heldout, dim)
+        del W, C
+    assert pn.skipped() == 0
+    init = np.log(2.0) * (1 + K)
+    assert res["atomic"] < 0.97 * init, res
+    assert res["hybrid"] <= 1.01 * res["atomic"], res
+
+
 @pytest.fixture(scope="module")
 def c3(smore):
     return _config_pair(smore, "c3", nm="no_degrees")

@@ -115,6 +115,37 @@ def test_go_deepwalk_directed_dead_ends(smore):
     np.testing.assert_array_equal(pn.get_table(1), C)
 
 
+def test_go_deepwalk_hogwild_matches_atomic(smore):
+    """Go DeepWalk in the plain-store (Hogwild) mode keeps W_v in registers for
+    a walk position's run of pairs and ADDS the run's gradient at the end
+    (ADVICE r2): its held-out skip-gram AUC matches the lossless atomic mode."""
+    g, pn = pair(smore, "pl1k.txt", 1)
+    dim, K, times = 32, 5, 4
+    order = smore.deepwalk_order(g.V, times, 0)
+    rng = np.random.default_rng(3)
+    src = np.repeat(np.arange(g.V), np.diff(g.offsets))
+    pick = rng.integers(0, g.E, 20000)
+    negv, negc = rng.integers(0, g.V, 2000), rng.integers(0, g.V, 2000)
+
+    def auc(W, C):
+        pos = np.einsum("ij,ij->i", W[src[pick]], C[g.targets[pick]])
+        neg = np.einsum("ij,ij->i", W[negv], C[negc])
+        return (pos[:, None] > neg[None, :]).mean()
+
+    res = {}
+    for mode in ("atomic", "hogwild"):
+        W0, C0 = tables(g.V, dim, 17)
+        pn.alloc_tables(dim, 2)
+        pn.set_table(0, W0 / dim)
+        pn.set_table(1, C0 / dim)
+        pn.train_deepwalk(0, times * g.V, times, 20, 5, K, 0.025, SEED, order, mode)
+        W, C = pn.get_table(0), pn.get_table(1)
+        assert np.isfinite(W).all() and np.isfinite(C).all()
+        res[mode] = auc(W, C)
+    assert res["atomic"] > 0.7, res
+    assert abs(res["hogwild"] - res["atomic"]) < 0.02, res
+
+
 @pytest.mark.parametrize("model", ["line2", "line1", "bpr"])
 def test_go_atomic_single_sample(smore, model):
     fname, und = ("bip.txt", 0) if model == "bpr" else ("pl100w.txt", 1)

@@ -163,3 +163,51 @@ def test_built_graph_cache(tmp_path):
             np.testing.assert_array_equal(a, b)
     # the methods matter: the negative tables differ between the two builds
     assert not np.array_equal(t1[1][0], t3[1][0])
+
+
+def test_cache_key_independent_of_threads(tmp_path):
+    """The cache key is a function of the input bytes only: a file above one
+    hash piece's worth of threads (> 4 MiB) cached by a 1-thread load is found
+    by an 8-thread load (the key used to depend on the thread count)."""
+    path = str(tmp_path / "g.txt")
+    _ragged_file(path, lines=700_000)
+    assert os.path.getsize(path) > (5 << 20)
+    cache = str(tmp_path / "cache")
+    os.makedirs(cache)
+    _, _, _, i1 = _load(path, 1, cache=cache, threads=1)
+    assert not i1[2]
+    _, _, _, i2 = _load(path, 1, cache=cache, threads=8)
+    assert i2[2], "8-thread load missed the 1-thread cache"
+
+
+def test_corrupt_graph_cache_is_rebuilt(tmp_path):
+    """A built-graph cache whose CSR targets were overwritten with an id >= V
+    is rejected by the read-back checks and the graph is built again (same
+    result as a fresh build), never uploaded as read."""
+    import smore_amd
+    path = str(tmp_path / "g.txt")
+    _ragged_file(path, lines=20_000)
+    cache = str(tmp_path / "cache")
+    os.makedirs(cache)
+
+    def load():
+        pn = smore_amd.ProNet(-1)
+        pn.set_load_cache(cache)
+        pn.LoadEdgeList(path, 1)
+        return pn.last_load_info()[2], pn.csr()
+
+    h1, c1 = load()
+    gc = [f for f in os.listdir(cache) if f.endswith(".smoregc")]
+    assert h1 == 0 and len(gc) == 1
+    fn = os.path.join(cache, gc[0])
+    V = len(c1[0]) - 1
+    hdr = 8 + 9 * 8
+    with open(fn, "r+b") as f:
+        f.seek(hdr)
+        nb = int(np.frombuffer(open(fn, "rb").read(hdr)[8 + 5 * 8:8 + 6 * 8], np.uint64)[0])
+        f.seek(hdr + nb + (V + 1) * 8 + 4 * 10)          # the 11th CSR target
+        f.write(np.array([V + 7], np.int32).tobytes())
+    h2, c2 = load()
+    assert h2 != 2, "corrupt graph cache was used"
+    np.testing.assert_array_equal(c1[0], c2[0])
+    np.testing.assert_array_equal(c1[1], c2[1])

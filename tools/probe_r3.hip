@@ -1,0 +1,253 @@
+// probe_r3.hip -- round-3 measurements that decide the draw and update kernels'
+// next shape, before any product change:
+//
+//  rand  : random reads of W bytes (8 / 16 / 32) from a table of F bytes, R = 5
+//          independent reads per thread, one 4-B result per thread: the read
+//          rate against the footprint (L2 4 MiB per XCD, Infinity Cache 256 MiB,
+//          HBM beyond) -- the draw kernel reads 8-B entries of an 80-MB table
+//          (negatives), 16 B of 6.4 GB (context) and 32 B of 320 MB (vertex).
+//  rows  : the LINE-2 update's row pattern at config c4 (V = 10M, d = 64, 7
+//          rows of 256 B per sample: W[v], C[c], 5 x C[n], Zipf ids, permuted),
+//          read-modify-write, for two lane layouts -- interleaved dwords (lane l
+//          owns elements l, l+16, l+32, l+48: four 64-B segments per row, today's
+//          kernels) and float4 (lane l owns 4l..4l+3: one 256-B segment per row
+//          per wave-instruction) -- with and without the W row (the bound on
+//          what grouping samples by source can save), on hipMalloc and on
+//          uncached memory.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/probe_r3 tools/probe_r3.hip
+// Run:   tools/probe_r3 rand            (the footprint x width sweep)
+//        tools/probe_r3 rand1 F W R     (one config, 3 launches: for rocprofv3 --pmc)
+//        tools/probe_r3 rows [samples]  (the row-pattern sweep)
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <numeric>
+#include <random>
+#include <vector>
+
+#define CHK(x)                                                                             \
+    do {                                                                                   \
+        hipError_t e = (x);                                                                \
+        if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); }   \
+    } while (0)
+
+typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t mix(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+    return (uint32_t)x;
+}
+
+template <typename T>
+__device__ __forceinline__ uint32_t fold(const T& v) {
+    uint32_t a = 0;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); ++i) a ^= v[i];
+    return a;
+}
+
+// R random reads of T per thread from n entries
+template <typename T, int R>
+__global__ void __launch_bounds__(256) rand_kernel(const T* __restrict__ tab, uint64_t n, uint64_t threads,
+                                                   uint32_t* out, uint32_t salt) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= threads) return;
+    uint32_t acc = 0;
+    T v[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) v[j] = tab[__umulhi(mix(t * 8 + j + salt), (uint32_t)n)];
+#pragma unroll
+    for (int j = 0; j < R; ++j) acc ^= fold(v[j]);
+    if (acc == 0x9e3779b9u) out[0] = acc;   // keeps the loads, writes ~nothing
+}
+
+template <typename T>
+static float time_rand(const void* tab, uint64_t entries, uint64_t threads, uint32_t* out, int reps) {
+    hipEvent_t a, b;
+    CHK(hipEventCreate(&a));
+    CHK(hipEventCreate(&b));
+    float best = 1e30f;
+    for (int r = 0; r < reps; ++r) {
+        CHK(hipEventRecord(a));
+        hipLaunchKernelGGL((rand_kernel<T, 5>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, 0,
+                           (const T*)tab, entries, threads, out, (uint32_t)r * 977u);
+        CHK(hipGetLastError());
+        CHK(hipEventRecord(b));
+        CHK(hipEventSynchronize(b));
+        float ms;
+        CHK(hipEventElapsedTime(&ms, a, b));
+        best = std::min(best, ms);
+    }
+    CHK(hipEventDestroy(a));
+    CHK(hipEventDestroy(b));
+    return best;
+}
+
+static float run_rand(size_t F, int W, uint64_t threads, void* tab, uint32_t* out, int reps) {
+    const uint64_t entries = F / W;
+    if (W == 8) return time_rand<u2>(tab, entries, threads, out, reps);
+    if (W == 16) return time_rand<u4>(tab, entries, threads, out, reps);
+    return time_rand<u8>(tab, entries, threads, out, reps);
+}
+
+// ------------------------------------------------------------------ rows
+// LAYOUT 0: interleaved dwords, 1: float4 per lane; WROW: include W[v]
+template <int LAYOUT, bool WROW>
+__global__ void __launch_bounds__(256) rows_kernel(float* W, float* C, const int* ids, long n, float* sink) {
+    const int lane = threadIdx.x & 15;
+    const long g = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    const long ng = ((long)gridDim.x * blockDim.x) >> 4;
+    float acc = 0.f;
+    for (long s = g; s < n; s += ng) {
+        const int* id = ids + s * 8;
+        int r_id[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) r_id[k] = id[k];
+        f4 r[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            if (!WROW && k == 0) { r[k] = f4{0, 0, 0, 0}; continue; }
+            const float* p = (k == 0 ? W : C) + (long)r_id[k] * 64;
+            if (LAYOUT == 0) {
+                r[k] = f4{p[lane], p[lane + 16], p[lane + 32], p[lane + 48]};
+            } else {
+                r[k] = *reinterpret_cast<const f4*>(p + 4 * lane);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 7; ++k) acc += r[k][0] + r[k][1] + r[k][2] + r[k][3];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            if (!WROW && k == 0) continue;
+            float* p = (k == 0 ? W : C) + (long)r_id[k] * 64;
+            const f4 v = r[k] * 0.999f;
+            if (LAYOUT == 0) {
+                p[lane] = v[0]; p[lane + 16] = v[1]; p[lane + 32] = v[2]; p[lane + 48] = v[3];
+            } else {
+                *reinterpret_cast<f4*>(p + 4 * lane) = v;
+            }
+        }
+    }
+    if (acc == 12345.f) sink[0] = acc;
+}
+
+struct Zipf {   // inverse CDF of p(r) ~ (r+1)^-s over [0, V)
+    std::vector<double> cdf;
+    Zipf(long V, double s) : cdf(V) {
+        double a = 0;
+        for (long i = 0; i < V; ++i) { a += std::pow((double)(i + 1), -s); cdf[i] = a; }
+    }
+    int draw(double u) const {
+        long j = std::lower_bound(cdf.begin(), cdf.end(), u * cdf.back()) - cdf.begin();
+        return (int)std::min<long>(j, (long)cdf.size() - 1);
+    }
+};
+
+static void* alloc(size_t n, int kind) {
+    void* p = nullptr;
+    if (kind == 0) CHK(hipMalloc(&p, n));
+    else CHK(hipExtMallocWithFlags(&p, n, hipDeviceMallocUncached));
+    CHK(hipMemset(p, 0, n));
+    return p;
+}
+
+int main(int argc, char** argv) {
+    const char* what = argc > 1 ? argv[1] : "rand";
+    uint32_t* out;
+    CHK(hipMalloc(&out, 64));
+    if (!strcmp(what, "rand") || !strcmp(what, "rand1")) {
+        const uint64_t threads = 1ull << 27;
+        if (!strcmp(what, "rand1")) {
+            const size_t F = strtoull(argv[2], nullptr, 10);
+            const int W = atoi(argv[3]);
+            void* tab = alloc(F, 0);
+            CHK(hipMemset(tab, 0x5a, F));
+            const float ms = run_rand(F, W, threads, tab, out, 3);
+            printf("{\"probe\": \"rand1\", \"footprint\": %zu, \"width\": %d, \"reads\": %llu, \"bytes\": %llu, "
+                   "\"ms\": %.3f}\n", F, W, (unsigned long long)(threads * 5), (unsigned long long)(threads * 5 * W), ms);
+            return 0;
+        }
+        const size_t Fs[] = {(size_t)2 << 20, (size_t)16 << 20, (size_t)80000000, (size_t)192 << 20,
+                             (size_t)320000000, (size_t)1280000000, (size_t)6400000000ull};
+        void* tab = alloc(Fs[6], 0);
+        CHK(hipMemset(tab, 0x5a, Fs[6]));
+        for (size_t F : Fs)
+            for (int W : {8, 16, 32}) {
+                const float ms = run_rand(F, W, threads, tab, out, 3);
+                const double reads = (double)threads * 5;
+                printf("{\"probe\": \"rand\", \"footprint\": %zu, \"width\": %d, \"reads_per_thread\": 5, "
+                       "\"threads\": %llu, \"ms\": %.3f, \"Greads_per_s\": %.2f, \"GBs_payload\": %.1f}\n",
+                       F, W, (unsigned long long)threads, ms, reads / ms / 1e6, reads * W / ms / 1e6);
+                fflush(stdout);
+            }
+        return 0;
+    }
+    // rows
+    const long V = 10000000;
+    const long n = argc > 2 ? atol(argv[2]) : 1 << 24;
+    int cus = 0;
+    CHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    float* sink;
+    int* ids;
+    CHK(hipMalloc(&sink, 4));
+    CHK(hipMalloc(&ids, n * 8 * sizeof(int)));
+    Zipf z6(V, 0.6), z8(V, 0.8);
+    std::mt19937_64 rng(1);
+    std::uniform_real_distribution<double> U(0, 1);
+    std::vector<int> perm(V);
+    std::iota(perm.begin(), perm.end(), 0);
+    std::shuffle(perm.begin(), perm.end(), rng);
+    std::vector<int> h(n * 8);
+    for (long s = 0; s < n; ++s) {
+        h[s * 8 + 0] = perm[z6.draw(U(rng))];
+        h[s * 8 + 1] = perm[z8.draw(U(rng))];
+        for (int k = 0; k < 5; ++k) h[s * 8 + 2 + k] = perm[z6.draw(U(rng))];
+        h[s * 8 + 7] = 0;
+    }
+    CHK(hipMemcpy(ids, h.data(), h.size() * sizeof(int), hipMemcpyHostToDevice));
+    hipEvent_t a, b;
+    CHK(hipEventCreate(&a));
+    CHK(hipEventCreate(&b));
+    for (int kind = 0; kind < 2; ++kind) {
+        float* W = (float*)alloc((size_t)V * 64 * 4, kind);
+        float* C = (float*)alloc((size_t)V * 64 * 4, kind);
+        for (int layout = 0; layout < 2; ++layout)
+            for (int wrow = 1; wrow >= 0; --wrow)
+                for (int bpc : {4, 8}) {
+                    const int grid = cus * bpc;
+                    float best = 1e30f;
+                    for (int rep = 0; rep < 3; ++rep) {
+                        CHK(hipEventRecord(a));
+#define L(LA, WR) hipLaunchKernelGGL((rows_kernel<LA, WR>), dim3(grid), dim3(256), 0, 0, W, C, ids, n, sink)
+                        if (layout == 0) { if (wrow) L(0, true); else L(0, false); }
+                        else { if (wrow) L(1, true); else L(1, false); }
+#undef L
+                        CHK(hipGetLastError());
+                        CHK(hipEventRecord(b));
+                        CHK(hipEventSynchronize(b));
+                        float ms;
+                        CHK(hipEventElapsedTime(&ms, a, b));
+                        best = std::min(best, ms);
+                    }
+                    const int nrows = wrow ? 7 : 6;
+                    printf("{\"probe\": \"rows\", \"mem\": \"%s\", \"layout\": \"%s\", \"rows\": %d, "
+                           "\"blocks_per_cu\": %d, \"samples\": %ld, \"ms\": %.3f, \"ms_per_2^27\": %.2f, "
+                           "\"Msamples_per_s\": %.1f, \"TBs_rw\": %.2f}\n",
+                           kind ? "uncached" : "hipMalloc", layout ? "float4" : "interleaved", nrows, bpc, n, best,
+                           best * (double)(1ull << 27) / n, n / best / 1e3, 2.0 * nrows * 256 * n / best / 1e9);
+                    fflush(stdout);
+                }
+        CHK(hipFree(W));
+        CHK(hipFree(C));
+    }
+    return 0;
+}
