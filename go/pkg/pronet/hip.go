@@ -171,6 +171,65 @@ func (pn *ProNet) NewHIP(cfg HIPConfig) (*HIP, error) {
 	return h, nil
 }
 
+// NewHIPEdges uploads a graph that is not a *ProNet -- the typed graph of
+// pkg/hetero (metapath2vec) or the temporal graph of pkg/temporal (CTDNE) --
+// as V vertices and the directed slots src[i] -> dst[i] with weights w[i] in
+// adjacency order, switches to the Go rules and injects negativeAT (the table
+// the Go model's Train builds with BuildAliasMethod; nil keeps the library's
+// Go table of this graph).
+func NewHIPEdges(V int64, src, dst []int64, w []float64, negativeAT []AliasTable, cfg HIPConfig) (*HIP, error) {
+	pn := &ProNet{MaxVid: V, Graph: make(map[int64][]int64), EdgeWeights: make(map[int64][]float64)}
+	for i := range src {
+		pn.Graph[src[i]] = append(pn.Graph[src[i]], dst[i])
+		pn.EdgeWeights[src[i]] = append(pn.EdgeWeights[src[i]], w[i])
+	}
+	pn.NegativeAT = negativeAT
+	return pn.NewHIP(cfg)
+}
+
+// SetNodeTypes hands pkg/hetero's node types over (type ids in [0, ntypes))
+// for TrainMetapath2Vec: the library groups every vertex's neighbours by type
+// in adjacency order, as buildTypeIndices does (hetero_graph.go:169-183).
+func (h *HIP) SetNodeTypes(types []int64, ntypes int) error {
+	n := len(types)
+	if int64(n) != h.maxVid || n == 0 {
+		return fmt.Errorf("SetNodeTypes: %d types for %d vertices", n, h.maxVid)
+	}
+	t := (*[1 << 40]C.int32_t)(C.malloc(C.size_t(4 * n)))[:n:n]
+	defer C.free(unsafe.Pointer(&t[0]))
+	for i, x := range types {
+		t[i] = C.int32_t(x)
+	}
+	if rc := C.smore_group_set_node_types(h.group, &t[0], C.int(ntypes)); rc != C.SMORE_OK {
+		return h.err("smore_group_set_node_types")
+	}
+	return nil
+}
+
+// SetTemporalEdges hands pkg/temporal's out-edge lists over for TrainCTDNE:
+// the slots src[i] -> dst[i] at time ts[i], each source's edges in the order
+// of tg.OutEdges[src] (already sorted by timestamp by the Go loader; the
+// library's per-source stable sort keeps that order, ties included).
+func (h *HIP) SetTemporalEdges(src, dst []int64, ts []float64) error {
+	n := len(src)
+	if n == 0 {
+		return fmt.Errorf("SetTemporalEdges: no edges")
+	}
+	s := (*[1 << 40]C.int32_t)(C.malloc(C.size_t(4 * n)))[:n:n]
+	d := (*[1 << 40]C.int32_t)(C.malloc(C.size_t(4 * n)))[:n:n]
+	t := (*[1 << 40]C.double)(C.malloc(C.size_t(8 * n)))[:n:n]
+	defer C.free(unsafe.Pointer(&s[0]))
+	defer C.free(unsafe.Pointer(&d[0]))
+	defer C.free(unsafe.Pointer(&t[0]))
+	for i := 0; i < n; i++ {
+		s[i], d[i], t[i] = C.int32_t(src[i]), C.int32_t(dst[i]), C.double(ts[i])
+	}
+	if rc := C.smore_group_set_temporal_edges(h.group, C.int64_t(n), &s[0], &d[0], &t[0]); rc != C.SMORE_OK {
+		return h.err("smore_group_set_temporal_edges")
+	}
+	return nil
+}
+
 // Close releases the GPUs.
 func (h *HIP) Close() {
 	if h.group != nil {
@@ -269,12 +328,11 @@ func (h *HIP) TrainEdges(model int, w, c [][]float64, dim int, total uint64, K i
 	return h.transfer([][][]float64{w, c}, false)
 }
 
-// TrainDeepWalk runs walks [0, len(order)) of the Go DeepWalk (walk from
-// order[i], dead-end stop, fixed-window SkipGrams, UpdatePair per pair) and
-// copies W and C back.  order holds walkTimes x MaxVid start vertices, built
-// by the caller exactly as (*DeepWalk).Train shuffles them.
-func (h *HIP) TrainDeepWalk(w, c [][]float64, dim int, order []int64, walkTimes, walkSteps, window, K int,
-	alpha float64, progress func(done uint64)) error {
+// trainWalks: tables up, walks [0, len(order)) in library calls of `step`
+// walks per replica (progress granularity), tables back.  call runs walks
+// [done, done+n) with the start order in C memory.
+func (h *HIP) trainWalks(w, c [][]float64, dim int, order []int64, name string,
+	call func(done, n uint64, ord *C.int64_t) C.int, progress func(done uint64)) error {
 	if err := h.alloc(dim, 2); err != nil {
 		return err
 	}
@@ -296,10 +354,8 @@ func (h *HIP) TrainDeepWalk(w, c [][]float64, dim int, order []int64, walkTimes,
 		if n > step {
 			n = step
 		}
-		if rc := C.smore_group_train_deepwalk(h.group, C.uint64_t(done), C.uint64_t(done+n), C.int(walkTimes),
-			C.int(walkSteps), C.int(window), C.int(K), C.double(alpha), C.uint64_t(h.cfg.Seed), &ord[0],
-			C.int(h.cfg.Mode), 0, 0); rc != C.SMORE_OK {
-			return h.err("smore_group_train_deepwalk")
+		if rc := call(done, n, &ord[0]); rc != C.SMORE_OK {
+			return h.err(name)
 		}
 		done += n
 		if progress != nil {
@@ -309,41 +365,74 @@ func (h *HIP) TrainDeepWalk(w, c [][]float64, dim int, order []int64, walkTimes,
 	return h.transfer([][][]float64{w, c}, false)
 }
 
+// TrainDeepWalk runs walks [0, len(order)) of the Go DeepWalk (walk from
+// order[i], dead-end stop, fixed-window SkipGrams, UpdatePair per pair) and
+// copies W and C back.  order holds walkTimes x MaxVid start vertices, built
+// by the caller exactly as (*DeepWalk).Train shuffles them.
+func (h *HIP) TrainDeepWalk(w, c [][]float64, dim int, order []int64, walkTimes, walkSteps, window, K int,
+	alpha float64, progress func(done uint64)) error {
+	return h.trainWalks(w, c, dim, order, "smore_group_train_deepwalk", func(done, n uint64, ord *C.int64_t) C.int {
+		return C.smore_group_train_deepwalk(h.group, C.uint64_t(done), C.uint64_t(done+n), C.int(walkTimes),
+			C.int(walkSteps), C.int(window), C.int(K), C.double(alpha), C.uint64_t(h.cfg.Seed), ord,
+			C.int(h.cfg.Mode), 0, 0)
+	}, progress)
+}
+
 // TrainNode2Vec is TrainDeepWalk with node2vec's biased second-order walk
 // (internal/models/node2vec/node2vec.go:82-175: 1/p back to the previous
 // vertex, 1 to its neighbours, 1/q otherwise) in place of RandomWalk.
 func (h *HIP) TrainNode2Vec(w, c [][]float64, dim int, order []int64, walkTimes, walkSteps, window, K int,
 	alpha, p, q float64, progress func(done uint64)) error {
-	if err := h.alloc(dim, 2); err != nil {
-		return err
-	}
-	if err := h.transfer([][][]float64{w, c}, true); err != nil {
-		return err
-	}
-	total := uint64(len(order))
-	if total == 0 {
-		return nil
-	}
-	ord := (*[1 << 40]C.int64_t)(C.malloc(C.size_t(8 * total)))[:total:total]
-	defer C.free(unsafe.Pointer(&ord[0]))
-	for i, v := range order {
-		ord[i] = C.int64_t(v)
-	}
-	step := uint64(1<<20) * uint64(h.cfg.GPUs)
-	for done := uint64(0); done < total; {
-		n := total - done
-		if n > step {
-			n = step
-		}
-		if rc := C.smore_group_train_node2vec(h.group, C.uint64_t(done), C.uint64_t(done+n), C.int(walkTimes),
+	return h.trainWalks(w, c, dim, order, "smore_group_train_node2vec", func(done, n uint64, ord *C.int64_t) C.int {
+		return C.smore_group_train_node2vec(h.group, C.uint64_t(done), C.uint64_t(done+n), C.int(walkTimes),
 			C.int(walkSteps), C.int(window), C.int(K), C.double(alpha), C.double(p), C.double(q),
-			C.uint64_t(h.cfg.Seed), &ord[0], C.int(h.cfg.Mode), 0, 0); rc != C.SMORE_OK {
-			return h.err("smore_group_train_node2vec")
-		}
-		done += n
-		if progress != nil {
-			progress(done)
+			C.uint64_t(h.cfg.Seed), ord, C.int(h.cfg.Mode), 0, 0)
+	}, progress)
+}
+
+// TrainMetapath2Vec is (*Metapath2Vec).Train's loop
+// (internal/models/metapath2vec/metapath2vec.go:147-200) on the GPUs: walk i
+// starts at order[i] and picks one of metaPaths (node-type ids, SetNodeTypes
+// first) uniformly, MetaPathWalk (pkg/hetero/hetero_graph.go:221-256), then
+// fixed-window SkipGrams and UpdatePairs.
+func (h *HIP) TrainMetapath2Vec(w, c [][]float64, dim int, order []int64, metaPaths [][]int64,
+	walkTimes, walkSteps, window, K int, alpha float64, progress func(done uint64)) error {
+	np, tot := len(metaPaths), 0
+	for _, p := range metaPaths {
+		tot += len(p)
+	}
+	if np == 0 || tot == 0 {
+		return fmt.Errorf("TrainMetapath2Vec: no meta-paths")
+	}
+	paths := (*[1 << 40]C.int32_t)(C.malloc(C.size_t(4 * tot)))[:tot:tot]
+	lens := (*[1 << 40]C.int32_t)(C.malloc(C.size_t(4 * np)))[:np:np]
+	defer C.free(unsafe.Pointer(&paths[0]))
+	defer C.free(unsafe.Pointer(&lens[0]))
+	k := 0
+	for i, p := range metaPaths {
+		lens[i] = C.int32_t(len(p))
+		for _, t := range p {
+			paths[k] = C.int32_t(t)
+			k++
 		}
 	}
-	return h.transfer([][][]float64{w, c}, false)
+	return h.trainWalks(w, c, dim, order, "smore_group_train_metapath2vec", func(done, n uint64, ord *C.int64_t) C.int {
+		return C.smore_group_train_metapath2vec(h.group, C.uint64_t(done), C.uint64_t(done+n), C.int(walkTimes),
+			C.int(walkSteps), C.int(window), C.int(K), C.double(alpha), &paths[0], &lens[0], C.int(np),
+			C.uint64_t(h.cfg.Seed), ord, C.int(h.cfg.Mode), 0, 0)
+	}, progress)
+}
+
+// TrainCTDNE is (*CTDNE).Train's loop (internal/models/ctdne/ctdne.go:133-200)
+// on the GPUs: a start without edges trains nothing, the start time is drawn in
+// its active range, TemporalRandomWalk with timeWindow (pkg/temporal/
+// temporal_graph.go:225-252; SetTemporalEdges first), then fixed-window
+// SkipGrams and UpdatePairs.
+func (h *HIP) TrainCTDNE(w, c [][]float64, dim int, order []int64, walkTimes, walkSteps, window, K int,
+	alpha, timeWindow float64, progress func(done uint64)) error {
+	return h.trainWalks(w, c, dim, order, "smore_group_train_ctdne", func(done, n uint64, ord *C.int64_t) C.int {
+		return C.smore_group_train_ctdne(h.group, C.uint64_t(done), C.uint64_t(done+n), C.int(walkTimes),
+			C.int(walkSteps), C.int(window), C.int(K), C.double(alpha), C.double(timeWindow),
+			C.uint64_t(h.cfg.Seed), ord, C.int(h.cfg.Mode), 0, 0)
+	}, progress)
 }

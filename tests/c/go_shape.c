@@ -7,7 +7,12 @@
  * gpus, mode; double alpha, lambda; uint64 seed; int32 src[E], dst[E];
  * double w[E]; double nprob[V]; int64 nalias[V]; double W0[V*dim],
  * C0[V*dim]; DeepWalk only: int64 walk_times, walk_steps, window, n,
- * order[n].  output: double W[V*dim], C[V*dim] (C = C0 when not trained). */
+ * order[n]; node2vec (model -2): double p, q; metapath2vec (model -3, the
+ * calls of metapath2vec_hip.go: NewHIPEdges, SetNodeTypes, TrainMetapath2Vec):
+ * int64 ntypes, int32 type[V], int64 npaths, total, int32 lens[npaths],
+ * paths[total]; CTDNE (model -4, ctdne_hip.go: NewHIPEdges, SetTemporalEdges,
+ * TrainCTDNE): double time_window, int64 Et, int32 tsrc[Et], tdst[Et], double
+ * ts[Et].  output: double W[V*dim], C[V*dim] (C = C0 when not trained). */
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -68,6 +73,24 @@ int main(int argc, char** argv) {
     }
     double pq[2] = {1.0, 1.0};   /* node2vec (model -2): p, q */
     if (model == -2 && fread(pq, 8, 2, f) != 2) return 3;
+    int64_t ntypes = 0, npaths = 0, ptotal = 0, Et = 0;
+    int32_t *types = NULL, *plens = NULL, *paths = NULL, *tsrc = NULL, *tdst = NULL;
+    double twin = 0.0, *ts = NULL;
+    if (model == -3) {
+        ntypes = rd64(f);
+        types = rd(f, 4 * V);
+        npaths = rd64(f);
+        ptotal = rd64(f);
+        plens = rd(f, 4 * npaths);
+        paths = rd(f, 4 * ptotal);
+    }
+    if (model == -4) {
+        if (fread(&twin, 8, 1, f) != 1) return 3;
+        Et = rd64(f);
+        tsrc = rd(f, 4 * Et);
+        tdst = rd(f, 4 * Et);
+        ts = rd(f, 8 * Et);
+    }
     fclose(f);
 
     /* NewHIP */
@@ -78,6 +101,8 @@ int main(int argc, char** argv) {
     CHECK("set_semantics", smore_group_set_semantics(G, SMORE_SEM_GO));
     for (int r = 0; r < gpus; ++r)
         CHECK("set_alias", smore_set_alias(smore_group_ctx(G, r), SMORE_AT_NEGATIVE, nprob, nalias, V));
+    if (model == -3) CHECK("set_node_types", smore_group_set_node_types(G, types, (int)ntypes));    /* SetNodeTypes */
+    if (model == -4) CHECK("set_temporal", smore_group_set_temporal_edges(G, Et, tsrc, tdst, ts)); /* SetTemporalEdges */
     /* TrainEdges / TrainDeepWalk: alloc, put + broadcast, chunked train, get */
     const int ntab = model == SMORE_LINE1 ? 1 : 2;
     CHECK("alloc_tables", smore_group_alloc_tables(G, (int)dim, ntab));
@@ -102,7 +127,16 @@ int main(int argc, char** argv) {
         for (uint64_t done = 0; done < (uint64_t)n_order;) {
             uint64_t n = (uint64_t)n_order - done;
             if (n > step) n = step;
-            if (model == -2)   /* TrainNode2Vec */
+            if (model == -3)   /* TrainMetapath2Vec */
+                CHECK("train_metapath2vec",
+                      smore_group_train_metapath2vec(G, done, done + n, (int)walk_times, (int)walk_steps, (int)window,
+                                                     (int)K, ad[0], paths, plens, (int)npaths, seed, order,
+                                                     (int)mode, 0, 0));
+            else if (model == -4)   /* TrainCTDNE */
+                CHECK("train_ctdne", smore_group_train_ctdne(G, done, done + n, (int)walk_times, (int)walk_steps,
+                                                             (int)window, (int)K, ad[0], twin, seed, order,
+                                                             (int)mode, 0, 0));
+            else if (model == -2)   /* TrainNode2Vec */
                 CHECK("train_node2vec", smore_group_train_node2vec(G, done, done + n, (int)walk_times, (int)walk_steps,
                                                                    (int)window, (int)K, ad[0], pq[0], pq[1], seed,
                                                                    order, (int)mode, 0, 0));

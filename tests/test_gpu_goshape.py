@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 BIN = os.path.join(ROOT, "tests", "c", "go_shape")
 SEED = 4242
 SERIAL, ATOMIC = 2, 1
-MODEL = {"line2": 0, "line1": 1, "bpr": 3, "deepwalk": -1, "node2vec": -2}
+MODEL = {"line2": 0, "line1": 1, "bpr": 3, "deepwalk": -1, "node2vec": -2, "metapath2vec": -3, "ctdne": -4}
 
 
 def _shim_inputs(g):
@@ -32,13 +32,14 @@ def _shim_inputs(g):
     return src, dst, w
 
 
-def _run(tmp_path, g, model, dim, K, total, mode, alpha, lam, W0, C0, walk=None):
+def _run(tmp_path, g, model, dim, K, total, mode, alpha, lam, W0, C0, walk=None, neg=None, extra=b""):
     src, dst, w = _shim_inputs(g)
+    nprob, nalias = neg if neg is not None else (g.nprob, g.nalias)
     p_in, p_out = str(tmp_path / "in.bin"), str(tmp_path / "out.bin")
     with open(p_in, "wb") as f:
         f.write(struct.pack("<8q", g.V, g.E, dim, MODEL[model], K, total, 1, mode))
         f.write(struct.pack("<2dQ", alpha, lam, SEED))
-        for a in (src, dst, w, g.nprob.astype(np.float64), g.nalias.astype(np.int64),
+        for a in (src, dst, w, np.asarray(nprob, np.float64), np.asarray(nalias, np.int64),
                   W0.astype(np.float64), C0.astype(np.float64)):
             f.write(np.ascontiguousarray(a).tobytes())
         if walk is not None:
@@ -47,6 +48,7 @@ def _run(tmp_path, g, model, dim, K, total, mode, alpha, lam, W0, C0, walk=None)
             f.write(np.ascontiguousarray(order, np.int64).tobytes())
             if model == "node2vec":
                 f.write(struct.pack("<2d", *walk[4]))
+        f.write(extra)
     r = subprocess.run([BIN, p_in, p_out], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     out = np.fromfile(p_out, np.float64).reshape(2, g.V, dim)
@@ -124,5 +126,57 @@ def test_go_shim_node2vec_serial_bit_exact(tmp_path):
                 (times, steps, window, order, (0.25, 4.0)))
     Wr, Cr = _padded(W0, dim), _padded(C0, dim)
     orc.go_node2vec_f32(g, Wr, Cr, dim, times, steps, window, K, 0.025, 0.25, 4.0, SEED, order)
+    np.testing.assert_array_equal(W.astype(np.float32), Wr[:, :dim])
+    np.testing.assert_array_equal(C.astype(np.float32), Cr[:, :dim])
+
+
+def test_go_shim_metapath2vec_serial_bit_exact(tmp_path):
+    """metapath2vec_hip.go's call sequence (NewHIPEdges with hg.Edges in vertex
+    order and Train's BuildAliasMethod(ones, 0.75), SetNodeTypes,
+    TrainMetapath2Vec) vs the oracle's Go-rule fp32 spec."""
+    from smore_amd.go_models import load_hetero
+    names, ntype, tkeys, s, d, w = load_hetero(os.path.join(GOLDEN, "hetero.txt"), True)
+    g = orc.GoGraph(len(names), s, d, w, names)
+    U, I, Cat = (tkeys.index(x) for x in ("User", "Item", "Category"))
+    paths = [[U, I, U], [I, Cat, I], [U, I, Cat, I, U]]
+    dim, K, times, steps, window = 16, 5, 2, 10, 2
+    order = np.concatenate([np.random.default_rng(t + 7).permutation(g.V) for t in range(times)]).astype(np.int64)
+    W0, C0 = _tables(g.V, dim, 21)
+    flat = np.concatenate([np.array(p, np.int32) for p in paths])
+    extra = (struct.pack("<q", len(tkeys)) + np.asarray(ntype, np.int32).tobytes() +
+             struct.pack("<2q", len(paths), len(flat)) + np.array([len(p) for p in paths], np.int32).tobytes() +
+             flat.tobytes())
+    neg = orc.go_uniform_negatives(g)
+    W, C = _run(tmp_path, g, "metapath2vec", dim, K, 0, SERIAL, 0.025, 0.0, W0, C0, (times, steps, window, order),
+                neg=neg, extra=extra)
+    Wr, Cr = _padded(W0, dim), _padded(C0, dim)
+    orc.go_metapath_f32(g, ntype, paths, Wr, Cr, dim, times, steps, window, K, 0.025, SEED, order)
+    np.testing.assert_array_equal(W.astype(np.float32), Wr[:, :dim])
+    np.testing.assert_array_equal(C.astype(np.float32), Cr[:, :dim])
+
+
+def test_go_shim_ctdne_serial_bit_exact(tmp_path):
+    """ctdne_hip.go's call sequence (tg.OutEdges in vertex order, each sorted
+    by timestamp as pkg/temporal's loader leaves them, as the graph with unit
+    weights and as the temporal edges; Train's BuildAliasMethod(activity,
+    0.75); TrainCTDNE) vs the oracle's Go-rule fp32 spec."""
+    from smore_amd.go_models import load_temporal
+    names, s, d, ts = load_temporal(os.path.join(GOLDEN, "temporal.txt"))
+    V = len(names)
+    o = np.lexsort((ts, s))                       # OutEdges[v] sorted by timestamp, v in order
+    so, do, tso = s[o], d[o], ts[o]
+    g = orc.GoGraph(V, so, do, np.ones(len(so)), names)   # Go table of activity = in + out counts
+    act = np.bincount(s, minlength=V) + np.bincount(d, minlength=V)
+    assert (act > 0).all()
+    dim, K, times, steps, window = 16, 5, 2, 10, 2
+    twin = 30.0
+    order = np.concatenate([np.random.default_rng(t + 9).permutation(V) for t in range(times)]).astype(np.int64)
+    W0, C0 = _tables(V, dim, 23)
+    extra = (struct.pack("<dq", twin, len(so)) + so.astype(np.int32).tobytes() + do.astype(np.int32).tobytes() +
+             tso.astype(np.float64).tobytes())
+    W, C = _run(tmp_path, g, "ctdne", dim, K, 0, SERIAL, 0.025, 0.0, W0, C0, (times, steps, window, order),
+                extra=extra)
+    Wr, Cr = _padded(W0, dim), _padded(C0, dim)
+    orc.go_ctdne_f32(g, s, d, ts, twin, Wr, Cr, dim, times, steps, window, K, 0.025, SEED, order)
     np.testing.assert_array_equal(W.astype(np.float32), Wr[:, :dim])
     np.testing.assert_array_equal(C.astype(np.float32), Cr[:, :dim])
