@@ -70,20 +70,41 @@ def parse():
     return ap.parse_args()
 
 
+def cgroup_cpu_quota():
+    """CPUs' worth of time this process's cgroup may use (cgroup v2 cpu.max /
+    v1 cfs quota), or None when unlimited."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, -(-int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return max(1, -(-q // p))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def host_cores():
-    """(cores this process may run on, cores of the machine)."""
+    """(CPUs this process can actually use: its affinity mask capped by its
+    cgroup's CPU quota; CPUs of the machine; the quota or None)."""
     try:
         mine = len(os.sched_getaffinity(0))
     except AttributeError:
         mine = os.cpu_count() or 1
-    return mine, os.cpu_count() or mine
+    quota = cgroup_cpu_quota()
+    return (min(mine, quota) if quota else mine), os.cpu_count() or mine, quota
 
 
 def _cpu_rate(orc, g, W, C, K, seconds, threads):
     """LINE-2 samples/s of the oracle's fp64 OpenMP Hogwild loop on `threads`
     host threads, over >= `seconds` of training in 1M-sample chunks per thread."""
     total = 1 << 40
-    chunk = 1_000_000 * threads
+    chunk = 250_000 * threads
     done, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         orc.train_edge_f64(g, "line2", W, C, K, 0.025, 0.0, total, done, done + chunk, 7, threads)
@@ -98,7 +119,7 @@ def cpu_baseline(V, src, dst, w, dim, K, seconds, config):
     on the same graph, bounded in time: on every host CPU this process may run
     on (SURVEY.md 8d "threads = nproc") and on 1 thread."""
     from oracle import oracle as orc
-    mine, machine = host_cores()
+    mine, machine, quota = host_cores()
     g = orc.Graph(V, src, dst, w)
     W = (np.random.default_rng(1).random((V, dim)) - 0.5) / dim
     C = np.zeros_like(W)
@@ -107,9 +128,11 @@ def cpu_baseline(V, src, dst, w, dim, K, seconds, config):
     return {"value": round(n_all / t_all / 1e6, 4), "unit": "M edge-updates/s", "cores": mine, "kind": "port",
             "arithmetic": "f64 (the reference's)", "host_cpus_available": mine, "host_cpus_machine": machine,
             "value_1thread": round(n_one / t_one / 1e6, 4),
+            "host_cpu_quota": quota,
             "sample": "LINE-2 (d=%d, K=%d) on the same %s graph, fp64 rows: %d samples on %d OpenMP Hogwild threads "
-                      "(every CPU available to this process; %d on the machine) in %.1f s, and %d samples on 1 "
-                      "thread in %.1f s" % (dim, K, config, n_all, mine, machine, t_all, n_one, t_one)}
+                      "(every CPU this process can use: affinity capped by the cgroup CPU quota %s; %d CPUs on the "
+                      "machine) in %.1f s, and %d samples on 1 thread in %.1f s"
+                      % (dim, K, config, n_all, mine, quota, machine, t_all, n_one, t_one)}
 
 
 def main():

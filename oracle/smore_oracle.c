@@ -617,11 +617,11 @@ int orc_train_deepwalk_f64(const orc_graph* g, double* W, double* C, int dim,
 /* ========================================================================== */
 /* fp32 spec (DESIGN.md "Arithmetic spec"), what the HIP kernels compute.      */
 /* Rows are padded to dpad (multiple of 4) floats.  A sample is owned by G      */
-/* lanes (G = min(64, pow2ceil(dpad/4))); lane l owns the elements l, l+G,      */
-/* l+2G, ... below dpad (interleaved, so one wave instruction touches a         */
-/* contiguous 4G-byte row segment).  dot = pairwise tree over the G lane        */
-/* partials, each an fmaf chain over its elements in increasing order from     */
-/* +0.0f.                                                                      */
+/* lanes (G = min(64, pow2ceil(dpad/4))); lane l owns the 16-B chunks l, l+G,   */
+/* l+2G, ... below dpad/4 (elements 4q .. 4q+3 of chunk q, so one wave          */
+/* instruction moves 16G contiguous bytes of a row).  dot = pairwise tree over  */
+/* the G lane partials, each an fmaf chain over the lane's elements in          */
+/* increasing order from +0.0f.                                                 */
 /* ========================================================================== */
 int orc_lane_width(int dpad) {
     int nq = dpad / 4, G = 1;
@@ -634,7 +634,8 @@ static float dot_spec(const float* a, const float* b, int dpad) {
     int G = orc_lane_width(dpad);
     for (int l = 0; l < G; ++l) {
         float p = 0.0f;
-        for (int e = l; e < dpad; e += G) p = fmaf(a[e], b[e], p);
+        for (int q = l; q < dpad / 4; q += G)
+            for (int e = 4 * q; e < 4 * q + 4; ++e) p = fmaf(a[e], b[e], p);
         part[l] = p;
     }
     for (int w = 1; w < G; w <<= 1)

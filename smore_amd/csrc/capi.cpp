@@ -704,8 +704,9 @@ int smore_skipped(smore_ctx* c, uint64_t* skipped) {
 }
 
 // streaming-copy bandwidth of this GPU (membw.hip): two fresh buffers of
-// `bytes`, one warm-up copy, then `reps` timed copies per variant (default
-// policy, non-temporal) at 4 and 8 blocks per CU; the best variant's (read +
+// `bytes`, one warm-up copy, then `reps` timed copies per variant (grid-
+// stride default policy / non-temporal at 4 and 8 blocks per CU, one word per
+// thread over the whole buffer); the best variant's (read +
 // written bytes) / time.  Measurement only: nothing of the context changes.
 int smore_copy_bandwidth(smore_ctx* c, uint64_t bytes, int reps, double* gbs) {
     if (!c || !gbs || reps < 1 || bytes < 4096) return SMORE_EINVAL;
@@ -721,8 +722,8 @@ int smore_copy_bandwidth(smore_ctx* c, uint64_t bytes, int reps, double* gbs) {
     }
     double best = 0.0;
     hipError_t e = hipMemsetAsync(src, 0x3c, n16 * 16, c->stream);
-    for (int variant = 0; variant < 2 && e == hipSuccess; ++variant)
-        for (int per_cu = 4; per_cu <= 8 && e == hipSuccess; per_cu *= 2) {
+    for (int variant = 0; variant < 3 && e == hipSuccess; ++variant)
+        for (int per_cu = 4; per_cu <= (variant == 2 ? 4 : 8) && e == hipSuccess; per_cu *= 2) {
             const int blocks = c->cus * per_cu;
             e = launch_copy(src, dst, n16, blocks, variant, c->stream);
             if (e == hipSuccess) e = hipEventRecord(c->ev0, c->stream);

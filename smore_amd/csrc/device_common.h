@@ -132,6 +132,72 @@ __device__ __forceinline__ float group_sum(float p) {
 }
 
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// ---- row layout (DESIGN.md "Arithmetic spec").  A sample's G lanes own the
+// row's 16-B chunks: lane l owns chunks q = l + G*k (k = 0 .. M/4 - 1), and its
+// register m holds element 4*(l + G*(m/4)) + m%4.  Every row access is one
+// global_load/store_dwordx4 per chunk round: a wave instruction moves 16G
+// contiguous bytes of each of the 64/G rows it touches (d = 64: four whole
+// 256-B rows).  dpad is a multiple of 4, so a chunk is wholly valid or not.
+template <int G>
+__device__ __forceinline__ int elem_off(int lane, int m) {
+    return 4 * (lane + G * (m >> 2)) + (m & 3);
+}
+
+template <int G, int M>
+__device__ __forceinline__ void row_valid(bool (&ev)[M], int lane, int dpad) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) ev[m] = lane + G * (m >> 2) < (dpad >> 2);
+}
+
+// r = row (zeros where the chunk does not exist or !use)
+template <int G, int M>
+__device__ __forceinline__ void ld_row(float (&r)[M], const float* row, int lane, const bool (&ev)[M],
+                                       bool use = true) {
+#pragma unroll
+    for (int k = 0; k < M / 4; ++k) {
+        f32x4 x = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (use && ev[4 * k]) x = *reinterpret_cast<const f32x4*>(row + 4 * (lane + G * k));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[4 * k + i] = x[i];
+    }
+}
+
+template <int G, int M>
+__device__ __forceinline__ void st_row(float* row, const float (&r)[M], int lane, const bool (&ev)[M]) {
+#pragma unroll
+    for (int k = 0; k < M / 4; ++k)
+        if (ev[4 * k])
+            *reinterpret_cast<f32x4*>(row + 4 * (lane + G * k)) = f32x4{r[4 * k], r[4 * k + 1], r[4 * k + 2], r[4 * k + 3]};
+}
+
+// row += d by float atomics.  A float atomic moves one dword per lane, so the
+// chunks are transposed across the group first (lane shuffles): atomic
+// instruction i of round k has lane l add element 4Gk + iG + l, held by lane
+// iG/4 + l/4 in register 4k + l%4 -- each instruction covers 4G contiguous
+// bytes of the row, not 4 dwords of every 16 B (G < 4: element by element).
+template <int G, int M>
+__device__ __forceinline__ void atomic_row(float* row, const float (&d)[M], int lane, int dpad) {
+    if constexpr (G < 4) {
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+            if (lane + G * (m >> 2) < (dpad >> 2)) unsafeAtomicAdd(row + elem_off<G>(lane, m), d[m]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < M / 4; ++k)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int s = i * (G / 4) + (lane >> 2);
+                float t[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) t[j] = __shfl(d[4 * k + j], s, G);
+                const int j = lane & 3;
+                const float v = j == 0 ? t[0] : j == 1 ? t[1] : j == 2 ? t[2] : t[3];
+                if (G * k + s < (dpad >> 2)) unsafeAtomicAdd(row + 4 * G * k + i * G + lane, v);
+            }
+    }
+}
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, const float4& v) { *reinterpret_cast<float4*>(p) = v; }

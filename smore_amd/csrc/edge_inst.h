@@ -16,7 +16,7 @@ struct EdgeInst {
         return hipGetLastError();
     }
     static hipError_t launch(const EdgeArgs& a, int grid, hipStream_t st) {
-        const int G = lanes_of(a.dpad), M = (a.dpad + G - 1) / G;
+        const int G = lanes_of(a.dpad), M = regs_of(a.dpad);
 #define X(g, m)                                                                           \
     if (G == g && M == m) {                                                               \
         if (a.model == 3) {                                                               \
@@ -30,7 +30,7 @@ struct EdgeInst {
         return hipErrorInvalidValue;
     }
     static const void* symbol(const EdgeArgs& a) {
-        const int G = lanes_of(a.dpad), M = (a.dpad + G - 1) / G;
+        const int G = lanes_of(a.dpad), M = regs_of(a.dpad);
 #define X(g, m)                                                                          \
     if (G == g && M == m) {                                                              \
         if (a.model == 3) {                                                              \
@@ -50,7 +50,7 @@ struct EdgeInst {
 template <int KMAX, int MODE>
 struct PairInst {
     static hipError_t launch(const EdgeArgs& a, int grid, hipStream_t st) {
-        const int G = lanes_of(a.dpad), M = (a.dpad + G - 1) / G;
+        const int G = lanes_of(a.dpad), M = regs_of(a.dpad);
         const size_t lds = MODE == MODE_HYBRID ? sh_lds_bytes(a.sh_rows, a.dpad) : 0;
 #define X(g, m)                                                                                      \
     if (G == g && M == m) {                                                                          \
@@ -62,7 +62,7 @@ struct PairInst {
         return hipErrorInvalidValue;
     }
     static const void* symbol(const EdgeArgs& a) {
-        const int G = lanes_of(a.dpad), M = (a.dpad + G - 1) / G;
+        const int G = lanes_of(a.dpad), M = regs_of(a.dpad);
 #define X(g, m) \
     if (G == g && M == m) return (const void*)pair_train_kernel<g, m, KMAX, MODE>;
         SMORE_FOR_EACH_GM(X)

@@ -1,10 +1,11 @@
 // edge_kernels.h -- the fused sampled-SGD kernels for gfx950 (templates).
 //
 // One "sample group" of G lanes owns one edge sample at a time.  Lane l of
-// the group owns the row elements l, l+G, l+2G, ... (M of them), so every
-// row load / store / atomic of a wave instruction covers a contiguous
-// 4G-byte segment of each row it touches (d=64: G=16, four 64-B segments per
-// wave instruction; d=128: G=32, two 128-B segments).
+// the group owns the row's 16-B chunks l, l+G, ... (M elements in M/4 chunks,
+// device_common.h elem_off), so every row load / store of a wave instruction
+// is a dwordx4 per lane covering 16G contiguous bytes of each row it touches
+// (d=64: G=16, four whole 256-B rows per wave instruction; d=128: G=32, two
+// whole 512-B rows).
 //
 // Per sample:
 //   [edge models: the draws come pre-drawn from train_draw.hip, one 32-B
@@ -150,17 +151,10 @@ __device__ __forceinline__ void gather_rows(const EdgeArgs& a, int lane, const b
                                             float (&rows)[KMAX + 1][M]) {
     const int dpad = a.dpad;
     const float* const Tc = shared ? a.W : a.C;
-    {
-        const float* wp = a.W + (int64_t)(v < 0 ? 0 : v) * dpad + lane;
+    ld_row<G, M>(wv, a.W + (int64_t)(v < 0 ? 0 : v) * dpad, lane, ev, v >= 0);
 #pragma unroll
-        for (int m = 0; m < M; ++m) wv[m] = (ev[m] && v >= 0) ? wp[m * G] : 0.0f;
-    }
-#pragma unroll
-    for (int k = 0; k <= KMAX; ++k) {
-        const float* cp = Tc + (int64_t)(id[k] < 0 ? 0 : id[k]) * dpad + lane;
-#pragma unroll
-        for (int m = 0; m < M; ++m) rows[k][m] = (ev[m] && id[k] >= 0) ? cp[m * G] : 0.0f;
-    }
+    for (int k = 0; k <= KMAX; ++k)
+        ld_row<G, M>(rows[k], Tc + (int64_t)(id[k] < 0 ? 0 : id[k]) * dpad, lane, ev, id[k] >= 0);
 }
 
 // the K+1 context rows only (W_v held by the caller)
@@ -168,11 +162,8 @@ template <int G, int M, int KMAX>
 __device__ __forceinline__ void gather_ctx_rows(const EdgeArgs& a, int lane, const bool (&ev)[M],
                                                 const int32_t (&id)[KMAX + 1], float (&rows)[KMAX + 1][M]) {
 #pragma unroll
-    for (int k = 0; k <= KMAX; ++k) {
-        const float* cp = a.C + (int64_t)(id[k] < 0 ? 0 : id[k]) * a.dpad + lane;
-#pragma unroll
-        for (int m = 0; m < M; ++m) rows[k][m] = (ev[m] && id[k] >= 0) ? cp[m * G] : 0.0f;
-    }
+    for (int k = 0; k <= KMAX; ++k)
+        ld_row<G, M>(rows[k], a.C + (int64_t)(id[k] < 0 ? 0 : id[k]) * a.dpad, lane, ev, id[k] >= 0);
 }
 
 // sgd_update on rows already gathered by gather_rows (wv, rows are consumed).
@@ -208,19 +199,19 @@ __device__ __forceinline__ void sgd_update_rows(const EdgeArgs& a, const float* 
             for (int k = 0; k <= KMAX; ++k) {
                 if (id[k] >= 0 && hot[k]) slot[k] = sh_lookup(sh.hash, id[k]);
                 if (slot[k] >= 0) {
-                    const float* pp = sh.pend + slot[k] * dpad + lane;
+                    const float* pp = sh.pend + slot[k] * dpad;
 #pragma unroll
                     for (int m = 0; m < M; ++m)
-                        if (ev[m]) rows[k][m] += pp[m * G];
+                        if (ev[m]) rows[k][m] += pp[elem_off<G>(lane, m)];
                 }
             }
             if (shared && hotw) {
                 slotw = sh_lookup(sh.hash, v);
                 if (slotw >= 0) {
-                    const float* pp = sh.pend + slotw * dpad + lane;
+                    const float* pp = sh.pend + slotw * dpad;
 #pragma unroll
                     for (int m = 0; m < M; ++m)
-                        if (ev[m]) wv[m] += pp[m * G];
+                        if (ev[m]) wv[m] += pp[elem_off<G>(lane, m)];
                 }
             }
         }
@@ -308,19 +299,24 @@ __device__ __forceinline__ void sgd_update_rows(const EdgeArgs& a, const float* 
     // ---- scatter
     static_assert(WOUT || SHARED == 0, "W_v stays in registers only with two tables");
     if constexpr (WOUT) {
-        float* wq = Tw + (int64_t)v * dpad + lane;
+        float* wq = Tw + (int64_t)v * dpad;
+        if (DELTA && hotw) {
+            float d[M];
 #pragma unroll
-        for (int m = 0; m < M; ++m) {
-            if (!ev[m]) continue;
-            if (DELTA && hotw) {
-                float d = e[m];
+            for (int m = 0; m < M; ++m) {
+                d[m] = e[m];
                 if constexpr (SHARED != 0)
-                    if (shared) d = wv[m] - wv0[m];
-                if (MODE == MODE_HYBRID && slotw >= 0) atomicAdd(sh.pend + slotw * dpad + lane + m * G, d);
-                else unsafeAtomicAdd(wq + m * G, d);
-            } else {
-                wq[m * G] = wv[m];
+                    if (shared) d[m] = wv[m] - wv0[m];
             }
+            if (MODE == MODE_HYBRID && slotw >= 0) {
+#pragma unroll
+                for (int m = 0; m < M; ++m)
+                    if (ev[m]) atomicAdd(sh.pend + slotw * dpad + elem_off<G>(lane, m), d[m]);
+            } else {
+                atomic_row<G, M>(wq, d, lane, dpad);
+            }
+        } else {
+            st_row<G, M>(wq, wv, lane, ev);
         }
     }
 #pragma unroll
@@ -328,26 +324,18 @@ __device__ __forceinline__ void sgd_update_rows(const EdgeArgs& a, const float* 
         if (id[k] < 0 || id[k] == vs) continue;
         if (DELTA && hot[k]) {
             if (MODE == MODE_HYBRID && slot[k] >= 0) {
-                float* pq = sh.pend + slot[k] * dpad + lane;
+                float* pq = sh.pend + slot[k] * dpad;
 #pragma unroll
                 for (int m = 0; m < M; ++m)
-                    if (ev[m]) atomicAdd(pq + m * G, rows[k][m]);
+                    if (ev[m]) atomicAdd(pq + elem_off<G>(lane, m), rows[k][m]);
             } else {
-                float* cq = Tc + (int64_t)id[k] * dpad + lane;
-#pragma unroll
-                for (int m = 0; m < M; ++m)
-                    if (ev[m]) unsafeAtomicAdd(cq + m * G, rows[k][m]);
+                atomic_row<G, M>(Tc + (int64_t)id[k] * dpad, rows[k], lane, dpad);
             }
         } else {
             bool last = true;
 #pragma unroll
             for (int k2 = k + 1; k2 <= KMAX; ++k2) last = last && (id[k2] != id[k]);
-            if (last) {
-                float* cq = Tc + (int64_t)id[k] * dpad + lane;
-#pragma unroll
-                for (int m = 0; m < M; ++m)
-                    if (ev[m]) cq[m * G] = rows[k][m];
-            }
+            if (last) st_row<G, M>(Tc + (int64_t)id[k] * dpad, rows[k], lane, ev);
         }
     }
 }
@@ -456,17 +444,16 @@ _Pragma("unroll") for (int k2 = 0; k2 < NS; ++k2) if (k2 != (K_) && id[k2] == id
 #pragma unroll
         for (int k2 = k + 1; k2 < NS; ++k2) last = last && (id[k2] != id[k]);
         if (last) {
-            float* q = T + (int64_t)id[k] * dpad + lane;
-            const bool atom = hot[k];
+            float* q = T + (int64_t)id[k] * dpad;
+            bool atom = false;
+            if constexpr (DELTA) atom = hot[k];
+            if (atom) {
+                float dd[M];
 #pragma unroll
-            for (int m = 0; m < M; ++m) {
-                if (!ev[m]) continue;
-                if constexpr (DELTA) {
-                    if (atom) unsafeAtomicAdd(q + m * G, row[k][m] - orig[k][m]);
-                    else q[m * G] = row[k][m];
-                } else {
-                    q[m * G] = row[k][m];
-                }
+                for (int m = 0; m < M; ++m) dd[m] = row[k][m] - orig[DELTA ? k : 0][m];
+                atomic_row<G, M>(q, dd, lane, dpad);
+            } else {
+                st_row<G, M>(q, row[k], lane, ev);
             }
         }
     }
@@ -537,9 +524,8 @@ edge_train_kernel(EdgeArgs a) {
     }
     const bool shared = SHARED >= 1;  // LINE-1 / MF / BPR: one table (host dispatches on a.model)
     const bool mf = SHARED == 1 && a.model == 2;
-    bool ev[M];                      // element lane + G*m exists
-#pragma unroll
-    for (int m = 0; m < M; ++m) ev[m] = lane + G * m < a.dpad;
+    bool ev[M];                      // register m's element exists
+    row_valid<G, M>(ev, lane, a.dpad);
     const uint64_t base = (mf || SHARED == 2) ? 0 : 1;   // LINE counts from 1, MF and BPR from 0
     float* const Tc = a.C;
 
@@ -736,8 +722,7 @@ pair_train_kernel(EdgeArgs a) {
     const uint64_t count = a.count_dev ? *a.count_dev : a.count;
     const uint64_t gpb = blockDim.x / G, gib = threadIdx.x / G;
     bool ev[M];
-#pragma unroll
-    for (int m = 0; m < M; ++m) ev[m] = lane + G * m < a.dpad;
+    row_valid<G, M>(ev, lane, a.dpad);
     constexpr int RW = rec_width(KMAX);
     uint32_t round = 0;
     __shared__ uint64_t s_next;
@@ -767,10 +752,10 @@ pair_train_kernel(EdgeArgs a) {
         };
         auto flush_w = [&]() {
             if (cv < 0) return;
-            float* wq = a.W + (int64_t)cv * a.dpad + lane;
+            float d[M];
 #pragma unroll
-            for (int m = 0; m < M; ++m)
-                if (ev[m]) unsafeAtomicAdd(wq + m * G, wv[m] - wv0[m]);
+            for (int m = 0; m < M; ++m) d[m] = wv[m] - wv0[m];
+            atomic_row<G, M>(a.W + (int64_t)cv * a.dpad, d, lane, a.dpad);
         };
         load_rec(s0);
         for (uint64_t t = s0; t < s1; ++t) {
@@ -791,9 +776,9 @@ pair_train_kernel(EdgeArgs a) {
             if (v != cv) {
                 flush_w();
                 cv = v;
-                const float* wp = a.W + (int64_t)cv * a.dpad + lane;
+                ld_row<G, M>(wv, a.W + (int64_t)cv * a.dpad, lane, ev);
 #pragma unroll
-                for (int m = 0; m < M; ++m) wv[m] = wv0[m] = ev[m] ? wp[m * G] : 0.0f;
+                for (int m = 0; m < M; ++m) wv0[m] = wv[m];
             }
             gather_ctx_rows<G, M, KMAX>(a, lane, ev, id, rows);
             // word 0 bit 31: HPE community record (Opt_SigmoidRegSGD)
@@ -817,18 +802,10 @@ pair_train_kernel(EdgeArgs a) {
 }
 
 // ---------------------------------------------------------------- dispatch
-// (G, M) pairs for dpad in [4, 512]: G = min(64, pow2ceil(dpad / SMORE_EPL)),
-// M = ceil(dpad / G) (train_kernels.hip lanes_of; oracle orc_lane_width).
-#if SMORE_EPL == 1
+// (G, M) pairs for dpad in [4, 512]: G = min(64, pow2ceil(dpad / 4)) lanes,
+// M = 4 * ceil(dpad / 4 / G) registers (train_kernels.h lanes_of / regs_of;
+// oracle orc_lane_width).
 #define SMORE_FOR_EACH_GM(X) \
-    X(4, 1) X(8, 1) X(16, 1) X(32, 1) X(64, 1) X(64, 2) X(64, 3) X(64, 4) X(64, 5) X(64, 6) X(64, 7) X(64, 8)
-#elif SMORE_EPL == 2
-#define SMORE_FOR_EACH_GM(X) \
-    X(2, 2) X(4, 2) X(8, 2) X(16, 2) X(32, 2) X(64, 2) X(64, 3) X(64, 4) X(64, 5) X(64, 6) X(64, 7) X(64, 8)
-#else
-#define SMORE_FOR_EACH_GM(X) \
-    X(1, 4) X(2, 4) X(4, 3) X(4, 4) X(8, 3) X(8, 4) X(16, 3) X(16, 4) X(32, 3) X(32, 4) \
-    X(64, 3) X(64, 4) X(64, 5) X(64, 6) X(64, 7) X(64, 8)
-#endif
+    X(1, 4) X(2, 4) X(4, 4) X(8, 4) X(16, 4) X(32, 4) X(64, 4) X(64, 8)
 
 }  // namespace smore

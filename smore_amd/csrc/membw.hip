@@ -28,11 +28,22 @@ __global__ void __launch_bounds__(256) copy_kernel(const f32x4* __restrict__ src
     for (; i < n; i += stride) dst[i] = src[i];
 }
 
-// variant 0: default cache policy, 1: non-temporal loads and stores
+// one 16-B word per thread, as many blocks as words / 256 (the dispatcher
+// keeps every CU full)
+__global__ void __launch_bounds__(256) copy_flat_kernel(const f32x4* __restrict__ src, f32x4* __restrict__ dst,
+                                                        uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[i];
+}
+
+// variant 0: default cache policy, 1: non-temporal loads and stores (grid-
+// stride, `blocks` blocks); 2: one word per thread over the whole buffer
 hipError_t launch_copy(const void* src, void* dst, uint64_t n16, int blocks, int variant, hipStream_t st) {
     const f32x4* s = reinterpret_cast<const f32x4*>(src);
     f32x4* d = reinterpret_cast<f32x4*>(dst);
-    if (variant == 1) hipLaunchKernelGGL((copy_kernel<4, true>), dim3(blocks), dim3(256), 0, st, s, d, n16);
+    if (variant == 2)
+        hipLaunchKernelGGL(copy_flat_kernel, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, st, s, d, n16);
+    else if (variant == 1) hipLaunchKernelGGL((copy_kernel<4, true>), dim3(blocks), dim3(256), 0, st, s, d, n16);
     else hipLaunchKernelGGL((copy_kernel<4, false>), dim3(blocks), dim3(256), 0, st, s, d, n16);
     return hipGetLastError();
 }

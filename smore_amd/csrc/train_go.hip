@@ -44,22 +44,15 @@ __device__ __forceinline__ int32_t go_target(const DevGraph& g, const double* tc
 template <int G, int M>
 __device__ __forceinline__ void load_row(float (&r)[M], const float* T, int64_t row, int dpad, int lane,
                                          const bool (&ev)[M]) {
-    const float* p = T + row * dpad + lane;
-#pragma unroll
-    for (int m = 0; m < M; ++m) r[m] = ev[m] ? p[m * G] : 0.0f;
+    ld_row<G, M>(r, T + row * dpad, lane, ev);
 }
 
 // scatter of a row: plain store of `val`, or atomic add of `delta`
 template <int G, int M, int MODE>
 __device__ __forceinline__ void put_row(float* T, int64_t row, int dpad, int lane, const bool (&ev)[M],
                                         const float (&val)[M], const float (&delta)[M]) {
-    float* p = T + row * dpad + lane;
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-        if (!ev[m]) continue;
-        if constexpr (MODE == MODE_ATOMIC) unsafeAtomicAdd(p + m * G, delta[m]);
-        else p[m * G] = val[m];
-    }
+    if constexpr (MODE == MODE_ATOMIC) atomic_row<G, M>(T + row * dpad, delta, lane, dpad);
+    else st_row<G, M>(T + row * dpad, val, lane, ev);
 }
 
 template <int G, int M>
@@ -84,9 +77,7 @@ __device__ __forceinline__ void go_pair_ctx(const EdgeArgs& a, const float* s_si
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) {
         const bool use = negs[j] >= 0 && negs[j] != c;
-        const float* p = a.C + (int64_t)(use ? negs[j] : 0) * dpad + lane;
-#pragma unroll
-        for (int m = 0; m < M; ++m) rows[j][m] = (use && ev[m]) ? p[m * G] : 0.0f;
+        ld_row<G, M>(rows[j], a.C + (int64_t)(use ? negs[j] : 0) * dpad, lane, ev, use);
     }
 #pragma unroll
     for (int j = 1; j < KMAX; ++j)
@@ -154,9 +145,7 @@ __device__ __forceinline__ void go_first_order(const EdgeArgs& a, const float* s
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) {
         const bool use = negs[j] >= 0 && negs[j] != s && negs[j] != t;
-        const float* p = a.W + (int64_t)(use ? negs[j] : 0) * dpad + lane;
-#pragma unroll
-        for (int m = 0; m < M; ++m) rows[j][m] = (use && ev[m]) ? p[m * G] : 0.0f;
+        ld_row<G, M>(rows[j], a.W + (int64_t)(use ? negs[j] : 0) * dpad, lane, ev, use);
     }
 #pragma unroll
     for (int j = 1; j < KMAX; ++j)
@@ -266,8 +255,7 @@ __global__ void __launch_bounds__(256) go_edge_kernel(EdgeArgs a) {
         ngroups = 1;
     }
     bool ev[M];
-#pragma unroll
-    for (int m = 0; m < M; ++m) ev[m] = lane + G * m < a.dpad;
+    row_valid<G, M>(ev, lane, a.dpad);
     const int nk = a.model == 3 ? 1 : a.K;
     for (uint64_t t = group; t < a.count; t += ngroups) {
         const uint64_t s = a.begin + t;
@@ -511,8 +499,7 @@ __global__ void __launch_bounds__(256) go_walk_pairs_kernel(EdgeArgs a, WalkArgs
         ngroups = 1;
     }
     bool ev[M];
-#pragma unroll
-    for (int m = 0; m < M; ++m) ev[m] = lane + G * m < a.dpad;
+    row_valid<G, M>(ev, lane, a.dpad);
     const int stride = w.steps + 1;
     for (uint64_t t = group; t < w.nwalks; t += ngroups) {
         const uint64_t unit = w.walk_begin + t;
@@ -608,7 +595,7 @@ static hipError_t go_pairs(const EdgeArgs& a, const WalkArgs& w, int grid, hipSt
 }
 
 hipError_t launch_go_edge(const EdgeArgs& a, int grid, hipStream_t st) {
-    const int G = lanes_of(a.dpad), M = (a.dpad + G - 1) / G;
+    const int G = lanes_of(a.dpad), M = regs_of(a.dpad);
 #define X(g, m)                                                  \
     if (G == g && M == m) {                                      \
         if (a.K <= 5 || a.model == 3) return go_edge<g, m, 5>(a, grid, st); \
@@ -620,7 +607,7 @@ hipError_t launch_go_edge(const EdgeArgs& a, int grid, hipStream_t st) {
 }
 
 hipError_t launch_go_pairs(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st) {
-    const int G = lanes_of(a.dpad), M = (a.dpad + G - 1) / G;
+    const int G = lanes_of(a.dpad), M = regs_of(a.dpad);
 #define X(g, m)                                                  \
     if (G == g && M == m) {                                      \
         if (a.K <= 5) return go_pairs<g, m, 5>(a, w, grid, st);  \

@@ -69,12 +69,14 @@ struct AppArgs {
     double jump;
 };
 
-// lanes per sample group: G = min(64, pow2ceil(dpad / SMORE_EPL)); lane l owns
-// row elements l, l+G, l+2G, ... (DESIGN.md "Arithmetic spec")
-#ifndef SMORE_EPL
-#define SMORE_EPL 4
-#endif
+// lanes per sample group: G = min(64, pow2ceil(dpad / 4)); lane l owns the
+// row's 16-B chunks l, l+G, ... in M = regs_of(dpad) registers
+// (device_common.h elem_off; DESIGN.md "Arithmetic spec")
 int lanes_of(int dpad);
+inline int regs_of(int dpad) {
+    const int G = lanes_of(dpad);
+    return 4 * ((dpad / 4 + G - 1) / G);
+}
 // int32 words per pre-drawn edge-sample record {v, c, n_1..n_K, pad}: the
 // smallest power of two >= 2 + KMAX, at least 4 (whole 16-B words)
 constexpr int rec_width(int kmax) {

@@ -55,7 +55,7 @@ __global__ void init_uniform_kernel(float* T, int64_t rows, int dim, int dpad, u
 
 // ------------------------------------------------------------------ dispatch
 int lanes_of(int dpad) {
-    int nq = (dpad + SMORE_EPL - 1) / SMORE_EPL, G = 1;
+    int nq = (dpad + 3) / 4, G = 1;
     while (G < nq && G < 64) G <<= 1;
     return G;
 }

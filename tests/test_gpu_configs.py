@@ -179,12 +179,12 @@ def test_c4_serial_bit_exact(c4):
 
 @pytest.mark.timeout(600)
 def test_c4_full_grid_hybrid_matches_atomic(c4):
-    """The bench's workload and default scatter: one full-grid hybrid launch of
-    2^27 samples is finite and tags hot rows at V = 10M; after 2^28 samples the
-    held-out LINE-2 loss of the hybrid scatter is within 1 % of the lossless
-    atomic scatter's."""
+    """The bench's workload and default scatter: full-grid hybrid launches of
+    2^27 samples are finite and tag hot rows at V = 10M; after 2^30 samples
+    (~107 per vertex) the held-out LINE-2 loss of the hybrid scatter is within
+    1 % of the lossless atomic scatter's."""
     g, pn = c4
-    dim, K, total = 64, 5, 1 << 28
+    dim, K, launch, total = 64, 5, 1 << 27, 1 << 30
     heldout = orc.sample_line(g, SEED + 1, 0, 100_000, K)
     res = {}
     for mode in ("atomic", "hybrid"):
@@ -193,21 +193,19 @@ def test_c4_full_grid_hybrid_matches_atomic(c4):
         pn.zero_table(1)
         pn.set_hot_threshold(0.3)
         pn.set_write_combine(128, 0)
-        pn.train_edges("line2", 0, 1 << 27, total, K, 0.025, 0.0, SEED, mode)
-        if mode == "hybrid":
-            W = pn.get_table(0)
-            assert np.isfinite(W).all()
-            hw, hc = pn.hot_rows()
-            assert hw > 0 and hc > 0, (hw, hc)
-            del W
-        pn.train_edges("line2", 1 << 27, 1 << 27, total, K, 0.025, 0.0, SEED, mode)
+        for b in range(0, total, launch):
+            pn.train_edges("line2", b, launch, total, K, 0.025, 0.0, SEED, mode)
+            if mode == "hybrid" and b == 0:
+                assert np.isfinite(pn.get_table(0)).all()
+                hw, hc = pn.hot_rows()
+                assert hw > 0 and hc > 0, (hw, hc)
         W, C = pn.get_table(0), pn.get_table(1)
         assert np.isfinite(W).all() and np.isfinite(C).all()
         res[mode] = _heldout_loss(W, C, heldout, dim)
         del W, C
     assert pn.skipped() == 0
     init = np.log(2.0) * (1 + K)
-    assert res["atomic"] < 0.97 * init, res
+    assert res["atomic"] < 0.9 * init, res
     assert res["hybrid"] <= 1.01 * res["atomic"], res
 
 

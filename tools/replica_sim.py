@@ -1,0 +1,131 @@
+#!/usr/bin/env python3
+"""What the replica exchange does to training at N GPUs, measured
+on ONE GPU: N library contexts hold N replicas of a config's graph and tables,
+each runs its own global-sample ranges exactly as bench.py's ranks do
+(2^27 / 10 * V/1M samples per step per replica = the C4 bench's samples per
+row per step), and after every step the snapshot-delta exchange runs with the
+bench's one-exchange-late schedule (begin = [end of the previous exchange +]
+D = T - S; R = D; S = T; the all-reduce is the sum of the replicas' R; end =
+X = scale * R - D; T += X; S += X).  The replicas run one after another on the
+GPU, which changes nothing in the arithmetic: each trains from its own state.
+
+Reports the held-out LINE-2 loss of replica 0 after `--total` samples, against
+one replica trained on the same total, for the sum and mean exchanges.
+
+    python tools/replica_sim.py --config c2 --ranks 1 2 4 8 --sync sum mean
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def heldout_loss(W, C, draws, dim):
+    v, c, negs = draws[:, 0], draws[:, 1], draws[:, 2:]
+    keep = c >= 0
+    v, c, negs = v[keep], c[keep], negs[keep]
+    Wv = W[v, :dim].astype(np.float64)
+    loss = np.logaddexp(0.0, -np.einsum("ij,ij->i", Wv, C[c, :dim].astype(np.float64)))
+    for k in range(negs.shape[1]):
+        loss += np.logaddexp(0.0, np.einsum("ij,ij->i", Wv, C[negs[:, k], :dim].astype(np.float64)))
+    return float(loss.mean())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--ranks", type=int, nargs="+", default=[1, 2, 4, 8])
+    ap.add_argument("--sync", nargs="+", default=["sum", "mean"])
+    ap.add_argument("--total", type=int, default=1 << 30)
+    ap.add_argument("--per-row", type=float, default=13.42, help="samples per vertex per step per replica")
+    ap.add_argument("--mode", default="hybrid")
+    ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--seed", type=int, default=20251015)
+    args = ap.parse_args()
+
+    import torch
+    import smore_amd
+    from smore_amd import graphgen
+    from smore_amd.dist import TorchPasses, table_tensor
+
+    torch.cuda.set_device(0)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    V, (src, dst, w) = graphgen.config_edges(args.config)
+    K, dim = 5, args.dim
+    S = int(args.per_row * V)
+    ctxs = []
+
+    def ctx(i):
+        while len(ctxs) <= i:
+            pn = smore_amd.ProNet(0)
+            pn.set_graph_edges(V, src, dst, w)
+            pn.set_stream(stream.cuda_stream)
+            pn.alloc_tables(dim, 2)
+            ctxs.append(pn)
+        return ctxs[i]
+
+    heldout = ctx(0).sample_edges("line2", (1 << 40) + 17, 100_000, K, args.seed + 1)
+    results = []
+    for n in args.ranks:
+        for sync in (args.sync if n > 1 else ["none"]):
+            reps = [ctx(i) for i in range(n)]
+            for pn in reps:
+                pn.init_table_uniform(0, 5)
+                pn.zero_table(1)
+            T = [[table_tensor(pn, t) for t in (0, 1)] for pn in reps]
+            Ss = [[t.clone() for t in ts] for ts in T]
+            Ds = [[torch.zeros_like(t) for t in ts] for ts in T]
+            Rs = [[torch.zeros_like(t) for t in ts] for ts in T]
+            scale = 1.0 / n if sync == "mean" else 1.0
+            steps = max(1, args.total // (n * S))
+            pending = False
+            t0 = time.perf_counter()
+
+            def reduce_all():
+                for t in range(2):
+                    tot = sum(Rs[r][t] for r in range(n))
+                    for r in range(n):
+                        Rs[r][t].copy_(tot)
+
+            for k in range(steps):
+                for r, pn in enumerate(reps):
+                    pn.train_edges("line2", (k * n + r) * S, S, steps * n * S, K, 0.025, 0.0, args.seed, args.mode,
+                                   sync=False)
+                if n > 1:
+                    for r in range(n):
+                        for t in range(2):
+                            if pending:
+                                TorchPasses.cycle(T[r][t], Ss[r][t], Ds[r][t], Rs[r][t], scale)
+                            else:
+                                TorchPasses.begin(T[r][t], Ss[r][t], Ds[r][t], Rs[r][t])
+                    reduce_all()       # the all-reduce of this exchange (lands before the next end)
+                    pending = True
+            if pending:
+                for r in range(n):
+                    for t in range(2):
+                        TorchPasses.end(T[r][t], Ss[r][t], Ds[r][t], Rs[r][t], scale)
+            torch.cuda.synchronize()
+            W0, C0 = reps[0].get_table(0), reps[0].get_table(1)
+            spread = 0.0
+            if n > 1:
+                W1 = reps[n - 1].get_table(0)
+                spread = float(np.abs(W1 - W0).max() / max(1e-30, np.abs(W0).max()))
+            row = {"config": args.config, "ranks": n, "sync": sync, "steps": steps, "samples_per_step": S,
+                   "total": steps * n * S, "mode": args.mode, "finite": bool(np.isfinite(W0).all()),
+                   "loss": round(heldout_loss(W0, C0, heldout, dim), 5), "replica_spread_rel": spread,
+                   "wall_s": round(time.perf_counter() - t0, 1)}
+            results.append(row)
+            print(json.dumps(row), flush=True)
+            del T, Ss, Ds, Rs
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
