@@ -179,7 +179,11 @@ __device__ __forceinline__ void st_row(float* row, const float (&r)[M], int lane
 // bytes of the row, not 4 dwords of every 16 B (G < 4: element by element).
 template <int G, int M>
 __device__ __forceinline__ void atomic_row(float* row, const float (&d)[M], int lane, int dpad) {
+#ifdef SMORE_ATOMIC_STRIDED
+    if constexpr (true) {
+#else
     if constexpr (G < 4) {
+#endif
 #pragma unroll
         for (int m = 0; m < M; ++m)
             if (lane + G * (m >> 2) < (dpad >> 2)) unsafeAtomicAdd(row + elem_off<G>(lane, m), d[m]);

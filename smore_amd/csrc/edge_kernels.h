@@ -37,7 +37,7 @@ enum { MODE_STORE = 0, MODE_ATOMIC = 1, MODE_HYBRID = 3 };
 #define SMORE_WAVES_ATOMIC 0
 #endif
 #ifndef SMORE_WAVES_HYBRID
-#define SMORE_WAVES_HYBRID 4
+#define SMORE_WAVES_HYBRID 3
 #endif
 #ifndef SMORE_WAVES_BPR
 #define SMORE_WAVES_BPR 0
@@ -604,22 +604,30 @@ edge_train_kernel(EdgeArgs a) {
         // this sample is about to write -- the staleness every other resident
         // group already has (Hogwild); the serial mode above keeps strict order.
         constexpr int RW = rec_width(KMAX);
+        // a decoded sample keeps its TAGGED words (v, c, negatives; -1 = none)
+        // across the pipeline; ids and hot flags are split off where used,
+        // which keeps two samples' state in fewer registers
         struct Ids {
-            int32_t v, id[KMAX + 1];
-            bool hotw, hot[KMAX + 1], live;
+            int32_t w[KMAX + 2];
+            bool live;
             float alpha;
+            __device__ __forceinline__ int32_t v() const { return live ? untag(w[0]) : -1; }
+            __device__ __forceinline__ void ids(int32_t (&id)[KMAX + 1]) const {
+#pragma unroll
+                for (int k = 0; k <= KMAX; ++k) id[k] = (!live || w[k + 1] < 0) ? -1 : untag(w[k + 1]);
+            }
+            __device__ __forceinline__ void hots(bool (&hot)[KMAX + 1]) const {
+#pragma unroll
+                for (int k = 0; k <= KMAX; ++k) hot[k] = scatter_atomic<MODE>(w[k + 1]);
+            }
         };
         auto decode = [&](uint64_t t, uint64_t lim, const i32x4 (&r)[RW / 4], Ids& x) {
             x.live = t < lim && r[0][1] >= 0;   // c < 0: counted by the draw kernel
             x.alpha = rec_alpha(t, r);
-            x.hotw = scatter_atomic<MODE>(r[0][0]);
-            x.v = x.live ? untag(r[0][0]) : -1;
+            x.w[0] = r[0][0];
 #pragma unroll
-            for (int k = 0; k <= KMAX; ++k) {
-                const int32_t w = (k == 0) ? r[0][1] : (k - 1 < a.K ? r[(k + 1) / 4][(k + 1) % 4] : -1);
-                x.hot[k] = scatter_atomic<MODE>(w);
-                x.id[k] = (!x.live || w < 0) ? -1 : untag(w);
-            }
+            for (int k = 0; k <= KMAX; ++k)
+                x.w[k + 1] = (k == 0) ? r[0][1] : (k - 1 < a.K ? r[(k + 1) / 4][(k + 1) % 4] : -1);
         };
         auto load_rec = [&](uint64_t t, uint64_t lim, i32x4 (&r)[RW / 4]) {
 #pragma unroll
@@ -659,10 +667,14 @@ edge_train_kernel(EdgeArgs a) {
                     decode(t, lim, rr, xa);
                     load_rec(t + gpb, lim, rr);
                     if (xa.live) {
-                        gather_rows<G, M, KMAX>(a, lane, ev, xa.v, xa.id, shared, wva, rowsa);
+                        int32_t id[KMAX + 1];
+                        bool hot[KMAX + 1];
+                        xa.ids(id);
+                        xa.hots(hot);
+                        gather_rows<G, M, KMAX>(a, lane, ev, xa.v(), id, shared, wva, rowsa);
                         if constexpr (KMAX == 5)
-                            bpr_update_rows<G, M, KMAX, MODE>(a, s_sig, lane, ev, xa.v, xa.id, xa.hotw, xa.hot,
-                                                              xa.alpha, wva, rowsa);
+                            bpr_update_rows<G, M, KMAX, MODE>(a, s_sig, lane, ev, xa.v(), id,
+                                                              scatter_atomic<MODE>(xa.w[0]), hot, xa.alpha, wva, rowsa);
                     }
                     maybe_flush();
                 }
@@ -671,17 +683,31 @@ edge_train_kernel(EdgeArgs a) {
             uint64_t t = c0 + gib;
             load_rec(t, lim, rr);
             decode(t, lim, rr, xa);
-            gather_rows<G, M, KMAX>(a, lane, ev, xa.v, xa.id, shared, wva, rowsa);
+            {
+                int32_t id[KMAX + 1];
+                xa.ids(id);
+                gather_rows<G, M, KMAX>(a, lane, ev, xa.v(), id, shared, wva, rowsa);
+            }
             load_rec(t + gpb, lim, rr);
             for (uint64_t r = c0; r < lim; r += gpb) {
                 t = r + gib;
                 decode(t + gpb, lim, rr, xb);
                 load_rec(t + 2 * gpb, lim, rr);
-                gather_rows<G, M, KMAX>(a, lane, ev, xb.v, xb.id, shared, wvb, rowsb);
+                {
+                    int32_t id[KMAX + 1];
+                    xb.ids(id);
+                    gather_rows<G, M, KMAX>(a, lane, ev, xb.v(), id, shared, wvb, rowsb);
+                }
                 if (xa.live) {
-                    if constexpr (SHARED != 2)
-                        sgd_update_rows<G, M, KMAX, MODE, SHARED>(a, s_sig, lane, ev, xa.v, xa.id, xa.hotw, xa.hot,
-                                                                 xa.alpha, shared, mf, sh, wva, rowsa);
+                    if constexpr (SHARED != 2) {
+                        int32_t id[KMAX + 1];
+                        bool hot[KMAX + 1];
+                        xa.ids(id);
+                        xa.hots(hot);
+                        sgd_update_rows<G, M, KMAX, MODE, SHARED>(a, s_sig, lane, ev, xa.v(), id,
+                                                                 scatter_atomic<MODE>(xa.w[0]), hot, xa.alpha, shared,
+                                                                 mf, sh, wva, rowsa);
+                    }
                 }
                 xa = xb;
 #pragma unroll

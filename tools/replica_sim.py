@@ -12,6 +12,12 @@ GPU, which changes nothing in the arithmetic: each trains from its own state.
 Reports the held-out LINE-2 loss of replica 0 after `--total` samples, against
 one replica trained on the same total, for the sum and mean exchanges.
 
+--sub k --hot H: every step runs as k launches, and after each one the H rows of
+each table with the highest expected touch rate (the hub rows: source law for
+W, context + K x negative law for C) are exchanged synchronously
+(D' = T_h - S_h; R' = sum of the replicas' D'; T_h += R' - D'; S_h += R'),
+composing with the one-late full exchange (no update counted twice).
+
     python tools/replica_sim.py --config c2 --ranks 1 2 4 8 --sync sum mean
 """
 import argparse
@@ -47,6 +53,8 @@ def main():
     ap.add_argument("--mode", default="hybrid")
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--seed", type=int, default=20251015)
+    ap.add_argument("--sub", type=int, nargs="+", default=[1], help="launches (hot exchanges) per step")
+    ap.add_argument("--hot", type=int, nargs="+", default=[0], help="hot rows per table exchanged per launch")
     args = ap.parse_args()
 
     import torch
@@ -72,8 +80,23 @@ def main():
         return ctxs[i]
 
     heldout = ctx(0).sample_edges("line2", (1 << 40) + 17, 100_000, K, args.seed + 1)
+    # expected touches per sample (unit weights): W rows by the source law
+    # out_deg^0.75, C rows by the context law (source law / out-degree per
+    # edge) plus K x the negative law (in + out)^0.75
+    od = np.bincount(src, minlength=V).astype(np.float64)
+    idg = np.bincount(dst, minlength=V).astype(np.float64)
+    ps = od ** 0.75
+    ps /= ps.sum()
+    pn_ = (od + idg) ** 0.75
+    pn_ /= pn_.sum()
+    pc = np.bincount(dst, weights=(ps / np.maximum(od, 1))[src], minlength=V)
+    rate = [ps, pc + K * pn_]
+    order_by_rate = [torch.from_numpy(np.argsort(-r, kind="stable").astype(np.int64)).cuda() for r in rate]
     results = []
-    for n in args.ranks:
+    import itertools
+    for n, sub, hot in itertools.product(args.ranks, args.sub, args.hot):
+        if n == 1 and (sub != args.sub[0] or hot != args.hot[0]):
+            continue
         for sync in (args.sync if n > 1 else ["none"]):
             reps = [ctx(i) for i in range(n)]
             for pn in reps:
@@ -94,10 +117,25 @@ def main():
                     for r in range(n):
                         Rs[r][t].copy_(tot)
 
+            hidx = [o[:hot] for o in order_by_rate] if hot > 0 else None
+
+            def hot_sync():
+                for t in range(2):
+                    idx = hidx[t]
+                    Dh = [T[r][t][idx] - Ss[r][t][idx] for r in range(n)]
+                    Rh = sum(Dh)
+                    for r in range(n):
+                        T[r][t][idx] += Rh - Dh[r]
+                        Ss[r][t][idx] += Rh
+
+            sub_n = S // sub
             for k in range(steps):
-                for r, pn in enumerate(reps):
-                    pn.train_edges("line2", (k * n + r) * S, S, steps * n * S, K, 0.025, 0.0, args.seed, args.mode,
-                                   sync=False)
+                for j in range(sub):
+                    for r, pn in enumerate(reps):
+                        pn.train_edges("line2", (k * n + r) * S + j * sub_n, sub_n if j + 1 < sub else S - j * sub_n,
+                                       steps * n * S, K, 0.025, 0.0, args.seed, args.mode, sync=False)
+                    if n > 1 and hidx is not None and sync == "sum":
+                        hot_sync()
                 if n > 1:
                     for r in range(n):
                         for t in range(2):
@@ -117,7 +155,8 @@ def main():
             if n > 1:
                 W1 = reps[n - 1].get_table(0)
                 spread = float(np.abs(W1 - W0).max() / max(1e-30, np.abs(W0).max()))
-            row = {"config": args.config, "ranks": n, "sync": sync, "steps": steps, "samples_per_step": S,
+            row = {"config": args.config, "ranks": n, "sync": sync, "sub": sub, "hot_rows": hot, "steps": steps,
+                   "samples_per_step": S,
                    "total": steps * n * S, "mode": args.mode, "finite": bool(np.isfinite(W0).all()),
                    "loss": round(heldout_loss(W0, C0, heldout, dim), 5), "replica_spread_rel": spread,
                    "wall_s": round(time.perf_counter() - t0, 1)}
