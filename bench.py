@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=20251015)
+    ap.add_argument("--semantics", default="cpp", choices=["cpp", "go"],
+                    help="update rule: the C++ reference's (default) or the Go tree's (pkg/pronet)")
     return ap.parse_args()
 
 
@@ -165,6 +167,8 @@ def main():
         print("[bench] %s: generated in %.1f s, graph built + uploaded in %.1f s"
               % (args.config, t_build - t_gen, t_ready - t_build), file=sys.stderr, flush=True)
     E = pn.MAX_line
+    if args.semantics == "go":
+        pn.set_semantics("go")
     pn.set_hot_threshold(args.hot_tau)
     pn.set_write_combine(args.combine_rows, args.combine_flush)
     pn.alloc_tables(args.dim, 2)
@@ -261,7 +265,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic power-law (Zipf 0.8 endpoints, seeded), random-init tables",
-            "config": {"workload": "LINE order-2 sampled negative-sampling SGD, config %s" % args.config,
+            "config": {"workload": "LINE order-2 sampled negative-sampling SGD, config %s%s"
+                                   % (args.config, "" if args.semantics == "cpp" else ", Go rules (pkg/pronet)"),
                        "vertices": V, "edge_slots": E, "dim": args.dim, "negative": K,
                        "samples_per_step_per_gpu": S, "scatter": args.mode,
                        "sync": ("%s every %d steps" % (args.sync, args.sync_every)) if world > 1 else "none",

@@ -452,10 +452,20 @@ static int ensure_packed(smore_ctx* c) {
 }
 
 // ---------------------------------------------------------------- training
-static int edge_grid(smore_ctx* c, const EdgeArgs& a, bool leave_slot = false) {
+static const void* go_rec_symbol(const EdgeArgs& a) {
+    return a.mode == SMORE_ATOMIC ? go_rec_symbol_a(a) : a.mode == SMORE_HYBRID ? go_rec_symbol_h(a) : go_rec_symbol_s(a);
+}
+
+static hipError_t launch_go_rec(const EdgeArgs& a, int grid, hipStream_t st) {
+    return a.mode == SMORE_ATOMIC   ? launch_go_rec_a(a, grid, st)
+           : a.mode == SMORE_HYBRID ? launch_go_rec_h(a, grid, st)
+                                    : launch_go_rec_s(a, grid, st);
+}
+
+static int edge_grid(smore_ctx* c, const EdgeArgs& a, bool leave_slot = false, bool go = false) {
     if (a.mode == SMORE_SERIAL) return 1;
     int per_cu = 0;
-    const void* sym = edge_kernel_symbol(a);
+    const void* sym = go ? go_rec_symbol(a) : edge_kernel_symbol(a);
     if (!sym ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sym, 256, sh_lds_bytes(a.sh_rows, a.dpad)) !=
             hipSuccess ||
@@ -518,32 +528,29 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
     a.model = model;
     a.mode = mode;
     a.tcum = c->d_tcum;
-    if (c->semantics == SMORE_SEM_GO) {
+    // Go semantics (SMORE_SEM_GO): Go draws into the same records
+    // (go_draw_kernel) and the Go rules on them (go_rec.h), with every
+    // scatter mode; BPR is Go's two-table, one-negative rule
+    const bool go = c->semantics == SMORE_SEM_GO;
+    if (go) {
         if (model == SMORE_MF) return fail(c, SMORE_EINVAL, "Go semantics has no MF model");
-        if (mode == SMORE_HYBRID) return fail(c, SMORE_EINVAL, "Go semantics: hybrid scatter not built");
         if (K > 10) return fail(c, SMORE_EINVAL, "Go semantics: K <= 10");
         if (model == SMORE_BPR && c->ntables < 2) return fail(c, SMORE_ESTATE, "Go BPR needs W (users) and C (items)");
-        if (model == SMORE_BPR) a.C = c->d_table[1];
-        a.K = K;
-        const int G = lanes_of(c->dpad);
-        int grid = 1;
-        if (mode != SMORE_SERIAL) {
-            grid = c->cus * 4;
-            const int64_t need = ((int64_t)count + 256 / G - 1) / (256 / G);
-            if (need < grid) grid = (int)std::max<int64_t>(1, need);
+        if (model == SMORE_BPR) {
+            a.C = c->d_table[1];
+            a.K = 1;
+        } else {
+            a.K = K;
         }
-        HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-        HIPCHK(c, launch_go_edge(a, grid, c->stream));
-        HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-        c->timed = true;
-        return SMORE_OK;
     }
-    const bool combine = mode == SMORE_HYBRID && model != SMORE_BPR;
+    const bool combine = mode == SMORE_HYBRID && (go || model != SMORE_BPR);
     a.sh_rows = combine ? std::min(c->sh_max, 8192 / std::max(1, c->dpad)) : 0;   // LDS bound for the grid
-    const int grid = edge_grid(c, a);
+    const int grid = edge_grid(c, a, false, go);
     if (mode == SMORE_HYBRID) {
         const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
-        if ((rc = build_hot_maps(c, model, a.K, M))) return rc;
+        // Go BPR has two tables (users W, items C): the LINE-2 row roles
+        const int hot_model = go && model == SMORE_BPR ? SMORE_LINE2 : model;
+        if ((rc = build_hot_maps(c, hot_model, a.K, M))) return rc;
     }
     a.sh_rows = combine ? c->sh_rows : 0;
     a.sh_hash = c->d_sh_hash;
@@ -579,15 +586,16 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
     };
     if ((rc = grow(c->phase_ev, 2 * (size_t)nch + 1))) return rc;
     if ((rc = grow(c->sync_ev, 2 * (size_t)nch))) return rc;
-    if ((rc = ensure_packed(c))) return rc;
+    if (!go && (rc = ensure_packed(c))) return rc;
     const DevGraph dg = dev_graph(c);
-    const int ugrid = nch > 1 ? edge_grid(c, a, true) : grid;
+    const int ugrid = nch > 1 ? edge_grid(c, a, true, go) : grid;
     hipStream_t ds = nch > 1 ? c->draw_stream : c->stream;
     auto recbuf = [&](int k) { return c->d_rec + (size_t)(k % nbuf) * chunk * RW; };
     auto draw = [&](int k) -> int {
         const uint64_t b = (uint64_t)k * chunk, n = std::min<uint64_t>(chunk, count - b);
         if (k >= 2) HIPCHK(c, hipStreamWaitEvent(ds, c->sync_ev[2 * (k - 2) + 1], 0));   // buffer free
-        HIPCHK(c, launch_draw(dg, seed, begin + b, n, a.K, recbuf(k), c->d_skipped, ds));
+        if (go) HIPCHK(c, launch_go_draw(dg, c->d_tcum, c->go_unit_w, seed, begin + b, n, a.K, recbuf(k), c->d_skipped, ds));
+        else HIPCHK(c, launch_draw(dg, seed, begin + b, n, a.K, recbuf(k), c->d_skipped, ds));
         HIPCHK(c, hipEventRecord(c->sync_ev[2 * k], ds));
         return SMORE_OK;
     };
@@ -606,7 +614,8 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
         ak.rec = recbuf(k);
         ak.work = c->d_work;
         HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
-        HIPCHK(c, launch_edge_train(ak, ugrid, c->stream));
+        if (go) HIPCHK(c, launch_go_rec(ak, ugrid, c->stream));
+        else HIPCHK(c, launch_edge_train(ak, ugrid, c->stream));
         HIPCHK(c, hipEventRecord(c->phase_ev[2 * k + 2], c->stream));
         HIPCHK(c, hipEventRecord(c->sync_ev[2 * k + 1], c->stream));
     }
@@ -649,6 +658,9 @@ int smore_set_semantics(smore_ctx* c, int semantics) {
     std::vector<double> tcum;
     if (semantics == SMORE_SEM_GO) build_go_tables(*c->g, tcum);
     else build_cpp_vn_tables(*c->g);
+    c->go_unit_w = 1;
+    for (int64_t e = 0; e < c->g->E && c->go_unit_w; ++e)
+        if (c->g->weights[e] != 1.0) c->go_unit_w = 0;
     c->semantics = semantics;
     c->hot_key.clear();
     if (c->device < 0) return SMORE_OK;

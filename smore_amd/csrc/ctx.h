@@ -61,6 +61,7 @@ struct smore_ctx {
     // semantics: SMORE_SEM_CPP (default) or SMORE_SEM_GO
     int semantics = 0;
     double* d_tcum = nullptr;
+    int go_unit_w = 0;             // Go semantics: every edge weight is 1 (O(1) CDF target draws)
     // node2vec (Go): raw CSR weights and per-vertex sorted CSR targets, built on first use
     double* d_wts = nullptr;
     int32_t* d_nbr_sorted = nullptr;

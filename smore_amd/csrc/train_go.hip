@@ -6,8 +6,8 @@
 //   * UpdatePair (optimizer.go:21-58): negatives equal to the positive are
 //     skipped (not redrawn), negatives update C_n immediately, the positive
 //     context's gradient and W_v's are applied at the end;
-//   * LINE order 1: updateFirstOrder (internal/models/line/line.go:153-200);
-//   * BPR: UpdateBPRPair with W (users) and C (items), lambda (optimizer.go:87-117);
+//   * LINE order 1, BPR: on records, go_rec.h (this file draws them:
+//     go_draw_kernel);
 //   * DeepWalk: walks stop at a dead end, fixed window (pronet.go:292-333);
 //   * node2vec: the biased second-order walk (internal/models/node2vec), then
 //     the DeepWalk pairs;
@@ -118,164 +118,6 @@ __device__ __forceinline__ void go_pair_ctx(const EdgeArgs& a, const float* s_si
 #pragma unroll
     for (int m = 0; m < M; ++m) nc[m] = cc[m] + cg[m];
     put_row<G, M, MODE>(a.C, c, dpad, lane, ev, nc, cg);
-}
-
-// Go UpdatePair on W (vertex) and C (context); negs[] already drawn.
-template <int G, int M, int KMAX, int MODE>
-__device__ __forceinline__ void go_update_pair(const EdgeArgs& a, const float* s_sig, int lane, const bool (&ev)[M],
-                                               int32_t v, int32_t c, const int32_t (&negs)[KMAX], float alpha) {
-    float wv[M], vg[M];
-    load_row<G, M>(wv, a.W, v, a.dpad, lane, ev);
-    go_pair_ctx<G, M, KMAX, MODE>(a, s_sig, lane, ev, wv, vg, c, negs, alpha);
-    float nw[M];
-#pragma unroll
-    for (int m = 0; m < M; ++m) nw[m] = wv[m] + vg[m];
-    put_row<G, M, MODE>(a.W, v, a.dpad, lane, ev, nw, vg);
-}
-
-// Go updateFirstOrder on one table W (source s, target t).
-template <int G, int M, int KMAX, int MODE>
-__device__ __forceinline__ void go_first_order(const EdgeArgs& a, const float* s_sig, int lane, const bool (&ev)[M],
-                                               int32_t s, int32_t t, const int32_t (&negs)[KMAX], float alpha) {
-    const int dpad = a.dpad;
-    float ws[M], wt[M], vg[M], cg[M];
-    load_row<G, M>(ws, a.W, s, dpad, lane, ev);
-    load_row<G, M>(wt, a.W, t, dpad, lane, ev);
-    float rows[KMAX][M];
-#pragma unroll
-    for (int j = 0; j < KMAX; ++j) {
-        const bool use = negs[j] >= 0 && negs[j] != s && negs[j] != t;
-        ld_row<G, M>(rows[j], a.W + (int64_t)(use ? negs[j] : 0) * dpad, lane, ev, use);
-    }
-#pragma unroll
-    for (int j = 1; j < KMAX; ++j)
-#pragma unroll
-        for (int j2 = 0; j2 < j; ++j2)
-            if (negs[j2] == negs[j]) {
-#pragma unroll
-                for (int m = 0; m < M; ++m) rows[j][m] = rows[j2][m];
-            }
-    {
-        const float grad = alpha * (1.0f - fast_sigmoid(dotg<G, M>(ws, wt), s_sig));
-#pragma unroll
-        for (int m = 0; m < M; ++m) { vg[m] = grad * wt[m]; cg[m] = grad * ws[m]; }
-    }
-#pragma unroll
-    for (int j = 0; j < KMAX; ++j) {
-        if (negs[j] < 0 || negs[j] == s || negs[j] == t) continue;
-        const float gr = alpha * (0.0f - fast_sigmoid(dotg<G, M>(ws, rows[j]), s_sig));
-        float nk[M], dk[M];
-#pragma unroll
-        for (int m = 0; m < M; ++m) {
-            vg[m] = vg[m] + gr * rows[j][m];
-            dk[m] = gr * ws[m];
-            nk[m] = rows[j][m] + dk[m];
-        }
-#pragma unroll
-        for (int j2 = j + 1; j2 < KMAX; ++j2)
-            if (negs[j2] == negs[j]) {
-#pragma unroll
-                for (int m = 0; m < M; ++m) rows[j2][m] = nk[m];
-            }
-        bool last = true;
-#pragma unroll
-        for (int j2 = j + 1; j2 < KMAX; ++j2) last = last && negs[j2] != negs[j];
-        if (MODE == MODE_ATOMIC || last) put_row<G, M, MODE>(a.W, negs[j], dpad, lane, ev, nk, dk);
-    }
-    float ns[M], nt[M];
-#pragma unroll
-    for (int m = 0; m < M; ++m) ns[m] = ws[m] + vg[m];
-    if (s == t) {
-#pragma unroll
-        for (int m = 0; m < M; ++m) nt[m] = ns[m] + cg[m];
-        float d2[M];
-#pragma unroll
-        for (int m = 0; m < M; ++m) d2[m] = vg[m] + cg[m];
-        put_row<G, M, MODE>(a.W, s, dpad, lane, ev, nt, d2);
-    } else {
-#pragma unroll
-        for (int m = 0; m < M; ++m) nt[m] = wt[m] + cg[m];
-        put_row<G, M, MODE>(a.W, s, dpad, lane, ev, ns, vg);
-        put_row<G, M, MODE>(a.W, t, dpad, lane, ev, nt, cg);
-    }
-}
-
-// Go UpdateBPRPair: W users (u), C items (i, j).
-template <int G, int M, int MODE>
-__device__ __forceinline__ void go_bpr(const EdgeArgs& a, const float* s_sig, int lane, const bool (&ev)[M], int32_t u,
-                                       int32_t i, int32_t j, float alpha) {
-    const int dpad = a.dpad;
-    float wu[M], ci[M], cj[M];
-    load_row<G, M>(wu, a.W, u, dpad, lane, ev);
-    load_row<G, M>(ci, a.C, i, dpad, lane, ev);
-    load_row<G, M>(cj, a.C, j, dpad, lane, ev);
-    if (i == j) {
-#pragma unroll
-        for (int m = 0; m < M; ++m) cj[m] = ci[m];
-    }
-    const float pos = dotg<G, M>(wu, ci), neg = dotg<G, M>(wu, cj);
-    const float gc = alpha * fast_sigmoid(neg - pos, s_sig);
-    const float la = a.reg * alpha;
-    float nu[M], ni[M], nj[M], du[M], di[M], dj[M];
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-        const float vgr = gc * (ci[m] - cj[m]);
-        const float pg = gc * wu[m];
-        const float ngr = -gc * wu[m];
-        nu[m] = wu[m] + (vgr - la * wu[m]);
-        ni[m] = ci[m] + (pg - la * ci[m]);
-        nj[m] = (i == j ? ni[m] : cj[m]) + (ngr - la * (i == j ? ni[m] : cj[m]));
-        du[m] = nu[m] - wu[m];
-        di[m] = ni[m] - ci[m];
-        dj[m] = nj[m] - (i == j ? ni[m] : cj[m]);
-    }
-    put_row<G, M, MODE>(a.W, u, dpad, lane, ev, nu, du);
-    if (i == j) {
-        float dd[M];
-#pragma unroll
-        for (int m = 0; m < M; ++m) dd[m] = nj[m] - ci[m];
-        put_row<G, M, MODE>(a.C, i, dpad, lane, ev, nj, dd);
-    } else {
-        put_row<G, M, MODE>(a.C, i, dpad, lane, ev, ni, di);
-        put_row<G, M, MODE>(a.C, j, dpad, lane, ev, nj, dj);
-    }
-}
-
-template <int G, int M, int KMAX, int MODE>
-__global__ void __launch_bounds__(256) go_edge_kernel(EdgeArgs a) {
-    __shared__ float s_sig[1001];
-    for (int i = threadIdx.x; i < 1001; i += blockDim.x) s_sig[i] = a.sig[i];
-    __syncthreads();
-    constexpr int NSLOT = 3 + 2 * KMAX;
-    const int lane = threadIdx.x & (G - 1);
-    uint64_t group = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
-    uint64_t ngroups = ((uint64_t)gridDim.x * blockDim.x) / G;
-    if (a.mode == 2) {
-        if (group != 0) return;
-        ngroups = 1;
-    }
-    bool ev[M];
-    row_valid<G, M>(ev, lane, a.dpad);
-    const int nk = a.model == 3 ? 1 : a.K;
-    for (uint64_t t = group; t < a.count; t += ngroups) {
-        const uint64_t s = a.begin + t;
-        SampleWords<G, NSLOT> wd;
-        wd.draw(a.seed, 0, s, lane);
-        const int32_t v = go_alias(a.g.vtab, a.g.V, wd.w[0], wd.w[1]);
-        const int32_t c = go_target(a.g, a.tcum, v, wd.w[2]);
-        if (c < 0) {
-            if (lane == 0) atomicAdd(a.skipped, 1ull);
-            continue;
-        }
-        int32_t negs[KMAX];
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j)
-            negs[j] = j < nk ? go_alias(a.g.ntab, a.g.V, wd.w[3 + 2 * j], wd.w[4 + 2 * j]) : -1;
-        const float alpha = alpha_walk(s, a.alpha0, a.total);
-        if (a.model == 0) go_update_pair<G, M, KMAX, MODE>(a, s_sig, lane, ev, v, c, negs, alpha);
-        else if (a.model == 1) go_first_order<G, M, KMAX, MODE>(a, s_sig, lane, ev, v, c, negs, alpha);
-        else go_bpr<G, M, MODE>(a, s_sig, lane, ev, v, c, negs[0], alpha);
-    }
 }
 
 // Go RandomWalk: stops at a dead end; step s draws slot s (stream 1).
@@ -546,6 +388,87 @@ __global__ void __launch_bounds__(256) go_walk_pairs_kernel(EdgeArgs a, WalkArgs
     }
 }
 
+// Go TargetSample keeping the target's tag (hybrid scatter).  unit_w: every
+// edge weight is 1, so tcum[off + e] == e + 1 exactly and the first e with
+// r <= tcum[off + e] is max(0, ceil(r) - 1) -- the binary search's answer
+// without its reads (r is the same fp64 product as go_target's).
+__device__ __forceinline__ int32_t go_target_tagged(const DevGraph& g, const double* tcum, int32_t v, uint32_t kr,
+                                                    int unit_w) {
+    const int64_t off = g.offsets[v];
+    const int64_t br = g.offsets[v + 1] - off;
+    if (br == 0) return -1;
+    int64_t lo;
+    if (unit_w) {
+        const double r = ldexp((double)kr, -32) * (double)br;
+        lo = (int64_t)ceil(r) - 1;
+        lo = lo < 0 ? 0 : (lo > br - 1 ? br - 1 : lo);
+    } else {
+        const double r = ldexp((double)kr, -32) * tcum[off + br - 1];
+        int64_t hi = br - 1;
+        lo = 0;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (r <= tcum[off + mid]) hi = mid;
+            else lo = mid + 1;
+        }
+    }
+    return g.targets[off + lo];
+}
+
+// The sampling half of the Go edge models (LINE::Train / BPR::Train / HPE
+// loops of internal/models): per sample one record {v, c, n_1 .. n_K, -1 ..}
+// of tagged ids for go_rec_kernel (go_rec.h), Go slot layout (stream 0: 0
+// source index, 1 source p, 2 target, 3 + 2j negative index, 4 + 2j its p).
+// c = -1 when the source has no out-edge (counted in *skipped).
+template <int KMAX>
+__global__ void __launch_bounds__(256) go_draw_kernel(DevGraph g, const double* tcum, int unit_w, uint64_t seed,
+                                                      uint64_t begin, uint64_t count, int K, int32_t* rec,
+                                                      unsigned long long* skipped) {
+    constexpr int RW = rec_width(KMAX);
+    constexpr int NW = 3 + 2 * KMAX;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= count) return;
+    const uint64_t s = begin + t;
+    uint32_t w[(NW + 3) / 4 * 4];
+#pragma unroll
+    for (int b = 0; b < (NW + 3) / 4; ++b) {
+        if (4 * b < 3 + 2 * K) {
+            const uint4 x = philox_block(seed, 0, s, (uint32_t)b);
+            w[4 * b] = x.x; w[4 * b + 1] = x.y; w[4 * b + 2] = x.z; w[4 * b + 3] = x.w;
+        }
+    }
+    const uint32_t vi = draw_index(w[0], g.V);
+    const int32_t v = alias_pick(vi, g.vtab[vi], w[1]);
+    const int32_t c = go_target_tagged(g, tcum, untag(v), w[2], unit_w);
+    int32_t o[RW];
+    o[0] = v;
+    o[1] = c;
+#pragma unroll
+    for (int j = 0; j < RW - 2; ++j) {
+        o[2 + j] = -1;
+        if (j < KMAX && j < K) {
+            const uint32_t ni = draw_index(w[3 + 2 * j], g.V);
+            o[2 + j] = alias_pick(ni, g.ntab[ni], w[4 + 2 * j]);
+        }
+    }
+    i32x4* out = reinterpret_cast<i32x4*>(rec + t * RW);
+#pragma unroll
+    for (int q = 0; q < RW / 4; ++q) __builtin_nontemporal_store(i32x4{o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]}, out + q);
+    if (c < 0) atomicAdd(skipped, 1ull);
+}
+
+hipError_t launch_go_draw(const DevGraph& g, const double* tcum, int unit_w, uint64_t seed, uint64_t begin,
+                          uint64_t count, int K, int32_t* rec, unsigned long long* skipped, hipStream_t st) {
+    const dim3 grid((unsigned)((count + 255) / 256));
+    if (K <= 5)
+        hipLaunchKernelGGL((go_draw_kernel<5>), grid, dim3(256), 0, st, g, tcum, unit_w, seed, begin, count, K, rec,
+                           skipped);
+    else
+        hipLaunchKernelGGL((go_draw_kernel<10>), grid, dim3(256), 0, st, g, tcum, unit_w, seed, begin, count, K, rec,
+                           skipped);
+    return hipGetLastError();
+}
+
 // draws only (parity tests): {v, c, n1..nK} per sample, Go slot layout
 __global__ void go_sample_kernel(DevGraph g, const double* tcum, uint64_t seed, uint64_t begin, uint64_t count, int K,
                                  int32_t* out) {
@@ -579,31 +502,12 @@ hipError_t launch_go_sample(const DevGraph& g, const double* tcum, uint64_t seed
 
 // ------------------------------------------------------------------ dispatch
 template <int G, int M, int KMAX>
-static hipError_t go_edge(const EdgeArgs& a, int grid, hipStream_t st) {
-    if (a.mode == 1) hipLaunchKernelGGL((go_edge_kernel<G, M, KMAX, MODE_ATOMIC>), dim3(grid), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((go_edge_kernel<G, M, KMAX, MODE_STORE>), dim3(grid), dim3(256), 0, st, a);
-    return hipGetLastError();
-}
-
-template <int G, int M, int KMAX>
 static hipError_t go_pairs(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st) {
     if (a.mode == 1)
         hipLaunchKernelGGL((go_walk_pairs_kernel<G, M, KMAX, MODE_ATOMIC>), dim3(grid), dim3(256), 0, st, a, w);
     else
         hipLaunchKernelGGL((go_walk_pairs_kernel<G, M, KMAX, MODE_STORE>), dim3(grid), dim3(256), 0, st, a, w);
     return hipGetLastError();
-}
-
-hipError_t launch_go_edge(const EdgeArgs& a, int grid, hipStream_t st) {
-    const int G = lanes_of(a.dpad), M = regs_of(a.dpad);
-#define X(g, m)                                                  \
-    if (G == g && M == m) {                                      \
-        if (a.K <= 5 || a.model == 3) return go_edge<g, m, 5>(a, grid, st); \
-        return go_edge<g, m, 10>(a, grid, st);                   \
-    }
-    SMORE_FOR_EACH_GM(X)
-#undef X
-    return hipErrorInvalidValue;
 }
 
 hipError_t launch_go_pairs(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st) {

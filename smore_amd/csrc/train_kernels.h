@@ -113,7 +113,15 @@ inline size_t sh_lds_bytes(int sh_rows, int dpad) {
     return sh_rows > 0 ? SH_HASH * 8 + (size_t)sh_rows * 4 + (size_t)sh_rows * dpad * 4 : 0;
 }
 inline uint32_t sh_hash_of(int32_t id) { return ((uint32_t)id * 2654435761u) >> 24; }
-hipError_t launch_go_edge(const EdgeArgs& a, int grid, hipStream_t st);
+// Go edge models on records: go_draw_kernel (train_go.hip; unit_w: every edge
+// weight is 1) then go_rec_kernel (go_rec.h; train_go_rec_<mode>.hip)
+hipError_t launch_go_draw(const DevGraph& g, const double* tcum, int unit_w, uint64_t seed, uint64_t begin,
+                          uint64_t count, int K, int32_t* rec, unsigned long long* skipped, hipStream_t st);
+#define SMORE_DECL_GO_REC(name)                                                  \
+    hipError_t launch_go_rec_##name(const EdgeArgs& a, int grid, hipStream_t st); \
+    const void* go_rec_symbol_##name(const EdgeArgs& a);
+SMORE_DECL_GO_REC(s) SMORE_DECL_GO_REC(a) SMORE_DECL_GO_REC(h)
+#undef SMORE_DECL_GO_REC
 hipError_t launch_go_walk(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st);
 hipError_t launch_go_sample(const DevGraph& g, const double* tcum, uint64_t seed, uint64_t begin, uint64_t count,
                             int K, int32_t* out, hipStream_t st);

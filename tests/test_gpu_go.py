@@ -357,3 +357,44 @@ def test_go_ctdne_model_driver(smore, tmp_path):
     m.SaveEmbeddings(str(out))
     lines = out.read_text().splitlines()
     assert lines[0] == "%d 16" % len(m.names) and len(lines) == len(m.names) + 1
+
+
+def test_go_c2_full_grid_hybrid_matches_atomic(smore):
+    """The Go rules on the record path at full grid (config 2's graph, 2^28
+    samples, d=64, K=5): the hybrid scatter (hot rows by atomic add, the
+    hottest context rows write-combined in LDS) trains like the lossless atomic
+    scatter -- held-out Go LINE-2 loss within 1 % -- and Go BPR's hybrid run on
+    the same graph is finite."""
+    from smore_amd import graphgen
+    V, (src, dst, w) = graphgen.config_edges("c2")
+    pn = smore.ProNet(0)
+    pn.set_graph_edges(V, src, dst, w)
+    pn.set_semantics("go")
+    dim, K, total = 64, 5, 1 << 28
+    held = pn.sample_edges("line2", 1 << 40, 100_000, K, SEED + 1)
+    res = {}
+    for mode in ("atomic", "hybrid"):
+        W0, C0 = [(t / dim).astype(np.float32) for t in tables(V, dim, 5)]
+        pn.alloc_tables(dim, 2)
+        pn.set_table(0, W0)
+        pn.set_table(1, C0)
+        pn.set_hot_threshold(0.3)
+        pn.set_write_combine(128, 0)
+        pn.train_edges("line2", 0, total, total, K, 0.025, 0.0, SEED, mode)
+        W, C = pn.get_table(0), pn.get_table(1)
+        assert np.isfinite(W).all() and np.isfinite(C).all()
+        v, c, negs = held[:, 0], held[:, 1], held[:, 2:]
+        keep = c >= 0
+        v, c, negs = v[keep], c[keep], negs[keep]
+        Wv = W[v].astype(np.float64)
+        loss = np.logaddexp(0.0, -np.einsum("ij,ij->i", Wv, C[c].astype(np.float64)))
+        for k in range(K):
+            loss += np.logaddexp(0.0, np.einsum("ij,ij->i", Wv, C[negs[:, k]].astype(np.float64)))
+        res[mode] = float(loss.mean())
+        if mode == "hybrid":
+            hw, hc = pn.hot_rows()
+            assert hw > 0 and hc > 0, (hw, hc)
+    assert res["atomic"] < 0.9 * np.log(2.0) * (1 + K), res
+    assert abs(res["hybrid"] - res["atomic"]) <= 0.01 * res["atomic"], res
+    pn.train_edges("bpr", 0, 1 << 26, 1 << 26, 1, 0.025, 0.001, SEED, "hybrid")
+    assert np.isfinite(pn.get_table(0)).all() and np.isfinite(pn.get_table(1)).all()
