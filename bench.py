@@ -63,7 +63,13 @@ def parse():
     ap.add_argument("--combine-flush", type=int, default=0, help="hybrid: rounds between LDS drains (0: automatic)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
     ap.add_argument("--sync-every", type=int, default=1)
-    ap.add_argument("--sync", default="sum", choices=["sum", "mean"])
+    ap.add_argument("--sync", default="mean", choices=["sum", "mean"],
+                    help="N > 1: average the replicas' deltas (default; stable) or sum them (every update applied "
+                         "once; diverges at >= 4 ranks at this exchange period, DESIGN.md 10)")
+    ap.add_argument("--hot-rows", type=int, default=65536,
+                    help="N > 1, --sync sum: hub rows per table exchanged after every launch")
+    ap.add_argument("--launches", type=int, default=8,
+                    help="N > 1: training launches per step, each followed by the hub-row exchange")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=20251015)
@@ -177,14 +183,28 @@ def main():
     stream = torch.cuda.Stream()             # a real stream: the default one is the null stream
     torch.cuda.set_stream(stream)
     pn.set_stream(stream.cuda_stream)
-    sync = ReplicaSync(pn, mean=(args.sync == "mean")) if world > 1 else None
+    sync = (ReplicaSync(pn, mean=(args.sync == "mean"), hot_rows=args.hot_rows, model="line2", K=args.negative)
+            if world > 1 else None)
+    n_launch = max(1, args.launches) if (sync is not None and sync.hot_idx) else 1
+    phase = [0.0, 0.0, 0]     # exposed draw ms, update ms, update launches (timed steps)
 
     S, K = args.samples, args.negative
     total = (args.warmup + args.steps) * S * world     # alpha schedule over the whole job
 
-    def step(k):
+    def step(k, timed=False):
         begin = (k * world + rank) * S
-        pn.train_edges("line2", begin, S, total, K, 0.025, 0.0, args.seed, args.mode, sync=False)
+        sub = S // n_launch
+        for j in range(n_launch):
+            n = sub if j + 1 < n_launch else S - j * sub
+            pn.train_edges("line2", begin + j * sub, n, total, K, 0.025, 0.0, args.seed, args.mode, sync=False)
+            if timed:
+                ph = pn.last_phase_ms()      # waits for this launch's events (a few us of host gap)
+                if ph is not None:
+                    phase[0] += ph[0]
+                    phase[1] += ph[1]
+                    phase[2] += ph[2]
+            if n_launch > 1:
+                sync.hot()    # the hub rows of every rank, synchronously
         if sync is not None and (k + 1) % args.sync_every == 0:
             sync.begin()      # folds the previous exchange in; this one overlaps the next step
 
@@ -199,15 +219,9 @@ def main():
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    draw_ms = upd_ms = 0.0
-    launches = 0
     for k in range(args.warmup, args.warmup + args.steps):
-        step(k)
-        ph = pn.last_phase_ms()      # waits for this step's events (a few us of host gap)
-        if ph is not None:
-            draw_ms += ph[0]
-            upd_ms += ph[1]
-            launches += ph[2]
+        step(k, timed=True)
+    draw_ms, upd_ms, launches = phase
     if sync is not None:
         sync.end()            # the last exchange lands inside the timed region
     ev1.record(stream)
@@ -269,7 +283,10 @@ def main():
                                    % (args.config, "" if args.semantics == "cpp" else ", Go rules (pkg/pronet)"),
                        "vertices": V, "edge_slots": E, "dim": args.dim, "negative": K,
                        "samples_per_step_per_gpu": S, "scatter": args.mode,
-                       "sync": ("%s every %d steps" % (args.sync, args.sync_every)) if world > 1 else "none",
+                       "sync": ("%s every %d steps%s" % (args.sync, args.sync_every,
+                                                           ", %d hub rows per table after each of %d launches per step"
+                                                           % (args.hot_rows, n_launch) if n_launch > 1 else ""))
+                               if world > 1 else "none",
                        "parallelism": "replicas%d" % world},
             # achieved = updates/s x 1868 B (the whole path's algorithmic
             # reads) over the 8 TB/s HBM read roofline; the dominant kernel's own

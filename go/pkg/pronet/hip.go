@@ -49,26 +49,38 @@ const (
 	HIPBPR   = int(C.SMORE_BPR)   // UpdateBPRPair(W, C, λ) -- BPR
 )
 
-// HIP scatter modes: Hogwild plain stores, float atomics (lossless; the default
-// for Go callers), strict serial order (parity runs).
+// HIP scatter modes: hybrid (the default: atomic adds for the hub rows, the
+// hottest write-combined in LDS, plain stores for the rest; trains like the
+// lossless atomic mode), Hogwild plain stores, float atomics, strict serial
+// order (parity runs).
 const (
+	HIPHybrid  = int(C.SMORE_HYBRID)
 	HIPHogwild = int(C.SMORE_HOGWILD)
 	HIPAtomic  = int(C.SMORE_ATOMIC)
 	HIPSerial  = int(C.SMORE_SERIAL)
 )
 
+func (h *HIP) mean() C.int {
+	if h.cfg.Sum {
+		return 0
+	}
+	return 1
+}
+
 // HIPConfig selects the GPUs and the scatter mode of a run.
 type HIPConfig struct {
 	Device int    // first GPU
 	GPUs   int    // replicas on Device .. Device+GPUs-1 (tables all-reduced over RCCL)
-	Mode   int    // HIPAtomic unless set
+	Mode   int    // HIPHybrid unless set
 	Seed   uint64 // Philox seed of the draws
+	Sum    bool   // GPUs > 1: sum the replicas' deltas instead of averaging them (diverges at >= 4 GPUs)
 }
 
 // HIPConfigFromEnv reads SMORE_HIP_DEVICE, SMORE_HIP_GPUS, SMORE_HIP_MODE
-// (hogwild|atomic|serial) and SMORE_HIP_SEED; defaults 0, 1, atomic, seed.
+// (hybrid|atomic|hogwild|serial), SMORE_HIP_SEED and SMORE_SYNC (mean|sum);
+// defaults 0, 1, hybrid, seed, mean.
 func HIPConfigFromEnv(seed uint64) HIPConfig {
-	c := HIPConfig{Device: 0, GPUs: 1, Mode: HIPAtomic, Seed: seed}
+	c := HIPConfig{Device: 0, GPUs: 1, Mode: HIPHybrid, Seed: seed}
 	if v, err := strconv.Atoi(os.Getenv("SMORE_HIP_DEVICE")); err == nil {
 		c.Device = v
 	}
@@ -78,9 +90,12 @@ func HIPConfigFromEnv(seed uint64) HIPConfig {
 	switch os.Getenv("SMORE_HIP_MODE") {
 	case "hogwild":
 		c.Mode = HIPHogwild
+	case "atomic":
+		c.Mode = HIPAtomic
 	case "serial":
 		c.Mode = HIPSerial
 	}
+	c.Sum = os.Getenv("SMORE_SYNC") == "sum"
 	if v, err := strconv.ParseUint(os.Getenv("SMORE_HIP_SEED"), 10, 64); err == nil {
 		c.Seed = v
 	}
@@ -317,7 +332,7 @@ func (h *HIP) TrainEdges(model int, w, c [][]float64, dim int, total uint64, K i
 			n = step
 		}
 		if rc := C.smore_group_train_edges(h.group, C.int(model), C.uint64_t(done), C.uint64_t(n), C.uint64_t(total),
-			C.int(K), C.double(alpha), C.double(lambda), C.uint64_t(h.cfg.Seed), C.int(h.cfg.Mode), 0, 0); rc != C.SMORE_OK {
+			C.int(K), C.double(alpha), C.double(lambda), C.uint64_t(h.cfg.Seed), C.int(h.cfg.Mode), 0, h.mean()); rc != C.SMORE_OK {
 			return h.err("smore_group_train_edges")
 		}
 		done += n
@@ -374,7 +389,7 @@ func (h *HIP) TrainDeepWalk(w, c [][]float64, dim int, order []int64, walkTimes,
 	return h.trainWalks(w, c, dim, order, "smore_group_train_deepwalk", func(done, n uint64, ord *C.int64_t) C.int {
 		return C.smore_group_train_deepwalk(h.group, C.uint64_t(done), C.uint64_t(done+n), C.int(walkTimes),
 			C.int(walkSteps), C.int(window), C.int(K), C.double(alpha), C.uint64_t(h.cfg.Seed), ord,
-			C.int(h.cfg.Mode), 0, 0)
+			C.int(h.cfg.Mode), 0, h.mean())
 	}, progress)
 }
 
@@ -386,7 +401,7 @@ func (h *HIP) TrainNode2Vec(w, c [][]float64, dim int, order []int64, walkTimes,
 	return h.trainWalks(w, c, dim, order, "smore_group_train_node2vec", func(done, n uint64, ord *C.int64_t) C.int {
 		return C.smore_group_train_node2vec(h.group, C.uint64_t(done), C.uint64_t(done+n), C.int(walkTimes),
 			C.int(walkSteps), C.int(window), C.int(K), C.double(alpha), C.double(p), C.double(q),
-			C.uint64_t(h.cfg.Seed), ord, C.int(h.cfg.Mode), 0, 0)
+			C.uint64_t(h.cfg.Seed), ord, C.int(h.cfg.Mode), 0, h.mean())
 	}, progress)
 }
 
@@ -419,7 +434,7 @@ func (h *HIP) TrainMetapath2Vec(w, c [][]float64, dim int, order []int64, metaPa
 	return h.trainWalks(w, c, dim, order, "smore_group_train_metapath2vec", func(done, n uint64, ord *C.int64_t) C.int {
 		return C.smore_group_train_metapath2vec(h.group, C.uint64_t(done), C.uint64_t(done+n), C.int(walkTimes),
 			C.int(walkSteps), C.int(window), C.int(K), C.double(alpha), &paths[0], &lens[0], C.int(np),
-			C.uint64_t(h.cfg.Seed), ord, C.int(h.cfg.Mode), 0, 0)
+			C.uint64_t(h.cfg.Seed), ord, C.int(h.cfg.Mode), 0, h.mean())
 	}, progress)
 }
 
@@ -433,6 +448,6 @@ func (h *HIP) TrainCTDNE(w, c [][]float64, dim int, order []int64, walkTimes, wa
 	return h.trainWalks(w, c, dim, order, "smore_group_train_ctdne", func(done, n uint64, ord *C.int64_t) C.int {
 		return C.smore_group_train_ctdne(h.group, C.uint64_t(done), C.uint64_t(done+n), C.int(walkTimes),
 			C.int(walkSteps), C.int(window), C.int(K), C.double(alpha), C.double(timeWindow),
-			C.uint64_t(h.cfg.Seed), ord, C.int(h.cfg.Mode), 0, 0)
+			C.uint64_t(h.cfg.Seed), ord, C.int(h.cfg.Mode), 0, h.mean())
 	}, progress)
 }

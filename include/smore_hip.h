@@ -187,6 +187,11 @@ int smore_set_write_combine(smore_ctx* ctx, int rows, int flush_rounds);
 /* the combined rows and the drain interval the last hybrid launch used */
 int smore_write_combine_info(const smore_ctx* ctx, int* rows, int* flush_rounds);
 int smore_hot_rows(const smore_ctx* ctx, int64_t* hot_w, int64_t* hot_c);
+/* multi-GPU: the n rows of table `which` (0 = W, 1 = C) with
+ * the highest expected touches per sample of `model` with K negatives (the
+ * sampler marginals of the context's graph), highest first: the hub rows the
+ * replica exchange also syncs after every launch (smore_hot_exchange) */
+int smore_hot_row_ids(smore_ctx* ctx, int model, int K, int which, int64_t n, int32_t* ids);
 /* samples whose source had no out-edge (reference: TargetSample -> -1) */
 int smore_skipped(smore_ctx* ctx, uint64_t* skipped);
 /* milliseconds of the last training launch (HIP events on the launch stream) */
@@ -252,6 +257,12 @@ typedef struct smore_group smore_group;
 int smore_group_create(const int* devices, int n, smore_group** out);
 void smore_group_destroy(smore_group* g);
 int smore_group_size(const smore_group* g);
+/* the hub-row exchange of the sum exchange: each replica's
+ * share of an exchange round runs as `launches` training launches, and after
+ * each the `rows` hub rows per table (smore_hot_row_ids) are all-reduced
+ * synchronously.  rows -1 = automatic (min(65536, V/8), the default), 0 = off
+ * (then one launch per round); launches >= 1 (default 8). */
+int smore_group_set_hot_exchange(smore_group* g, int64_t rows, int launches);
 smore_ctx* smore_group_ctx(smore_group* g, int rank);
 const char* smore_group_last_error(const smore_group* g);
 int smore_group_load_edgelist(smore_group* g, const char* path, int undirected, int vertex_method,

@@ -61,6 +61,8 @@ def _load():
         "smore_write_combine_info": (i32, [P, C.POINTER(i32), C.POINTER(i32)]),
         "smore_gen_powerlaw": (i32, [i64, i64, i32, dbl, u64, P, P]),
         "smore_hot_rows": (i32, [P, C.POINTER(i64), C.POINTER(i64)]),
+        "smore_hot_row_ids": (i32, [P, i32, i32, i32, i64, P]),
+        "smore_group_set_hot_exchange": (i32, [P, i64, i32]),
         "smore_last_kernel_ms": (C.c_float, [P]),
         "smore_copy_bandwidth": (i32, [P, u64, i32, C.POINTER(C.c_double)]),
         "smore_last_phase_ms": (i32, [P, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(i32)]),

@@ -374,6 +374,11 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
             // M * p * sh_flush updates; rows above SH_STALE_MAX stay on atomics
             // (on small graphs that is every hot row)
             if (hc[v] && (double)M * p * flush_cap <= stale_max) r.push_back({p, (int32_t)v});
+            // two tables: the hub W rows compete for the same slots (key
+            // v | SH_WKEY) -- the Go source law (out_degree^1) puts ~1 % of
+            // all samples on one W row
+            if (model == SMORE_LINE2 && hw[v] && (double)M * ps[v] * flush_cap <= stale_max)
+                r.push_back({ps[v], (int32_t)(v | SH_WKEY)});
         }
         const int64_t cap = std::max<int64_t>(0, std::min<int64_t>(c->sh_max, 8192 / std::max(1, c->dpad)));
         const int64_t n = std::min<int64_t>(cap, (int64_t)r.size());
@@ -586,7 +591,7 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
     };
     if ((rc = grow(c->phase_ev, 2 * (size_t)nch + 1))) return rc;
     if ((rc = grow(c->sync_ev, 2 * (size_t)nch))) return rc;
-    if (!go && (rc = ensure_packed(c))) return rc;
+    if ((rc = ensure_packed(c))) return rc;
     const DevGraph dg = dev_graph(c);
     const int ugrid = nch > 1 ? edge_grid(c, a, true, go) : grid;
     hipStream_t ds = nch > 1 ? c->draw_stream : c->stream;
@@ -694,6 +699,32 @@ int smore_write_combine_info(const smore_ctx* c, int* rows, int* flush_rounds) {
     if (!c) return SMORE_EINVAL;
     if (rows) *rows = c->sh_rows;
     if (flush_rounds) *flush_rounds = c->sh_flush_eff;
+    return SMORE_OK;
+}
+
+// the n rows of table `which` (0: W, 1: C) with the highest expected touches
+// per sample under the context's samplers and the model's row roles (LINE-2 /
+// Go BPR: W = sources, C = contexts + K x negatives; one-table models: the
+// union), highest first -- the rows the replica exchange syncs every launch
+int smore_hot_row_ids(smore_ctx* c, int model, int K, int which, int64_t n, int32_t* ids) {
+    if (!c || !ids || n < 0 || which < 0 || which > 1 || model < 0 || model > 3 || K < 0)
+        return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    const int64_t V = c->g->V;
+    if (n > V) return fail(c, SMORE_EINVAL, "more hot rows than vertices");
+    std::vector<double> ps, pn, pc;
+    draw_probabilities(*c->g, ps, pn, pc);
+    const bool two = model == SMORE_LINE2 || (model == SMORE_BPR && c->semantics == SMORE_SEM_GO);
+    const int negs = model == SMORE_BPR ? (c->semantics == SMORE_SEM_GO ? 1 : 5) : K;
+    std::vector<double> rate((size_t)V);
+    for (int64_t v = 0; v < V; ++v)
+        rate[v] = two ? (which == 0 ? ps[v] : pc[v] + negs * pn[v]) : ps[v] + pc[v] + negs * pn[v];
+    std::vector<int32_t> order((size_t)V);
+    for (int64_t v = 0; v < V; ++v) order[v] = (int32_t)v;
+    std::partial_sort(order.begin(), order.begin() + n, order.end(), [&](int32_t a, int32_t b) {
+        return rate[a] > rate[b] || (rate[a] == rate[b] && a < b);
+    });
+    std::copy(order.begin(), order.begin() + n, ids);
     return SMORE_OK;
 }
 
@@ -1011,7 +1042,13 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
     a.begin = 0; a.count = 0; a.total = total; a.seed = seed; a.alpha0 = alpha0; a.reg = 0.0f;
     a.dpad = c->dpad; a.K = K; a.model = SMORE_LINE2; a.mode = mode;
     a.tcum = c->d_tcum;
-    if (c->semantics == SMORE_SEM_GO && mode == SMORE_HYBRID) return fail(c, SMORE_EINVAL, "Go semantics: no hybrid");
+    // the Go walk models' pair kernel (train_go.hip go_walk_pairs_kernel)
+    // keeps W_v in registers over a walk position's run and adds it back; its
+    // context rows take the lossless atomic scatter when hybrid is asked for
+    if (c->semantics == SMORE_SEM_GO && mode == SMORE_HYBRID) {
+        mode = SMORE_ATOMIC;
+        a.mode = mode;
+    }
     const int grid = mode != SMORE_SERIAL ? c->cus * 4 : 1;   // Go walk kernel (as the Go edge path)
     EdgeArgs ar = a;   // the update kernel over pair records (C++ semantics)
     int ugrid = 1;
@@ -1301,7 +1338,7 @@ int smore_train_hpe_async(smore_ctx* c, uint64_t begin, uint64_t count, uint64_t
     if (!c) return SMORE_EINVAL;
     if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
     if (c->ntables < 2) return fail(c, SMORE_ESTATE, "HPE needs W and C tables");
-    if (c->semantics == SMORE_SEM_GO) return fail(c, SMORE_EINVAL, "HPE has no Go semantics in this build");
+    if (c->semantics == SMORE_SEM_GO) return fail(c, SMORE_EINVAL, "HPE in Go semantics is the Go LINE-2 rule (internal/models/hpe/hpe.go:72-124): smore_train_edges with SMORE_LINE2");
     if (walk_steps < 1 || walk_steps > 4096 || K < 0 || K > 10 || mode < 0 || mode > 3 || total == 0)
         return fail(c, SMORE_EINVAL, "bad HPE arguments");
     if (count == 0) return SMORE_OK;

@@ -60,7 +60,7 @@ int main(int argc, char** argv) {
         uint64_t e = b + chunk < units ? b + chunk : units;
         if (run.g)
             SMORE_RUN_CHECK(run, smore_group_train_app(run.g, b, e, walk_times, sample_times, jump, negative_samples,
-                                                       init_alpha, seed, order.data(), mode, 0, 0));
+                                                       init_alpha, seed, order.data(), mode, 0, run.mean));
         else
             SMORE_RUN_CHECK(run, smore_train_app(ctx, b, e, walk_times, sample_times, jump, negative_samples,
                                                  init_alpha, seed, order.data(), mode));

@@ -53,6 +53,11 @@ static smore_ctx* open_context(int device) {
 struct Run {
     smore_group* g = nullptr;
     smore_ctx* ctx = nullptr;
+    // -gpus N: the replicas' exchange averages their deltas (SMORE_SYNC=mean,
+    // the default) or sums them (SMORE_SYNC=sum: every update applied once,
+    // with the hub rows synced between launches; it diverges at 4 and more
+    // replicas at the default exchange period)
+    int mean = 1;
 };
 
 static Run open_run(int device, int gpus) {
@@ -68,6 +73,7 @@ static Run open_run(int device, int gpus) {
         exit(2);
     }
     r.ctx = smore_group_ctx(r.g, 0);
+    if (const char* e = getenv("SMORE_SYNC")) r.mean = strcmp(e, "sum") != 0;
     return r;
 }
 
@@ -117,7 +123,7 @@ static void train_chunks(Run& r, int model, unsigned long long total, unsigned l
     const unsigned long long chunk = (1ull << 26) * (unsigned long long)gpus;
     for (unsigned long long done = 0; done < n;) {
         unsigned long long c = n - done < chunk ? n - done : chunk;
-        if (r.g) SMORE_RUN_CHECK(r, smore_group_train_edges(r.g, model, done, c, total, K, alpha, reg, seed, mode, 0, 0));
+        if (r.g) SMORE_RUN_CHECK(r, smore_group_train_edges(r.g, model, done, c, total, K, alpha, reg, seed, mode, 0, r.mean));
         else SMORE_RUN_CHECK(r, smore_train_edges(r.ctx, model, done, c, total, K, alpha, reg, seed, mode));
         done += c;
         printf("\tProgress: %.3f %%%c", (double)done / total * 100, 13);

@@ -65,7 +65,7 @@ int main(int argc, char** argv) {
         uint64_t e = b + chunk < total ? b + chunk : total;
         if (run.g)
             SMORE_RUN_CHECK(run, smore_group_train_deepwalk(run.g, b, e, walk_times, walk_steps, window_size,
-                                                            negative_samples, init_alpha, seed, order.data(), mode, 0, 0));
+                                                            negative_samples, init_alpha, seed, order.data(), mode, 0, run.mean));
         else
             SMORE_RUN_CHECK(run, smore_train_deepwalk(ctx, b, e, walk_times, walk_steps, window_size, negative_samples,
                                                       init_alpha, seed, order.data(), mode));

@@ -62,7 +62,7 @@ int main(int argc, char** argv) {
         uint64_t n = b + chunk < total ? chunk : total - b;
         if (run.g)
             SMORE_RUN_CHECK(run, smore_group_train_hpe(run.g, b, n, total, walk_steps, negative_samples, reg,
-                                                       init_alpha, seed, mode, 0, 0));
+                                                       init_alpha, seed, mode, 0, run.mean));
         else
             SMORE_RUN_CHECK(run, smore_train_hpe(ctx, b, n, total, walk_steps, negative_samples, reg, init_alpha,
                                                  seed, mode));

@@ -56,7 +56,7 @@ int main(int argc, char** argv) {
         uint64_t e = b + chunk < total ? b + chunk : total;
         if (run.g)
             SMORE_RUN_CHECK(run, smore_group_train_walklets(run.g, b, e, walk_times, walk_steps, window_min, window_max,
-                                                            negative_samples, init_alpha, seed, mode, 0, 0));
+                                                            negative_samples, init_alpha, seed, mode, 0, run.mean));
         else
             SMORE_RUN_CHECK(run, smore_train_walklets(ctx, b, e, walk_times, walk_steps, window_min, window_max,
                                                       negative_samples, init_alpha, seed, mode));

@@ -114,6 +114,12 @@ struct smore_ctx {
     int ex_tables = 0;
     bool ex_pending = false;            // an all-reduce is in flight
     int ex_mean = 0;
+    // hub-row exchange between launches (hot_exchange.h): row ids and the
+    // packed own-delta / all-reduced buffers per table
+    int32_t* hot_idx[2] = {nullptr, nullptr};
+    float* hot_buf[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};   // [table][P, R]
+    int64_t hot_n = 0;
+    std::string hot_ex_key;
 };
 
 // exchange.cpp: frees the exchange buffers and the communicator

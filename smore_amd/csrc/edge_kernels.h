@@ -205,8 +205,9 @@ __device__ __forceinline__ void sgd_update_rows(const EdgeArgs& a, const float* 
                         if (ev[m]) rows[k][m] += pp[elem_off<G>(lane, m)];
                 }
             }
-            if (shared && hotw) {
-                slotw = sh_lookup(sh.hash, v);
+            if (hotw) {
+                // W rows of two-table models are combined too (key v | SH_WKEY)
+                slotw = sh_lookup(sh.hash, shared ? v : (v | SH_WKEY));
                 if (slotw >= 0) {
                     const float* pp = sh.pend + slotw * dpad;
 #pragma unroll
@@ -487,8 +488,9 @@ __device__ __forceinline__ ShState block_setup(const EdgeArgs& a, float* s_sig, 
 // Wave w of the block drains its share of the pending rows with an LDS
 // exchange (read-and-zero in one atomic), so there is no workgroup barrier:
 // an LDS add racing with the drain lands either in this drain or in the
-// wave's next one, never lost.
-__device__ __forceinline__ void sh_drain(const ShState& sh, const int32_t* sh_ids, float* Tc, int dpad) {
+// wave's next one, never lost.  A slot's key is a Tc row id, or (two-table
+// models) a Tw row id | SH_WKEY.
+__device__ __forceinline__ void sh_drain(const ShState& sh, const int32_t* sh_ids, float* Tw, float* Tc, int dpad) {
     const int nwaves = blockDim.x / 64, wave = threadIdx.x / 64;
     const int n = sh.n * dpad;
     const int per = (n + nwaves - 1) / nwaves;
@@ -497,7 +499,9 @@ __device__ __forceinline__ void sh_drain(const ShState& sh, const int32_t* sh_id
         const float x = atomicExch(&sh.pend[i], 0.0f);
         if (x != 0.0f) {
             const int s = i / dpad, e = i - s * dpad;
-            unsafeAtomicAdd(Tc + (int64_t)sh_ids[s] * dpad + e, x);
+            const int32_t key = sh_ids[s];
+            float* const T = (key & SH_WKEY) ? Tw : Tc;
+            unsafeAtomicAdd(T + (int64_t)(key & ~SH_WKEY) * dpad + e, x);
         }
     }
 }
@@ -530,7 +534,7 @@ edge_train_kernel(EdgeArgs a) {
     float* const Tc = a.C;
 
     // pending super-hot deltas -> HBM (sh_drain)
-    auto drain = [&]() { sh_drain(sh, sh_ids, Tc, a.dpad); };
+    auto drain = [&]() { sh_drain(sh, sh_ids, a.W, Tc, a.dpad); };
     auto flush = [&]() {   // end of the kernel: every wave is done adding
         __syncthreads();
         drain();
@@ -812,7 +816,7 @@ pair_train_kernel(EdgeArgs a) {
                                                               false, sh, wv, rows, tv < 0);
             if constexpr (MODE == MODE_HYBRID) {
                 if (sh.n > 0 && ++round == (uint32_t)a.sh_flush) {
-                    sh_drain(sh, sh_ids, a.C, a.dpad);
+                    sh_drain(sh, sh_ids, a.W, a.C, a.dpad);
                     round = 0;
                 }
             }
@@ -822,7 +826,7 @@ pair_train_kernel(EdgeArgs a) {
     if constexpr (MODE == MODE_HYBRID) {
         if (sh.n > 0) {
             __syncthreads();
-            sh_drain(sh, sh_ids, a.C, a.dpad);
+            sh_drain(sh, sh_ids, a.W, a.C, a.dpad);
         }
     }
 }

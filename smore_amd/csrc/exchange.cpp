@@ -26,6 +26,7 @@
 #include <mutex>
 
 #include "ctx.h"
+#include "hot_exchange.h"
 
 using namespace smore_host;
 
@@ -189,6 +190,13 @@ void smore_exchange_release(smore_ctx* c) {
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
     for (auto& t : c->ex_buf)
         for (float*& p : t) dfree(p);
+    for (int t = 0; t < 2; ++t) {
+        dfree(c->hot_idx[t]);
+        dfree(c->hot_buf[t][0]);
+        dfree(c->hot_buf[t][1]);
+    }
+    c->hot_n = 0;
+    c->hot_ex_key.clear();
     if (c->comm && c->own_comm) {
         if (Rccl* L = rccl()) (void)L->destroy((ncclComm_t)c->comm);
     }
@@ -204,6 +212,10 @@ struct smore_group {
     std::vector<smore_ctx*> ctx;
     std::vector<ncclComm_t> comms;
     std::string err;
+    // hub-row exchange (smore_group_set_hot_exchange): rows per table (-1:
+    // automatic, 0: off) and training launches per exchange round
+    int64_t hot_rows = -1;
+    int launches = 8;
 };
 
 namespace {
@@ -247,6 +259,73 @@ int group_exchange_begin(smore_group* g, int mean) {
     return SMORE_OK;
 }
 
+// the hub rows of every replica (replica 0's host graph: all replicas share it)
+int ensure_hot(smore_group* g, int model, int K, int64_t rows) {
+    smore_ctx* c0 = g->ctx[0];
+    const std::string key = std::to_string(model) + "/" + std::to_string(K) + "/" + std::to_string(rows) + "/" +
+                            std::to_string(c0->dpad) + "/" + std::to_string(c0->ntables);
+    if (c0->hot_ex_key == key) return SMORE_OK;
+    std::vector<int32_t> ids[2];
+    for (int t = 0; t < c0->ntables; ++t) {
+        ids[t].resize((size_t)rows);
+        int rc = smore_hot_row_ids(c0, model, K, t, rows, ids[t].data());
+        if (rc) return gfail(g, 0, rc);
+    }
+    for (size_t r = 0; r < g->ctx.size(); ++r) {
+        smore_ctx* c = g->ctx[r];
+        int rc;
+        if ((rc = set_device(c))) return gfail(g, (int)r, rc);
+        for (int t = 0; t < 2; ++t) {
+            dfree(c->hot_idx[t]);
+            dfree(c->hot_buf[t][0]);
+            dfree(c->hot_buf[t][1]);
+        }
+        for (int t = 0; t < c->ntables; ++t) {
+            if ((rc = upload(c, c->hot_idx[t], ids[t].data(), ids[t].size()))) return gfail(g, (int)r, rc);
+            for (float*& p : c->hot_buf[t])
+                if (hipMalloc((void**)&p, (size_t)rows * c->dpad * sizeof(float)) != hipSuccess)
+                    return gfail(g, (int)r, fail(c, SMORE_EHIP, "hub-row exchange buffers"));
+        }
+        c->hot_n = rows;
+        c->hot_ex_key = key;
+    }
+    return SMORE_OK;
+}
+
+// the synchronous hub-row exchange on every replica's compute stream
+int group_hot_exchange(smore_group* g) {
+    int rc;
+    for (size_t r = 0; r < g->ctx.size(); ++r) {
+        smore_ctx* c = g->ctx[r];
+        if ((rc = set_device(c))) return gfail(g, (int)r, rc);
+        for (int t = 0; t < c->ntables; ++t)
+            if (launch_hot_pack(c->d_table[t], c->ex_buf[t][0], c->hot_idx[t], (uint64_t)c->hot_n, c->dpad,
+                                c->hot_buf[t][0], c->hot_buf[t][1], c->cus, c->stream) != hipSuccess)
+                return gfail(g, (int)r, fail(c, SMORE_EHIP, "hot_pack"));
+    }
+    Rccl* L = rccl();
+    ncclResult_t nr = L->group_start();
+    for (size_t r = 0; r < g->ctx.size() && nr == ncclSuccess; ++r) {
+        smore_ctx* c = g->ctx[r];
+        (void)hipSetDevice(c->device);
+        for (int t = 0; t < c->ntables && nr == ncclSuccess; ++t)
+            nr = L->all_reduce(c->hot_buf[t][1], c->hot_buf[t][1], (size_t)c->hot_n * c->dpad, ncclFloat32, ncclSum,
+                               (ncclComm_t)c->comm, c->stream);
+    }
+    ncclResult_t ne = L->group_end();
+    if (nr == ncclSuccess) nr = ne;
+    if (nr != ncclSuccess) return gfail(g, 0, nccl_fail(g->ctx[0], "hub-row ncclAllReduce", nr));
+    for (size_t r = 0; r < g->ctx.size(); ++r) {
+        smore_ctx* c = g->ctx[r];
+        if ((rc = set_device(c))) return gfail(g, (int)r, rc);
+        for (int t = 0; t < c->ntables; ++t)
+            if (launch_hot_unpack(c->d_table[t], c->ex_buf[t][0], c->hot_idx[t], (uint64_t)c->hot_n, c->dpad,
+                                  c->hot_buf[t][0], c->hot_buf[t][1], c->cus, c->stream) != hipSuccess)
+                return gfail(g, (int)r, fail(c, SMORE_EHIP, "hot_unpack"));
+    }
+    return SMORE_OK;
+}
+
 int group_sync(smore_group* g) {
     int rc;
     for (size_t r = 0; r < g->ctx.size(); ++r)
@@ -259,21 +338,34 @@ int group_sync(smore_group* g) {
 // The group training round structure: round k, replica r queues units
 // [begin + (k n + r) per, + per) of the global range on its stream (run(ctx, b, e)
 // must not synchronize), then the group folds the previous exchange in and
-// starts this round's all-reduce, which overlaps round k+1
+// starts this round's all-reduce, which overlaps round k+1.  With the hub-row
+// exchange on (sum exchange, hub rows of `model` with K negatives), each
+// replica's share of a round runs as g->launches launches and the hub rows are
+// synced after each.
 template <class F>
-static int group_rounds(smore_group* g, uint64_t begin, uint64_t end, uint64_t per, int mean, F&& run) {
+static int group_rounds(smore_group* g, uint64_t begin, uint64_t end, uint64_t per, int mean, F&& run,
+                        int model = SMORE_LINE2, int K = 5) {
     const size_t n = g->ctx.size();
     int rc;
     if (end <= begin) return SMORE_OK;
     for (size_t r = 0; r < n; ++r)
         if ((rc = exchange_reset(g->ctx[r]))) return gfail(g, (int)r, rc);
+    int64_t rows = g->hot_rows < 0 ? std::min<int64_t>(65536, g->ctx[0]->g->V / 8) : g->hot_rows;
+    rows = std::min<int64_t>(rows, g->ctx[0]->g->V);
+    const bool hot = !mean && rows > 0 && g->launches > 1;
+    if (hot && (rc = ensure_hot(g, model, K, rows))) return rc;
+    const int sub = hot ? g->launches : 1;
     const uint64_t count = end - begin;
     for (uint64_t base = 0; base < count; base += per * n) {
-        for (size_t r = 0; r < n; ++r) {
-            const uint64_t b = base + r * per;
-            if (b >= count) break;
-            const uint64_t m = std::min<uint64_t>(per, count - b);
-            if ((rc = run(g->ctx[r], begin + b, begin + b + m))) return gfail(g, (int)r, rc);
+        for (int j = 0; j < sub; ++j) {
+            for (size_t r = 0; r < n; ++r) {
+                const uint64_t b = base + r * per;
+                if (b >= count) break;
+                const uint64_t m = std::min<uint64_t>(per, count - b);
+                const uint64_t lo = b + m * (uint64_t)j / sub, hi = b + m * (uint64_t)(j + 1) / sub;
+                if (hi > lo && (rc = run(g->ctx[r], begin + lo, begin + hi))) return gfail(g, (int)r, rc);
+            }
+            if (hot && (rc = group_hot_exchange(g))) return rc;
         }
         if ((rc = group_exchange_begin(g, mean))) return rc;
     }
@@ -374,6 +466,13 @@ void smore_group_destroy(smore_group* g) {
 }
 
 int smore_group_size(const smore_group* g) { return g ? (int)g->ctx.size() : 0; }
+
+int smore_group_set_hot_exchange(smore_group* g, int64_t rows, int launches) {
+    if (!g || launches < 1) return SMORE_EINVAL;
+    g->hot_rows = rows < 0 ? -1 : rows;
+    g->launches = launches;
+    return SMORE_OK;
+}
 
 smore_ctx* smore_group_ctx(smore_group* g, int rank) {
     if (!g || rank < 0 || rank >= (int)g->ctx.size()) return nullptr;
@@ -478,7 +577,8 @@ int smore_group_train_edges(smore_group* g, int model, uint64_t begin, uint64_t 
     return group_rounds(g, begin, begin + count, sync_samples ? sync_samples : (uint64_t)1 << 27, mean,
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_edges_async(c, model, b, e - b, total, K, alpha0, reg, seed, mode);
-                        });
+                        },
+                        model, K);
 }
 
 int smore_group_train_deepwalk(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
@@ -492,7 +592,8 @@ int smore_group_train_deepwalk(smore_group* g, uint64_t walk_begin, uint64_t wal
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_deepwalk_async(c, b, e, walk_times, walk_steps, window, K, alpha0,
                                                               seed, order, mode);
-                        });
+                        },
+                        SMORE_LINE2, K);
 }
 
 int smore_group_train_node2vec(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
@@ -506,7 +607,8 @@ int smore_group_train_node2vec(smore_group* g, uint64_t walk_begin, uint64_t wal
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_node2vec_async(c, b, e, walk_times, walk_steps, window, K, alpha0, p,
                                                               q, seed, order, mode);
-                        });
+                        },
+                        SMORE_LINE2, K);
 }
 
 int smore_group_train_metapath2vec(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
@@ -522,7 +624,8 @@ int smore_group_train_metapath2vec(smore_group* g, uint64_t walk_begin, uint64_t
                             return smore_train_metapath2vec_async(c, b, e, walk_times, walk_steps, window, K,
                                                                   alpha0, paths, path_lens, npaths, seed, order,
                                                                   mode);
-                        });
+                        },
+                        SMORE_LINE2, K);
 }
 
 int smore_group_train_ctdne(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
@@ -536,7 +639,8 @@ int smore_group_train_ctdne(smore_group* g, uint64_t walk_begin, uint64_t walk_e
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_ctdne_async(c, b, e, walk_times, walk_steps, window, K, alpha0,
                                                            time_window, seed, order, mode);
-                        });
+                        },
+                        SMORE_LINE2, K);
 }
 
 int smore_group_train_walklets(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
@@ -550,7 +654,8 @@ int smore_group_train_walklets(smore_group* g, uint64_t walk_begin, uint64_t wal
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_walklets_async(c, b, e, walk_times, walk_steps, window_min,
                                                               window_max, K, alpha0, seed, mode);
-                        });
+                        },
+                        SMORE_LINE2, K);
 }
 
 int smore_group_train_app(smore_group* g, uint64_t unit_begin, uint64_t unit_end, int walk_times, int sample_times,
@@ -564,7 +669,8 @@ int smore_group_train_app(smore_group* g, uint64_t unit_begin, uint64_t unit_end
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_app_async(c, b, e, walk_times, sample_times, jump, K, alpha0, seed,
                                                          order, mode);
-                        });
+                        },
+                        SMORE_LINE2, K);
 }
 
 int smore_group_train_hpe(smore_group* g, uint64_t begin, uint64_t count, uint64_t total, int walk_steps, int K,
@@ -575,7 +681,8 @@ int smore_group_train_hpe(smore_group* g, uint64_t begin, uint64_t count, uint64
     return group_rounds(g, begin, begin + count, sync_samples ? sync_samples : (uint64_t)1 << 24, mean,
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_hpe_async(c, b, e - b, total, walk_steps, K, reg, alpha0, seed, mode);
-                        });
+                        },
+                        SMORE_LINE2, K);
 }
 
 }  // extern "C"

@@ -85,8 +85,8 @@ __device__ __forceinline__ void go_update_rows(const EdgeArgs& a, const float* s
     go_sh_pending<G, M, KMAX, MODE>(sh, dpad, lane, ev, id, hot, slot, rows);
     int slotw = -1;
     if constexpr (MODE == MODE_HYBRID) {
-        if (one && sh.n > 0 && hotw) {
-            slotw = sh_lookup(sh.hash, v);
+        if (sh.n > 0 && hotw) {
+            slotw = sh_lookup(sh.hash, one ? v : (v | SH_WKEY));
             if (slotw >= 0) {
 #pragma unroll
                 for (int m = 0; m < M; ++m)
@@ -119,7 +119,7 @@ __device__ __forceinline__ void go_update_rows(const EdgeArgs& a, const float* s
             di[m] = ni[m] - ci;
             dj[m] = nj[m] - base;
         }
-        go_put<G, M, MODE>(a.W + (int64_t)v * dpad, sh, -1, dpad, lane, ev, hotw, nu, du);
+        go_put<G, M, MODE>(a.W + (int64_t)v * dpad, sh, slotw, dpad, lane, ev, hotw, nu, du);
         if (i == j) {
             float dd[M];
 #pragma unroll
@@ -194,7 +194,7 @@ __device__ __forceinline__ void go_update_rows(const EdgeArgs& a, const float* s
         go_put<G, M, MODE>(a.W + (int64_t)id[0] * dpad, sh, slot[0], dpad, lane, ev, hot[0], nc, cg);
     } else {
         go_put<G, M, MODE>(a.C + (int64_t)id[0] * dpad, sh, slot[0], dpad, lane, ev, hot[0], nc, cg);
-        go_put<G, M, MODE>(a.W + (int64_t)v * dpad, sh, -1, dpad, lane, ev, hotw, nw, vg);
+        go_put<G, M, MODE>(a.W + (int64_t)v * dpad, sh, slotw, dpad, lane, ev, hotw, nw, vg);
     }
 }
 
@@ -268,7 +268,7 @@ go_rec_kernel(EdgeArgs a) {
     auto maybe_flush = [&]() {
         if constexpr (MODE == MODE_HYBRID) {
             if (sh.n > 0 && ++round == (uint32_t)a.sh_flush) {
-                sh_drain(sh, sh_ids, Tc, a.dpad);
+                sh_drain(sh, sh_ids, a.W, Tc, a.dpad);
                 round = 0;
             }
         }
@@ -319,7 +319,7 @@ go_rec_kernel(EdgeArgs a) {
     if constexpr (MODE == MODE_HYBRID) {
         if (sh.n > 0) {
             __syncthreads();
-            sh_drain(sh, sh_ids, Tc, a.dpad);
+            sh_drain(sh, sh_ids, a.W, Tc, a.dpad);
         }
     }
 }

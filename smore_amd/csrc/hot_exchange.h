@@ -1,0 +1,18 @@
+// hot_exchange.h -- the hub-row exchange of the multi-GPU replicas (DESIGN.md
+// 10): between two training launches the n rows idx[] of a table are synced
+// synchronously,
+//   pack   (compute stream):  P = T[idx] - S[idx];  R = P
+//   all-reduce R (SUM) over RCCL on the compute stream
+//   unpack (compute stream):  T[idx] += R - P;  S[idx] += R
+// composing with the one-late full exchange (replica_sync.hip): the next
+// begin sees only the hub rows' changes since the last unpack.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace smore {
+hipError_t launch_hot_pack(const float* T, const float* S, const int32_t* idx, uint64_t n, int dpad, float* P,
+                           float* R, int cus, hipStream_t st);
+hipError_t launch_hot_unpack(float* T, float* S, const int32_t* idx, uint64_t n, int dpad, const float* P,
+                             const float* R, int cus, hipStream_t st);
+}  // namespace smore

@@ -10,6 +10,7 @@
 // and the next begin's D is again only this rank's own updates.  Streaming,
 // 16 B per lane, HBM-bound (begin moves 5 and end 6 table-sized streams).
 #include "train_kernels.h"
+#include "hot_exchange.h"
 
 namespace smore {
 
@@ -61,6 +62,36 @@ __global__ void __launch_bounds__(256) delta_cycle_kernel(float4* __restrict__ T
     }
 }
 
+// hub-row exchange passes (hot_exchange.h): element i of the packed buffers
+// is element i % dpad of row idx[i / dpad]; 16 B per lane (dpad % 4 == 0)
+__global__ void __launch_bounds__(256) hot_pack_kernel(const float4* __restrict__ T, const float4* __restrict__ S,
+                                                       const int32_t* __restrict__ idx, uint64_t n4, int dp4,
+                                                       float4* __restrict__ P, float4* __restrict__ R) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t row = (uint64_t)idx[i / dp4], j = row * dp4 + i % dp4;
+        const float4 t = T[j], s = S[j];
+        const float4 d = make_float4(t.x - s.x, t.y - s.y, t.z - s.z, t.w - s.w);
+        P[i] = d;
+        R[i] = d;
+    }
+}
+
+__global__ void __launch_bounds__(256) hot_unpack_kernel(float4* __restrict__ T, float4* __restrict__ S,
+                                                         const int32_t* __restrict__ idx, uint64_t n4, int dp4,
+                                                         const float4* __restrict__ P, const float4* __restrict__ R) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t row = (uint64_t)idx[i / dp4], j = row * dp4 + i % dp4;
+        const float4 r = R[i], p = P[i];
+        float4 t = T[j], s = S[j];
+        t.x += r.x - p.x; t.y += r.y - p.y; t.z += r.z - p.z; t.w += r.w - p.w;
+        s.x += r.x; s.y += r.y; s.z += r.z; s.w += r.w;
+        T[j] = t;
+        S[j] = s;
+    }
+}
+
 static unsigned stream_grid(uint64_t n4, int cus) {
     const uint64_t want = (n4 + 255) / 256, cap = (uint64_t)(cus > 0 ? cus : 256) * 16;
     return (unsigned)(want < cap ? (want ? want : 1) : cap);
@@ -89,6 +120,28 @@ hipError_t launch_delta_cycle(float* T, float* S, float* D, float* R, float scal
     hipLaunchKernelGGL(delta_cycle_kernel, dim3(stream_grid(n4, cus)), dim3(256), 0, st, reinterpret_cast<float4*>(T),
                        reinterpret_cast<float4*>(S), reinterpret_cast<float4*>(D), reinterpret_cast<float4*>(R), scale,
                        n4);
+    return hipGetLastError();
+}
+
+}  // namespace smore
+
+namespace smore {
+
+hipError_t launch_hot_pack(const float* T, const float* S, const int32_t* idx, uint64_t n, int dpad, float* P,
+                           float* R, int cus, hipStream_t st) {
+    const uint64_t n4 = n * (uint64_t)(dpad / 4);
+    hipLaunchKernelGGL(hot_pack_kernel, dim3(stream_grid(n4, cus)), dim3(256), 0, st,
+                       reinterpret_cast<const float4*>(T), reinterpret_cast<const float4*>(S), idx, n4, dpad / 4,
+                       reinterpret_cast<float4*>(P), reinterpret_cast<float4*>(R));
+    return hipGetLastError();
+}
+
+hipError_t launch_hot_unpack(float* T, float* S, const int32_t* idx, uint64_t n, int dpad, const float* P,
+                             const float* R, int cus, hipStream_t st) {
+    const uint64_t n4 = n * (uint64_t)(dpad / 4);
+    hipLaunchKernelGGL(hot_unpack_kernel, dim3(stream_grid(n4, cus)), dim3(256), 0, st, reinterpret_cast<float4*>(T),
+                       reinterpret_cast<float4*>(S), idx, n4, dpad / 4, reinterpret_cast<const float4*>(P),
+                       reinterpret_cast<const float4*>(R));
     return hipGetLastError();
 }
 

@@ -438,8 +438,37 @@ __global__ void __launch_bounds__(256) go_draw_kernel(DevGraph g, const double* 
         }
     }
     const uint32_t vi = draw_index(w[0], g.V);
-    const int32_t v = alias_pick(vi, g.vtab[vi], w[1]);
-    const int32_t c = go_target_tagged(g, tcum, untag(v), w[2], unit_w);
+    int32_t v, c;
+    if (g.vt32) {
+        // the source draw and its CSR row from one packed 32-B entry
+        // (train_draw.hip pack_vertex_kernel), as the C++ draw kernel
+        const uint4 p0 = g.vt32[2 * (uint64_t)vi], p1 = g.vt32[2 * (uint64_t)vi + 1];
+        const bool acc = w[1] < p0.x;
+        v = alias_pick(vi, make_uint2(p0.x, p0.y), w[1]);
+        const uint64_t off = acc ? p0.z : p1.x;
+        const uint32_t br = acc ? p0.w : p1.y;
+        c = -1;
+        if (br != 0) {
+            int64_t lo;
+            if (unit_w) {
+                lo = (int64_t)ceil(ldexp((double)w[2], -32) * (double)br) - 1;
+                lo = lo < 0 ? 0 : (lo > (int64_t)br - 1 ? (int64_t)br - 1 : lo);
+            } else {
+                const double r = ldexp((double)w[2], -32) * tcum[off + br - 1];
+                int64_t hi = br - 1;
+                lo = 0;
+                while (lo < hi) {
+                    const int64_t mid = (lo + hi) >> 1;
+                    if (r <= tcum[off + mid]) hi = mid;
+                    else lo = mid + 1;
+                }
+            }
+            c = g.targets[off + lo];
+        }
+    } else {
+        v = alias_pick(vi, g.vtab[vi], w[1]);
+        c = go_target_tagged(g, tcum, untag(v), w[2], unit_w);
+    }
     int32_t o[RW];
     o[0] = v;
     o[1] = c;

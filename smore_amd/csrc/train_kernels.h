@@ -108,6 +108,7 @@ hipError_t launch_pack(const DevGraph& g, uint64_t E, uint4* vt32, uint4* ct16, 
 hipError_t launch_draw(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K, int32_t* rec,
                        unsigned long long* skipped, hipStream_t st);
 constexpr int SH_HASH = 256;   // entries of the super-hot row hash (power of two)
+constexpr int32_t SH_WKEY = 1 << 30;   // write-combine key bit: a W row of a two-table model
 // dynamic LDS of the hybrid edge kernel: hash, slot ids, pending deltas
 inline size_t sh_lds_bytes(int sh_rows, int dpad) {
     return sh_rows > 0 ? SH_HASH * 8 + (size_t)sh_rows * 4 + (size_t)sh_rows * dpad * 4 : 0;

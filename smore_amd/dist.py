@@ -112,7 +112,7 @@ class OverlapSync:
     After end() every replica holds every rank's updates up to the matching
     begin(), plus its own since."""
 
-    def __init__(self, tensors, mean=False, group=None, passes=None):
+    def __init__(self, tensors, mean=False, group=None, passes=None, hot_idx=None):
         self.T = list(tensors)
         self.S = [t.clone() for t in self.T]
         self.D = [torch.zeros_like(t) for t in self.T]
@@ -121,6 +121,21 @@ class OverlapSync:
         self.group = group
         self.passes = passes or TorchPasses()
         self.works = None
+        # hub rows (one int64 index tensor per table) exchanged by hot(); sum only
+        self.hot_idx = [] if (mean or not hot_idx) else list(hot_idx)
+
+    def hot(self):
+        """Synchronous exchange of the hub rows between two training launches:
+        D' = T_h - S_h;  R' = all_reduce(D');  T_h += R' - D';  S_h += R'.
+        Between a begin() and its end() S holds the rank's own snapshot, so D'
+        is the change since then and the pending end() adds only the older
+        deltas: every update still lands once on every replica."""
+        for T, S, idx in zip(self.T, self.S, self.hot_idx):
+            D = T.index_select(0, idx) - S.index_select(0, idx)
+            R = D.clone()
+            dist.all_reduce(R, op=dist.ReduceOp.SUM, group=self.group)
+            T.index_add_(0, idx, R - D)
+            S.index_add_(0, idx, R)
 
     def begin(self):
         if self.works is not None:      # fold the previous exchange in and start this one: one pass
@@ -156,9 +171,23 @@ class OverlapSync:
 class ReplicaSync(OverlapSync):
     """OverlapSync over a ProNet context's device tables (W and C), with the
     fused HIP passes; the context runs on torch's current stream so the
-    passes, the training kernels and the collective are ordered on it."""
+    passes, the training kernels and the collective are ordered on it.
 
-    def __init__(self, pn, mean=False, tables=(0, 1), group=None):
+    hot_rows > 0 (sum exchange only): the hub rows of each table -- the
+    hot_rows rows with the highest expected touches per sample of `model`
+    (smore_hot_row_ids) -- are also exchanged synchronously by hot(), which
+    the caller runs after every training launch inside a step:
+
+        D' = T_h - S_h;  R' = all_reduce(D');  T_h += R' - D';  S_h += R'
+
+    This composes with the one-late full exchange (no update counted twice:
+    the next begin() sees only the hub rows' changes since the last hot()).
+    Why: a hub row collects every rank's thousands of updates per step; added
+    up one step late they overshoot and training diverges at 4 and 8 ranks
+    (tools/replica_sim.py), while the cold rows' few stale
+    updates per step do no harm."""
+
+    def __init__(self, pn, mean=False, tables=(0, 1), group=None, hot_rows=0, model="line2", K=5):
         # the passes, the training kernels and the collective must be ordered
         # on ONE stream.  The context runs on its own non-blocking stream when
         # handed the null stream (handle 0), which the legacy null stream does
@@ -166,4 +195,10 @@ class ReplicaSync(OverlapSync):
         if torch.cuda.current_stream().cuda_stream == 0:
             torch.cuda.set_stream(torch.cuda.Stream())
         pn.set_stream(torch.cuda.current_stream().cuda_stream)
-        super().__init__([table_tensor(pn, w) for w in tables], mean=mean, group=group, passes=HipPasses(pn))
+        T = [table_tensor(pn, w) for w in tables]
+        hot_idx = None
+        if hot_rows > 0 and not mean:
+            n = min(int(hot_rows), pn.MAX_vid)
+            hot_idx = [torch.as_tensor(pn.hot_row_ids(model, K, min(w, 1), n).astype("int64"), device=T[0].device)
+                       for w in tables]
+        super().__init__(T, mean=mean, group=group, passes=HipPasses(pn), hot_idx=hot_idx)

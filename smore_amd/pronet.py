@@ -279,6 +279,14 @@ class ProNet:
         self._chk(lib.smore_hot_rows(self.ctx, C.byref(w), C.byref(c)), "hot_rows")
         return w.value, c.value
 
+    def hot_row_ids(self, model, K, which, n):
+        """The n hub rows of table `which` (0 W, 1 C) by expected touches per
+        sample, highest first (int32)."""
+        ids = np.zeros(max(1, n), np.int32)
+        self._chk(lib.smore_hot_row_ids(self.ctx, _lib.MODEL[model], int(K), int(which), int(n),
+                                        ids.ctypes.data_as(C.c_void_p)), "hot_row_ids")
+        return ids[:n]
+
     def synchronize(self):
         self._chk(lib.smore_synchronize(self.ctx), "synchronize")
 
@@ -402,6 +410,11 @@ class Group:
         self._chk(lib.smore_group_set_graph_edges(self.g, int(V), len(src), ptr(src), ptr(dst), ptr(w),
                                                   _lib.VM[vertex_method], _lib.NM[negative_method]),
                   "set_graph_edges")
+
+    def set_hot_exchange(self, rows=-1, launches=8):
+        """smore_group_set_hot_exchange: hub rows per table synced after every
+        one of `launches` launches per exchange round (-1 automatic, 0 off)."""
+        self._chk(lib.smore_group_set_hot_exchange(self.g, int(rows), int(launches)), "set_hot_exchange")
 
     def set_semantics(self, semantics):
         self._chk(lib.smore_group_set_semantics(self.g, _lib.SEM[semantics]), "set_semantics")

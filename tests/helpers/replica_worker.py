@@ -4,7 +4,11 @@ smore_amd/dist.py ReplicaSync (the fused HIP passes of replica_sync.hip around a
 torch.distributed all-reduce; gloo here, since every rank shares one GPU).
 TEST INFRASTRUCTURE.
 
-    python tests/helpers/replica_worker.py RANK WORLD PORT TOTAL STEPS OUT.npz
+    python tests/helpers/replica_worker.py RANK WORLD PORT TOTAL STEPS OUT.npz [HOT_ROWS LAUNCHES [MEAN]]
+
+HOT_ROWS > 0 (sum exchange): the hub-row exchange after each of LAUNCHES
+launches per step (ReplicaSync.hot).  MEAN 1: the averaging exchange
+(bench.py's N > 1 default).
 """
 import os
 import sys
@@ -16,6 +20,9 @@ sys.path.insert(0, ROOT)
 def main():
     rank, world, port, total, steps = (int(x) for x in sys.argv[1:6])
     out = sys.argv[6]
+    hot_rows = int(sys.argv[7]) if len(sys.argv) > 7 else 0
+    launches = int(sys.argv[8]) if len(sys.argv) > 8 else 1
+    mean = bool(int(sys.argv[9])) if len(sys.argv) > 9 else False
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -29,11 +36,17 @@ def main():
     pn.alloc_tables(32, 2)
     pn.init_table_glibc(0, 0)
     pn.zero_table(1)
-    sync = ReplicaSync(pn) if world > 1 else None
+    sync = ReplicaSync(pn, mean=mean, hot_rows=hot_rows, model="line2", K=5) if world > 1 else None
+    nl = launches if (sync is not None and sync.hot_idx) else 1
     per = total // world // steps
     for k in range(steps):
         begin = (k * world + rank) * per
-        pn.train_edges("line2", begin, per, total, 5, 0.025, 0.0, 20251015, "atomic", sync=False)
+        sub = per // nl
+        for j in range(nl):
+            n = sub if j + 1 < nl else per - j * sub
+            pn.train_edges("line2", begin + j * sub, n, total, 5, 0.025, 0.0, 20251015, "atomic", sync=False)
+            if nl > 1:
+                sync.hot()
         if sync is not None:
             sync.begin()
     if sync is not None:

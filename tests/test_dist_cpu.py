@@ -73,3 +73,60 @@ def test_delta_allreduce_gloo_world2(mean, overlap):
         p.join(120)
         assert p.exitcode == 0
     assert list(out) == [1, 1]
+
+
+def _hot_worker(rank, world, port, out):
+    """Hub-row exchange between launches + the one-late full exchange."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from smore_amd.dist import OverlapSync
+    torch.manual_seed(0)
+    base = [torch.randn(60, 8), torch.randn(60, 8)]
+    tabs = [b.clone() for b in base]
+    hot = [torch.tensor([3, 17, 0, 44]), torch.tensor([59, 1, 30])]
+    sync = OverlapSync(tabs, hot_idx=hot)
+    expect = [b.clone() for b in base]
+    for step in range(4):
+        for sub in range(3):
+            deltas = []
+            for r in range(world):
+                g = torch.Generator().manual_seed(1000 * step + 10 * sub + r)
+                deltas.append([torch.randn(60, 8, generator=g) * 0.01 for _ in tabs])
+            for t, d in zip(tabs, deltas[rank]):
+                t.add_(d)
+            sync.hot()
+            for i in range(len(tabs)):
+                expect[i] += sum(deltas[r][i] for r in range(world))
+                # after hot(): the hub rows already hold every rank's updates
+                agreed = [torch.empty_like(tabs[i][hot[i]]) for _ in range(world)]
+                dist.all_gather(agreed, tabs[i][hot[i]].contiguous())
+                if not all(torch.allclose(agreed[0], x, atol=1e-6, rtol=0) for x in agreed):
+                    out[rank] = 0
+                    return
+        sync.begin()
+    sync.end()
+    ok = all(torch.allclose(t, e, atol=1e-5) for t, e in zip(tabs, expect))
+    same = [torch.empty_like(tabs[1]) for _ in range(world)]
+    dist.all_gather(same, tabs[1])
+    ok = ok and all(torch.allclose(same[0], x, atol=1e-6, rtol=0) for x in same)
+    out[rank] = int(ok)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_hot_row_exchange_gloo(world):
+    """ReplicaSync's hub-row exchange (dist.py OverlapSync.hot) between the
+    launches of a step, composed with the one-late full exchange: after every
+    hot() the hub rows agree on all ranks, and at the end every rank holds
+    base + every rank's every delta exactly once."""
+    ctx = mp.get_context("spawn")
+    out = ctx.Array("i", [0] * world)
+    port = _free_port()
+    procs = [ctx.Process(target=_hot_worker, args=(r, world, port, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert list(out) == [1] * world

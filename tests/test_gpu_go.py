@@ -134,10 +134,9 @@ def test_go_deepwalk_hogwild_matches_atomic(smore):
 
     res = {}
     for mode in ("atomic", "hogwild"):
-        W0, C0 = tables(g.V, dim, 17)
         pn.alloc_tables(dim, 2)
-        pn.set_table(0, W0 / dim)
-        pn.set_table(1, C0 / dim)
+        pn.init_table_glibc(0, 0)
+        pn.zero_table(1)
         pn.train_deepwalk(0, times * g.V, times, 20, 5, K, 0.025, SEED, order, mode)
         W, C = pn.get_table(0), pn.get_table(1)
         assert np.isfinite(W).all() and np.isfinite(C).all()
