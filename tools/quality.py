@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--modes", nargs="+", default=["hogwild", "atomic"])
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--semantics", default="cpp", choices=["cpp", "go"])
     args = ap.parse_args()
     import smore_amd
     from smore_amd import graphgen
@@ -48,6 +49,9 @@ def main():
     res = {"config": args.config, "samples": args.samples, "dim": args.dim}
     pn = smore_amd.ProNet(0)
     pn.set_graph_edges(V, src, dst, w)
+    if args.semantics == "go":
+        pn.set_semantics("go")
+        res["semantics"] = "go"
     draws = pn.sample_edges("line2", 1 << 40, 200000, 5, 99991)   # held-out draws
     total = args.samples + 1
     for spec in args.modes:

@@ -55,6 +55,9 @@ def main():
     ap.add_argument("--seed", type=int, default=20251015)
     ap.add_argument("--sub", type=int, nargs="+", default=[1], help="launches (hot exchanges) per step")
     ap.add_argument("--hot", type=int, nargs="+", default=[0], help="hot rows per table exchanged per launch")
+    ap.add_argument("--c0", type=float, nargs="+", default=[64.0],
+                    help="adaptive: a row whose expected updates per exchange over all ranks, n*k, is at most c0 "
+                         "is summed, a hotter one scaled by s + (1 - s)/n with s = c0/(n*k)")
     args = ap.parse_args()
 
     import torch
@@ -94,10 +97,11 @@ def main():
     order_by_rate = [torch.from_numpy(np.argsort(-r, kind="stable").astype(np.int64)).cuda() for r in rate]
     results = []
     import itertools
+    syncs = [x for x in args.sync if x != "adaptive"] + ["adaptive:%g" % c for c in args.c0 if "adaptive" in args.sync]
     for n, sub, hot in itertools.product(args.ranks, args.sub, args.hot):
         if n == 1 and (sub != args.sub[0] or hot != args.hot[0]):
             continue
-        for sync in (args.sync if n > 1 else ["none"]):
+        for sync in (syncs if n > 1 else ["none"]):
             reps = [ctx(i) for i in range(n)]
             for pn in reps:
                 pn.init_table_uniform(0, 5)
@@ -107,6 +111,15 @@ def main():
             Ds = [[torch.zeros_like(t) for t in ts] for ts in T]
             Rs = [[torch.zeros_like(t) for t in ts] for ts in T]
             scale = 1.0 / n if sync == "mean" else 1.0
+            if sync.startswith("adaptive"):
+                # per-row scale of the summed deltas: sum for rows with few
+                # updates per exchange, towards the mean for the hub rows
+                c0 = float(sync.split(":")[1])
+                scale = []
+                for r_ in rate:
+                    k = r_ * S * n
+                    sv = np.minimum(1.0, c0 / np.maximum(k, 1e-30))
+                    scale.append(torch.from_numpy((sv + (1.0 - sv) / n).astype(np.float32)).cuda().view(-1, 1))
             steps = max(1, args.total // (n * S))
             pending = False
             t0 = time.perf_counter()
@@ -139,8 +152,9 @@ def main():
                 if n > 1:
                     for r in range(n):
                         for t in range(2):
+                            sc = scale[t] if isinstance(scale, list) else scale
                             if pending:
-                                TorchPasses.cycle(T[r][t], Ss[r][t], Ds[r][t], Rs[r][t], scale)
+                                TorchPasses.cycle(T[r][t], Ss[r][t], Ds[r][t], Rs[r][t], sc)
                             else:
                                 TorchPasses.begin(T[r][t], Ss[r][t], Ds[r][t], Rs[r][t])
                     reduce_all()       # the all-reduce of this exchange (lands before the next end)
@@ -148,7 +162,8 @@ def main():
             if pending:
                 for r in range(n):
                     for t in range(2):
-                        TorchPasses.end(T[r][t], Ss[r][t], Ds[r][t], Rs[r][t], scale)
+                        TorchPasses.end(T[r][t], Ss[r][t], Ds[r][t], Rs[r][t],
+                                        scale[t] if isinstance(scale, list) else scale)
             torch.cuda.synchronize()
             W0, C0 = reps[0].get_table(0), reps[0].get_table(1)
             spread = 0.0
