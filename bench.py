@@ -63,9 +63,11 @@ def parse():
     ap.add_argument("--combine-flush", type=int, default=0, help="hybrid: rounds between LDS drains (0: automatic)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
     ap.add_argument("--sync-every", type=int, default=1)
-    ap.add_argument("--sync", default="mean", choices=["sum", "mean"],
-                    help="N > 1: average the replicas' deltas (default; stable) or sum them (every update applied "
-                         "once; diverges at >= 4 ranks at this exchange period, DESIGN.md 10)")
+    ap.add_argument("--sync", default="adaptive", choices=["sum", "mean", "adaptive"],
+                    help="N > 1 exchange rule: adaptive (default: per row the sum for rows with few updates per "
+                         "exchange, towards the mean for the hubs), mean (model averaging) or sum (every update "
+                         "applied once; diverges at >= 4 ranks at this exchange period), DESIGN.md 10")
+    ap.add_argument("--sync-c0", type=float, default=64.0, help="adaptive rule: c0")
     ap.add_argument("--hot-rows", type=int, default=65536,
                     help="N > 1, --sync sum: hub rows per table exchanged after every launch")
     ap.add_argument("--launches", type=int, default=8,
@@ -183,7 +185,8 @@ def main():
     stream = torch.cuda.Stream()             # a real stream: the default one is the null stream
     torch.cuda.set_stream(stream)
     pn.set_stream(stream.cuda_stream)
-    sync = (ReplicaSync(pn, mean=(args.sync == "mean"), hot_rows=args.hot_rows, model="line2", K=args.negative)
+    sync = (ReplicaSync(pn, sync=args.sync, hot_rows=args.hot_rows, model="line2", K=args.negative,
+                        updates=args.samples * args.sync_every, c0=args.sync_c0)
             if world > 1 else None)
     n_launch = max(1, args.launches) if (sync is not None and sync.hot_idx) else 1
     phase = [0.0, 0.0, 0]     # exposed draw ms, update ms, update launches (timed steps)

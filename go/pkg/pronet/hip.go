@@ -60,11 +60,15 @@ const (
 	HIPSerial  = int(C.SMORE_SERIAL)
 )
 
+// the exchange rule of the group training calls (smore_hip.h SMORE_SYNC_*)
 func (h *HIP) mean() C.int {
-	if h.cfg.Sum {
-		return 0
+	switch h.cfg.Sync {
+	case "sum":
+		return C.SMORE_SYNC_SUM
+	case "mean":
+		return C.SMORE_SYNC_MEAN
 	}
-	return 1
+	return C.SMORE_SYNC_ADAPTIVE
 }
 
 // HIPConfig selects the GPUs and the scatter mode of a run.
@@ -73,12 +77,12 @@ type HIPConfig struct {
 	GPUs   int    // replicas on Device .. Device+GPUs-1 (tables all-reduced over RCCL)
 	Mode   int    // HIPHybrid unless set
 	Seed   uint64 // Philox seed of the draws
-	Sum    bool   // GPUs > 1: sum the replicas' deltas instead of averaging them (diverges at >= 4 GPUs)
+	Sync   string // GPUs > 1: exchange rule, "adaptive" (default), "mean" or "sum" (diverges at >= 4 GPUs)
 }
 
 // HIPConfigFromEnv reads SMORE_HIP_DEVICE, SMORE_HIP_GPUS, SMORE_HIP_MODE
-// (hybrid|atomic|hogwild|serial), SMORE_HIP_SEED and SMORE_SYNC (mean|sum);
-// defaults 0, 1, hybrid, seed, mean.
+// (hybrid|atomic|hogwild|serial), SMORE_HIP_SEED and SMORE_SYNC
+// (adaptive|mean|sum); defaults 0, 1, hybrid, seed, adaptive.
 func HIPConfigFromEnv(seed uint64) HIPConfig {
 	c := HIPConfig{Device: 0, GPUs: 1, Mode: HIPHybrid, Seed: seed}
 	if v, err := strconv.Atoi(os.Getenv("SMORE_HIP_DEVICE")); err == nil {
@@ -95,7 +99,7 @@ func HIPConfigFromEnv(seed uint64) HIPConfig {
 	case "serial":
 		c.Mode = HIPSerial
 	}
-	c.Sum = os.Getenv("SMORE_SYNC") == "sum"
+	c.Sync = os.Getenv("SMORE_SYNC")
 	if v, err := strconv.ParseUint(os.Getenv("SMORE_HIP_SEED"), 10, 64); err == nil {
 		c.Seed = v
 	}

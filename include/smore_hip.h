@@ -222,6 +222,33 @@ int smore_delta_end(smore_ctx* ctx, void* T, void* S, const void* D, const void*
  * X = scale*R - D; T += X; then D = T - S (the rank's delta since the last begin),
  * R = D, S = T */
 int smore_delta_cycle(smore_ctx* ctx, void* T, void* S, void* D, void* R, float scale, int64_t n);
+/* the same two passes with a per-row scale: row i (`stride` floats, stride % 4
+ * == 0, n = rows * stride) uses scale[i] (device, `rows` floats) -- the
+ * adaptive exchange (SMORE_SYNC_ADAPTIVE below) */
+int smore_delta_end_rows(smore_ctx* ctx, void* T, void* S, const void* D, const void* R, const void* scale,
+                         int64_t rows, int64_t stride);
+int smore_delta_cycle_rows(smore_ctx* ctx, void* T, void* S, void* D, void* R, const void* scale, int64_t rows,
+                           int64_t stride);
+/* expected touches per sample of every row of table `which` (0 = W, 1 = C)
+ * under `model` with K negatives (the sampler marginals of the context's graph;
+ * the ranking smore_hot_row_ids sorts by); rate[V] */
+int smore_row_rates(smore_ctx* ctx, int model, int K, int which, int64_t n, double* rate);
+/* Exchange rules (the `mean` argument of smore_exchange_begin and the group
+ * training calls):
+ *   SMORE_SYNC_SUM       scale 1: every rank's update lands once on every replica
+ *   SMORE_SYNC_MEAN      scale 1/N: model averaging
+ *   SMORE_SYNC_ADAPTIVE  per row: with k = the row's expected updates per
+ *                        exchange over all ranks (rate * samples per exchange * N),
+ *                        s = min(1, c0 / k), scale = s + (1 - s) / N -- the sum for
+ *                        rows updated a few times per exchange, towards the mean for
+ *                        the hub rows whose summed one-late deltas overshoot
+ *                        (the default; c0 = 64, smore_group_set_adaptive) */
+#define SMORE_SYNC_SUM 0
+#define SMORE_SYNC_MEAN 1
+#define SMORE_SYNC_ADAPTIVE 2
+/* the row scales of the adaptive rule for `updates` samples of `model` per rank
+ * per exchange (smore_exchange_begin with SMORE_SYNC_ADAPTIVE needs them) */
+int smore_exchange_set_adaptive(smore_ctx* ctx, int model, int K, double updates, double c0);
 
 /* ---- multi-GPU replicas over RCCL, in the library (smore_amd/csrc/exchange.cpp) ------
  * replaces: the fan-out of one training run over the reference's workers
@@ -242,7 +269,7 @@ int smore_delta_cycle(smore_ctx* ctx, void* T, void* S, void* D, void* R, float 
 int smore_comm_unique_id(unsigned char* id /* SMORE_COMM_ID_BYTES */);
 int smore_comm_init(smore_ctx* ctx, int nranks, int rank, const unsigned char* id);
 int smore_exchange_reset(smore_ctx* ctx);
-int smore_exchange_begin(smore_ctx* ctx, int mean);
+int smore_exchange_begin(smore_ctx* ctx, int mean /* SMORE_SYNC_* */);
 int smore_exchange_end(smore_ctx* ctx);
 
 /* One process driving N GPUs (`smore_create(dev_ids, n_dev)` with
@@ -263,6 +290,8 @@ int smore_group_size(const smore_group* g);
  * synchronously.  rows -1 = automatic (min(65536, V/8), the default), 0 = off
  * (then one launch per round); launches >= 1 (default 8). */
 int smore_group_set_hot_exchange(smore_group* g, int64_t rows, int launches);
+/* c0 of the adaptive exchange (default 64) */
+int smore_group_set_adaptive(smore_group* g, double c0);
 smore_ctx* smore_group_ctx(smore_group* g, int rank);
 const char* smore_group_last_error(const smore_group* g);
 int smore_group_load_edgelist(smore_group* g, const char* path, int undirected, int vertex_method,
@@ -277,7 +306,7 @@ int smore_group_set_temporal_edges(smore_group* g, int64_t E, const int32_t* src
                                    const double* ts);
 int smore_group_alloc_tables(smore_group* g, int dim, int ntables);
 int smore_group_broadcast_tables(smore_group* g);
-/* per = samples per replica per exchange (0: 2^27) */
+/* per = samples per replica per exchange (0: 2^27); mean = SMORE_SYNC_* */
 int smore_group_train_edges(smore_group* g, int model, uint64_t begin, uint64_t count, uint64_t total, int K,
                             double alpha0, double reg, uint64_t seed, int mode, uint64_t per, int mean);
 /* per = walks per replica per exchange (0: 2^18) */

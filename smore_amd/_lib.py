@@ -15,6 +15,17 @@ NM = {"degrees": 0, "in_degrees": 1, "no_degrees": 2}
 AT_VERTEX, AT_NEGATIVE, AT_CONTEXT = 0, 1, 2
 W, CTX = 0, 1
 MODEL = {"line2": 0, "line1": 1, "mf": 2, "bpr": 3}
+# exchange rules of the replica exchange (smore_hip.h SMORE_SYNC_*)
+SYNC = {"sum": 0, "mean": 1, "adaptive": 2}
+
+
+def sync_rule(sync):
+    """SMORE_SYNC_* of a rule name; booleans are the old mean flag."""
+    if isinstance(sync, bool):
+        return int(sync)
+    return SYNC[sync]
+
+
 MODE = {"hogwild": 0, "atomic": 1, "serial": 2, "hybrid": 3}
 SEM = {"cpp": 0, "go": 1}
 
@@ -69,6 +80,11 @@ def _load():
         "smore_delta_begin": (i32, [P, P, P, P, P, i64]),
         "smore_delta_end": (i32, [P, P, P, P, P, C.c_float, i64]),
         "smore_delta_cycle": (i32, [P, P, P, P, P, C.c_float, i64]),
+        "smore_delta_end_rows": (i32, [P, P, P, P, P, P, i64, i64]),
+        "smore_delta_cycle_rows": (i32, [P, P, P, P, P, P, i64, i64]),
+        "smore_row_rates": (i32, [P, i32, i32, i32, i64, P]),
+        "smore_exchange_set_adaptive": (i32, [P, i32, i32, dbl, dbl]),
+        "smore_group_set_adaptive": (i32, [P, dbl]),
         "smore_train_deepwalk": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, u64, P, i32]),
         "smore_train_deepwalk_async": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, u64, P, i32]),
         "smore_set_temporal_edges": (i32, [P, i64, P, P, P]),

@@ -5,6 +5,7 @@
 // uploaded once; training calls only launch kernels on the context stream.
 #include "ctx.h"
 #include "go_walks.h"
+#include "hot_exchange.h"
 
 #include <algorithm>
 #include <chrono>
@@ -344,8 +345,11 @@ constexpr double SH_AUTO_BUDGET = 6144.0;
 static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
     char key[128];
     const char* stale_env = getenv("SMORE_SH_STALE");
-    snprintf(key, sizeof key, "%d/%d/%lld/%.9g/%d/%d/%s", model, K, (long long)M, c->hot_tau, c->sh_max, c->sh_flush,
-             stale_env ? stale_env : "");
+    // tuning knob: SMORE_SH_WROWS=0 keeps W rows out of the write-combined set
+    const char* wrows_env = getenv("SMORE_SH_WROWS");
+    const bool wrows = !wrows_env || atoi(wrows_env) != 0;
+    snprintf(key, sizeof key, "%d/%d/%lld/%.9g/%d/%d/%s/%d", model, K, (long long)M, c->hot_tau, c->sh_max,
+             c->sh_flush, stale_env ? stale_env : "", (int)wrows);
     if (c->hot_key == key) return SMORE_OK;
     if (c->g->V >= ((int64_t)1 << 30)) return fail(c, SMORE_EINVAL, "hybrid scatter needs V < 2^30");
     std::vector<double> ps, pn, pc;
@@ -377,7 +381,7 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
             // two tables: the hub W rows compete for the same slots (key
             // v | SH_WKEY) -- the Go source law (out_degree^1) puts ~1 % of
             // all samples on one W row
-            if (model == SMORE_LINE2 && hw[v] && (double)M * ps[v] * flush_cap <= stale_max)
+            if (wrows && model == SMORE_LINE2 && hw[v] && (double)M * ps[v] * flush_cap <= stale_max)
                 r.push_back({ps[v], (int32_t)(v | SH_WKEY)});
         }
         const int64_t cap = std::max<int64_t>(0, std::min<int64_t>(c->sh_max, 8192 / std::max(1, c->dpad)));
@@ -467,10 +471,14 @@ static hipError_t launch_go_rec(const EdgeArgs& a, int grid, hipStream_t st) {
                                     : launch_go_rec_s(a, grid, st);
 }
 
-static int edge_grid(smore_ctx* c, const EdgeArgs& a, bool leave_slot = false, bool go = false) {
+// kind: 0 the C++ edge/pair kernel, 1 Go records (go_rec_kernel), 2 Go walk
+// pairs (go_pair_kernel)
+static int edge_grid(smore_ctx* c, const EdgeArgs& a, bool leave_slot = false, int kind = 0) {
     if (a.mode == SMORE_SERIAL) return 1;
     int per_cu = 0;
-    const void* sym = go ? go_rec_symbol(a) : edge_kernel_symbol(a);
+    const void* sym = kind == 1   ? go_rec_symbol(a)
+                      : kind == 2 ? (a.mode == SMORE_ATOMIC ? go_pair_symbol_a(a) : go_pair_symbol_s(a))
+                                  : edge_kernel_symbol(a);
     if (!sym ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sym, 256, sh_lds_bytes(a.sh_rows, a.dpad)) !=
             hipSuccess ||
@@ -550,7 +558,7 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
     }
     const bool combine = mode == SMORE_HYBRID && (go || model != SMORE_BPR);
     a.sh_rows = combine ? std::min(c->sh_max, 8192 / std::max(1, c->dpad)) : 0;   // LDS bound for the grid
-    const int grid = edge_grid(c, a, false, go);
+    const int grid = edge_grid(c, a, false, go ? 1 : 0);
     if (mode == SMORE_HYBRID) {
         const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
         // Go BPR has two tables (users W, items C): the LINE-2 row roles
@@ -593,7 +601,7 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
     if ((rc = grow(c->sync_ev, 2 * (size_t)nch))) return rc;
     if ((rc = ensure_packed(c))) return rc;
     const DevGraph dg = dev_graph(c);
-    const int ugrid = nch > 1 ? edge_grid(c, a, true, go) : grid;
+    const int ugrid = nch > 1 ? edge_grid(c, a, true, go ? 1 : 0) : grid;
     hipStream_t ds = nch > 1 ? c->draw_stream : c->stream;
     auto recbuf = [&](int k) { return c->d_rec + (size_t)(k % nbuf) * chunk * RW; };
     auto draw = [&](int k) -> int {
@@ -706,19 +714,29 @@ int smore_write_combine_info(const smore_ctx* c, int* rows, int* flush_rounds) {
 // per sample under the context's samplers and the model's row roles (LINE-2 /
 // Go BPR: W = sources, C = contexts + K x negatives; one-table models: the
 // union), highest first -- the rows the replica exchange syncs every launch
+int smore_row_rates(smore_ctx* c, int model, int K, int which, int64_t n, double* rate) {
+    if (!c || !rate || which < 0 || which > 1 || model < 0 || model > 3 || K < 0) return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    const int64_t V = c->g->V;
+    if (n != V) return fail(c, SMORE_EINVAL, "row_rates: n must be the vertex count");
+    std::vector<double> ps, pn, pc;
+    draw_probabilities(*c->g, ps, pn, pc);
+    const bool two = model == SMORE_LINE2 || (model == SMORE_BPR && c->semantics == SMORE_SEM_GO);
+    const int negs = model == SMORE_BPR ? (c->semantics == SMORE_SEM_GO ? 1 : 5) : K;
+    for (int64_t v = 0; v < V; ++v)
+        rate[v] = two ? (which == 0 ? ps[v] : pc[v] + negs * pn[v]) : ps[v] + pc[v] + negs * pn[v];
+    return SMORE_OK;
+}
+
 int smore_hot_row_ids(smore_ctx* c, int model, int K, int which, int64_t n, int32_t* ids) {
     if (!c || !ids || n < 0 || which < 0 || which > 1 || model < 0 || model > 3 || K < 0)
         return SMORE_EINVAL;
     if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
     const int64_t V = c->g->V;
     if (n > V) return fail(c, SMORE_EINVAL, "more hot rows than vertices");
-    std::vector<double> ps, pn, pc;
-    draw_probabilities(*c->g, ps, pn, pc);
-    const bool two = model == SMORE_LINE2 || (model == SMORE_BPR && c->semantics == SMORE_SEM_GO);
-    const int negs = model == SMORE_BPR ? (c->semantics == SMORE_SEM_GO ? 1 : 5) : K;
     std::vector<double> rate((size_t)V);
-    for (int64_t v = 0; v < V; ++v)
-        rate[v] = two ? (which == 0 ? ps[v] : pc[v] + negs * pn[v]) : ps[v] + pc[v] + negs * pn[v];
+    int rc;
+    if ((rc = smore_row_rates(c, model, K, which, V, rate.data()))) return rc;
     std::vector<int32_t> order((size_t)V);
     for (int64_t v = 0; v < V; ++v) order[v] = (int32_t)v;
     std::partial_sort(order.begin(), order.begin() + n, order.end(), [&](int32_t a, int32_t b) {
@@ -1010,15 +1028,15 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
     if (order)
         HIPCHK(c, hipMemcpyAsync(c->d_order, order + walk_begin, nw_call * sizeof(int64_t), hipMemcpyHostToDevice,
                                  c->stream));
-    // C++ semantics: walks -> pair records -> update kernel; chunks of up to
-    // 2^18 walks whose pair records (sized by the per-walk upper bound, so no
-    // host read-back of the pair count) stay under 4 GiB.  Go semantics: fused
-    // walk kernel, 2^20 walks per chunk.
-    const bool cpp = c->semantics != SMORE_SEM_GO;
+    // walks -> pair records -> update kernel (C++: edge_kernels.h over the
+    // pair_emit records; Go: go_rec.h go_pair_kernel over go_pair_emit's);
+    // chunks of up to 2^18 walks whose pair records (sized by the per-walk
+    // upper bound, so no host read-back of the pair count) stay under 4 GiB
+    const bool go = c->semantics == SMORE_SEM_GO;
     const int RW = rec_width(kmax_of(K));
     const uint64_t pb = std::max<uint64_t>(1, pair_bound(walk_steps, window, rule, window_min));
-    uint64_t chunk_cap = (uint64_t)1 << (cpp ? 18 : 20);
-    if (cpp) chunk_cap = std::max<uint64_t>(1, std::min<uint64_t>(chunk_cap, ((uint64_t)1 << 30) / (pb * RW)));
+    uint64_t chunk_cap = (uint64_t)1 << 18;
+    chunk_cap = std::max<uint64_t>(1, std::min<uint64_t>(chunk_cap, ((uint64_t)1 << 30) / (pb * RW)));
     const uint64_t chunk = std::min<uint64_t>(nw_call, chunk_cap);
     const size_t need = chunk * (size_t)(walk_steps + 1);
     if (c->walk_buf_n < need) {
@@ -1042,47 +1060,43 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
     a.begin = 0; a.count = 0; a.total = total; a.seed = seed; a.alpha0 = alpha0; a.reg = 0.0f;
     a.dpad = c->dpad; a.K = K; a.model = SMORE_LINE2; a.mode = mode;
     a.tcum = c->d_tcum;
-    // the Go walk models' pair kernel (train_go.hip go_walk_pairs_kernel)
-    // keeps W_v in registers over a walk position's run and adds it back; its
-    // context rows take the lossless atomic scatter when hybrid is asked for
-    if (c->semantics == SMORE_SEM_GO && mode == SMORE_HYBRID) {
+    // the Go pair kernel keeps W_v in registers over a walk position's run and
+    // adds it back; its context rows take the lossless atomic scatter when
+    // hybrid is asked for
+    if (go && mode == SMORE_HYBRID) {
         mode = SMORE_ATOMIC;
         a.mode = mode;
     }
-    const int grid = mode != SMORE_SERIAL ? c->cus * 4 : 1;   // Go walk kernel (as the Go edge path)
-    EdgeArgs ar = a;   // the update kernel over pair records (C++ semantics)
-    int ugrid = 1;
-    if (cpp) {
-        if (c->pair_walks < chunk + 1) {
-            dfree(c->d_pcount);
-            dfree(c->d_poff);
-            c->pair_walks = 0;
-            HIPCHK(c, hipMalloc((void**)&c->d_pcount, (chunk + 1) * sizeof(uint32_t)));
-            HIPCHK(c, hipMalloc((void**)&c->d_poff, (chunk + 1) * sizeof(uint64_t)));
-            c->pair_walks = chunk + 1;
-        }
-        if (c->rec_cap < chunk * pb * RW) {
-            dfree(c->d_rec);
-            c->rec_cap = 0;
-            HIPCHK(c, hipMalloc(&c->d_rec, chunk * pb * RW * sizeof(int32_t)));
-            c->rec_cap = chunk * pb * RW;
-        }
-        const bool combine = mode == SMORE_HYBRID;
-        ar.sh_rows = combine ? std::min(c->sh_max, 8192 / std::max(1, c->dpad)) : 0;
-        ar.alpha_rec = 1;
-        ar.work = c->d_work;
-        ar.count = chunk * pb;   // grid for the most pairs a chunk can have
-        ugrid = edge_grid(c, ar);
-        if (mode == SMORE_HYBRID) {
-            const int64_t M = (int64_t)ugrid * (256 / lanes_of(c->dpad));
-            if ((rc = build_hot_maps(c, SMORE_LINE2, K, M))) return rc;
-        }
-        ar.g = dev_graph(c);
-        ar.sh_rows = combine ? c->sh_rows : 0;
-        ar.sh_hash = c->d_sh_hash;
-        ar.sh_ids = c->d_sh_ids;
-        ar.sh_flush = std::max(1, c->sh_flush_eff);
+    EdgeArgs ar = a;   // the update kernel over pair records
+    if (c->pair_walks < chunk + 1) {
+        dfree(c->d_pcount);
+        dfree(c->d_poff);
+        c->pair_walks = 0;
+        HIPCHK(c, hipMalloc((void**)&c->d_pcount, (chunk + 1) * sizeof(uint32_t)));
+        HIPCHK(c, hipMalloc((void**)&c->d_poff, (chunk + 1) * sizeof(uint64_t)));
+        c->pair_walks = chunk + 1;
     }
+    if (c->rec_cap < chunk * pb * RW) {
+        dfree(c->d_rec);
+        c->rec_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_rec, chunk * pb * RW * sizeof(int32_t)));
+        c->rec_cap = chunk * pb * RW;
+    }
+    const bool combine = mode == SMORE_HYBRID;
+    ar.sh_rows = combine ? std::min(c->sh_max, 8192 / std::max(1, c->dpad)) : 0;
+    ar.alpha_rec = 1;
+    ar.work = c->d_work;
+    ar.count = chunk * pb;   // grid for the most pairs a chunk can have
+    const int ugrid = edge_grid(c, ar, false, go ? 2 : 0);
+    if (mode == SMORE_HYBRID) {
+        const int64_t M = (int64_t)ugrid * (256 / lanes_of(c->dpad));
+        if ((rc = build_hot_maps(c, SMORE_LINE2, K, M))) return rc;
+    }
+    ar.g = dev_graph(c);
+    ar.sh_rows = combine ? c->sh_rows : 0;
+    ar.sh_hash = c->d_sh_hash;
+    ar.sh_ids = c->d_sh_ids;
+    ar.sh_flush = std::max(1, c->sh_flush_eff);
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     for (uint64_t b = walk_begin; b < walk_end; b += chunk) {
         WalkArgs w;
@@ -1109,34 +1123,34 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
         w.ntypes = c->ntypes;
         w.npaths = npaths;
         w.slot_extra = rule >= 3 ? 1 : 0;   // metapath2vec: the path pick; CTDNE: the start time
-        const int64_t groups_per_block = 256 / lanes_of(c->dpad);
-        int g2 = grid;
-        if ((int64_t)g2 * groups_per_block > (int64_t)w.nwalks && mode != SMORE_SERIAL)
-            g2 = (int)std::max<int64_t>(1, ((int64_t)w.nwalks + groups_per_block - 1) / groups_per_block);
+        // walks, then their pair counts plus a zero at n: the exclusive scan's
+        // entry n is the chunk's pair total, which the update kernel reads on
+        // the device (no host round trip between chunks)
         if (rule == 4) {
             TemporalArgs tg{c->d_t_off, c->d_t_tgt, c->d_t_ts, c->d_t_min, c->d_t_max, c->t_max_time, time_window};
             HIPCHK(c, launch_go_ctdne_walk(tg, w, seed, c->stream));
-            HIPCHK(c, launch_go_pairs(a, w, g2, c->stream));
-        } else if (c->semantics == SMORE_SEM_GO) {
-            HIPCHK(c, launch_go_walk(a, w, g2, c->stream));
+        } else if (go) {
+            HIPCHK(c, launch_go_walk(a, w, 1, c->stream));
         } else {
-            // counts of walks [0, n) plus a zero at n: the exclusive scan's entry
-            // n is the chunk's pair total, which the update kernel reads on the
-            // device (no host round trip between chunks)
             HIPCHK(c, launch_walk_gen(ar.g, w, seed, c->stream));
-            HIPCHK(c, hipMemsetAsync(c->d_pcount + w.nwalks, 0, sizeof(uint32_t), c->stream));
-            HIPCHK(c, launch_pair_count(w, seed, c->d_pcount, c->stream));
-            HIPCHK(c, scan_pair_counts(c->d_pcount, c->d_poff, w.nwalks + 1, &c->d_scan_tmp, &c->scan_tmp_bytes,
-                                       c->stream));
-            HIPCHK(c, launch_pair_emit(ar.g, w, seed, K, alpha0, c->d_poff, c->d_rec, c->stream));
-            EdgeArgs ak = ar;
-            ak.begin = 0;
-            ak.count = w.nwalks * pb;
-            ak.count_dev = c->d_poff + w.nwalks;
-            ak.rec = c->d_rec;
-            HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
-            HIPCHK(c, launch_edge_train(ak, mode == SMORE_SERIAL ? 1 : ugrid, c->stream));
         }
+        HIPCHK(c, hipMemsetAsync(c->d_pcount + w.nwalks, 0, sizeof(uint32_t), c->stream));
+        if (go) HIPCHK(c, launch_go_pair_count(w, c->d_pcount, c->stream));
+        else HIPCHK(c, launch_pair_count(w, seed, c->d_pcount, c->stream));
+        HIPCHK(c, scan_pair_counts(c->d_pcount, c->d_poff, w.nwalks + 1, &c->d_scan_tmp, &c->scan_tmp_bytes,
+                                   c->stream));
+        if (go) HIPCHK(c, launch_go_pair_emit(ar.g, w, seed, K, alpha0, c->d_poff, c->d_rec, c->stream));
+        else HIPCHK(c, launch_pair_emit(ar.g, w, seed, K, alpha0, c->d_poff, c->d_rec, c->stream));
+        EdgeArgs ak = ar;
+        ak.begin = 0;
+        ak.count = w.nwalks * pb;
+        ak.count_dev = c->d_poff + w.nwalks;
+        ak.rec = c->d_rec;
+        HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
+        const int g = mode == SMORE_SERIAL ? 1 : ugrid;
+        if (!go) HIPCHK(c, launch_edge_train(ak, g, c->stream));
+        else if (mode == SMORE_ATOMIC) HIPCHK(c, launch_go_pair_a(ak, g, c->stream));
+        else HIPCHK(c, launch_go_pair_s(ak, g, c->stream));
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
@@ -1441,6 +1455,32 @@ int smore_delta_cycle(smore_ctx* c, void* T, void* S, void* D, void* R, float sc
     int rc;
     if ((rc = delta_args(c, T, S, D, R, n))) return rc;
     HIPCHK(c, launch_delta_cycle((float*)T, (float*)S, (float*)D, (float*)R, scale, (uint64_t)n, c->cus, c->stream));
+    return SMORE_OK;
+}
+
+static int delta_rows_args(smore_ctx* c, const void* T, const void* S, const void* D, const void* R,
+                           const void* scale, int64_t rows, int64_t stride) {
+    if (!c || !scale || rows < 0 || stride <= 0 || (stride & 3) || stride > (1 << 20))
+        return fail(c, SMORE_EINVAL, "delta rows: bad shape");
+    if ((uintptr_t)scale & 3) return fail(c, SMORE_EINVAL, "delta rows: scale must be 4-byte aligned");
+    return delta_args(c, T, S, D, R, rows * stride);
+}
+
+int smore_delta_end_rows(smore_ctx* c, void* T, void* S, const void* D, const void* R, const void* scale,
+                         int64_t rows, int64_t stride) {
+    int rc;
+    if ((rc = delta_rows_args(c, T, S, D, R, scale, rows, stride))) return rc;
+    HIPCHK(c, launch_delta_end_rows((float*)T, (float*)S, (const float*)D, (const float*)R, (const float*)scale,
+                                    (uint64_t)rows, (int)stride, c->cus, c->stream));
+    return SMORE_OK;
+}
+
+int smore_delta_cycle_rows(smore_ctx* c, void* T, void* S, void* D, void* R, const void* scale, int64_t rows,
+                           int64_t stride) {
+    int rc;
+    if ((rc = delta_rows_args(c, T, S, D, R, scale, rows, stride))) return rc;
+    HIPCHK(c, launch_delta_cycle_rows((float*)T, (float*)S, (float*)D, (float*)R, (const float*)scale,
+                                      (uint64_t)rows, (int)stride, c->cus, c->stream));
     return SMORE_OK;
 }
 

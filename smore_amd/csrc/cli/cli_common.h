@@ -53,11 +53,12 @@ static smore_ctx* open_context(int device) {
 struct Run {
     smore_group* g = nullptr;
     smore_ctx* ctx = nullptr;
-    // -gpus N: the replicas' exchange averages their deltas (SMORE_SYNC=mean,
-    // the default) or sums them (SMORE_SYNC=sum: every update applied once,
-    // with the hub rows synced between launches; it diverges at 4 and more
-    // replicas at the default exchange period)
-    int mean = 1;
+    // -gpus N: the replicas' exchange rule, SMORE_SYNC=adaptive (the default:
+    // per row the sum of the deltas for rows updated a few times per exchange,
+    // towards their mean for the hub rows), mean, or sum (every update applied
+    // once, with the hub rows synced between launches; it diverges at 4 and
+    // more replicas at the default exchange period), DESIGN.md 10
+    int mean = SMORE_SYNC_ADAPTIVE;
 };
 
 static Run open_run(int device, int gpus) {
@@ -73,7 +74,8 @@ static Run open_run(int device, int gpus) {
         exit(2);
     }
     r.ctx = smore_group_ctx(r.g, 0);
-    if (const char* e = getenv("SMORE_SYNC")) r.mean = strcmp(e, "sum") != 0;
+    if (const char* e = getenv("SMORE_SYNC"))
+        r.mean = !strcmp(e, "sum") ? SMORE_SYNC_SUM : !strcmp(e, "mean") ? SMORE_SYNC_MEAN : SMORE_SYNC_ADAPTIVE;
     return r;
 }
 

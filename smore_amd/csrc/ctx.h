@@ -113,7 +113,11 @@ struct smore_ctx {
     size_t ex_n = 0;                    // floats per exchanged table
     int ex_tables = 0;
     bool ex_pending = false;            // an all-reduce is in flight
-    int ex_mean = 0;
+    int ex_mode = 0;                    // SMORE_SYNC_* of the in-flight exchange
+    // adaptive exchange: per-row scales of the summed deltas per table and
+    // the (model, K, updates, c0, N) they were made for
+    float* ex_scale[2] = {nullptr, nullptr};
+    std::string ex_scale_key;
     // hub-row exchange between launches (hot_exchange.h): row ids and the
     // packed own-delta / all-reduced buffers per table
     int32_t* hot_idx[2] = {nullptr, nullptr};

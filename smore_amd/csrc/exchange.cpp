@@ -132,22 +132,30 @@ int exchange_reset(smore_ctx* c) {
     return SMORE_OK;
 }
 
+// the uniform scale of the summed deltas under the in-flight exchange's rule
+float rule_scale(const smore_ctx* c) { return c->ex_mode == SMORE_SYNC_MEAN ? 1.0f / (float)c->nranks : 1.0f; }
+
 // the fused passes of an exchange's begin on the context stream (folding the
 // in-flight exchange in first), then the hand-off event for the collective
-int exchange_passes(smore_ctx* c, int mean) {
+int exchange_passes(smore_ctx* c, int mode) {
     int rc;
     if ((rc = set_device(c))) return rc;
-    const float scale_prev = c->ex_mean ? 1.0f / (float)c->nranks : 1.0f;
+    if (mode < SMORE_SYNC_SUM || mode > SMORE_SYNC_ADAPTIVE) return fail(c, SMORE_EINVAL, "bad exchange rule");
+    if (mode == SMORE_SYNC_ADAPTIVE && !c->ex_scale[0])
+        return fail(c, SMORE_ESTATE, "adaptive exchange without row scales (smore_exchange_set_adaptive)");
     if (c->ex_pending) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ex_done, 0));
     for (int t = 0; t < c->ntables; ++t) {
         float* T = c->d_table[t];
         float* const* b = c->ex_buf[t];
-        if (c->ex_pending) HIPCHK(c, launch_delta_cycle(T, b[0], b[1], b[2], scale_prev, c->ex_n, c->cus, c->stream));
-        else HIPCHK(c, launch_delta_begin(T, b[0], b[1], b[2], c->ex_n, c->cus, c->stream));
+        if (!c->ex_pending) HIPCHK(c, launch_delta_begin(T, b[0], b[1], b[2], c->ex_n, c->cus, c->stream));
+        else if (c->ex_mode == SMORE_SYNC_ADAPTIVE)
+            HIPCHK(c, launch_delta_cycle_rows(T, b[0], b[1], b[2], c->ex_scale[t], (uint64_t)c->g->V, c->dpad, c->cus,
+                                              c->stream));
+        else HIPCHK(c, launch_delta_cycle(T, b[0], b[1], b[2], rule_scale(c), c->ex_n, c->cus, c->stream));
     }
     HIPCHK(c, hipEventRecord(c->ex_ready, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->ex_ready, 0));
-    c->ex_mean = mean;
+    c->ex_mode = mode;
     return SMORE_OK;
 }
 
@@ -172,14 +180,57 @@ int exchange_end(smore_ctx* c) {
     int rc;
     if ((rc = check_comm(c))) return rc;
     if (!c->ex_pending) return SMORE_OK;
-    const float scale = c->ex_mean ? 1.0f / (float)c->nranks : 1.0f;
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->ex_done, 0));
     for (int t = 0; t < c->ntables; ++t) {
         float* const* b = c->ex_buf[t];
-        HIPCHK(c, launch_delta_end(c->d_table[t], b[0], b[1], b[2], scale, c->ex_n, c->cus, c->stream));
+        if (c->ex_mode == SMORE_SYNC_ADAPTIVE)
+            HIPCHK(c, launch_delta_end_rows(c->d_table[t], b[0], b[1], b[2], c->ex_scale[t], (uint64_t)c->g->V,
+                                            c->dpad, c->cus, c->stream));
+        else HIPCHK(c, launch_delta_end(c->d_table[t], b[0], b[1], b[2], rule_scale(c), c->ex_n, c->cus, c->stream));
     }
     c->ex_pending = false;
     return SMORE_OK;
+}
+
+// the adaptive rule's per-row scales (smore_hip.h SMORE_SYNC_ADAPTIVE) for
+// `updates` samples of `model` per rank per exchange over `nranks` ranks, from
+// the sampler marginals of c's graph
+int adaptive_scales(smore_ctx* c, int model, int K, double updates, double c0, int nranks,
+                    std::vector<float> (&out)[2]) {
+    const int64_t V = c->g->V;
+    std::vector<double> rate((size_t)V);
+    for (int t = 0; t < c->ntables; ++t) {
+        int rc;
+        if ((rc = smore_row_rates(c, model, K, t, V, rate.data()))) return rc;
+        out[t].resize((size_t)V);
+        for (int64_t v = 0; v < V; ++v) {
+            const double k = rate[v] * updates * nranks;
+            const double sv = k > c0 ? c0 / k : 1.0;
+            out[t][v] = (float)(sv + (1.0 - sv) / nranks);
+        }
+    }
+    return SMORE_OK;
+}
+
+int upload_scales(smore_ctx* c, const std::vector<float> (&sc)[2], const std::string& key) {
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    // an in-flight exchange's end reads the old scales on the stream: replace
+    // them only after it drained
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int t = 0; t < 2; ++t) {
+        dfree(c->ex_scale[t]);
+        if (t < c->ntables && (rc = upload(c, c->ex_scale[t], sc[t].data(), sc[t].size()))) return rc;
+    }
+    c->ex_scale_key = key;
+    return SMORE_OK;
+}
+
+std::string scale_key(int model, int K, double updates, double c0, int nranks, const smore_ctx* c) {
+    char key[160];
+    snprintf(key, sizeof key, "%d/%d/%.17g/%.17g/%d/%lld/%d", model, K, updates, c0, nranks, (long long)c->g->V,
+             c->ntables);
+    return key;
 }
 
 }  // namespace
@@ -197,6 +248,8 @@ void smore_exchange_release(smore_ctx* c) {
     }
     c->hot_n = 0;
     c->hot_ex_key.clear();
+    for (float*& p : c->ex_scale) dfree(p);
+    c->ex_scale_key.clear();
     if (c->comm && c->own_comm) {
         if (Rccl* L = rccl()) (void)L->destroy((ncclComm_t)c->comm);
     }
@@ -216,6 +269,7 @@ struct smore_group {
     // automatic, 0: off) and training launches per exchange round
     int64_t hot_rows = -1;
     int launches = 8;
+    double c0 = 64.0;   // adaptive exchange (smore_group_set_adaptive)
 };
 
 namespace {
@@ -239,10 +293,10 @@ int replicate_graph(smore_group* g) {
     return SMORE_OK;
 }
 
-int group_exchange_begin(smore_group* g, int mean) {
+int group_exchange_begin(smore_group* g, int rule) {
     int rc;
     for (size_t r = 0; r < g->ctx.size(); ++r)
-        if ((rc = exchange_passes(g->ctx[r], mean))) return gfail(g, (int)r, rc);
+        if ((rc = exchange_passes(g->ctx[r], rule))) return gfail(g, (int)r, rc);
     Rccl* L = rccl();
     ncclResult_t nr = L->group_start();
     for (size_t r = 0; r < g->ctx.size() && nr == ncclSuccess; ++r) {
@@ -338,21 +392,34 @@ int group_sync(smore_group* g) {
 // The group training round structure: round k, replica r queues units
 // [begin + (k n + r) per, + per) of the global range on its stream (run(ctx, b, e)
 // must not synchronize), then the group folds the previous exchange in and
-// starts this round's all-reduce, which overlaps round k+1.  With the hub-row
-// exchange on (sum exchange, hub rows of `model` with K negatives), each
-// replica's share of a round runs as g->launches launches and the hub rows are
-// synced after each.
+// starts this round's all-reduce, which overlaps round k+1.  rule: SMORE_SYNC_*;
+// the adaptive rule's row scales are made for `model` with K negatives at per
+// * upu updates per replica per exchange (upu: updates per unit, e.g. the
+// expected pairs of a walk).  With the hub-row exchange on (sum rule), each
+// replica's share of a round runs as g->launches launches and the hub rows
+// are synced after each.
 template <class F>
-static int group_rounds(smore_group* g, uint64_t begin, uint64_t end, uint64_t per, int mean, F&& run,
-                        int model = SMORE_LINE2, int K = 5) {
+static int group_rounds(smore_group* g, uint64_t begin, uint64_t end, uint64_t per, int rule, F&& run,
+                        int model = SMORE_LINE2, int K = 5, double upu = 1.0) {
     const size_t n = g->ctx.size();
     int rc;
     if (end <= begin) return SMORE_OK;
+    if (rule < SMORE_SYNC_SUM || rule > SMORE_SYNC_ADAPTIVE) return gfail(g, 0, fail(g->ctx[0], SMORE_EINVAL, "bad exchange rule"));
     for (size_t r = 0; r < n; ++r)
         if ((rc = exchange_reset(g->ctx[r]))) return gfail(g, (int)r, rc);
+    if (rule == SMORE_SYNC_ADAPTIVE) {
+        const double updates = (double)per * upu;
+        const std::string key = scale_key(model, K, updates, g->c0, (int)n, g->ctx[0]);
+        if (g->ctx[0]->ex_scale_key != key) {
+            std::vector<float> sc[2];
+            if ((rc = adaptive_scales(g->ctx[0], model, K, updates, g->c0, (int)n, sc))) return gfail(g, 0, rc);
+            for (size_t r = 0; r < n; ++r)
+                if ((rc = upload_scales(g->ctx[r], sc, key))) return gfail(g, (int)r, rc);
+        }
+    }
     int64_t rows = g->hot_rows < 0 ? std::min<int64_t>(65536, g->ctx[0]->g->V / 8) : g->hot_rows;
     rows = std::min<int64_t>(rows, g->ctx[0]->g->V);
-    const bool hot = !mean && rows > 0 && g->launches > 1;
+    const bool hot = rule == SMORE_SYNC_SUM && rows > 0 && g->launches > 1;
     if (hot && (rc = ensure_hot(g, model, K, rows))) return rc;
     const int sub = hot ? g->launches : 1;
     const uint64_t count = end - begin;
@@ -367,11 +434,19 @@ static int group_rounds(smore_group* g, uint64_t begin, uint64_t end, uint64_t p
             }
             if (hot && (rc = group_hot_exchange(g))) return rc;
         }
-        if ((rc = group_exchange_begin(g, mean))) return rc;
+        if ((rc = group_exchange_begin(g, rule))) return rc;
     }
     for (size_t r = 0; r < n; ++r)
         if ((rc = exchange_end(g->ctx[r]))) return gfail(g, (int)r, rc);
     return group_sync(g);
+}
+
+// expected skip-gram pairs of one walk (the adaptive rule's updates per walk):
+// C++ DeepWalk shrinks the window uniformly (window + 1 pairs per position on
+// average), Go's is fixed (2 window)
+static double walk_pairs(const smore_ctx* c, int steps, int window) {
+    const double L = (double)steps + 1.0, w = std::max(1, window);
+    return L * (c->semantics == SMORE_SEM_GO ? std::min(2.0 * w, L - 1.0) : std::min(w + 1.0, L - 1.0));
 }
 
 extern "C" {
@@ -409,12 +484,24 @@ int smore_exchange_reset(smore_ctx* c) { return exchange_reset(c); }
 int smore_exchange_begin(smore_ctx* c, int mean) {
     int rc;
     if ((rc = check_comm(c))) return rc;
-    if ((rc = exchange_passes(c, mean != 0))) return rc;
+    if ((rc = exchange_passes(c, mean))) return rc;
     if ((rc = exchange_collective(c))) return rc;
     return exchange_posted(c);
 }
 
 int smore_exchange_end(smore_ctx* c) { return exchange_end(c); }
+
+int smore_exchange_set_adaptive(smore_ctx* c, int model, int K, double updates, double c0) {
+    if (!c || !(updates > 0.0) || !(c0 > 0.0)) return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    if (c->ntables < 1) return fail(c, SMORE_ESTATE, "tables not allocated");
+    const std::string key = scale_key(model, K, updates, c0, c->nranks, c);
+    if (c->ex_scale_key == key) return SMORE_OK;
+    std::vector<float> sc[2];
+    int rc;
+    if ((rc = adaptive_scales(c, model, K, updates, c0, c->nranks, sc))) return rc;
+    return upload_scales(c, sc, key);
+}
 
 // ---------------------------------------------------------------- one process, N GPUs
 int smore_group_create(const int* devices, int n, smore_group** out) {
@@ -466,6 +553,12 @@ void smore_group_destroy(smore_group* g) {
 }
 
 int smore_group_size(const smore_group* g) { return g ? (int)g->ctx.size() : 0; }
+
+int smore_group_set_adaptive(smore_group* g, double c0) {
+    if (!g || !(c0 > 0.0)) return SMORE_EINVAL;
+    g->c0 = c0;
+    return SMORE_OK;
+}
 
 int smore_group_set_hot_exchange(smore_group* g, int64_t rows, int launches) {
     if (!g || launches < 1) return SMORE_EINVAL;
@@ -593,7 +686,7 @@ int smore_group_train_deepwalk(smore_group* g, uint64_t walk_begin, uint64_t wal
                             return smore_train_deepwalk_async(c, b, e, walk_times, walk_steps, window, K, alpha0,
                                                               seed, order, mode);
                         },
-                        SMORE_LINE2, K);
+                        SMORE_LINE2, K, walk_pairs(g->ctx[0], walk_steps, window));
 }
 
 int smore_group_train_node2vec(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
@@ -608,7 +701,7 @@ int smore_group_train_node2vec(smore_group* g, uint64_t walk_begin, uint64_t wal
                             return smore_train_node2vec_async(c, b, e, walk_times, walk_steps, window, K, alpha0, p,
                                                               q, seed, order, mode);
                         },
-                        SMORE_LINE2, K);
+                        SMORE_LINE2, K, walk_pairs(g->ctx[0], walk_steps, window));
 }
 
 int smore_group_train_metapath2vec(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
@@ -625,7 +718,7 @@ int smore_group_train_metapath2vec(smore_group* g, uint64_t walk_begin, uint64_t
                                                                   alpha0, paths, path_lens, npaths, seed, order,
                                                                   mode);
                         },
-                        SMORE_LINE2, K);
+                        SMORE_LINE2, K, walk_pairs(g->ctx[0], walk_steps, window));
 }
 
 int smore_group_train_ctdne(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
@@ -640,7 +733,7 @@ int smore_group_train_ctdne(smore_group* g, uint64_t walk_begin, uint64_t walk_e
                             return smore_train_ctdne_async(c, b, e, walk_times, walk_steps, window, K, alpha0,
                                                            time_window, seed, order, mode);
                         },
-                        SMORE_LINE2, K);
+                        SMORE_LINE2, K, walk_pairs(g->ctx[0], walk_steps, window));
 }
 
 int smore_group_train_walklets(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
@@ -655,7 +748,7 @@ int smore_group_train_walklets(smore_group* g, uint64_t walk_begin, uint64_t wal
                             return smore_train_walklets_async(c, b, e, walk_times, walk_steps, window_min,
                                                               window_max, K, alpha0, seed, mode);
                         },
-                        SMORE_LINE2, K);
+                        SMORE_LINE2, K, 2.0 * walk_pairs(g->ctx[0], walk_steps, window_max - window_min));
 }
 
 int smore_group_train_app(smore_group* g, uint64_t unit_begin, uint64_t unit_end, int walk_times, int sample_times,
@@ -670,7 +763,7 @@ int smore_group_train_app(smore_group* g, uint64_t unit_begin, uint64_t unit_end
                             return smore_train_app_async(c, b, e, walk_times, sample_times, jump, K, alpha0, seed,
                                                          order, mode);
                         },
-                        SMORE_LINE2, K);
+                        SMORE_LINE2, K, (double)sample_times);
 }
 
 int smore_group_train_hpe(smore_group* g, uint64_t begin, uint64_t count, uint64_t total, int walk_steps, int K,
@@ -682,7 +775,7 @@ int smore_group_train_hpe(smore_group* g, uint64_t begin, uint64_t count, uint64
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_hpe_async(c, b, e - b, total, walk_steps, K, reg, alpha0, seed, mode);
                         },
-                        SMORE_LINE2, K);
+                        SMORE_LINE2, K, (double)walk_steps);
 }
 
 }  // extern "C"

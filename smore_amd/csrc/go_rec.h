@@ -324,6 +324,169 @@ go_rec_kernel(EdgeArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ Go walk pairs
+// Go SkipGrams pair records (train_go.hip go_pair_emit_kernel: {walk[i],
+// walk[j], negatives, .., alpha bits at word 2 + KMAX}, walk-major) -> Go
+// UpdatePair (optimizer.go:21-58) per pair, for Go DeepWalk, node2vec,
+// metapath2vec and CTDNE.  A walk position's pairs are consecutive and share
+// W_v, which only they change (contexts and negatives are C rows): each group
+// takes a contiguous slice of CH_ROUNDS records and keeps W_v in registers
+// while v repeats, the Go loop's per-pair W_v += vg included, and puts the row
+// back when v changes -- stored in the serial mode (the sequential value),
+// otherwise the run's summed gradient added atomically (no W update lost).
+// Context rows: atomic adds of each update's delta (MODE_ATOMIC) or plain
+// stores (MODE_STORE).  Serial (a.mode 2): one group, all records in order.
+template <int G, int M, int KMAX, int MODE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(waves_of(MODE))))
+go_pair_kernel(EdgeArgs a) {
+    static_assert(MODE != MODE_HYBRID, "Go walk pairs: atomic or plain stores");
+    __shared__ float s_sig[1001];
+    for (int i = threadIdx.x; i < 1001; i += blockDim.x) s_sig[i] = a.sig[i];
+    __syncthreads();
+    const int lane = threadIdx.x & (G - 1);
+    const uint64_t count = a.count_dev ? *a.count_dev : a.count;
+    const uint64_t gpb = blockDim.x / G, gib = threadIdx.x / G;
+    bool ev[M];
+    row_valid<G, M>(ev, lane, a.dpad);
+    constexpr int RW = rec_width(KMAX);
+    const int dpad = a.dpad;
+    const bool serial = a.mode == 2;
+    auto slice = [&](uint64_t s0, uint64_t s1) {
+        int32_t cv = -1;
+        float wv[M], wsum[M];
+        auto flush = [&]() {
+            if (cv < 0) return;
+            if (serial) st_row<G, M>(a.W + (int64_t)cv * dpad, wv, lane, ev);
+            else atomic_row<G, M>(a.W + (int64_t)cv * dpad, wsum, lane, dpad);
+        };
+        for (uint64_t t = s0; t < s1; ++t) {
+            const i32x4* p = reinterpret_cast<const i32x4*>(a.rec + t * RW);
+            i32x4 r[RW / 4];
+#pragma unroll
+            for (int q = 0; q < RW / 4; ++q) r[q] = __builtin_nontemporal_load(p + q);
+            const int32_t v = r[0][0], c = r[0][1];
+            if (c < 0) continue;
+            const float alpha = __int_as_float(r[(2 + KMAX) / 4][(2 + KMAX) % 4]);
+            if (v != cv) {
+                flush();
+                cv = v;
+                ld_row<G, M>(wv, a.W + (int64_t)v * dpad, lane, ev);
+#pragma unroll
+                for (int m = 0; m < M; ++m) wsum[m] = 0.0f;
+            }
+            // the context's row and the negatives' (a negative equal to the
+            // context is skipped, not redrawn; repeats start from the first)
+            int32_t id[KMAX + 1];
+            id[0] = c;
+#pragma unroll
+            for (int k = 1; k <= KMAX; ++k) {
+                const int32_t x = k - 1 < a.K ? r[(k + 1) / 4][(k + 1) % 4] : -1;
+                id[k] = (x < 0 || x == c) ? -1 : x;
+            }
+            float rows[KMAX + 1][M];
+#pragma unroll
+            for (int k = 0; k <= KMAX; ++k)
+                ld_row<G, M>(rows[k], a.C + (int64_t)(id[k] < 0 ? 0 : id[k]) * dpad, lane, ev, id[k] >= 0);
+#pragma unroll
+            for (int k = 2; k <= KMAX; ++k)
+#pragma unroll
+                for (int k2 = 1; k2 < k; ++k2)
+                    if (id[k2] >= 0 && id[k2] == id[k]) {
+#pragma unroll
+                        for (int m = 0; m < M; ++m) rows[k][m] = rows[k2][m];
+                    }
+            float vg[M], cg[M];
+            {
+                const float grad = alpha * (1.0f - fast_sigmoid(go_dot<G, M>(wv, rows[0]), s_sig));
+#pragma unroll
+                for (int m = 0; m < M; ++m) {
+                    vg[m] = grad * rows[0][m];
+                    cg[m] = grad * wv[m];
+                }
+            }
+#pragma unroll
+            for (int k = 1; k <= KMAX; ++k) {
+                if (id[k] < 0) continue;
+                const float gr = alpha * (0.0f - fast_sigmoid(go_dot<G, M>(wv, rows[k]), s_sig));
+                float nk[M], dk[M];
+#pragma unroll
+                for (int m = 0; m < M; ++m) {
+                    dk[m] = gr * wv[m];
+                    vg[m] = vg[m] + gr * rows[k][m];
+                    nk[m] = rows[k][m] + dk[m];
+                }
+                bool last = true;
+#pragma unroll
+                for (int k2 = k + 1; k2 <= KMAX; ++k2)
+                    if (id[k2] == id[k]) {
+                        last = false;
+#pragma unroll
+                        for (int m = 0; m < M; ++m) rows[k2][m] = nk[m];
+                    }
+                float* row = a.C + (int64_t)id[k] * dpad;
+                if (MODE == MODE_ATOMIC) atomic_row<G, M>(row, dk, lane, dpad);
+                else if (last) st_row<G, M>(row, nk, lane, ev);
+            }
+            {
+                float* row = a.C + (int64_t)c * dpad;
+                if (MODE == MODE_ATOMIC) {
+                    atomic_row<G, M>(row, cg, lane, dpad);
+                } else {
+                    float nc[M];
+#pragma unroll
+                    for (int m = 0; m < M; ++m) nc[m] = rows[0][m] + cg[m];
+                    st_row<G, M>(row, nc, lane, ev);
+                }
+            }
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+                wv[m] = wv[m] + vg[m];
+                wsum[m] = wsum[m] + vg[m];
+            }
+        }
+        flush();
+    };
+    if (serial) {
+        if (blockIdx.x == 0 && gib == 0) slice(0, count);
+        return;
+    }
+    __shared__ uint64_t s_next;
+    const uint64_t span = CH_ROUNDS * gpb;
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) s_next = atomicAdd(a.work, 1ull) * span;
+        __syncthreads();
+        const uint64_t c0 = s_next;
+        if (c0 >= count) break;
+        const uint64_t lim = c0 + span < count ? c0 + span : count;
+        const uint64_t s0 = c0 + gib * CH_ROUNDS;
+        slice(s0 < lim ? s0 : lim, s0 + CH_ROUNDS < lim ? s0 + CH_ROUNDS : lim);
+    }
+}
+
+template <int KMAX, int MODE>
+struct GoPairInst {
+    static hipError_t launch(const EdgeArgs& a, int grid, hipStream_t st) {
+        const int G = lanes_of(a.dpad), M = regs_of(a.dpad);
+#define X(g, m)                                                                          \
+    if (G == g && M == m) {                                                              \
+        hipLaunchKernelGGL((go_pair_kernel<g, m, KMAX, MODE>), dim3(grid), dim3(256), 0, st, a); \
+        return hipGetLastError();                                                        \
+    }
+        SMORE_FOR_EACH_GM(X)
+#undef X
+        return hipErrorInvalidValue;
+    }
+    static const void* symbol(const EdgeArgs& a) {
+        const int G = lanes_of(a.dpad), M = regs_of(a.dpad);
+#define X(g, m) \
+    if (G == g && M == m) return (const void*)go_pair_kernel<g, m, KMAX, MODE>;
+        SMORE_FOR_EACH_GM(X)
+#undef X
+        return nullptr;
+    }
+};
+
 template <int KMAX, int MODE>
 struct GoRecInst {
     static hipError_t launch(const EdgeArgs& a, int grid, hipStream_t st) {
@@ -358,5 +521,16 @@ struct GoRecInst {
     }                                                                                           \
     const void* go_rec_symbol_##name(const EdgeArgs& a) {                                       \
         return a.K <= 5 ? GoRecInst<5, MODE>::symbol(a) : GoRecInst<10, MODE>::symbol(a);        \
+    }                                                                                           \
+    }
+
+// defines launch_go_pair_<name>(a, grid, st) and go_pair_symbol_<name>(a)
+#define SMORE_GO_PAIR_INST(name, MODE)                                                          \
+    namespace smore {                                                                           \
+    hipError_t launch_go_pair_##name(const EdgeArgs& a, int grid, hipStream_t st) {             \
+        return a.K <= 5 ? GoPairInst<5, MODE>::launch(a, grid, st) : GoPairInst<10, MODE>::launch(a, grid, st); \
+    }                                                                                           \
+    const void* go_pair_symbol_##name(const EdgeArgs& a) {                                      \
+        return a.K <= 5 ? GoPairInst<5, MODE>::symbol(a) : GoPairInst<10, MODE>::symbol(a);      \
     }                                                                                           \
     }

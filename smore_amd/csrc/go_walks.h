@@ -18,7 +18,17 @@ struct TemporalArgs {
 
 // walk kernel: walks of [w.walk_begin, + w.nwalks) into w.walks / w.lens
 hipError_t launch_go_ctdne_walk(const TemporalArgs& t, const WalkArgs& w, uint64_t seed, hipStream_t st);
-// Go SkipGrams + UpdatePair over walks already in w.walks / w.lens
-hipError_t launch_go_pairs(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st);
+// Go SkipGrams of the walks in w.walks / w.lens as pair records (train_go.hip):
+// per-walk pair counts (fixed window: a function of the length), then, at the
+// exclusive-scanned offsets, the records
+hipError_t launch_go_pair_count(const WalkArgs& w, uint32_t* count, hipStream_t st);
+hipError_t launch_go_pair_emit(const DevGraph& g, const WalkArgs& w, uint64_t seed, int K, double alpha0,
+                               const uint64_t* off, int32_t* rec, hipStream_t st);
+// Go UpdatePair over pair records (go_rec.h go_pair_kernel; train_go_rec_*.hip):
+// mode 2 serial (the Go loop's order), 1 atomic, 0 plain stores
+hipError_t launch_go_pair_s(const EdgeArgs& a, int grid, hipStream_t st);
+hipError_t launch_go_pair_a(const EdgeArgs& a, int grid, hipStream_t st);
+const void* go_pair_symbol_s(const EdgeArgs& a);
+const void* go_pair_symbol_a(const EdgeArgs& a);
 
 }  // namespace smore

@@ -13,6 +13,12 @@
 namespace smore {
 hipError_t launch_hot_pack(const float* T, const float* S, const int32_t* idx, uint64_t n, int dpad, float* P,
                            float* R, int cus, hipStream_t st);
+// the delta end / cycle passes with a per-row scale (adaptive exchange):
+// row i of `rows` (dpad floats each) uses scale[i]
+hipError_t launch_delta_end_rows(float* T, float* S, const float* D, const float* R, const float* scale,
+                                 uint64_t rows, int dpad, int cus, hipStream_t st);
+hipError_t launch_delta_cycle_rows(float* T, float* S, float* D, float* R, const float* scale, uint64_t rows,
+                                   int dpad, int cus, hipStream_t st);
 hipError_t launch_hot_unpack(float* T, float* S, const int32_t* idx, uint64_t n, int dpad, const float* P,
                              const float* R, int cus, hipStream_t st);
 }  // namespace smore

@@ -62,6 +62,44 @@ __global__ void __launch_bounds__(256) delta_cycle_kernel(float4* __restrict__ T
     }
 }
 
+// the adaptive exchange's end / cycle: the same arithmetic with row i / dp4's
+// scale (a float4 never straddles two rows: dpad % 4 == 0)
+__global__ void __launch_bounds__(256) delta_end_rows_kernel(float4* __restrict__ T, float4* __restrict__ S,
+                                                             const float4* __restrict__ D,
+                                                             const float4* __restrict__ R,
+                                                             const float* __restrict__ scale, uint64_t n4, int dp4) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const float sc = scale[i / (uint64_t)dp4];
+        const float4 r = R[i], d = D[i];
+        const float4 x = make_float4(sc * r.x - d.x, sc * r.y - d.y, sc * r.z - d.z, sc * r.w - d.w);
+        float4 t = T[i], s = S[i];
+        t.x += x.x; t.y += x.y; t.z += x.z; t.w += x.w;
+        s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
+        T[i] = t;
+        S[i] = s;
+    }
+}
+
+__global__ void __launch_bounds__(256) delta_cycle_rows_kernel(float4* __restrict__ T, float4* __restrict__ S,
+                                                               float4* __restrict__ D, float4* __restrict__ R,
+                                                               const float* __restrict__ scale, uint64_t n4,
+                                                               int dp4) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const float sc = scale[i / (uint64_t)dp4];
+        const float4 r = R[i], d = D[i], t = T[i], s = S[i];
+        const float4 x = make_float4(sc * r.x - d.x, sc * r.y - d.y, sc * r.z - d.z, sc * r.w - d.w);
+        const float4 tn = make_float4(t.x + x.x, t.y + x.y, t.z + x.z, t.w + x.w);
+        const float4 sn = make_float4(s.x + x.x, s.y + x.y, s.z + x.z, s.w + x.w);
+        const float4 dn = make_float4(tn.x - sn.x, tn.y - sn.y, tn.z - sn.z, tn.w - sn.w);
+        T[i] = tn;
+        D[i] = dn;
+        R[i] = dn;
+        S[i] = tn;
+    }
+}
+
 // hub-row exchange passes (hot_exchange.h): element i of the packed buffers
 // is element i % dpad of row idx[i / dpad]; 16 B per lane (dpad % 4 == 0)
 __global__ void __launch_bounds__(256) hot_pack_kernel(const float4* __restrict__ T, const float4* __restrict__ S,
@@ -142,6 +180,24 @@ hipError_t launch_hot_unpack(float* T, float* S, const int32_t* idx, uint64_t n,
     hipLaunchKernelGGL(hot_unpack_kernel, dim3(stream_grid(n4, cus)), dim3(256), 0, st, reinterpret_cast<float4*>(T),
                        reinterpret_cast<float4*>(S), idx, n4, dpad / 4, reinterpret_cast<const float4*>(P),
                        reinterpret_cast<const float4*>(R));
+    return hipGetLastError();
+}
+
+hipError_t launch_delta_end_rows(float* T, float* S, const float* D, const float* R, const float* scale,
+                                 uint64_t rows, int dpad, int cus, hipStream_t st) {
+    const uint64_t n4 = rows * (uint64_t)(dpad / 4);
+    hipLaunchKernelGGL(delta_end_rows_kernel, dim3(stream_grid(n4, cus)), dim3(256), 0, st,
+                       reinterpret_cast<float4*>(T), reinterpret_cast<float4*>(S),
+                       reinterpret_cast<const float4*>(D), reinterpret_cast<const float4*>(R), scale, n4, dpad / 4);
+    return hipGetLastError();
+}
+
+hipError_t launch_delta_cycle_rows(float* T, float* S, float* D, float* R, const float* scale, uint64_t rows,
+                                   int dpad, int cus, hipStream_t st) {
+    const uint64_t n4 = rows * (uint64_t)(dpad / 4);
+    hipLaunchKernelGGL(delta_cycle_rows_kernel, dim3(stream_grid(n4, cus)), dim3(256), 0, st,
+                       reinterpret_cast<float4*>(T), reinterpret_cast<float4*>(S), reinterpret_cast<float4*>(D),
+                       reinterpret_cast<float4*>(R), scale, n4, dpad / 4);
     return hipGetLastError();
 }
 

@@ -9,6 +9,8 @@
 //   * LINE order 1, BPR: on records, go_rec.h (this file draws them:
 //     go_draw_kernel);
 //   * DeepWalk: walks stop at a dead end, fixed window (pronet.go:292-333);
+//     the walks' pairs become records (go_pair_emit_kernel) for go_rec.h
+//     go_pair_kernel;
 //   * node2vec: the biased second-order walk (internal/models/node2vec), then
 //     the DeepWalk pairs;
 //   * metapath2vec: meta-path-typed uniform walks (internal/models/metapath2vec,
@@ -39,85 +41,6 @@ __device__ __forceinline__ int32_t go_target(const DevGraph& g, const double* tc
         else lo = mid + 1;
     }
     return untag(g.targets[off + lo]);
-}
-
-template <int G, int M>
-__device__ __forceinline__ void load_row(float (&r)[M], const float* T, int64_t row, int dpad, int lane,
-                                         const bool (&ev)[M]) {
-    ld_row<G, M>(r, T + row * dpad, lane, ev);
-}
-
-// scatter of a row: plain store of `val`, or atomic add of `delta`
-template <int G, int M, int MODE>
-__device__ __forceinline__ void put_row(float* T, int64_t row, int dpad, int lane, const bool (&ev)[M],
-                                        const float (&val)[M], const float (&delta)[M]) {
-    if constexpr (MODE == MODE_ATOMIC) atomic_row<G, M>(T + row * dpad, delta, lane, dpad);
-    else st_row<G, M>(T + row * dpad, val, lane, ev);
-}
-
-template <int G, int M>
-__device__ __forceinline__ float dotg(const float (&a)[M], const float (&b)[M]) {
-    float p = 0.0f;
-#pragma unroll
-    for (int m = 0; m < M; ++m) p = __builtin_fmaf(a[m], b[m], p);
-    return group_sum<G>(p);
-}
-
-// Go UpdatePair's context side (optimizer.go:21-58): given W_v in wv, updates
-// the negatives and C_c in memory and returns W_v's gradient in vg (the caller
-// applies it).  negs[] already drawn.
-template <int G, int M, int KMAX, int MODE>
-__device__ __forceinline__ void go_pair_ctx(const EdgeArgs& a, const float* s_sig, int lane, const bool (&ev)[M],
-                                            const float (&wv)[M], float (&vg)[M], int32_t c,
-                                            const int32_t (&negs)[KMAX], float alpha) {
-    const int dpad = a.dpad;
-    float cc[M], cg[M];
-    load_row<G, M>(cc, a.C, c, dpad, lane, ev);
-    float rows[KMAX][M];
-#pragma unroll
-    for (int j = 0; j < KMAX; ++j) {
-        const bool use = negs[j] >= 0 && negs[j] != c;
-        ld_row<G, M>(rows[j], a.C + (int64_t)(use ? negs[j] : 0) * dpad, lane, ev, use);
-    }
-#pragma unroll
-    for (int j = 1; j < KMAX; ++j)
-#pragma unroll
-        for (int j2 = 0; j2 < j; ++j2)
-            if (negs[j2] == negs[j]) {
-#pragma unroll
-                for (int m = 0; m < M; ++m) rows[j][m] = rows[j2][m];
-            }
-    {
-        const float grad = alpha * (1.0f - fast_sigmoid(dotg<G, M>(wv, cc), s_sig));
-#pragma unroll
-        for (int m = 0; m < M; ++m) { vg[m] = grad * cc[m]; cg[m] = grad * wv[m]; }
-    }
-#pragma unroll
-    for (int j = 0; j < KMAX; ++j) {
-        if (negs[j] < 0 || negs[j] == c) continue;
-        const float gr = alpha * (0.0f - fast_sigmoid(dotg<G, M>(wv, rows[j]), s_sig));
-        float nk[M], dk[M];
-#pragma unroll
-        for (int m = 0; m < M; ++m) {
-            dk[m] = gr * wv[m];
-            vg[m] = vg[m] + gr * rows[j][m];
-            nk[m] = rows[j][m] + dk[m];
-        }
-#pragma unroll
-        for (int j2 = j + 1; j2 < KMAX; ++j2)
-            if (negs[j2] == negs[j]) {
-#pragma unroll
-                for (int m = 0; m < M; ++m) rows[j2][m] = nk[m];
-            }
-        bool last = true;
-#pragma unroll
-        for (int j2 = j + 1; j2 < KMAX; ++j2) last = last && negs[j2] != negs[j];
-        if (MODE == MODE_ATOMIC || last) put_row<G, M, MODE>(a.C, negs[j], dpad, lane, ev, nk, dk);
-    }
-    float nc[M];
-#pragma unroll
-    for (int m = 0; m < M; ++m) nc[m] = cc[m] + cg[m];
-    put_row<G, M, MODE>(a.C, c, dpad, lane, ev, nc, cg);
 }
 
 // Go RandomWalk: stops at a dead end; step s draws slot s (stream 1).
@@ -326,68 +249,6 @@ hipError_t launch_go_ctdne_walk(const TemporalArgs& tg, const WalkArgs& w, uint6
     return hipGetLastError();
 }
 
-// Go SkipGrams (fixed window) + Go UpdatePair per pair; negatives from slot
-// L-1 (+ slot_extra).
-template <int G, int M, int KMAX, int MODE>
-__global__ void __launch_bounds__(256) go_walk_pairs_kernel(EdgeArgs a, WalkArgs w) {
-    __shared__ float s_sig[1001];
-    for (int i = threadIdx.x; i < 1001; i += blockDim.x) s_sig[i] = a.sig[i];
-    __syncthreads();
-    const int lane = threadIdx.x & (G - 1);
-    uint64_t group = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
-    uint64_t ngroups = ((uint64_t)gridDim.x * blockDim.x) / G;
-    if (a.mode == 2) {
-        if (group != 0) return;
-        ngroups = 1;
-    }
-    bool ev[M];
-    row_valid<G, M>(ev, lane, a.dpad);
-    const int stride = w.steps + 1;
-    for (uint64_t t = group; t < w.nwalks; t += ngroups) {
-        const uint64_t unit = w.walk_begin + t;
-        const int32_t* walk = w.walks + t * stride;
-        const int L = w.lens[t];
-        const float alpha = alpha_walk(unit, a.alpha0, w.total_walks);
-        uint32_t slot = (uint32_t)(L - 1 + w.slot_extra);
-        for (int i = 0; i < L; ++i) {
-            const int lo = i - w.window < 0 ? 0 : i - w.window;
-            const int hi = i + w.window + 1 > L ? L : i + w.window + 1;
-            // the pairs of position i share W_v = W[walk[i]], which only they
-            // change (contexts and negatives are C rows): it stays in registers
-            // over the run and goes back once -- the sequential values exactly
-            float wv[M], wsum[M];
-            load_row<G, M>(wv, a.W, walk[i], a.dpad, lane, ev);
-#pragma unroll
-            for (int m = 0; m < M; ++m) wsum[m] = 0.0f;
-            for (int j = lo; j < hi; ++j) {
-                if (j == i) continue;
-                SlotWords<G, 2 * KMAX> nw;
-                nw.draw(a.seed, 1, unit, slot, lane);
-                int32_t negs[KMAX];
-#pragma unroll
-                for (int n = 0; n < KMAX; ++n)
-                    negs[n] = n < a.K ? go_alias(a.g.ntab, a.g.V, nw.w[2 * n], nw.w[2 * n + 1]) : -1;
-                slot += 2 * a.K;
-                float vg[M];
-                go_pair_ctx<G, M, KMAX, MODE>(a, s_sig, lane, ev, wv, vg, walk[j], negs, alpha);
-#pragma unroll
-                for (int m = 0; m < M; ++m) {
-                    wv[m] = wv[m] + vg[m];
-                    wsum[m] = wsum[m] + vg[m];
-                }
-            }
-            // serial: the sequential value is stored; Hogwild (plain-store mode
-            // included): the run's summed gradient is ADDED, so updates other
-            // walks made to this row while the run held it are not overwritten
-            // (a run lasts up to 2 * window pairs, hub rows see many of them)
-            if (hi - lo > 1) {
-                if (a.mode == 2) put_row<G, M, MODE_STORE>(a.W, walk[i], a.dpad, lane, ev, wv, wsum);
-                else put_row<G, M, MODE_ATOMIC>(a.W, walk[i], a.dpad, lane, ev, wv, wsum);
-            }
-        }
-    }
-}
-
 // Go TargetSample keeping the target's tag (hybrid scatter).  unit_w: every
 // edge weight is 1, so tcum[off + e] == e + 1 exactly and the first e with
 // r <= tcum[off + e] is max(0, ceil(r) - 1) -- the binary search's answer
@@ -529,29 +390,90 @@ hipError_t launch_go_sample(const DevGraph& g, const double* tcum, uint64_t seed
     return hipGetLastError();
 }
 
-// ------------------------------------------------------------------ dispatch
-template <int G, int M, int KMAX>
-static hipError_t go_pairs(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st) {
-    if (a.mode == 1)
-        hipLaunchKernelGGL((go_walk_pairs_kernel<G, M, KMAX, MODE_ATOMIC>), dim3(grid), dim3(256), 0, st, a, w);
-    else
-        hipLaunchKernelGGL((go_walk_pairs_kernel<G, M, KMAX, MODE_STORE>), dim3(grid), dim3(256), 0, st, a, w);
+// ------------------------------------------------------------------ Go pair records
+// Go SkipGrams (pkg/pronet/pronet.go:310-333: fixed window, pairs (walk[i],
+// walk[j]) for j in [i - window, i + window], j != i, walk-major in i then j)
+// as records {walk[i], walk[j], n_1 .. n_K, -1 .., alpha bits at 2 + KMAX}
+// for go_pair_kernel (go_rec.h); pair p of a walk draws its K negatives from
+// slots L - 1 + slot_extra + 2K p .. (index, then p), stream 1 (the walk's
+// own steps take slots 0 .. L - 2, the start pick slot_extra of them).  The count of a walk depends on its length only.
+__device__ __forceinline__ uint32_t go_pair_count(int L, int window) {
+    uint32_t n = 0;
+    for (int i = 0; i < L; ++i) {
+        const int lo = i - window < 0 ? 0 : i - window;
+        const int hi = i + window + 1 > L ? L : i + window + 1;
+        n += (uint32_t)(hi - lo - 1);
+    }
+    return n;
+}
+
+__global__ void __launch_bounds__(256) go_pair_count_kernel(WalkArgs w, uint32_t* count) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= w.nwalks) return;
+    count[t] = go_pair_count(w.lens[t], w.window);
+}
+
+template <int KMAX>
+__global__ void __launch_bounds__(256) go_pair_emit_kernel(DevGraph g, WalkArgs w, uint64_t seed, int K,
+                                                           double alpha0, const uint64_t* off, int32_t* rec) {
+    constexpr int RW = rec_width(KMAX);
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= w.nwalks) return;
+    const int L = w.lens[t];
+    const int32_t* walk = w.walks + t * (uint64_t)(w.steps + 1);
+    const uint64_t unit = w.walk_begin + t;
+    const float alpha = alpha_walk(unit, alpha0, w.total_walks);
+    uint32_t slot = (uint32_t)(L - 1 + w.slot_extra);
+    uint32_t blk = 0xFFFFFFFFu;
+    uint4 b = make_uint4(0u, 0u, 0u, 0u);
+    auto word = [&](uint32_t j) -> uint32_t {
+        if ((j >> 2) != blk) {
+            blk = j >> 2;
+            b = philox_block(seed, 1, unit, blk);
+        }
+        return comp(b, (int)(j & 3));
+    };
+    int32_t* out = rec + off[t] * RW;
+    for (int i = 0; i < L; ++i) {
+        const int lo = i - w.window < 0 ? 0 : i - w.window;
+        const int hi = i + w.window + 1 > L ? L : i + w.window + 1;
+        for (int j = lo; j < hi; ++j) {
+            if (j == i) continue;
+            int32_t x[RW];
+            x[0] = walk[i];
+            x[1] = walk[j];
+#pragma unroll
+            for (int n = 0; n < RW - 2; ++n) x[2 + n] = -1;
+#pragma unroll
+            for (int n = 0; n < KMAX; ++n)
+                if (n < K) x[2 + n] = go_alias(g.ntab, g.V, word(slot + 2u * n), word(slot + 2u * n + 1u));
+            slot += 2u * (uint32_t)K;
+            x[2 + KMAX] = __float_as_int(alpha);
+            i32x4* o = reinterpret_cast<i32x4*>(out);
+#pragma unroll
+            for (int q = 0; q < RW / 4; ++q) o[q] = i32x4{x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]};
+            out += RW;
+        }
+    }
+}
+
+hipError_t launch_go_pair_count(const WalkArgs& w, uint32_t* count, hipStream_t st) {
+    hipLaunchKernelGGL(go_pair_count_kernel, dim3((unsigned)((w.nwalks + 255) / 256)), dim3(256), 0, st, w, count);
     return hipGetLastError();
 }
 
-hipError_t launch_go_pairs(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st) {
-    const int G = lanes_of(a.dpad), M = regs_of(a.dpad);
-#define X(g, m)                                                  \
-    if (G == g && M == m) {                                      \
-        if (a.K <= 5) return go_pairs<g, m, 5>(a, w, grid, st);  \
-        return go_pairs<g, m, 10>(a, w, grid, st);               \
-    }
-    SMORE_FOR_EACH_GM(X)
-#undef X
-    return hipErrorInvalidValue;
+hipError_t launch_go_pair_emit(const DevGraph& g, const WalkArgs& w, uint64_t seed, int K, double alpha0,
+                               const uint64_t* off, int32_t* rec, hipStream_t st) {
+    const dim3 grid((unsigned)((w.nwalks + 255) / 256));
+    if (K <= 5) hipLaunchKernelGGL((go_pair_emit_kernel<5>), grid, dim3(256), 0, st, g, w, seed, K, alpha0, off, rec);
+    else hipLaunchKernelGGL((go_pair_emit_kernel<10>), grid, dim3(256), 0, st, g, w, seed, K, alpha0, off, rec);
+    return hipGetLastError();
 }
 
+// the Go walk generators (DeepWalk, node2vec, metapath2vec): walks into
+// w.walks / w.lens; the pairs follow as records
 hipError_t launch_go_walk(const EdgeArgs& a, const WalkArgs& w, int grid, hipStream_t st) {
+    (void)grid;
     const int block = 256;
     if (w.rule == 3)
         hipLaunchKernelGGL(go_mp_walk_gen_kernel, dim3((unsigned)((w.nwalks + block - 1) / block)), dim3(block), 0, st,
@@ -562,9 +484,7 @@ hipError_t launch_go_walk(const EdgeArgs& a, const WalkArgs& w, int grid, hipStr
     else
         hipLaunchKernelGGL(go_walk_gen_kernel, dim3((unsigned)((w.nwalks + block - 1) / block)), dim3(block), 0, st,
                            a.g, a.tcum, w, a.seed);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    return launch_go_pairs(a, w, grid, st);
+    return hipGetLastError();
 }
 
 }  // namespace smore

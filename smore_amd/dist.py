@@ -10,7 +10,15 @@ rule
     T = T_snap + sum_r delta_r      (or the mean, --sync mean)
 
 With sum, every sample's update lands on every replica exactly once -- the
-multi-GPU analogue of the reference's single shared table.
+multi-GPU analogue of the reference's single shared table.  Added one
+exchange late, though, a hub row's summed deltas (thousands of updates per
+exchange on every rank, each computed against the stale row) overshoot, and
+training diverges at 4 and 8 ranks (tools/replica_sim.py).  The
+adaptive rule (the default) scales row i's summed delta by
+    s_i + (1 - s_i) / N,   s_i = min(1, c0 / k_i),
+k_i = the row's expected updates per exchange over all ranks (sampler
+marginals x samples per exchange x N): the sum for rows updated a few times
+per exchange, the mean for the hubs.
 
 Two schedules:
   DeltaAllReduce  synchronous: the collective runs between two steps.
@@ -74,6 +82,8 @@ class TorchPasses:
 
     @staticmethod
     def end(T, S, D, R, scale):
+        if torch.is_tensor(scale):          # per-row scale (adaptive rule)
+            scale = scale.view(-1, *([1] * (R.dim() - 1)))
         R.mul_(scale).sub_(D)
         T.add_(R)
         S.add_(R)
@@ -95,10 +105,18 @@ class HipPasses:
         self.pn.delta_begin(T.data_ptr(), S.data_ptr(), D.data_ptr(), R.data_ptr(), T.numel())
 
     def end(self, T, S, D, R, scale):
-        self.pn.delta_end(T.data_ptr(), S.data_ptr(), D.data_ptr(), R.data_ptr(), scale, T.numel())
+        if torch.is_tensor(scale):
+            self.pn.delta_end_rows(T.data_ptr(), S.data_ptr(), D.data_ptr(), R.data_ptr(), scale.data_ptr(),
+                                   T.shape[0], T.shape[1])
+        else:
+            self.pn.delta_end(T.data_ptr(), S.data_ptr(), D.data_ptr(), R.data_ptr(), scale, T.numel())
 
     def cycle(self, T, S, D, R, scale):
-        self.pn.delta_cycle(T.data_ptr(), S.data_ptr(), D.data_ptr(), R.data_ptr(), scale, T.numel())
+        if torch.is_tensor(scale):
+            self.pn.delta_cycle_rows(T.data_ptr(), S.data_ptr(), D.data_ptr(), R.data_ptr(), scale.data_ptr(),
+                                     T.shape[0], T.shape[1])
+        else:
+            self.pn.delta_cycle(T.data_ptr(), S.data_ptr(), D.data_ptr(), R.data_ptr(), scale, T.numel())
 
 
 class OverlapSync:
@@ -112,7 +130,7 @@ class OverlapSync:
     After end() every replica holds every rank's updates up to the matching
     begin(), plus its own since."""
 
-    def __init__(self, tensors, mean=False, group=None, passes=None, hot_idx=None):
+    def __init__(self, tensors, mean=False, group=None, passes=None, hot_idx=None, row_scale=None):
         self.T = list(tensors)
         self.S = [t.clone() for t in self.T]
         self.D = [torch.zeros_like(t) for t in self.T]
@@ -121,8 +139,10 @@ class OverlapSync:
         self.group = group
         self.passes = passes or TorchPasses()
         self.works = None
+        # adaptive rule: one per-row scale tensor per table (replaces `mean`)
+        self.row_scale = list(row_scale) if row_scale is not None else None
         # hub rows (one int64 index tensor per table) exchanged by hot(); sum only
-        self.hot_idx = [] if (mean or not hot_idx) else list(hot_idx)
+        self.hot_idx = [] if (mean or row_scale is not None or not hot_idx) else list(hot_idx)
 
     def hot(self):
         """Synchronous exchange of the hub rows between two training launches:
@@ -141,15 +161,16 @@ class OverlapSync:
         if self.works is not None:      # fold the previous exchange in and start this one: one pass
             for w in self.works:
                 w.wait()
-            scale = self._scale()
-            for T, S, D, R in zip(self.T, self.S, self.D, self.R):
-                self.passes.cycle(T, S, D, R, scale)
+            for i, (T, S, D, R) in enumerate(zip(self.T, self.S, self.D, self.R)):
+                self.passes.cycle(T, S, D, R, self._scale(i))
         else:
             for T, S, D, R in zip(self.T, self.S, self.D, self.R):
                 self.passes.begin(T, S, D, R)
         self.works = [dist.all_reduce(R, op=dist.ReduceOp.SUM, group=self.group, async_op=True) for R in self.R]
 
-    def _scale(self):
+    def _scale(self, i=0):
+        if self.row_scale is not None:
+            return self.row_scale[i]
         return 1.0 / dist.get_world_size(self.group) if self.mean else 1.0
 
     def end(self):
@@ -157,9 +178,8 @@ class OverlapSync:
             return
         for w in self.works:
             w.wait()
-        scale = self._scale()
-        for T, S, D, R in zip(self.T, self.S, self.D, self.R):
-            self.passes.end(T, S, D, R, scale)
+        for i, (T, S, D, R) in enumerate(zip(self.T, self.S, self.D, self.R)):
+            self.passes.end(T, S, D, R, self._scale(i))
         self.works = None
 
     def allreduce(self):
@@ -168,26 +188,36 @@ class OverlapSync:
         self.end()
 
 
+def adaptive_scale(rate, updates, world, c0=64.0):
+    """Per-row scale of the adaptive rule: rate = expected touches per sample
+    of each row, `updates` samples per rank per exchange (float32 numpy)."""
+    import numpy as np
+    k = np.asarray(rate, np.float64) * float(updates) * world
+    s = np.minimum(1.0, c0 / np.maximum(k, 1e-300))
+    return (s + (1.0 - s) / world).astype(np.float32)
+
+
 class ReplicaSync(OverlapSync):
     """OverlapSync over a ProNet context's device tables (W and C), with the
     fused HIP passes; the context runs on torch's current stream so the
     passes, the training kernels and the collective are ordered on it.
 
-    hot_rows > 0 (sum exchange only): the hub rows of each table -- the
-    hot_rows rows with the highest expected touches per sample of `model`
+    sync: "adaptive" (default; needs `updates`, the samples each rank trains
+    per exchange, and `model`/`K` for the row rates), "mean" or "sum"; the old
+    `mean` flag still selects mean (True) or sum (False) when sync is None.
+
+    hot_rows > 0 (sum rule only): the hub rows of each table -- the hot_rows
+    rows with the highest expected touches per sample of `model`
     (smore_hot_row_ids) -- are also exchanged synchronously by hot(), which
     the caller runs after every training launch inside a step:
 
         D' = T_h - S_h;  R' = all_reduce(D');  T_h += R' - D';  S_h += R'
 
     This composes with the one-late full exchange (no update counted twice:
-    the next begin() sees only the hub rows' changes since the last hot()).
-    Why: a hub row collects every rank's thousands of updates per step; added
-    up one step late they overshoot and training diverges at 4 and 8 ranks
-    (tools/replica_sim.py), while the cold rows' few stale
-    updates per step do no harm."""
+    the next begin() sees only the hub rows' changes since the last hot())."""
 
-    def __init__(self, pn, mean=False, tables=(0, 1), group=None, hot_rows=0, model="line2", K=5):
+    def __init__(self, pn, mean=False, tables=(0, 1), group=None, hot_rows=0, model="line2", K=5, sync=None,
+                 updates=None, c0=64.0):
         # the passes, the training kernels and the collective must be ordered
         # on ONE stream.  The context runs on its own non-blocking stream when
         # handed the null stream (handle 0), which the legacy null stream does
@@ -196,9 +226,22 @@ class ReplicaSync(OverlapSync):
             torch.cuda.set_stream(torch.cuda.Stream())
         pn.set_stream(torch.cuda.current_stream().cuda_stream)
         T = [table_tensor(pn, w) for w in tables]
+        if sync is None:
+            sync = "mean" if mean else "sum"
+        if sync not in ("sum", "mean", "adaptive"):
+            raise ValueError("sync must be sum, mean or adaptive")
+        row_scale = None
+        if sync == "adaptive":
+            if not updates:
+                raise ValueError("the adaptive rule needs updates (samples per rank per exchange)")
+            world = dist.get_world_size(group)
+            row_scale = [torch.as_tensor(adaptive_scale(pn.row_rates(model, K, min(w, 1)), updates, world, c0),
+                                         device=T[0].device) for w in tables]
         hot_idx = None
-        if hot_rows > 0 and not mean:
+        if hot_rows > 0 and sync == "sum":
             n = min(int(hot_rows), pn.MAX_vid)
             hot_idx = [torch.as_tensor(pn.hot_row_ids(model, K, min(w, 1), n).astype("int64"), device=T[0].device)
                        for w in tables]
-        super().__init__(T, mean=mean, group=group, passes=HipPasses(pn), hot_idx=hot_idx)
+        super().__init__(T, mean=sync == "mean", group=group, passes=HipPasses(pn), hot_idx=hot_idx,
+                         row_scale=row_scale)
+        self.sync = sync

@@ -287,6 +287,14 @@ class ProNet:
                                         ids.ctypes.data_as(C.c_void_p)), "hot_row_ids")
         return ids[:n]
 
+    def row_rates(self, model, K, which):
+        """Expected touches per sample of every row of table `which` (0 W, 1 C)
+        under `model` with K negatives (float64, V)."""
+        r = np.zeros(self.MAX_vid, np.float64)
+        self._chk(lib.smore_row_rates(self.ctx, _lib.MODEL[model], int(K), int(which), len(r),
+                                      r.ctypes.data_as(C.c_void_p)), "row_rates")
+        return r
+
     def synchronize(self):
         self._chk(lib.smore_synchronize(self.ctx), "synchronize")
 
@@ -310,6 +318,15 @@ class ProNet:
         """delta_end then delta_begin in one pass."""
         self._chk(lib.smore_delta_cycle(self.ctx, T, S, D, R, float(scale), int(n)), "delta_cycle")
 
+    def delta_end_rows(self, T, S, D, R, scale, rows, stride):
+        """delta_end with row i's scale scale[i] (device pointer, rows floats)."""
+        self._chk(lib.smore_delta_end_rows(self.ctx, T, S, D, R, scale, int(rows), int(stride)), "delta_end_rows")
+
+    def delta_cycle_rows(self, T, S, D, R, scale, rows, stride):
+        """delta_cycle with row i's scale scale[i]."""
+        self._chk(lib.smore_delta_cycle_rows(self.ctx, T, S, D, R, scale, int(rows), int(stride)),
+                  "delta_cycle_rows")
+
     # ---------------------------------------------------------------- replica exchange (RCCL, in the library)
     def comm_init(self, nranks, rank, uid):
         """Join an RCCL communicator (uid: bytes of comm_unique_id() from rank 0)."""
@@ -320,10 +337,16 @@ class ProNet:
         """S = T: the replicas start from identical tables."""
         self._chk(lib.smore_exchange_reset(self.ctx), "exchange_reset")
 
+    def exchange_set_adaptive(self, model, K, updates, c0=64.0):
+        """Row scales of the adaptive rule for `updates` samples per rank per exchange."""
+        self._chk(lib.smore_exchange_set_adaptive(self.ctx, _lib.MODEL[model], int(K), float(updates), float(c0)),
+                  "exchange_set_adaptive")
+
     def exchange_begin(self, mean=False):
         """After a step: fold the in-flight exchange in, snapshot this rank's
-        delta and start its all-reduce (overlaps the next step)."""
-        self._chk(lib.smore_exchange_begin(self.ctx, int(bool(mean))), "exchange_begin")
+        delta and start its all-reduce (overlaps the next step).  mean: a rule
+        name ("sum", "mean", "adaptive") or the old boolean."""
+        self._chk(lib.smore_exchange_begin(self.ctx, _lib.sync_rule(mean)), "exchange_begin")
 
     def exchange_end(self):
         self._chk(lib.smore_exchange_end(self.ctx), "exchange_end")
@@ -368,7 +391,9 @@ class Group:
     """One process driving N GPUs (smore_group_*): replica 0 (`primary`, a
     ProNet view) loads, initialises and saves; broadcast_tables() copies its
     tables to every replica; training calls split the global range over the
-    replicas and return with every replica holding every update."""
+    replicas and return with every replica holding every update.  `mean` of
+    the training calls is the exchange rule: "adaptive" (default), "sum",
+    "mean" (or the old boolean), smore_hip.h SMORE_SYNC_*."""
 
     def __init__(self, devices):
         devs = (C.c_int * len(devices))(*[int(d) for d in devices])
@@ -411,6 +436,10 @@ class Group:
                                                   _lib.VM[vertex_method], _lib.NM[negative_method]),
                   "set_graph_edges")
 
+    def set_adaptive(self, c0=64.0):
+        """smore_group_set_adaptive: c0 of the adaptive exchange rule."""
+        self._chk(lib.smore_group_set_adaptive(self.g, float(c0)), "set_adaptive")
+
     def set_hot_exchange(self, rows=-1, launches=8):
         """smore_group_set_hot_exchange: hub rows per table synced after every
         one of `launches` launches per exchange round (-1 automatic, 0 off)."""
@@ -436,7 +465,7 @@ class Group:
                   "set_temporal_edges")
 
     def train_metapath2vec(self, walk_begin, walk_end, walk_times, walk_steps, window, K, alpha0, paths, seed, order,
-                           mode="atomic", per=0, mean=False):
+                           mode="atomic", per=0, mean="adaptive"):
         """(*Metapath2Vec).Train (Go, internal/models/metapath2vec/metapath2vec.go:106-200) over the replicas."""
         order = np.ascontiguousarray(order, np.int64)
         flat = np.ascontiguousarray([t for p in paths for t in p] or [0], np.int32)
@@ -444,16 +473,16 @@ class Group:
         self._chk(lib.smore_group_train_metapath2vec(self.g, int(walk_begin), int(walk_end), int(walk_times),
                                                      int(walk_steps), int(window), int(K), float(alpha0), ptr(flat),
                                                      ptr(lens), len(paths), int(seed), ptr(order), _lib.MODE[mode],
-                                                     int(per), int(bool(mean))), "train_metapath2vec")
+                                                     int(per), _lib.sync_rule(mean)), "train_metapath2vec")
 
     def train_ctdne(self, walk_begin, walk_end, walk_times, walk_steps, window, K, alpha0, time_window, seed, order,
-                    mode="atomic", per=0, mean=False):
+                    mode="atomic", per=0, mean="adaptive"):
         """(*CTDNE).Train (Go, internal/models/ctdne/ctdne.go:80-200) over the replicas."""
         order = np.ascontiguousarray(order, np.int64)
         self._chk(lib.smore_group_train_ctdne(self.g, int(walk_begin), int(walk_end), int(walk_times),
                                               int(walk_steps), int(window), int(K), float(alpha0),
                                               float(time_window), int(seed), ptr(order), _lib.MODE[mode], int(per),
-                                              int(bool(mean))), "train_ctdne")
+                                              _lib.sync_rule(mean)), "train_ctdne")
 
     def alloc_tables(self, dim, ntables):
         self._chk(lib.smore_group_alloc_tables(self.g, int(dim), int(ntables)), "alloc_tables")
@@ -463,49 +492,49 @@ class Group:
     def broadcast_tables(self):
         self._chk(lib.smore_group_broadcast_tables(self.g), "broadcast_tables")
 
-    def train_edges(self, model, begin, count, total, K, alpha0, reg=0.0, seed=1, mode="hybrid", per=0, mean=False):
+    def train_edges(self, model, begin, count, total, K, alpha0, reg=0.0, seed=1, mode="hybrid", per=0, mean="adaptive"):
         self._chk(lib.smore_group_train_edges(self.g, _lib.MODEL[model], int(begin), int(count), int(total), int(K),
                                               float(alpha0), float(reg), int(seed), _lib.MODE[mode], int(per),
-                                              int(bool(mean))), "train_edges")
+                                              _lib.sync_rule(mean)), "train_edges")
 
     def train_deepwalk(self, walk_begin, walk_end, walk_times, walk_steps, window, K, alpha0, seed, order,
-                       mode="hybrid", per=0, mean=False):
+                       mode="hybrid", per=0, mean="adaptive"):
         order = np.ascontiguousarray(order, np.int64)
         self._chk(lib.smore_group_train_deepwalk(self.g, int(walk_begin), int(walk_end), int(walk_times),
                                                  int(walk_steps), int(window), int(K), float(alpha0), int(seed),
-                                                 ptr(order), _lib.MODE[mode], int(per), int(bool(mean))),
+                                                 ptr(order), _lib.MODE[mode], int(per), _lib.sync_rule(mean)),
                   "train_deepwalk")
 
     def train_node2vec(self, walk_begin, walk_end, walk_times, walk_steps, window, K, alpha0, p, q, seed, order,
-                       mode="atomic", per=0, mean=False):
+                       mode="atomic", per=0, mean="adaptive"):
         """(*Node2Vec).Train (Go, internal/models/node2vec/node2vec.go:178-258) over the replicas."""
         order = np.ascontiguousarray(order, np.int64)
         self._chk(lib.smore_group_train_node2vec(self.g, int(walk_begin), int(walk_end), int(walk_times),
                                                  int(walk_steps), int(window), int(K), float(alpha0), float(p),
                                                  float(q), int(seed), ptr(order), _lib.MODE[mode], int(per),
-                                                 int(bool(mean))), "train_node2vec")
+                                                 _lib.sync_rule(mean)), "train_node2vec")
 
     def train_walklets(self, walk_begin, walk_end, walk_times, walk_steps, window_min, window_max, K, alpha0, seed,
-                       mode="hybrid", per=0, mean=False):
+                       mode="hybrid", per=0, mean="adaptive"):
         """Walklets::Train (src/model/Walklets.cpp:24-63) over the replicas."""
         self._chk(lib.smore_group_train_walklets(self.g, int(walk_begin), int(walk_end), int(walk_times),
                                                  int(walk_steps), int(window_min), int(window_max), int(K),
-                                                 float(alpha0), int(seed), _lib.MODE[mode], int(per), int(bool(mean))),
+                                                 float(alpha0), int(seed), _lib.MODE[mode], int(per), _lib.sync_rule(mean)),
                   "train_walklets")
 
     def train_app(self, unit_begin, unit_end, walk_times, sample_times, jump, K, alpha0, seed, order,
-                  mode="hybrid", per=0, mean=False):
+                  mode="hybrid", per=0, mean="adaptive"):
         """APP::Train (src/model/APP.cpp:59-120) over the replicas."""
         order = np.ascontiguousarray(order, np.int64)
         self._chk(lib.smore_group_train_app(self.g, int(unit_begin), int(unit_end), int(walk_times),
                                             int(sample_times), float(jump), int(K), float(alpha0), int(seed),
-                                            ptr(order), _lib.MODE[mode], int(per), int(bool(mean))), "train_app")
+                                            ptr(order), _lib.MODE[mode], int(per), _lib.sync_rule(mean)), "train_app")
 
-    def train_hpe(self, begin, count, total, walk_steps, K, reg, alpha0, seed, mode="hybrid", per=0, mean=False):
+    def train_hpe(self, begin, count, total, walk_steps, K, reg, alpha0, seed, mode="hybrid", per=0, mean="adaptive"):
         """HPE::Train (src/model/HPE.cpp:94-150) over the replicas."""
         self._chk(lib.smore_group_train_hpe(self.g, int(begin), int(count), int(total), int(walk_steps), int(K),
                                             float(reg), float(alpha0), int(seed), _lib.MODE[mode], int(per),
-                                            int(bool(mean))), "train_hpe")
+                                            _lib.sync_rule(mean)), "train_hpe")
 
 
 def deepwalk_order(V, walk_times, skip):

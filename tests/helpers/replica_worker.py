@@ -4,11 +4,11 @@ smore_amd/dist.py ReplicaSync (the fused HIP passes of replica_sync.hip around a
 torch.distributed all-reduce; gloo here, since every rank shares one GPU).
 TEST INFRASTRUCTURE.
 
-    python tests/helpers/replica_worker.py RANK WORLD PORT TOTAL STEPS OUT.npz [HOT_ROWS LAUNCHES [MEAN]]
+    python tests/helpers/replica_worker.py RANK WORLD PORT TOTAL STEPS OUT.npz [HOT_ROWS LAUNCHES [SYNC]]
 
-HOT_ROWS > 0 (sum exchange): the hub-row exchange after each of LAUNCHES
-launches per step (ReplicaSync.hot).  MEAN 1: the averaging exchange
-(bench.py's N > 1 default).
+HOT_ROWS > 0 (sum rule): the hub-row exchange after each of LAUNCHES
+launches per step (ReplicaSync.hot).  SYNC: sum (default), mean, adaptive or
+adaptive:C0 (bench.py's N > 1 default is adaptive:64); 0 / 1 = sum / mean.
 """
 import os
 import sys
@@ -22,7 +22,10 @@ def main():
     out = sys.argv[6]
     hot_rows = int(sys.argv[7]) if len(sys.argv) > 7 else 0
     launches = int(sys.argv[8]) if len(sys.argv) > 8 else 1
-    mean = bool(int(sys.argv[9])) if len(sys.argv) > 9 else False
+    spec = sys.argv[9] if len(sys.argv) > 9 else "sum"
+    spec = {"0": "sum", "1": "mean"}.get(spec, spec)
+    rule, _, c0 = spec.partition(":")
+    c0 = float(c0) if c0 else 64.0
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -36,9 +39,10 @@ def main():
     pn.alloc_tables(32, 2)
     pn.init_table_glibc(0, 0)
     pn.zero_table(1)
-    sync = ReplicaSync(pn, mean=mean, hot_rows=hot_rows, model="line2", K=5) if world > 1 else None
-    nl = launches if (sync is not None and sync.hot_idx) else 1
     per = total // world // steps
+    sync = (ReplicaSync(pn, sync=rule, hot_rows=hot_rows, model="line2", K=5, updates=per, c0=c0)
+            if world > 1 else None)
+    nl = launches if (sync is not None and sync.hot_idx) else 1
     for k in range(steps):
         begin = (k * world + rank) * per
         sub = per // nl

@@ -1,6 +1,6 @@
 """Multi-process replica exchange (smore_amd/dist.py) on CPU with gloo,
 world_size 2: the snapshot-delta all-reduce applies every rank's updates
-exactly once (sum) or averages them (mean)."""
+exactly once (sum), averages them (mean) or scales them per row (adaptive)."""
 import os
 import socket
 
@@ -130,3 +130,64 @@ def test_hot_row_exchange_gloo(world):
         p.join(120)
         assert p.exitcode == 0
     assert list(out) == [1] * world
+
+
+def _adaptive_worker(rank, world, port, out):
+    """The adaptive rule: OverlapSync with one per-row scale tensor per table."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from smore_amd.dist import OverlapSync
+    torch.manual_seed(0)
+    base = [torch.randn(40, 8), torch.randn(40, 8)]
+    tabs = [b.clone() for b in base]
+    g0 = torch.Generator().manual_seed(7)
+    scale = [1.0 / world + (1.0 - 1.0 / world) * torch.rand(40, generator=g0) for _ in tabs]
+    sync = OverlapSync(tabs, row_scale=scale)
+    expect = [b.clone() for b in base]
+    for step in range(3):
+        deltas = []
+        for r in range(world):
+            g = torch.Generator().manual_seed(100 * step + r)
+            deltas.append([torch.randn(40, 8, generator=g) * 0.01 for _ in tabs])
+        for t, d in zip(tabs, deltas[rank]):
+            t.add_(d)
+        sync.begin()
+        for i in range(len(tabs)):
+            expect[i] += scale[i].view(-1, 1) * sum(deltas[r][i] for r in range(world))
+    sync.end()
+    ok = all(torch.allclose(t, e, atol=1e-5) for t, e in zip(tabs, expect))
+    same = [torch.empty_like(tabs[0]) for _ in range(world)]
+    dist.all_gather(same, tabs[0])
+    ok = ok and all(torch.allclose(same[0], x, atol=1e-6, rtol=0) for x in same)
+    out[rank] = int(ok)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_adaptive_exchange_gloo(world):
+    """The adaptive exchange rule (dist.py, smore_hip.h SMORE_SYNC_ADAPTIVE):
+    each row's summed one-late delta is scaled by its own factor, and at the
+    end every rank holds base + sum over steps of scale * (all ranks' deltas)."""
+    ctx = mp.get_context("spawn")
+    out = ctx.Array("i", [0] * world)
+    port = _free_port()
+    procs = [ctx.Process(target=_adaptive_worker, args=(r, world, port, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert list(out) == [1] * world
+
+
+def test_adaptive_scale_law():
+    """s = min(1, c0 / k), scale = s + (1 - s) / N with k = rate * updates * N:
+    the sum for rows with at most c0 updates per exchange, -> 1/N for hubs."""
+    import numpy as np
+    from smore_amd.dist import adaptive_scale
+    rate = np.array([0.0, 1e-9, 64.0 / (8 * 1000), 128.0 / (8 * 1000), 1.0])
+    sc = adaptive_scale(rate, 1000, 8, c0=64.0)
+    assert sc[0] == 1.0 and sc[1] == 1.0 and sc[2] == 1.0
+    np.testing.assert_allclose(sc[3], 0.5 + 0.5 / 8, rtol=1e-6)
+    np.testing.assert_allclose(sc[4], 64.0 / 8000 + (1 - 64.0 / 8000) / 8, rtol=1e-6)

@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Held-out LINE-2 loss of `world` replicas (gloo ranks sharing cuda:0,
+tests/helpers/replica_worker.py) per exchange rule, on the 1k-vertex golden
+graph at the C4 bench's updates per row per exchange (12k samples per rank per
+exchange over 920 rows), against one rank that ran all `total` samples and one
+that ran total/world.  TEST INFRASTRUCTURE (reads the oracle's sampler).
+
+    python tools/replica_quality.py --worlds 2 4 8 --rules sum mean adaptive:16 adaptive:64 adaptive:256
+"""
+import argparse
+import json
+import os
+import socket
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+SEED = 20251015
+
+
+def run(tmp, world, total, steps, rule):
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    worker = os.path.join(ROOT, "tests", "helpers", "replica_worker.py")
+    outs = [os.path.join(tmp, "w%d_r%d.npz" % (world, r)) for r in range(world)]
+    procs = [subprocess.Popen([sys.executable, "-u", worker, str(r), str(world), str(port), str(total), str(steps),
+                               outs[r], "0", "1", rule], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+             for r in range(world)]
+    for p in procs:
+        out, _ = p.communicate(timeout=600)
+        if p.returncode != 0:
+            raise RuntimeError(out[-3000:])
+    return [np.load(o) for o in outs]
+
+
+def heldout(W, C, draws):
+    W = W.astype(np.float64)
+    C = C.astype(np.float64)
+    v, c, negs = draws
+    loss = np.logaddexp(0.0, -np.einsum("ij,ij->i", W[v], C[c]))
+    for k in range(negs.shape[1]):
+        loss += np.logaddexp(0.0, np.einsum("ij,ij->i", W[v], C[negs[:, k]]))
+    return float(loss.mean())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--worlds", type=int, nargs="+", default=[2, 4, 8])
+    ap.add_argument("--rules", nargs="+", default=["sum", "mean", "adaptive:16", "adaptive:64", "adaptive:256"])
+    ap.add_argument("--per", type=int, default=12_000)
+    ap.add_argument("--total", type=int, default=4 * 10 ** 6)
+    args = ap.parse_args()
+    from oracle import oracle as orc
+    g = orc.Graph.from_file(os.path.join(ROOT, "tests", "golden", "pl1k.txt"), 1)
+    h = orc.sample_line(g, SEED + 7, 0, 50_000, 5)
+    h = h[h[:, 1] >= 0]
+    draws = (h[:, 0], h[:, 1], h[:, 2:])
+    with tempfile.TemporaryDirectory() as tmp:
+        for world in args.worlds:
+            steps = args.total // (world * args.per)
+            one_all = run(tmp, 1, args.total, steps * world, "sum")[0]
+            one_part = run(tmp, 1, args.total // world, steps, "sum")[0]
+            base = {"world": world, "l1_total": heldout(one_all["W"], one_all["C"], draws),
+                    "l1_part": heldout(one_part["W"], one_part["C"], draws)}
+            print(json.dumps(dict(base, rule="1 rank")), flush=True)
+            for rule in args.rules:
+                outs = run(tmp, world, args.total, steps, rule)
+                spread = max(float(np.abs(o["W"] - outs[0]["W"]).max()) for o in outs)
+                W, C = outs[0]["W"], outs[0]["C"]
+                ok = bool(np.isfinite(W).all() and np.isfinite(C).all())
+                ln = heldout(W, C, draws) if ok else float("nan")
+                print(json.dumps(dict(base, rule=rule, loss=ln, finite=ok, spread=spread,
+                                      vs_total=ln / base["l1_total"], vs_part=ln / base["l1_part"])), flush=True)
+
+
+if __name__ == "__main__":
+    main()
