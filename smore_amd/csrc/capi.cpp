@@ -345,9 +345,14 @@ constexpr double SH_AUTO_BUDGET = 6144.0;
 static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
     char key[128];
     const char* stale_env = getenv("SMORE_SH_STALE");
-    // tuning knob: SMORE_SH_WROWS=0 keeps W rows out of the write-combined set
+    // W rows of two-table models stay out of the write-combined set unless
+    // SMORE_SH_WROWS=1: combining the hub W rows makes their pending deltas
+    // invisible for a whole drain window, which cost Go LINE-2 (source law
+    // out_degree^1, ~1 % of samples on one W row) 4.7 % held-out loss at C2
+    // (0.7 % without), for +12 % C4 throughput; C++ LINE-2 gains nothing from
+    // it (1338 vs 1342 M/s), DESIGN.md 8
     const char* wrows_env = getenv("SMORE_SH_WROWS");
-    const bool wrows = !wrows_env || atoi(wrows_env) != 0;
+    const bool wrows = wrows_env && atoi(wrows_env) != 0;
     snprintf(key, sizeof key, "%d/%d/%lld/%.9g/%d/%d/%s/%d", model, K, (long long)M, c->hot_tau, c->sh_max,
              c->sh_flush, stale_env ? stale_env : "", (int)wrows);
     if (c->hot_key == key) return SMORE_OK;
@@ -378,9 +383,8 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
             // M * p * sh_flush updates; rows above SH_STALE_MAX stay on atomics
             // (on small graphs that is every hot row)
             if (hc[v] && (double)M * p * flush_cap <= stale_max) r.push_back({p, (int32_t)v});
-            // two tables: the hub W rows compete for the same slots (key
-            // v | SH_WKEY) -- the Go source law (out_degree^1) puts ~1 % of
-            // all samples on one W row
+            // two tables (SMORE_SH_WROWS=1 only): the hub W rows compete for
+            // the same slots (key v | SH_WKEY)
             if (wrows && model == SMORE_LINE2 && hw[v] && (double)M * ps[v] * flush_cap <= stale_max)
                 r.push_back({ps[v], (int32_t)(v | SH_WKEY)});
         }
@@ -477,7 +481,9 @@ static int edge_grid(smore_ctx* c, const EdgeArgs& a, bool leave_slot = false, i
     if (a.mode == SMORE_SERIAL) return 1;
     int per_cu = 0;
     const void* sym = kind == 1   ? go_rec_symbol(a)
-                      : kind == 2 ? (a.mode == SMORE_ATOMIC ? go_pair_symbol_a(a) : go_pair_symbol_s(a))
+                      : kind == 2 ? (a.mode == SMORE_ATOMIC   ? go_pair_symbol_a(a)
+                                     : a.mode == SMORE_HYBRID ? go_pair_symbol_h(a)
+                                                              : go_pair_symbol_s(a))
                                   : edge_kernel_symbol(a);
     if (!sym ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sym, 256, sh_lds_bytes(a.sh_rows, a.dpad)) !=
@@ -1060,13 +1066,6 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
     a.begin = 0; a.count = 0; a.total = total; a.seed = seed; a.alpha0 = alpha0; a.reg = 0.0f;
     a.dpad = c->dpad; a.K = K; a.model = SMORE_LINE2; a.mode = mode;
     a.tcum = c->d_tcum;
-    // the Go pair kernel keeps W_v in registers over a walk position's run and
-    // adds it back; its context rows take the lossless atomic scatter when
-    // hybrid is asked for
-    if (go && mode == SMORE_HYBRID) {
-        mode = SMORE_ATOMIC;
-        a.mode = mode;
-    }
     EdgeArgs ar = a;   // the update kernel over pair records
     if (c->pair_walks < chunk + 1) {
         dfree(c->d_pcount);
@@ -1082,7 +1081,7 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
         HIPCHK(c, hipMalloc(&c->d_rec, chunk * pb * RW * sizeof(int32_t)));
         c->rec_cap = chunk * pb * RW;
     }
-    const bool combine = mode == SMORE_HYBRID;
+    const bool combine = mode == SMORE_HYBRID && !go;   // the Go pair kernel: hot rows atomic, no LDS combining
     ar.sh_rows = combine ? std::min(c->sh_max, 8192 / std::max(1, c->dpad)) : 0;
     ar.alpha_rec = 1;
     ar.work = c->d_work;
@@ -1139,7 +1138,9 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
         else HIPCHK(c, launch_pair_count(w, seed, c->d_pcount, c->stream));
         HIPCHK(c, scan_pair_counts(c->d_pcount, c->d_poff, w.nwalks + 1, &c->d_scan_tmp, &c->scan_tmp_bytes,
                                    c->stream));
-        if (go) HIPCHK(c, launch_go_pair_emit(ar.g, w, seed, K, alpha0, c->d_poff, c->d_rec, c->stream));
+        if (go)
+            HIPCHK(c, launch_go_pair_emit(ar.g, w, seed, K, alpha0, c->d_poff, c->d_rec, mode == SMORE_HYBRID,
+                                          c->stream));
         else HIPCHK(c, launch_pair_emit(ar.g, w, seed, K, alpha0, c->d_poff, c->d_rec, c->stream));
         EdgeArgs ak = ar;
         ak.begin = 0;
@@ -1150,6 +1151,7 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
         const int g = mode == SMORE_SERIAL ? 1 : ugrid;
         if (!go) HIPCHK(c, launch_edge_train(ak, g, c->stream));
         else if (mode == SMORE_ATOMIC) HIPCHK(c, launch_go_pair_a(ak, g, c->stream));
+        else if (mode == SMORE_HYBRID) HIPCHK(c, launch_go_pair_h(ak, g, c->stream));
         else HIPCHK(c, launch_go_pair_s(ak, g, c->stream));
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));

@@ -334,12 +334,13 @@ go_rec_kernel(EdgeArgs a) {
 // while v repeats, the Go loop's per-pair W_v += vg included, and puts the row
 // back when v changes -- stored in the serial mode (the sequential value),
 // otherwise the run's summed gradient added atomically (no W update lost).
-// Context rows: atomic adds of each update's delta (MODE_ATOMIC) or plain
-// stores (MODE_STORE).  Serial (a.mode 2): one group, all records in order.
+// Context rows: atomic adds of each update's delta (MODE_ATOMIC), plain
+// stores (MODE_STORE), or by the records' hot tags (MODE_HYBRID: bit 30 of a
+// context / negative id, set by go_pair_emit_kernel from the C hot map).
+// Serial (a.mode 2): one group, all records in order.
 template <int G, int M, int KMAX, int MODE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(waves_of(MODE))))
 go_pair_kernel(EdgeArgs a) {
-    static_assert(MODE != MODE_HYBRID, "Go walk pairs: atomic or plain stores");
     __shared__ float s_sig[1001];
     for (int i = threadIdx.x; i < 1001; i += blockDim.x) s_sig[i] = a.sig[i];
     __syncthreads();
@@ -364,8 +365,9 @@ go_pair_kernel(EdgeArgs a) {
             i32x4 r[RW / 4];
 #pragma unroll
             for (int q = 0; q < RW / 4; ++q) r[q] = __builtin_nontemporal_load(p + q);
-            const int32_t v = r[0][0], c = r[0][1];
-            if (c < 0) continue;
+            const int32_t v = r[0][0], c_t = r[0][1];
+            if (c_t < 0) continue;
+            const int32_t c = untag(c_t);
             const float alpha = __int_as_float(r[(2 + KMAX) / 4][(2 + KMAX) % 4]);
             if (v != cv) {
                 flush();
@@ -377,11 +379,14 @@ go_pair_kernel(EdgeArgs a) {
             // the context's row and the negatives' (a negative equal to the
             // context is skipped, not redrawn; repeats start from the first)
             int32_t id[KMAX + 1];
+            bool hot[KMAX + 1];
             id[0] = c;
+            hot[0] = MODE == MODE_HYBRID && tag_hot(c_t);
 #pragma unroll
             for (int k = 1; k <= KMAX; ++k) {
                 const int32_t x = k - 1 < a.K ? r[(k + 1) / 4][(k + 1) % 4] : -1;
-                id[k] = (x < 0 || x == c) ? -1 : x;
+                id[k] = (x < 0 || untag(x) == c) ? -1 : untag(x);
+                hot[k] = MODE == MODE_HYBRID && x >= 0 && tag_hot(x);
             }
             float rows[KMAX + 1][M];
 #pragma unroll
@@ -424,12 +429,12 @@ go_pair_kernel(EdgeArgs a) {
                         for (int m = 0; m < M; ++m) rows[k2][m] = nk[m];
                     }
                 float* row = a.C + (int64_t)id[k] * dpad;
-                if (MODE == MODE_ATOMIC) atomic_row<G, M>(row, dk, lane, dpad);
+                if (MODE == MODE_ATOMIC || hot[k]) atomic_row<G, M>(row, dk, lane, dpad);
                 else if (last) st_row<G, M>(row, nk, lane, ev);
             }
             {
                 float* row = a.C + (int64_t)c * dpad;
-                if (MODE == MODE_ATOMIC) {
+                if (MODE == MODE_ATOMIC || hot[0]) {
                     atomic_row<G, M>(row, cg, lane, dpad);
                 } else {
                     float nc[M];

@@ -22,13 +22,16 @@ hipError_t launch_go_ctdne_walk(const TemporalArgs& t, const WalkArgs& w, uint64
 // per-walk pair counts (fixed window: a function of the length), then, at the
 // exclusive-scanned offsets, the records
 hipError_t launch_go_pair_count(const WalkArgs& w, uint32_t* count, hipStream_t st);
+// tagged: the context and negative ids carry the C hot map's bit 30 (hybrid)
 hipError_t launch_go_pair_emit(const DevGraph& g, const WalkArgs& w, uint64_t seed, int K, double alpha0,
-                               const uint64_t* off, int32_t* rec, hipStream_t st);
+                               const uint64_t* off, int32_t* rec, int tagged, hipStream_t st);
 // Go UpdatePair over pair records (go_rec.h go_pair_kernel; train_go_rec_*.hip):
-// mode 2 serial (the Go loop's order), 1 atomic, 0 plain stores
+// mode 2 serial (the Go loop's order), 1 atomic, 0 plain stores, 3 hybrid
 hipError_t launch_go_pair_s(const EdgeArgs& a, int grid, hipStream_t st);
 hipError_t launch_go_pair_a(const EdgeArgs& a, int grid, hipStream_t st);
+hipError_t launch_go_pair_h(const EdgeArgs& a, int grid, hipStream_t st);
 const void* go_pair_symbol_s(const EdgeArgs& a);
 const void* go_pair_symbol_a(const EdgeArgs& a);
+const void* go_pair_symbol_h(const EdgeArgs& a);
 
 }  // namespace smore

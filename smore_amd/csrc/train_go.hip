@@ -415,7 +415,8 @@ __global__ void __launch_bounds__(256) go_pair_count_kernel(WalkArgs w, uint32_t
 
 template <int KMAX>
 __global__ void __launch_bounds__(256) go_pair_emit_kernel(DevGraph g, WalkArgs w, uint64_t seed, int K,
-                                                           double alpha0, const uint64_t* off, int32_t* rec) {
+                                                           double alpha0, const uint64_t* off, int32_t* rec,
+                                                           int tagged) {
     constexpr int RW = rec_width(KMAX);
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= w.nwalks) return;
@@ -441,12 +442,18 @@ __global__ void __launch_bounds__(256) go_pair_emit_kernel(DevGraph g, WalkArgs 
             if (j == i) continue;
             int32_t x[RW];
             x[0] = walk[i];
-            x[1] = walk[j];
+            // hybrid: the context's C hot bit is bit 31 of its own negative
+            // alias word (build_hot_maps), the negatives' come with the draw
+            x[1] = tagged ? (int32_t)(walk[j] | ((g.ntab[walk[j]].y >> 31) << 30)) : walk[j];
 #pragma unroll
             for (int n = 0; n < RW - 2; ++n) x[2 + n] = -1;
 #pragma unroll
             for (int n = 0; n < KMAX; ++n)
-                if (n < K) x[2 + n] = go_alias(g.ntab, g.V, word(slot + 2u * n), word(slot + 2u * n + 1u));
+                if (n < K) {
+                    const uint32_t ki = word(slot + 2u * n), kp = word(slot + 2u * n + 1u);
+                    x[2 + n] = tagged ? alias_pick(draw_index(ki, g.V), g.ntab[draw_index(ki, g.V)], kp)
+                                      : go_alias(g.ntab, g.V, ki, kp);
+                }
             slot += 2u * (uint32_t)K;
             x[2 + KMAX] = __float_as_int(alpha);
             i32x4* o = reinterpret_cast<i32x4*>(out);
@@ -463,10 +470,12 @@ hipError_t launch_go_pair_count(const WalkArgs& w, uint32_t* count, hipStream_t 
 }
 
 hipError_t launch_go_pair_emit(const DevGraph& g, const WalkArgs& w, uint64_t seed, int K, double alpha0,
-                               const uint64_t* off, int32_t* rec, hipStream_t st) {
+                               const uint64_t* off, int32_t* rec, int tagged, hipStream_t st) {
     const dim3 grid((unsigned)((w.nwalks + 255) / 256));
-    if (K <= 5) hipLaunchKernelGGL((go_pair_emit_kernel<5>), grid, dim3(256), 0, st, g, w, seed, K, alpha0, off, rec);
-    else hipLaunchKernelGGL((go_pair_emit_kernel<10>), grid, dim3(256), 0, st, g, w, seed, K, alpha0, off, rec);
+    if (K <= 5)
+        hipLaunchKernelGGL((go_pair_emit_kernel<5>), grid, dim3(256), 0, st, g, w, seed, K, alpha0, off, rec, tagged);
+    else
+        hipLaunchKernelGGL((go_pair_emit_kernel<10>), grid, dim3(256), 0, st, g, w, seed, K, alpha0, off, rec, tagged);
     return hipGetLastError();
 }
 

@@ -115,10 +115,14 @@ def test_go_deepwalk_directed_dead_ends(smore):
     np.testing.assert_array_equal(pn.get_table(1), C)
 
 
-def test_go_deepwalk_hogwild_matches_atomic(smore):
-    """Go DeepWalk in the plain-store (Hogwild) mode keeps W_v in registers for
-    a walk position's run of pairs and ADDS the run's gradient at the end
-    (ADVICE r2): its held-out skip-gram AUC matches the lossless atomic mode."""
+def test_go_deepwalk_parallel_modes_train_like_serial(smore):
+    """Go DeepWalk's parallel modes on the record path (go_pair_emit_kernel ->
+    go_rec.h go_pair_kernel, concurrency capped at V/16 groups as the C++
+    walks): atomic and hybrid reach the serial order's held-out skip-gram AUC
+    (within 0.02).  Plain stores (hogwild) lose context-row updates on this
+    920-vertex graph -- C++ DeepWalk's hogwild sits at the same level
+    (tools/go_walk_check.py: 0.78 vs 0.87) -- but W_v's run gradient is added,
+    not stored, so it still trains (> 0.75)."""
     g, pn = pair(smore, "pl1k.txt", 1)
     dim, K, times = 32, 5, 4
     order = smore.deepwalk_order(g.V, times, 0)
@@ -133,7 +137,7 @@ def test_go_deepwalk_hogwild_matches_atomic(smore):
         return (pos[:, None] > neg[None, :]).mean()
 
     res = {}
-    for mode in ("atomic", "hogwild"):
+    for mode in ("serial", "atomic", "hybrid", "hogwild"):
         pn.alloc_tables(dim, 2)
         pn.init_table_glibc(0, 0)
         pn.zero_table(1)
@@ -141,8 +145,10 @@ def test_go_deepwalk_hogwild_matches_atomic(smore):
         W, C = pn.get_table(0), pn.get_table(1)
         assert np.isfinite(W).all() and np.isfinite(C).all()
         res[mode] = auc(W, C)
-    assert res["atomic"] > 0.7, res
-    assert abs(res["hogwild"] - res["atomic"]) < 0.02, res
+    assert res["serial"] > 0.85, res
+    assert abs(res["atomic"] - res["serial"]) < 0.02, res
+    assert abs(res["hybrid"] - res["serial"]) < 0.02, res
+    assert res["hogwild"] > 0.75, res
 
 
 @pytest.mark.parametrize("model", ["line2", "line1", "bpr"])
@@ -361,7 +367,8 @@ def test_go_ctdne_model_driver(smore, tmp_path):
 def test_go_c2_full_grid_hybrid_matches_atomic(smore):
     """The Go rules on the record path at full grid (config 2's graph, 2^28
     samples, d=64, K=5): the hybrid scatter (hot rows by atomic add, the
-    hottest context rows write-combined in LDS) trains like the lossless atomic
+    hottest context rows write-combined in LDS; W rows are not combined by
+    default) trains like the lossless atomic
     scatter -- held-out Go LINE-2 loss within 1 % -- and Go BPR's hybrid run on
     the same graph is finite."""
     from smore_amd import graphgen

@@ -28,7 +28,8 @@ def run(tmp, world, total, steps, rule):
     port = s.getsockname()[1]
     s.close()
     worker = os.path.join(ROOT, "tests", "helpers", "replica_worker.py")
-    outs = [os.path.join(tmp, "w%d_r%d.npz" % (world, r)) for r in range(world)]
+    run.n = getattr(run, "n", 0) + 1
+    outs = [os.path.join(tmp, "c%d_w%d_r%d.npz" % (run.n, world, r)) for r in range(world)]
     procs = [subprocess.Popen([sys.executable, "-u", worker, str(r), str(world), str(port), str(total), str(steps),
                                outs[r], "0", "1", rule], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
              for r in range(world)]
@@ -36,7 +37,11 @@ def run(tmp, world, total, steps, rule):
         out, _ = p.communicate(timeout=600)
         if p.returncode != 0:
             raise RuntimeError(out[-3000:])
-    return [np.load(o) for o in outs]
+    res = []
+    for o in outs:
+        with np.load(o) as z:
+            res.append({k: z[k] for k in z.files})
+    return res
 
 
 def heldout(W, C, draws):
