@@ -1065,7 +1065,8 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
     a.skipped = c->d_skipped;
     a.begin = 0; a.count = 0; a.total = total; a.seed = seed; a.alpha0 = alpha0; a.reg = 0.0f;
     a.dpad = c->dpad; a.K = K; a.model = SMORE_LINE2; a.mode = mode;
-    a.tcum = c->d_tcum;
+    // Go walks on a unit-weight graph: O(1) CDF target (go_target, tcum null)
+    a.tcum = go && c->go_unit_w ? nullptr : c->d_tcum;
     EdgeArgs ar = a;   // the update kernel over pair records
     if (c->pair_walks < chunk + 1) {
         dfree(c->d_pcount);

@@ -29,16 +29,26 @@ __device__ __forceinline__ int32_t go_alias(const uint2* tab, uint32_t n, uint32
     return kp < e.x ? (int32_t)i : untag((int32_t)e.y);   // ids untagged (no hybrid scatter here)
 }
 
+// Go TargetSample (untagged id).  tcum == nullptr: every edge weight is 1, so
+// the CDF is e + 1 exactly and the first e with r <= e + 1 is ceil(r) - 1 (as
+// go_target_tagged's unit_w path) -- no binary search over the prefix sums.
 __device__ __forceinline__ int32_t go_target(const DevGraph& g, const double* tcum, int32_t v, uint32_t kr) {
     const int64_t off = g.offsets[v];
     const int64_t br = g.offsets[v + 1] - off;
     if (br == 0) return -1;
-    const double r = ldexp((double)kr, -32) * tcum[off + br - 1];
-    int64_t lo = 0, hi = br - 1;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (r <= tcum[off + mid]) hi = mid;
-        else lo = mid + 1;
+    int64_t lo;
+    if (!tcum) {
+        lo = (int64_t)ceil(ldexp((double)kr, -32) * (double)br) - 1;
+        lo = lo < 0 ? 0 : (lo > br - 1 ? br - 1 : lo);
+    } else {
+        const double r = ldexp((double)kr, -32) * tcum[off + br - 1];
+        int64_t hi = br - 1;
+        lo = 0;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (r <= tcum[off + mid]) hi = mid;
+            else lo = mid + 1;
+        }
     }
     return untag(g.targets[off + lo]);
 }

@@ -5,7 +5,9 @@
   * two processes sharing the GPU, exchanging deltas through the fused HIP
     passes (replica_sync.hip) around a gloo all-reduce: the replicas agree
     within float rounding, and the held-out LINE-2 loss at equal total samples
-    is within 1 % of one process.
+    is within 2 % of one process (SURVEY.md 4(c));
+  * 4 and 8 such ranks under the adaptive exchange rule (bench.py's N > 1
+    default), against one rank, the averaging rule and one rank's own share.
 The 2..8-GPU RCCL runs are the driver's (bench.py under torchrun)."""
 import os
 import socket
@@ -114,29 +116,34 @@ def _heldout_loss(W, C, draws):
     return float(loss.mean())
 
 
-def _run_ranks(tmp_path, world, total, steps, hot_rows=0, launches=1, mean=False):
+def _run_ranks(tmp_path, world, total, steps, hot_rows=0, launches=1, sync="adaptive", tag=""):
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     worker = os.path.join(ROOT, "tests", "helpers", "replica_worker.py")
-    outs = [str(tmp_path / ("w%d_r%d.npz" % (world, r))) for r in range(world)]
+    outs = [str(tmp_path / ("%sw%d_r%d.npz" % (tag, world, r))) for r in range(world)]
     procs = [subprocess.Popen([sys.executable, "-u", worker, str(r), str(world), str(port), str(total), str(steps),
-                               outs[r], str(hot_rows), str(launches), str(int(mean))], stdout=subprocess.PIPE,
+                               outs[r], str(hot_rows), str(launches), sync], stdout=subprocess.PIPE,
                               stderr=subprocess.STDOUT, text=True)
              for r in range(world)]
     for p in procs:
         out, _ = p.communicate(timeout=240)
         assert p.returncode == 0, out[-3000:]
-    return [np.load(o) for o in outs]
+    res = []
+    for o in outs:
+        with np.load(o) as z:
+            res.append({k: z[k] for k in z.files})
+    return res
 
 
 def test_two_ranks_hip_passes_agree_and_train_like_one(tmp_path):
     """Exchange period: 8k samples per rank (~9 updates per row of the 920-row
     tables per rank between exchanges -- the C4 bench's 2^27 samples per rank
-    give ~13 per row).  Each rank sees the other's updates one exchange late,
-    so the 2-rank loss trails the 1-rank loss slightly: measured 1.2 % on this
-    graph (0.5779 vs 0.5848, uncached tables); the bound is 2 %."""
+    give ~13 per row), the adaptive exchange rule (the default).  Each rank
+    sees the other's updates one exchange late, so the 2-rank loss trails the
+    1-rank loss slightly: measured 1.2 % on this graph at 12k samples per
+    exchange (the sum rule 1.8 %, the mean 5.8 %); the bound is 2 %."""
     total, steps = 4 * 10 ** 6, 250
     one = _run_ranks(tmp_path, 1, total, steps)[0]
     two = _run_ranks(tmp_path, 2, total, steps)
@@ -155,19 +162,22 @@ def test_two_ranks_hip_passes_agree_and_train_like_one(tmp_path):
 def test_n_ranks_replicas_agree_and_train_like_one(tmp_path, world):
     """The driver's 4- and 8-GPU weak-scaling runs, rehearsed as `world` gloo
     ranks sharing one GPU (the exchange arithmetic is the same fused HIP passes
-    around an all-reduce), with bench.py's N > 1 default: the averaging
-    exchange once per step.  Each rank runs 12k samples between exchanges,
+    around an all-reduce), with bench.py's N > 1 default: the adaptive exchange
+    rule (c0 64) once per step.  Each rank runs 12k samples between exchanges,
     ~13 samples per row of the 920-row tables -- the C4 bench's 2^27 samples per
-    rank per step over 10M rows.  Replicas agree, and `world` ranks that each
-    ran total/world samples train at least as well as one rank that ran
-    total/world samples (model averaging: never worse than one replica's own
-    work), within 2 %.  The summing exchange diverges at this period from 4
-    ranks on, hub-row exchange or not (tools/replica_sim.py)."""
+    rank per step over 10M rows.  Replicas agree, and against one rank that ran
+    all `total` samples the held-out loss is within 6 % at 4 ranks and 40 % at
+    8 (measured 4.4 % and 28 %, tools/replica_quality.py; the one-exchange-late
+    deltas of 8 ranks are stale by 8x13 updates per row); it always beats the
+    averaging rule (measured 1.39x / 3.3x of one rank) and one rank that ran
+    only its own share.  The summing rule diverges here from 4 ranks on."""
     per = 12_000
     total = 4 * 10 ** 6
     steps = total // (world * per)
-    one = _run_ranks(tmp_path, 1, total // world, steps)[0]
-    outs = _run_ranks(tmp_path, world, total, steps, mean=True)
+    one = _run_ranks(tmp_path, 1, total, steps * world, sync="sum", tag="all")[0]
+    own = _run_ranks(tmp_path, 1, total // world, steps, sync="sum", tag="own")[0]
+    outs = _run_ranks(tmp_path, world, total, steps)
+    avg = _run_ranks(tmp_path, world, total, steps, sync="mean", tag="mean")[0]
     for r in range(1, world):
         for key in ("W", "C"):
             assert np.isfinite(outs[r][key]).all()
@@ -175,10 +185,14 @@ def test_n_ranks_replicas_agree_and_train_like_one(tmp_path, world):
     g = orc.Graph.from_file(PL1K, 1)
     heldout = orc.sample_line(g, SEED + 7, 0, 50_000, 5)
     l1 = _heldout_loss(one["W"], one["C"], heldout)
+    lown = _heldout_loss(own["W"], own["C"], heldout)
     ln = _heldout_loss(outs[0]["W"], outs[0]["C"], heldout)
-    print("world %d (mean, %d samples): loss %.4f; 1 rank with %d samples: %.4f" % (world, total, ln, total // world, l1))
-    assert ln < np.log(2.0) * 6, ln
-    assert ln <= 1.02 * l1, (l1, ln)
+    lmean = _heldout_loss(avg["W"], avg["C"], heldout)
+    print("world %d adaptive: loss %.4f; mean %.4f; 1 rank all %d samples %.4f, own share %.4f"
+          % (world, ln, lmean, total, l1, lown))
+    assert l1 < 0.9 * np.log(2.0) * 6, l1
+    assert ln <= (1.06 if world == 4 else 1.40) * l1, (l1, ln)
+    assert ln < lmean and ln < lown, (ln, lmean, lown)
 
 
 def test_group_of_one_go_walk_models_equal_single_context(smore):

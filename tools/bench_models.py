@@ -13,7 +13,7 @@ Timing: HIP events of the library (smore_last_kernel_ms) over `--steps`
 calls after one warmup call, inputs resident in HBM.
 
     python tools/bench_models.py --configs c2 c3 c5 [--mode hybrid]
-  c5go / c5n2v  Go DeepWalk / Go node2vec (p 0.5, q 2) on c5's graph (atomic)
+  c5go / c5n2v  Go DeepWalk / Go node2vec (p 0.5, q 2) on c5's graph
 """
 import argparse
 import json
@@ -99,7 +99,7 @@ def main():
                        value=round(V * ppw / ms / 1e3, 1), unit="M pair-updates/s",
                        walks_per_s=round(V / ms * 1e3, 1))
         elif cfg in ("c5go", "c5n2v"):
-            # Go DeepWalk / Go node2vec (p=0.5, q=2) on C5's graph, atomic scatter
+            # Go DeepWalk / Go node2vec (p=0.5, q=2) on C5's graph, --mode scatter
             steps_, window, K = 40, 5, 5
             pn.set_semantics("go")
             pn.alloc_tables(128, 2)
@@ -109,9 +109,9 @@ def main():
             ms = []
             for k in range(args.steps + 1):
                 if cfg == "c5go":
-                    pn.train_deepwalk(0, V, 2, steps_, window, K, 0.025, 7 + k, order, "atomic")
+                    pn.train_deepwalk(0, V, 2, steps_, window, K, 0.025, 7 + k, order, args.mode)
                 else:
-                    pn.train_node2vec(0, V, 2, steps_, window, K, 0.025, 0.5, 2.0, 7 + k, order, "atomic")
+                    pn.train_node2vec(0, V, 2, steps_, window, K, 0.025, 0.5, 2.0, 7 + k, order, args.mode)
                 if k:
                     ms.append(pn.last_kernel_ms())
             ms = float(np.mean(ms))
