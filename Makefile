@@ -15,7 +15,8 @@ LIB      ?= smore_amd/lib/libsmore_hip.so
 BIN      := smore_amd/bin
 # kernels depend on the device headers only; host objects on the host headers
 DEV_HDRS := $(SRC)/device_common.h $(SRC)/train_kernels.h $(SRC)/edge_kernels.h $(SRC)/edge_inst.h
-HOST_HDRS := $(SRC)/host_graph.h $(SRC)/ctx.h $(SRC)/train_kernels.h $(SRC)/device_common.h $(SRC)/go_walks.h include/smore_hip.h
+HOST_HDRS := $(SRC)/host_graph.h $(SRC)/ctx.h $(SRC)/train_kernels.h $(SRC)/device_common.h $(SRC)/go_walks.h \
+             $(SRC)/hot_exchange.h include/smore_hip.h
 
 .PHONY: all lib cli goshape oracle ref clean
 all: lib cli goshape
@@ -31,8 +32,11 @@ $(OBJ)/%.o: $(SRC)/%.hip $(DEV_HDRS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-# the Go walk kernels also depend on the CTDNE declarations
+# the Go walk kernels also depend on the CTDNE declarations; the Go record
+# kernels on go_rec.h; the exchange passes on their declarations
 $(OBJ)/train_go.o: $(SRC)/go_walks.h
+$(OBJ)/train_go_rec_s.o $(OBJ)/train_go_rec_a.o $(OBJ)/train_go_rec_h.o: $(SRC)/go_rec.h $(SRC)/go_walks.h
+$(OBJ)/replica_sync.o: $(SRC)/hot_exchange.h
 
 LIB_OBJS := $(patsubst %,$(OBJ)/%.o,$(HOST_SRCS)) $(patsubst $(SRC)/%.hip,$(OBJ)/%.o,$(wildcard $(SRC)/*.hip))
 

@@ -607,7 +607,11 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
     if ((rc = grow(c->sync_ev, 2 * (size_t)nch))) return rc;
     if ((rc = ensure_packed(c))) return rc;
     const DevGraph dg = dev_graph(c);
-    const int ugrid = nch > 1 ? edge_grid(c, a, true, go ? 1 : 0) : grid;
+    // tuning knob: SMORE_DRAW_LEAVE=0 keeps the update kernel's full grid
+    // while the next chunk's draws run beside it
+    const char* leave_env = getenv("SMORE_DRAW_LEAVE");
+    const bool leave = !leave_env || atoi(leave_env) != 0;
+    const int ugrid = nch > 1 ? edge_grid(c, a, leave, go ? 1 : 0) : grid;
     hipStream_t ds = nch > 1 ? c->draw_stream : c->stream;
     auto recbuf = [&](int k) { return c->d_rec + (size_t)(k % nbuf) * chunk * RW; };
     auto draw = [&](int k) -> int {
@@ -1082,7 +1086,7 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
         HIPCHK(c, hipMalloc(&c->d_rec, chunk * pb * RW * sizeof(int32_t)));
         c->rec_cap = chunk * pb * RW;
     }
-    const bool combine = mode == SMORE_HYBRID && !go;   // the Go pair kernel: hot rows atomic, no LDS combining
+    const bool combine = mode == SMORE_HYBRID;
     ar.sh_rows = combine ? std::min(c->sh_max, 8192 / std::max(1, c->dpad)) : 0;
     ar.alpha_rec = 1;
     ar.work = c->d_work;

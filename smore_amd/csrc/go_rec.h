@@ -336,14 +336,18 @@ go_rec_kernel(EdgeArgs a) {
 // otherwise the run's summed gradient added atomically (no W update lost).
 // Context rows: atomic adds of each update's delta (MODE_ATOMIC), plain
 // stores (MODE_STORE), or by the records' hot tags (MODE_HYBRID: bit 30 of a
-// context / negative id, set by go_pair_emit_kernel from the C hot map).
+// context / negative id, set by go_pair_emit_kernel from the C hot map; the
+// hottest are write-combined in LDS as in edge_train_kernel).  The next
+// record is loaded while this one updates.
 // Serial (a.mode 2): one group, all records in order.
 template <int G, int M, int KMAX, int MODE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(waves_of(MODE))))
 go_pair_kernel(EdgeArgs a) {
     __shared__ float s_sig[1001];
-    for (int i = threadIdx.x; i < 1001; i += blockDim.x) s_sig[i] = a.sig[i];
-    __syncthreads();
+    extern __shared__ float s_dyn[];   // hybrid: the write-combined hottest context rows
+    int32_t* sh_ids = nullptr;
+    const ShState sh = block_setup<MODE>(a, s_sig, s_dyn, sh_ids);
+    constexpr bool DELTA = MODE == MODE_ATOMIC || MODE == MODE_HYBRID;
     const int lane = threadIdx.x & (G - 1);
     const uint64_t count = a.count_dev ? *a.count_dev : a.count;
     const uint64_t gpb = blockDim.x / G, gib = threadIdx.x / G;
@@ -352,6 +356,7 @@ go_pair_kernel(EdgeArgs a) {
     constexpr int RW = rec_width(KMAX);
     const int dpad = a.dpad;
     const bool serial = a.mode == 2;
+    uint32_t round = 0;
     auto slice = [&](uint64_t s0, uint64_t s1) {
         int32_t cv = -1;
         float wv[M], wsum[M];
@@ -360,15 +365,36 @@ go_pair_kernel(EdgeArgs a) {
             if (serial) st_row<G, M>(a.W + (int64_t)cv * dpad, wv, lane, ev);
             else atomic_row<G, M>(a.W + (int64_t)cv * dpad, wsum, lane, dpad);
         };
-        for (uint64_t t = s0; t < s1; ++t) {
-            const i32x4* p = reinterpret_cast<const i32x4*>(a.rec + t * RW);
-            i32x4 r[RW / 4];
+        i32x4 r[RW / 4];
+        auto load_rec = [&](uint64_t t) {
 #pragma unroll
-            for (int q = 0; q < RW / 4; ++q) r[q] = __builtin_nontemporal_load(p + q);
+            for (int q = 0; q < RW / 4; ++q) r[q] = i32x4{-1, -1, -1, -1};
+            if (t < s1) {
+                const i32x4* p = reinterpret_cast<const i32x4*>(a.rec + t * RW);
+#pragma unroll
+                for (int q = 0; q < RW / 4; ++q) r[q] = __builtin_nontemporal_load(p + q);
+            }
+        };
+        load_rec(s0);
+        for (uint64_t t = s0; t < s1; ++t) {
+            // decode this record, then load the next one behind it
             const int32_t v = r[0][0], c_t = r[0][1];
-            if (c_t < 0) continue;
-            const int32_t c = untag(c_t);
             const float alpha = __int_as_float(r[(2 + KMAX) / 4][(2 + KMAX) % 4]);
+            const int32_t c = c_t < 0 ? -1 : untag(c_t);
+            // the context's row and the negatives' (a negative equal to the
+            // context is skipped, not redrawn; repeats start from the first)
+            int32_t id[KMAX + 1];
+            bool hot[KMAX + 1];
+            id[0] = c;
+            hot[0] = MODE == MODE_ATOMIC || (MODE == MODE_HYBRID && c_t >= 0 && tag_hot(c_t));
+#pragma unroll
+            for (int k = 1; k <= KMAX; ++k) {
+                const int32_t x = k - 1 < a.K ? r[(k + 1) / 4][(k + 1) % 4] : -1;
+                id[k] = (x < 0 || untag(x) == c) ? -1 : untag(x);
+                hot[k] = MODE == MODE_ATOMIC || (MODE == MODE_HYBRID && x >= 0 && tag_hot(x));
+            }
+            load_rec(t + 1);
+            if (c < 0) continue;
             if (v != cv) {
                 flush();
                 cv = v;
@@ -376,22 +402,12 @@ go_pair_kernel(EdgeArgs a) {
 #pragma unroll
                 for (int m = 0; m < M; ++m) wsum[m] = 0.0f;
             }
-            // the context's row and the negatives' (a negative equal to the
-            // context is skipped, not redrawn; repeats start from the first)
-            int32_t id[KMAX + 1];
-            bool hot[KMAX + 1];
-            id[0] = c;
-            hot[0] = MODE == MODE_HYBRID && tag_hot(c_t);
-#pragma unroll
-            for (int k = 1; k <= KMAX; ++k) {
-                const int32_t x = k - 1 < a.K ? r[(k + 1) / 4][(k + 1) % 4] : -1;
-                id[k] = (x < 0 || untag(x) == c) ? -1 : untag(x);
-                hot[k] = MODE == MODE_HYBRID && x >= 0 && tag_hot(x);
-            }
             float rows[KMAX + 1][M];
 #pragma unroll
             for (int k = 0; k <= KMAX; ++k)
                 ld_row<G, M>(rows[k], a.C + (int64_t)(id[k] < 0 ? 0 : id[k]) * dpad, lane, ev, id[k] >= 0);
+            int slot[KMAX + 1];
+            go_sh_pending<G, M, KMAX, MODE>(sh, dpad, lane, ev, id, hot, slot, rows);
 #pragma unroll
             for (int k = 2; k <= KMAX; ++k)
 #pragma unroll
@@ -428,25 +444,25 @@ go_pair_kernel(EdgeArgs a) {
 #pragma unroll
                         for (int m = 0; m < M; ++m) rows[k2][m] = nk[m];
                     }
-                float* row = a.C + (int64_t)id[k] * dpad;
-                if (MODE == MODE_ATOMIC || hot[k]) atomic_row<G, M>(row, dk, lane, dpad);
-                else if (last) st_row<G, M>(row, nk, lane, ev);
+                if ((DELTA && hot[k]) || last)
+                    go_put<G, M, MODE>(a.C + (int64_t)id[k] * dpad, sh, slot[k], dpad, lane, ev, hot[k], nk, dk);
             }
             {
-                float* row = a.C + (int64_t)c * dpad;
-                if (MODE == MODE_ATOMIC || hot[0]) {
-                    atomic_row<G, M>(row, cg, lane, dpad);
-                } else {
-                    float nc[M];
+                float nc[M];
 #pragma unroll
-                    for (int m = 0; m < M; ++m) nc[m] = rows[0][m] + cg[m];
-                    st_row<G, M>(row, nc, lane, ev);
-                }
+                for (int m = 0; m < M; ++m) nc[m] = rows[0][m] + cg[m];
+                go_put<G, M, MODE>(a.C + (int64_t)c * dpad, sh, slot[0], dpad, lane, ev, hot[0], nc, cg);
             }
 #pragma unroll
             for (int m = 0; m < M; ++m) {
                 wv[m] = wv[m] + vg[m];
                 wsum[m] = wsum[m] + vg[m];
+            }
+            if constexpr (MODE == MODE_HYBRID) {
+                if (sh.n > 0 && ++round == (uint32_t)a.sh_flush) {
+                    sh_drain(sh, sh_ids, a.W, a.C, dpad);
+                    round = 0;
+                }
             }
         }
         flush();
@@ -467,6 +483,12 @@ go_pair_kernel(EdgeArgs a) {
         const uint64_t s0 = c0 + gib * CH_ROUNDS;
         slice(s0 < lim ? s0 : lim, s0 + CH_ROUNDS < lim ? s0 + CH_ROUNDS : lim);
     }
+    if constexpr (MODE == MODE_HYBRID) {
+        if (sh.n > 0) {
+            __syncthreads();
+            sh_drain(sh, sh_ids, a.W, a.C, dpad);
+        }
+    }
 }
 
 template <int KMAX, int MODE>
@@ -475,7 +497,8 @@ struct GoPairInst {
         const int G = lanes_of(a.dpad), M = regs_of(a.dpad);
 #define X(g, m)                                                                          \
     if (G == g && M == m) {                                                              \
-        hipLaunchKernelGGL((go_pair_kernel<g, m, KMAX, MODE>), dim3(grid), dim3(256), 0, st, a); \
+        hipLaunchKernelGGL((go_pair_kernel<g, m, KMAX, MODE>), dim3(grid), dim3(256),              \
+                           sh_lds_bytes(MODE == MODE_HYBRID ? a.sh_rows : 0, a.dpad), st, a);    \
         return hipGetLastError();                                                        \
     }
         SMORE_FOR_EACH_GM(X)
