@@ -398,3 +398,50 @@ def test_exchange_kernels_r_ne_d(smore, scale):
     np.testing.assert_array_equal(s, Tn)
     np.testing.assert_array_equal(d, Dn)
     np.testing.assert_array_equal(r, Dn)
+
+
+@pytest.mark.parametrize("stride", [4, 64])
+def test_exchange_row_kernels_r_ne_d(smore, stride):
+    """delta_end_rows / delta_cycle_rows (the adaptive rule's per-row scale,
+    replica_sync.hip) with R != D, bit for bit against numpy float32: row i of
+    `stride` floats uses scale[i]."""
+    import torch
+    _, pn = make_pair(smore, "toy.txt", 1)
+    rows = 20_003
+    n = rows * stride
+    rng = np.random.default_rng(stride)
+    T, S, D, R = [(rng.standard_normal(n) * 0.1).astype(np.float32) for _ in range(4)]
+    sc = (0.125 + 0.875 * rng.random(rows)).astype(np.float32)
+    dev = [torch.from_numpy(x.copy()).cuda() for x in (T, S, D, R)]
+    dsc = torch.from_numpy(sc).cuda()
+    p = [t.data_ptr() for t in dev]
+    scn = np.repeat(sc, stride)
+
+    def host():
+        return [t.cpu().numpy() for t in dev]
+
+    # end: X = scale[row]*R - D; T += X; S += X
+    pn.delta_end_rows(*p, dsc.data_ptr(), rows, stride)
+    torch.cuda.synchronize()
+    X = scn * R - D
+    T1, S1 = T + X, S + X
+    t, s, d, r = host()
+    np.testing.assert_array_equal(t, T1)
+    np.testing.assert_array_equal(s, S1)
+    np.testing.assert_array_equal(d, D)
+    np.testing.assert_array_equal(r, R)
+    # cycle: the end fused with the next begin
+    R2 = (rng.standard_normal(n) * 0.05).astype(np.float32)
+    dev[3].copy_(torch.from_numpy(R2))
+    pn.delta_cycle_rows(*p, dsc.data_ptr(), rows, stride)
+    torch.cuda.synchronize()
+    X = scn * R2 - D
+    Tn, Sn = T1 + X, S1 + X
+    Dn = Tn - Sn
+    t, s, d, r = host()
+    np.testing.assert_array_equal(t, Tn)
+    np.testing.assert_array_equal(s, Tn)
+    np.testing.assert_array_equal(d, Dn)
+    np.testing.assert_array_equal(r, Dn)
+    with pytest.raises(Exception):
+        pn.delta_end_rows(*p, dsc.data_ptr(), rows, 6)    # stride % 4 != 0

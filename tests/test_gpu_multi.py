@@ -40,21 +40,27 @@ def _fresh(smore):
     return pn
 
 
-def test_capi_rccl_world1_exchange_adds_zero(smore):
+@pytest.mark.parametrize("rule", ["sum", "mean", "adaptive"])
+def test_capi_rccl_world1_exchange_adds_zero(smore, rule):
+    """At world size 1 every rule's factor is exactly 1 (adaptive: s + (1 - s)/1),
+    so each exchange adds R - D = 0: the tables equal the run without exchanges
+    bit for bit (uniform and per-row passes, through RCCL)."""
     total, n = 10 ** 6, 20000
     ref = _fresh(smore)
     for k in range(3):
         ref.train_edges("line2", k * n, n, total, 5, 0.025, 0.0, SEED, "serial")
     pn = _fresh(smore)
     pn.comm_init(1, 0, smore.comm_unique_id())
+    if rule == "adaptive":
+        pn.exchange_set_adaptive("line2", 5, n, 64.0)
     pn.exchange_reset()
     before = pn.get_table(0)
-    pn.exchange_begin()
+    pn.exchange_begin(rule)
     pn.exchange_end()
     np.testing.assert_array_equal(pn.get_table(0), before)
     for k in range(3):      # begin after every step: the 2nd and 3rd fold the previous one in (delta_cycle)
         pn.train_edges("line2", k * n, n, total, 5, 0.025, 0.0, SEED, "serial", sync=False)
-        pn.exchange_begin()
+        pn.exchange_begin(rule)
     pn.exchange_end()
     pn.synchronize()
     np.testing.assert_array_equal(pn.get_table(0), ref.get_table(0))
