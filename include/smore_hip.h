@@ -247,7 +247,8 @@ int smore_row_rates(smore_ctx* ctx, int model, int K, int which, int64_t n, doub
 #define SMORE_SYNC_MEAN 1
 #define SMORE_SYNC_ADAPTIVE 2
 /* the row scales of the adaptive rule for `updates` samples of `model` per rank
- * per exchange (smore_exchange_begin with SMORE_SYNC_ADAPTIVE needs them) */
+ * per exchange (smore_exchange_begin with SMORE_SYNC_ADAPTIVE needs them); after
+ * smore_comm_init (they depend on the world size) and smore_alloc_tables */
 int smore_exchange_set_adaptive(smore_ctx* ctx, int model, int K, double updates, double c0);
 
 /* ---- multi-GPU replicas over RCCL, in the library (smore_amd/csrc/exchange.cpp) ------

@@ -495,6 +495,8 @@ int smore_exchange_set_adaptive(smore_ctx* c, int model, int K, double updates, 
     if (!c || !(updates > 0.0) || !(c0 > 0.0)) return SMORE_EINVAL;
     if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
     if (c->ntables < 1) return fail(c, SMORE_ESTATE, "tables not allocated");
+    // the scales depend on the world size: only after smore_comm_init
+    if (!c->comm) return fail(c, SMORE_ESTATE, "adaptive exchange before smore_comm_init");
     const std::string key = scale_key(model, K, updates, c0, c->nranks, c);
     if (c->ex_scale_key == key) return SMORE_OK;
     std::vector<float> sc[2];
