@@ -67,7 +67,10 @@ def parse():
                     help="N > 1 exchange rule: adaptive (default: per row the sum for rows with few updates per "
                          "exchange, towards the mean for the hubs), mean (model averaging) or sum (every update "
                          "applied once; diverges at >= 4 ranks at this exchange period), DESIGN.md 10")
-    ap.add_argument("--sync-c0", type=float, default=64.0, help="adaptive rule: c0")
+    ap.add_argument("--sync-c0", type=float, default=None,
+                    help="adaptive rule: c0 (default 1024 with the source partition, 64 without)")
+    ap.add_argument("--no-partition", action="store_true",
+                    help="N > 1: replicate W too (default: W rows partitioned by source, only C exchanged)")
     ap.add_argument("--hot-rows", type=int, default=65536,
                     help="N > 1, --sync sum: hub rows per table exchanged after every launch")
     ap.add_argument("--launches", type=int, default=8,
@@ -185,8 +188,13 @@ def main():
     stream = torch.cuda.Stream()             # a real stream: the default one is the null stream
     torch.cuda.set_stream(stream)
     pn.set_stream(stream.cuda_stream)
+    # N > 1: each rank draws its sources from its own part of the vertex ids
+    # (equal source mass), so W rows are owned and only C is exchanged; the
+    # adaptive rule scales C's summed deltas per row
+    partition = world > 1 and not args.no_partition
+    c0 = args.sync_c0 if args.sync_c0 is not None else (1024.0 if partition else 64.0)
     sync = (ReplicaSync(pn, sync=args.sync, hot_rows=args.hot_rows, model="line2", K=args.negative,
-                        updates=args.samples * args.sync_every, c0=args.sync_c0)
+                        updates=args.samples * args.sync_every, c0=c0, partition=partition)
             if world > 1 else None)
     n_launch = max(1, args.launches) if (sync is not None and sync.hot_idx) else 1
     phase = [0.0, 0.0, 0]     # exposed draw ms, update ms, update launches (timed steps)
@@ -286,9 +294,11 @@ def main():
                                    % (args.config, "" if args.semantics == "cpp" else ", Go rules (pkg/pronet)"),
                        "vertices": V, "edge_slots": E, "dim": args.dim, "negative": K,
                        "samples_per_step_per_gpu": S, "scatter": args.mode,
-                       "sync": ("%s every %d steps%s" % (args.sync, args.sync_every,
-                                                           ", %d hub rows per table after each of %d launches per step"
-                                                           % (args.hot_rows, n_launch) if n_launch > 1 else ""))
+                       "sync": ("%s%s every %d steps%s%s" % (
+                           args.sync, " c0=%g" % c0 if args.sync == "adaptive" else "", args.sync_every,
+                           ", W partitioned by source (C exchanged, W gathered at the end)" if partition else "",
+                           ", %d hub rows per table after each of %d launches per step"
+                           % (args.hot_rows, n_launch) if n_launch > 1 else ""))
                                if world > 1 else "none",
                        "parallelism": "replicas%d" % world},
             # achieved = updates/s x 1868 B (the whole path's algorithmic

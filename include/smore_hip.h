@@ -229,6 +229,16 @@ int smore_delta_end_rows(smore_ctx* ctx, void* T, void* S, const void* D, const 
                          int64_t rows, int64_t stride);
 int smore_delta_cycle_rows(smore_ctx* ctx, void* T, void* S, void* D, void* R, const void* scale, int64_t rows,
                            int64_t stride);
+/* Source partition of the replicas: the vertex ids cut into
+ * nparts contiguous ranges of equal source mass under the current source law
+ * (bounds[p] .. bounds[p + 1] - 1 is part p; bounds has nparts + 1 entries) */
+int smore_source_parts(smore_ctx* ctx, int nparts, int64_t* bounds);
+/* this context draws its sources from part `part` only (the source law
+ * restricted and renormalised; W rows of other parts are never touched by its
+ * LINE-2 samples, so replicas own disjoint W rows and exchange only C).
+ * nparts 1 = the global law again.  Re-applied after smore_set_semantics /
+ * smore_set_alias(SMORE_AT_VERTEX); cleared by a new graph. */
+int smore_set_source_partition(smore_ctx* ctx, int nparts, int part);
 /* expected touches per sample of every row of table `which` (0 = W, 1 = C)
  * under `model` with K negatives (the sampler marginals of the context's graph;
  * the ranking smore_hot_row_ids sorts by); rate[V] */
@@ -291,8 +301,14 @@ int smore_group_size(const smore_group* g);
  * synchronously.  rows -1 = automatic (min(65536, V/8), the default), 0 = off
  * (then one launch per round); launches >= 1 (default 8). */
 int smore_group_set_hot_exchange(smore_group* g, int64_t rows, int launches);
-/* c0 of the adaptive exchange (default 64) */
+/* c0 of the adaptive exchange (-1 = default: 1024 with the source partition,
+ * 64 without) */
 int smore_group_set_adaptive(smore_group* g, double c0);
+/* LINE-2 group training partitions the W rows by source (default on): replica
+ * r draws its sources from part r (smore_set_source_partition, left set after
+ * the call), only C is exchanged, and the W parts are broadcast from their
+ * owners before the call returns */
+int smore_group_set_partition(smore_group* g, int on);
 smore_ctx* smore_group_ctx(smore_group* g, int rank);
 const char* smore_group_last_error(const smore_group* g);
 int smore_group_load_edgelist(smore_group* g, const char* path, int undirected, int vertex_method,

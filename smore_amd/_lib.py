@@ -83,8 +83,11 @@ def _load():
         "smore_delta_end_rows": (i32, [P, P, P, P, P, P, i64, i64]),
         "smore_delta_cycle_rows": (i32, [P, P, P, P, P, P, i64, i64]),
         "smore_row_rates": (i32, [P, i32, i32, i32, i64, P]),
+        "smore_source_parts": (i32, [P, i32, P]),
+        "smore_set_source_partition": (i32, [P, i32, i32]),
         "smore_exchange_set_adaptive": (i32, [P, i32, i32, dbl, dbl]),
         "smore_group_set_adaptive": (i32, [P, dbl]),
+        "smore_group_set_partition": (i32, [P, i32]),
         "smore_train_deepwalk": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, u64, P, i32]),
         "smore_train_deepwalk_async": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, u64, P, i32]),
         "smore_set_temporal_edges": (i32, [P, i64, P, P, P]),

@@ -173,6 +173,8 @@ int smore_get_csr(const smore_ctx* c, int64_t* offsets, int32_t* targets) {
     return SMORE_OK;
 }
 
+static int apply_partition(smore_ctx* c);   // source partition (below)
+
 int smore_set_alias(smore_ctx* c, int which, const double* prob, const int64_t* alias, int64_t n) {
     if (!c || !prob || !alias) return SMORE_EINVAL;
     if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
@@ -197,7 +199,8 @@ int smore_set_alias(smore_ctx* c, int which, const double* prob, const int64_t* 
     if ((rc = set_device(c))) return rc;
     AliasEntry*& d = which == 0 ? c->d_vtab : which == 1 ? c->d_ntab : c->d_ctab;
     c->packed_ok = false;
-    return upload(c, d, T.data(), T.size());
+    if ((rc = upload(c, d, T.data(), T.size()))) return rc;
+    return which == 0 && c->part_n > 1 ? apply_partition(c) : SMORE_OK;   // the new law, restricted again
 }
 
 int smore_get_alias(const smore_ctx* c, int which, double* prob, int64_t* alias, int64_t n) {
@@ -326,6 +329,93 @@ int smore_table_device(smore_ctx* c, int which, void** dptr, int64_t* stride) {
     return SMORE_OK;
 }
 
+// ---------------------------------------------------------------- source partition
+// Part bounds of the current (global) source law: vertex v belongs to the part
+// holding the midpoint of its probability mass, so parts are contiguous id
+// ranges of (nearly) equal mass; bound[p] .. bound[p + 1] - 1 is part p.
+static void source_bounds(const std::vector<double>& ps, int n, std::vector<int64_t>& bound) {
+    const int64_t V = (int64_t)ps.size();
+    double total = 0.0;
+    for (double p : ps) total += p;
+    bound.assign((size_t)n + 1, V);
+    bound[0] = 0;
+    double cum = 0.0;
+    int next = 1;
+    for (int64_t v = 0; v < V && next < n; ++v) {
+        const double mid = (cum + 0.5 * ps[v]) / total;
+        const int owner = std::min(n - 1, (int)std::floor(mid * n));
+        while (next <= owner && next < n) bound[next++] = v;
+        cum += ps[v];
+    }
+}
+
+// the source law restricted to part i of n and renormalised
+static void partition_law(const std::vector<double>& ps, int n, int i, std::vector<double>& law) {
+    std::vector<int64_t> bound;
+    source_bounds(ps, n, bound);
+    law.assign(ps.size(), 0.0);
+    double sum = 0.0;
+    for (int64_t v = bound[i]; v < bound[i + 1]; ++v) sum += ps[v];
+    if (sum > 0.0)
+        for (int64_t v = bound[i]; v < bound[i + 1]; ++v) law[v] = ps[v] / sum;
+}
+
+// Restrict the device vertex table to this context's part (renormalised, Go
+// alias rule with power 1: any valid encoding of the law; N > 1 only, where
+// draws are not compared with one GPU's) and upload it.
+static int apply_partition(smore_ctx* c) {
+    const HostGraph& g = *c->g;
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    c->packed_ok = false;
+    c->hot_key.clear();
+    if (c->part_n <= 1) {
+        c->part_vtab.clear();
+        c->part_bounds.clear();
+        return upload(c, c->d_vtab, g.vtab.data(), g.vtab.size());
+    }
+    std::vector<double> ps, pn, pc;
+    draw_probabilities(g, ps, pn, pc);
+    std::vector<int64_t>& bound = c->part_bounds;
+    source_bounds(ps, c->part_n, bound);
+    const int64_t lo = bound[c->part_i], hi = bound[c->part_i + 1];
+    if (hi <= lo) return fail(c, SMORE_EINVAL, "source partition: an empty part (more parts than vertices with mass)");
+    std::vector<double> w((size_t)g.V, 0.0), prob((size_t)g.V);
+    std::vector<int64_t> alias((size_t)g.V);
+    for (int64_t v = lo; v < hi; ++v) w[v] = ps[v];
+    alias_go(w.data(), g.V, 1.0, prob.data(), alias.data());
+    c->part_vtab.resize((size_t)g.V);
+    alias_encode(prob.data(), alias.data(), g.V, nullptr, c->part_vtab.data());
+    return upload(c, c->d_vtab, c->part_vtab.data(), c->part_vtab.size());
+}
+
+int smore_source_parts(smore_ctx* c, int nparts, int64_t* bounds) {
+    if (!c || !bounds || nparts < 1) return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    if (nparts > c->g->V) return fail(c, SMORE_EINVAL, "more parts than vertices");
+    if (c->part_n == nparts && (int)c->part_bounds.size() == nparts + 1) {   // the active partition's
+        std::copy(c->part_bounds.begin(), c->part_bounds.end(), bounds);
+        return SMORE_OK;
+    }
+    std::vector<double> ps, pn, pc;
+    draw_probabilities(*c->g, ps, pn, pc);
+    std::vector<int64_t> bound;
+    source_bounds(ps, nparts, bound);
+    std::copy(bound.begin(), bound.end(), bounds);
+    return SMORE_OK;
+}
+
+int smore_set_source_partition(smore_ctx* c, int nparts, int part) {
+    if (!c || nparts < 1 || part < 0 || part >= nparts) return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    if (nparts > c->g->V) return fail(c, SMORE_EINVAL, "more parts than vertices");
+    if (c->device < 0) return fail(c, SMORE_ESTATE, "host-only context");
+    if (c->part_n == nparts && c->part_i == part) return SMORE_OK;   // kept current by the table setters
+    c->part_n = nparts;
+    c->part_i = part;
+    return apply_partition(c);
+}
+
 // ---------------------------------------------------------------- hybrid scatter
 // A row is "hot" when the expected number of resident sample groups touching
 // it at once, M * p(row), exceeds tau; hot rows take float atomics, the rest
@@ -353,12 +443,19 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
     // it (1338 vs 1342 M/s), DESIGN.md 8
     const char* wrows_env = getenv("SMORE_SH_WROWS");
     const bool wrows = wrows_env && atoi(wrows_env) != 0;
-    snprintf(key, sizeof key, "%d/%d/%lld/%.9g/%d/%d/%s/%d", model, K, (long long)M, c->hot_tau, c->sh_max,
-             c->sh_flush, stale_env ? stale_env : "", (int)wrows);
+    snprintf(key, sizeof key, "%d/%d/%lld/%.9g/%d/%d/%s/%d/%d/%d", model, K, (long long)M, c->hot_tau, c->sh_max,
+             c->sh_flush, stale_env ? stale_env : "", (int)wrows, c->part_n, c->part_i);
     if (c->hot_key == key) return SMORE_OK;
     if (c->g->V >= ((int64_t)1 << 30)) return fail(c, SMORE_EINVAL, "hybrid scatter needs V < 2^30");
     std::vector<double> ps, pn, pc;
     draw_probabilities(*c->g, ps, pn, pc);
+    if (c->part_n > 1) {
+        // this replica draws its sources from its part only: the hot rows
+        // follow the restricted law (its part's W rows N times as hot)
+        std::vector<double> law;
+        partition_law(ps, c->part_n, c->part_i, law);
+        draw_probabilities(*c->g, ps, pn, pc, &law);
+    }
     const int64_t V = c->g->V, E = c->g->E;
     std::vector<uint8_t> hw((size_t)V, 0), hc((size_t)V, 0);
     const int negs = model == SMORE_BPR ? 5 : K;
@@ -425,7 +522,8 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
     int rc;
     if ((rc = set_device(c))) return rc;
     {
-        const std::vector<AliasEntry> vt = tag_tab(g.vtab, hw), nt = tag_tab(g.ntab, hc);
+        const std::vector<AliasEntry> vt = tag_tab(c->part_n > 1 ? c->part_vtab : g.vtab, hw),
+                                      nt = tag_tab(g.ntab, hc);
         HIPCHK(c, hipMemcpy(c->d_vtab, vt.data(), V * sizeof(AliasEntry), hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(c->d_ntab, nt.data(), V * sizeof(AliasEntry), hipMemcpyHostToDevice));
     }
@@ -696,7 +794,7 @@ int smore_set_semantics(smore_ctx* c, int semantics) {
     } else {
         dfree(c->d_tcum);
     }
-    return SMORE_OK;
+    return c->part_n > 1 ? apply_partition(c) : SMORE_OK;   // the semantics' source law, restricted
 }
 
 int smore_set_hot_threshold(smore_ctx* c, double tau) {

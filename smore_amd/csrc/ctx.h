@@ -114,6 +114,7 @@ struct smore_ctx {
     int ex_tables = 0;
     bool ex_pending = false;            // an all-reduce is in flight
     int ex_mode = 0;                    // SMORE_SYNC_* of the in-flight exchange
+    int ex_t0 = 0;                      // first exchanged table (1: W partitioned by source, C only)
     // adaptive exchange: per-row scales of the summed deltas per table and
     // the (model, K, updates, c0, N) they were made for
     float* ex_scale[2] = {nullptr, nullptr};
@@ -124,6 +125,13 @@ struct smore_ctx {
     float* hot_buf[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};   // [table][P, R]
     int64_t hot_n = 0;
     std::string hot_ex_key;
+    // source partition (smore_set_source_partition): this context draws its
+    // sources from part part_i of part_n -- contiguous vertex ranges of equal
+    // source mass -- through part_vtab, the restricted vertex table on the
+    // device; the host graph keeps the global one (shared by the replicas)
+    int part_n = 1, part_i = 0;
+    hvec<AliasEntry> part_vtab;
+    std::vector<int64_t> part_bounds;   // part_n + 1 bounds of the current partition
 };
 
 // exchange.cpp: frees the exchange buffers and the communicator
@@ -185,6 +193,10 @@ inline int upload_graph(smore_ctx* c) {
     if ((rc = set_device(c))) return rc;
     HostGraph& g = *c->g;
     c->packed_ok = false;
+    c->part_n = 1;          // a new graph: the global source law
+    c->part_i = 0;
+    c->part_vtab.clear();
+    c->part_bounds.clear();
     dfree(c->d_vt32);
     dfree(c->d_ct16);
     if ((rc = upload(c, c->d_offsets, g.offsets.data(), g.offsets.size()))) return rc;

@@ -126,7 +126,7 @@ int exchange_reset(smore_ctx* c) {
         HIPCHK(c, hipStreamWaitEvent(c->stream, c->ex_done, 0));
         c->ex_pending = false;
     }
-    for (int t = 0; t < c->ntables; ++t)
+    for (int t = c->ex_t0; t < c->ntables; ++t)
         HIPCHK(c, hipMemcpyAsync(c->ex_buf[t][0], c->d_table[t], c->ex_n * sizeof(float), hipMemcpyDeviceToDevice,
                                  c->stream));
     return SMORE_OK;
@@ -144,7 +144,7 @@ int exchange_passes(smore_ctx* c, int mode) {
     if (mode == SMORE_SYNC_ADAPTIVE && !c->ex_scale[0])
         return fail(c, SMORE_ESTATE, "adaptive exchange without row scales (smore_exchange_set_adaptive)");
     if (c->ex_pending) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ex_done, 0));
-    for (int t = 0; t < c->ntables; ++t) {
+    for (int t = c->ex_t0; t < c->ntables; ++t) {
         float* T = c->d_table[t];
         float* const* b = c->ex_buf[t];
         if (!c->ex_pending) HIPCHK(c, launch_delta_begin(T, b[0], b[1], b[2], c->ex_n, c->cus, c->stream));
@@ -161,7 +161,7 @@ int exchange_passes(smore_ctx* c, int mode) {
 
 int exchange_collective(smore_ctx* c) {
     Rccl* L = rccl();
-    for (int t = 0; t < c->ntables; ++t)
+    for (int t = c->ex_t0; t < c->ntables; ++t)
         NCCLCHK(c, "ncclAllReduce",
                 L->all_reduce(c->ex_buf[t][2], c->ex_buf[t][2], c->ex_n, ncclFloat32, ncclSum, (ncclComm_t)c->comm,
                               c->comm_stream));
@@ -181,7 +181,7 @@ int exchange_end(smore_ctx* c) {
     if ((rc = check_comm(c))) return rc;
     if (!c->ex_pending) return SMORE_OK;
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->ex_done, 0));
-    for (int t = 0; t < c->ntables; ++t) {
+    for (int t = c->ex_t0; t < c->ntables; ++t) {
         float* const* b = c->ex_buf[t];
         if (c->ex_mode == SMORE_SYNC_ADAPTIVE)
             HIPCHK(c, launch_delta_end_rows(c->d_table[t], b[0], b[1], b[2], c->ex_scale[t], (uint64_t)c->g->V,
@@ -269,7 +269,8 @@ struct smore_group {
     // automatic, 0: off) and training launches per exchange round
     int64_t hot_rows = -1;
     int launches = 8;
-    double c0 = 64.0;   // adaptive exchange (smore_group_set_adaptive)
+    double c0 = -1.0;   // adaptive exchange (smore_group_set_adaptive); -1: 1024 with the source partition, else 64
+    int partition = 1;  // LINE-2: W rows partitioned by source (smore_group_set_partition)
 };
 
 namespace {
@@ -380,6 +381,31 @@ int group_hot_exchange(smore_group* g) {
     return SMORE_OK;
 }
 
+// every replica gets every part's W rows from the part's owner (replica p
+// owns part p of the source partition): one in-place broadcast per part
+int gather_sources(smore_group* g) {
+    const size_t n = g->ctx.size();
+    std::vector<int64_t> b(n + 1);
+    int rc;
+    if ((rc = smore_source_parts(g->ctx[0], (int)n, b.data()))) return gfail(g, 0, rc);
+    Rccl* L = rccl();
+    for (size_t p = 0; p < n; ++p) {
+        if (b[p + 1] <= b[p]) continue;
+        ncclResult_t nr = L->group_start();
+        for (size_t r = 0; r < n && nr == ncclSuccess; ++r) {
+            smore_ctx* c = g->ctx[r];
+            (void)hipSetDevice(c->device);
+            float* rows = c->d_table[0] + (size_t)b[p] * c->dpad;
+            nr = L->broadcast(rows, rows, (size_t)(b[p + 1] - b[p]) * c->dpad, ncclFloat32, (int)p,
+                              (ncclComm_t)c->comm, c->stream);
+        }
+        ncclResult_t ne = L->group_end();
+        if (nr == ncclSuccess) nr = ne;
+        if (nr != ncclSuccess) return gfail(g, 0, nccl_fail(g->ctx[0], "W gather ncclBroadcast", nr));
+    }
+    return SMORE_OK;
+}
+
 int group_sync(smore_group* g) {
     int rc;
     for (size_t r = 0; r < g->ctx.size(); ++r)
@@ -400,19 +426,27 @@ int group_sync(smore_group* g) {
 // are synced after each.
 template <class F>
 static int group_rounds(smore_group* g, uint64_t begin, uint64_t end, uint64_t per, int rule, F&& run,
-                        int model = SMORE_LINE2, int K = 5, double upu = 1.0) {
+                        int model = SMORE_LINE2, int K = 5, double upu = 1.0, bool part = false) {
     const size_t n = g->ctx.size();
     int rc;
     if (end <= begin) return SMORE_OK;
     if (rule < SMORE_SYNC_SUM || rule > SMORE_SYNC_ADAPTIVE) return gfail(g, 0, fail(g->ctx[0], SMORE_EINVAL, "bad exchange rule"));
-    for (size_t r = 0; r < n; ++r)
-        if ((rc = exchange_reset(g->ctx[r]))) return gfail(g, (int)r, rc);
+    // LINE-2 with the source partition: replica r draws its sources from part
+    // r, owns those W rows, and only C is exchanged (W gathered at the end)
+    part = part && g->partition && n > 1;
+    for (size_t r = 0; r < n; ++r) {
+        smore_ctx* c = g->ctx[r];
+        if ((rc = smore_set_source_partition(c, part ? (int)n : 1, part ? (int)r : 0))) return gfail(g, (int)r, rc);
+        c->ex_t0 = part ? 1 : 0;
+        if ((rc = exchange_reset(c))) return gfail(g, (int)r, rc);
+    }
+    const double c0 = g->c0 > 0 ? g->c0 : (part ? 1024.0 : 64.0);
     if (rule == SMORE_SYNC_ADAPTIVE) {
         const double updates = (double)per * upu;
-        const std::string key = scale_key(model, K, updates, g->c0, (int)n, g->ctx[0]);
+        const std::string key = scale_key(model, K, updates, c0, (int)n, g->ctx[0]);
         if (g->ctx[0]->ex_scale_key != key) {
             std::vector<float> sc[2];
-            if ((rc = adaptive_scales(g->ctx[0], model, K, updates, g->c0, (int)n, sc))) return gfail(g, 0, rc);
+            if ((rc = adaptive_scales(g->ctx[0], model, K, updates, c0, (int)n, sc))) return gfail(g, 0, rc);
             for (size_t r = 0; r < n; ++r)
                 if ((rc = upload_scales(g->ctx[r], sc, key))) return gfail(g, (int)r, rc);
         }
@@ -438,6 +472,7 @@ static int group_rounds(smore_group* g, uint64_t begin, uint64_t end, uint64_t p
     }
     for (size_t r = 0; r < n; ++r)
         if ((rc = exchange_end(g->ctx[r]))) return gfail(g, (int)r, rc);
+    if (part && (rc = gather_sources(g))) return rc;
     return group_sync(g);
 }
 
@@ -557,8 +592,14 @@ void smore_group_destroy(smore_group* g) {
 int smore_group_size(const smore_group* g) { return g ? (int)g->ctx.size() : 0; }
 
 int smore_group_set_adaptive(smore_group* g, double c0) {
-    if (!g || !(c0 > 0.0)) return SMORE_EINVAL;
+    if (!g || !(c0 > 0.0 || c0 == -1.0)) return SMORE_EINVAL;
     g->c0 = c0;
+    return SMORE_OK;
+}
+
+int smore_group_set_partition(smore_group* g, int on) {
+    if (!g) return SMORE_EINVAL;
+    g->partition = on != 0;
     return SMORE_OK;
 }
 
@@ -673,7 +714,7 @@ int smore_group_train_edges(smore_group* g, int model, uint64_t begin, uint64_t 
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_edges_async(c, model, b, e - b, total, K, alpha0, reg, seed, mode);
                         },
-                        model, K);
+                        model, K, 1.0, model == SMORE_LINE2);
 }
 
 int smore_group_train_deepwalk(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,

@@ -315,11 +315,12 @@ static void alias_marginal(const hvec<double>& prob, const hvec<int64_t>& alias,
 }
 
 void draw_probabilities(const HostGraph& g, std::vector<double>& p_src, std::vector<double>& p_neg,
-                        std::vector<double>& p_ctx) {
+                        std::vector<double>& p_ctx, const std::vector<double>* src_law) {
     p_src.assign((size_t)g.V, 0.0);
     p_neg.assign((size_t)g.V, 0.0);
     p_ctx.assign((size_t)g.V, 0.0);
-    alias_marginal(g.vprob, g.valias, 0, g.V, nullptr, 1.0 / g.V, p_src);
+    if (src_law) p_src = *src_law;
+    else alias_marginal(g.vprob, g.valias, 0, g.V, nullptr, 1.0 / g.V, p_src);
     alias_marginal(g.nprob, g.nalias, 0, g.V, nullptr, 1.0 / g.V, p_neg);
     for (int64_t v = 0; v < g.V; ++v) {
         const int64_t off = g.offsets[v], br = g.offsets[v + 1] - off;

@@ -113,9 +113,10 @@ class GlibcRand {
 
 // Exact per-draw probabilities encoded by the alias tables: source
 // (vertex_AT), negative (negative_AT) and the marginal context-target
-// probability sum_v p_src(v) * P(target | v).
+// probability sum_v p_src(v) * P(target | v).  src_law: use this source law
+// instead of vertex_AT's (a replica's restricted law, capi source partition).
 void draw_probabilities(const HostGraph& g, std::vector<double>& p_src, std::vector<double>& p_neg,
-                        std::vector<double>& p_ctx);
+                        std::vector<double>& p_ctx, const std::vector<double>* src_law = nullptr);
 
 // DeepWalk walk-start order (src/model/DeepWalk.cpp:122-131).
 void deepwalk_order(int64_t V, int walk_times, uint64_t skip, int64_t* order);

@@ -214,10 +214,16 @@ class ReplicaSync(OverlapSync):
         D' = T_h - S_h;  R' = all_reduce(D');  T_h += R' - D';  S_h += R'
 
     This composes with the one-late full exchange (no update counted twice:
-    the next begin() sees only the hub rows' changes since the last hot())."""
+    the next begin() sees only the hub rows' changes since the last hot()).
+
+    partition=True (LINE-2): rank r draws its sources from part r of the
+    vertex ids (contiguous ranges of equal source mass,
+    smore_set_source_partition), so each W row is updated by one rank only
+    and only C is exchanged; end() then gathers W (each part broadcast from
+    its owner).  The adaptive scales come from the global law."""
 
     def __init__(self, pn, mean=False, tables=(0, 1), group=None, hot_rows=0, model="line2", K=5, sync=None,
-                 updates=None, c0=64.0):
+                 updates=None, c0=64.0, partition=False):
         # the passes, the training kernels and the collective must be ordered
         # on ONE stream.  The context runs on its own non-blocking stream when
         # handed the null stream (handle 0), which the legacy null stream does
@@ -225,6 +231,10 @@ class ReplicaSync(OverlapSync):
         if torch.cuda.current_stream().cuda_stream == 0:
             torch.cuda.set_stream(torch.cuda.Stream())
         pn.set_stream(torch.cuda.current_stream().cuda_stream)
+        if partition:
+            if model != "line2":
+                raise ValueError("source partition: LINE-2 (W rows are sources only)")
+            tables = (1,)
         T = [table_tensor(pn, w) for w in tables]
         if sync is None:
             sync = "mean" if mean else "sum"
@@ -245,3 +255,22 @@ class ReplicaSync(OverlapSync):
         super().__init__(T, mean=sync == "mean", group=group, passes=HipPasses(pn), hot_idx=hot_idx,
                          row_scale=row_scale)
         self.sync = sync
+        self.bounds = None
+        if partition:
+            world, rank = dist.get_world_size(group), dist.get_rank(group)
+            self.bounds = [int(b) for b in pn.source_parts(world)]
+            self.W = table_tensor(pn, 0)
+            pn.set_source_partition(world, rank)
+
+    def gather_sources(self):
+        """Every rank gets every part's W rows from the part's owner."""
+        ranks = dist.get_process_group_ranks(self.group) if self.group is not None else None
+        for p in range(len(self.bounds) - 1):
+            lo, hi = self.bounds[p], self.bounds[p + 1]
+            if hi > lo:
+                dist.broadcast(self.W[lo:hi], src=ranks[p] if ranks else p, group=self.group)
+
+    def end(self):
+        super().end()
+        if self.bounds is not None:
+            self.gather_sources()

@@ -295,6 +295,16 @@ class ProNet:
                                       r.ctypes.data_as(C.c_void_p)), "row_rates")
         return r
 
+    def source_parts(self, nparts):
+        """Bounds (nparts + 1, int64) of the contiguous equal-source-mass vertex parts."""
+        b = np.zeros(int(nparts) + 1, np.int64)
+        self._chk(lib.smore_source_parts(self.ctx, int(nparts), b.ctypes.data_as(C.c_void_p)), "source_parts")
+        return b
+
+    def set_source_partition(self, nparts, part):
+        """Draw sources from part `part` of `nparts` only (1 = the global law)."""
+        self._chk(lib.smore_set_source_partition(self.ctx, int(nparts), int(part)), "set_source_partition")
+
     def synchronize(self):
         self._chk(lib.smore_synchronize(self.ctx), "synchronize")
 
@@ -436,9 +446,13 @@ class Group:
                                                   _lib.VM[vertex_method], _lib.NM[negative_method]),
                   "set_graph_edges")
 
-    def set_adaptive(self, c0=64.0):
-        """smore_group_set_adaptive: c0 of the adaptive exchange rule."""
+    def set_adaptive(self, c0=-1.0):
+        """smore_group_set_adaptive: c0 of the adaptive exchange rule (-1: the default)."""
         self._chk(lib.smore_group_set_adaptive(self.g, float(c0)), "set_adaptive")
+
+    def set_partition(self, on=True):
+        """smore_group_set_partition: LINE-2 W rows partitioned by source (default on)."""
+        self._chk(lib.smore_group_set_partition(self.g, int(bool(on))), "set_partition")
 
     def set_hot_exchange(self, rows=-1, launches=8):
         """smore_group_set_hot_exchange: hub rows per table synced after every

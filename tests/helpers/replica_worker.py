@@ -24,6 +24,11 @@ def main():
     launches = int(sys.argv[8]) if len(sys.argv) > 8 else 1
     spec = sys.argv[9] if len(sys.argv) > 9 else "sum"
     spec = {"0": "sum", "1": "mean"}.get(spec, spec)
+    # "+part": W partitioned by source (ReplicaSync partition=True: each rank
+    # draws sources from its own part of the vertex law, only C is exchanged,
+    # W gathered from the owners at the end)
+    spec, plus, opt = spec.partition("+")
+    part = plus and opt == "part"
     rule, _, c0 = spec.partition(":")
     c0 = float(c0) if c0 else 64.0
     import numpy as np
@@ -40,7 +45,8 @@ def main():
     pn.init_table_glibc(0, 0)
     pn.zero_table(1)
     per = total // world // steps
-    sync = (ReplicaSync(pn, sync=rule, hot_rows=hot_rows, model="line2", K=5, updates=per, c0=c0)
+    sync = (ReplicaSync(pn, sync=rule, hot_rows=hot_rows, model="line2", K=5, updates=per, c0=c0,
+                        partition=part)
             if world > 1 else None)
     nl = launches if (sync is not None and sync.hot_idx) else 1
     for k in range(steps):

@@ -76,8 +76,10 @@ def main():
             print(json.dumps(dict(base, rule="1 rank")), flush=True)
             for rule in args.rules:
                 outs = run(tmp, world, args.total, steps, rule)
-                spread = max(float(np.abs(o["W"] - outs[0]["W"]).max()) for o in outs)
                 W, C = outs[0]["W"], outs[0]["C"]
+                # (with "+part" the worker gathered W from the owners: every rank
+                # holds all of it)
+                spread = max(max(float(np.abs(o[k] - outs[0][k]).max()) for k in ("W", "C")) for o in outs)
                 ok = bool(np.isfinite(W).all() and np.isfinite(C).all())
                 ln = heldout(W, C, draws) if ok else float("nan")
                 print(json.dumps(dict(base, rule=rule, loss=ln, finite=ok, spread=spread,
