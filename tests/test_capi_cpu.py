@@ -156,3 +156,34 @@ def test_go_semantics_tables_match_oracle(fname, und):
         tt, aa = pn.alias_encoded(which)
         np.testing.assert_array_equal(tt, t)
         np.testing.assert_array_equal(aa, a)
+
+
+@pytest.mark.parametrize("nparts", [1, 2, 3, 8])
+def test_source_parts_are_contiguous_equal_mass(nparts):
+    """smore_source_parts (host only): bounds 0 .. V, non-empty contiguous parts,
+    each vertex in the part that holds the midpoint of its source mass (the
+    exact vertex-table marginals), so every part's mass is within one vertex's
+    mass of 1/nparts; the row rates of W under LINE-2 are that law."""
+    from smore_amd import ProNet
+    from smore_amd import _lib
+    pn = ProNet(device=-1)
+    pn.LoadEdgeList(os.path.join(GOLDEN, "pl1k.txt"), 1)
+    V = pn.MAX_vid
+    b = pn.source_parts(nparts)
+    assert b[0] == 0 and b[-1] == V and (np.diff(b) > 0).all()
+    ps = pn.row_rates("line2", 5, 0)
+    assert abs(ps.sum() - 1.0) < 1e-9
+    # the exact marginal of the encoded vertex table
+    t, a = pn.alias_encoded(_lib.AT_VERTEX)
+    acc = t.astype(np.float64) / 2.0 ** 32
+    law = acc.copy()
+    np.add.at(law, a, 1.0 - acc)
+    np.testing.assert_allclose(ps, law / V, rtol=1e-9, atol=1e-15)
+    cum = np.concatenate([[0.0], np.cumsum(ps)])
+    mid = (cum[:-1] + 0.5 * ps) / cum[-1]
+    owner = np.minimum(np.floor(mid * nparts).astype(np.int64), nparts - 1)
+    for p in range(nparts):
+        assert (owner[b[p]:b[p + 1]] == p).all()
+        assert abs(ps[b[p]:b[p + 1]].sum() - 1.0 / nparts) <= ps.max() + 1e-12
+    with pytest.raises(_lib.SmoreError):
+        pn.source_parts(V + 1)
