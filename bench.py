@@ -68,7 +68,7 @@ def parse():
                          "exchange, towards the mean for the hubs), mean (model averaging) or sum (every update "
                          "applied once; diverges at >= 4 ranks at this exchange period), DESIGN.md 10")
     ap.add_argument("--sync-c0", type=float, default=None,
-                    help="adaptive rule: c0 (default 1024 with the source partition, 64 without)")
+                    help="adaptive rule: c0 (default 2048 with the source partition, 64 without)")
     ap.add_argument("--no-partition", action="store_true",
                     help="N > 1: replicate W too (default: W rows partitioned by source, only C exchanged)")
     ap.add_argument("--hot-rows", type=int, default=65536,
@@ -192,7 +192,7 @@ def main():
     # (equal source mass), so W rows are owned and only C is exchanged; the
     # adaptive rule scales C's summed deltas per row
     partition = world > 1 and not args.no_partition
-    c0 = args.sync_c0 if args.sync_c0 is not None else (1024.0 if partition else 64.0)
+    c0 = args.sync_c0 if args.sync_c0 is not None else (2048.0 if partition else 64.0)
     sync = (ReplicaSync(pn, sync=args.sync, hot_rows=args.hot_rows, model="line2", K=args.negative,
                         updates=args.samples * args.sync_every, c0=c0, partition=partition)
             if world > 1 else None)

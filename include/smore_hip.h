@@ -301,7 +301,7 @@ int smore_group_size(const smore_group* g);
  * synchronously.  rows -1 = automatic (min(65536, V/8), the default), 0 = off
  * (then one launch per round); launches >= 1 (default 8). */
 int smore_group_set_hot_exchange(smore_group* g, int64_t rows, int launches);
-/* c0 of the adaptive exchange (-1 = default: 1024 with the source partition,
+/* c0 of the adaptive exchange (-1 = default: 2048 with the source partition,
  * 64 without) */
 int smore_group_set_adaptive(smore_group* g, double c0);
 /* LINE-2 group training partitions the W rows by source (default on): replica

@@ -269,7 +269,7 @@ struct smore_group {
     // automatic, 0: off) and training launches per exchange round
     int64_t hot_rows = -1;
     int launches = 8;
-    double c0 = -1.0;   // adaptive exchange (smore_group_set_adaptive); -1: 1024 with the source partition, else 64
+    double c0 = -1.0;   // adaptive exchange (smore_group_set_adaptive); -1: 2048 with the source partition, else 64
     int partition = 1;  // LINE-2: W rows partitioned by source (smore_group_set_partition)
 };
 
@@ -440,7 +440,7 @@ static int group_rounds(smore_group* g, uint64_t begin, uint64_t end, uint64_t p
         c->ex_t0 = part ? 1 : 0;
         if ((rc = exchange_reset(c))) return gfail(g, (int)r, rc);
     }
-    const double c0 = g->c0 > 0 ? g->c0 : (part ? 1024.0 : 64.0);
+    const double c0 = g->c0 > 0 ? g->c0 : (part ? 2048.0 : 64.0);
     if (rule == SMORE_SYNC_ADAPTIVE) {
         const double updates = (double)per * upu;
         const std::string key = scale_key(model, K, updates, c0, (int)n, g->ctx[0]);

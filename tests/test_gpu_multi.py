@@ -122,7 +122,7 @@ def _heldout_loss(W, C, draws):
     return float(loss.mean())
 
 
-def _run_ranks(tmp_path, world, total, steps, hot_rows=0, launches=1, sync="adaptive:1024+part", tag=""):
+def _run_ranks(tmp_path, world, total, steps, hot_rows=0, launches=1, sync="adaptive:2048+part", tag=""):
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -147,7 +147,7 @@ def test_two_ranks_hip_passes_agree_and_train_like_one(tmp_path):
     """Exchange period: 8k samples per rank (~9 updates per row of the 920-row
     tables per rank between exchanges -- the C4 bench's 2^27 samples per rank
     give ~13 per row), bench.py's N > 1 default: W rows partitioned by source,
-    C exchanged under the adaptive rule (c0 1024).  Each rank sees the other's
+    C exchanged under the adaptive rule (c0 2048).  Each rank sees the other's
     C updates one exchange late, so the 2-rank loss trails the 1-rank loss
     slightly: measured 0.3 % on this graph at 12k samples per exchange
     (replicated W with the sum rule 1.8 %, the mean 5.8 %); the bound is 2 %."""
@@ -172,11 +172,11 @@ def test_n_ranks_replicas_agree_and_train_like_one(tmp_path, world):
     around an all-reduce), with bench.py's N > 1 default: W rows partitioned by
     source (each rank draws its sources from its own part, smore_set_source_partition;
     W gathered from the owners at the end), C exchanged once per step under the
-    adaptive rule (c0 1024).  Each rank runs 12k samples between exchanges, ~13
+    adaptive rule (c0 2048).  Each rank runs 12k samples between exchanges, ~13
     samples per row of the 920-row tables -- the C4 bench's 2^27 samples per
     rank per step over 10M rows.  Replicas agree, and against one rank that ran
     all `total` samples the held-out loss is within 3 % at 4 ranks and 8 % at 8
-    (measured 0.6 % and 4.2 %, tools/replica_quality.py); it beats full
+    (measured 0.9 % and 3.2 %, tools/replica_quality.py); it beats full
     replication under the averaging rule (measured 1.39x / 3.3x of one rank)
     and one rank that ran only its own share."""
     per = 12_000

@@ -101,9 +101,15 @@ def main():
     for n, sub, hot in itertools.product(args.ranks, args.sub, args.hot):
         if n == 1 and (sub != args.sub[0] or hot != args.hot[0]):
             continue
-        for sync in (syncs if n > 1 else ["none"]):
+        for sync_spec in (syncs if n > 1 else ["none"]):
+            # "<rule>+part": W partitioned by source (each replica draws its
+            # sources from its part, smore_set_source_partition; only C exchanged)
+            part = sync_spec.endswith("+part") and n > 1
+            sync = sync_spec[:-5] if sync_spec.endswith("+part") else sync_spec
+            tabs = [1] if part else [0, 1]
             reps = [ctx(i) for i in range(n)]
-            for pn in reps:
+            for r, pn in enumerate(reps):
+                pn.set_source_partition(n if part else 1, r if part else 0)
                 pn.init_table_uniform(0, 5)
                 pn.zero_table(1)
             T = [[table_tensor(pn, t) for t in (0, 1)] for pn in reps]
@@ -125,7 +131,7 @@ def main():
             t0 = time.perf_counter()
 
             def reduce_all():
-                for t in range(2):
+                for t in tabs:
                     tot = sum(Rs[r][t] for r in range(n))
                     for r in range(n):
                         Rs[r][t].copy_(tot)
@@ -151,7 +157,7 @@ def main():
                         hot_sync()
                 if n > 1:
                     for r in range(n):
-                        for t in range(2):
+                        for t in tabs:
                             sc = scale[t] if isinstance(scale, list) else scale
                             if pending:
                                 TorchPasses.cycle(T[r][t], Ss[r][t], Ds[r][t], Rs[r][t], sc)
@@ -161,16 +167,24 @@ def main():
                     pending = True
             if pending:
                 for r in range(n):
-                    for t in range(2):
+                    for t in tabs:
                         TorchPasses.end(T[r][t], Ss[r][t], Ds[r][t], Rs[r][t],
                                         scale[t] if isinstance(scale, list) else scale)
             torch.cuda.synchronize()
             W0, C0 = reps[0].get_table(0), reps[0].get_table(1)
             spread = 0.0
-            if n > 1:
+            if part:
+                # each W row from its owner
+                b = reps[0].source_parts(n)
+                for r in range(1, n):
+                    W0[b[r]:b[r + 1]] = reps[r].get_table(0)[b[r]:b[r + 1]]
+                spread = float(np.abs(reps[n - 1].get_table(1) - C0).max() / max(1e-30, np.abs(C0).max()))
+                for pn in reps:
+                    pn.set_source_partition(1, 0)
+            elif n > 1:
                 W1 = reps[n - 1].get_table(0)
                 spread = float(np.abs(W1 - W0).max() / max(1e-30, np.abs(W0).max()))
-            row = {"config": args.config, "ranks": n, "sync": sync, "sub": sub, "hot_rows": hot, "steps": steps,
+            row = {"config": args.config, "ranks": n, "sync": sync_spec, "sub": sub, "hot_rows": hot, "steps": steps,
                    "samples_per_step": S,
                    "total": steps * n * S, "mode": args.mode, "finite": bool(np.isfinite(W0).all()),
                    "loss": round(heldout_loss(W0, C0, heldout, dim), 5), "replica_spread_rel": spread,
