@@ -18,9 +18,13 @@ all-reduced over RCCL every `--sync-every` steps, overlapping the next step
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
+import csv
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -80,7 +84,61 @@ def parse():
     ap.add_argument("--seed", type=int, default=20251015)
     ap.add_argument("--semantics", default="cpp", choices=["cpp", "go"],
                     help="update rule: the C++ reference's (default) or the Go tree's (pkg/pronet)")
+    ap.add_argument("--pmc", default="auto", choices=["auto", "off"],
+                    help="N=1: measure roofline.traffic with rocprofv3 --pmc in child runs of this config "
+                         "before the timed run (off: the committed profiles/pmc_traffic.json)")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
+
+
+# gfx950: FETCH_SIZE counts half the bytes of these kernels' reads (calibrated on
+# their own access shapes, profiles/pmc_calibration.json); WRITE_SIZE the bytes
+FETCH_CORRECTION = 2.0
+PMC_KERNELS = ("draw_kernel", "edge_train_kernel")
+
+
+def pmc_traffic_live(args):
+    """HBM traffic per step of this config, measured now: this script re-run for
+    2 steps under `rocprofv3 --pmc FETCH_SIZE` and, separately, `--pmc
+    WRITE_SIZE` (MI355X_MICROARCH.md: one counter group per pass), as child
+    processes started before this process touches the GPU.  Returns
+    ({kernel: bytes per launch}, note) or (None, reason)."""
+    rocprof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(rocprof):
+        return None, "rocprofv3 not found"
+    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "2", "--warmup", "0",
+             "--config", args.config, "--dim", str(args.dim), "--negative", str(args.negative),
+             "--samples", str(args.samples), "--mode", args.mode, "--hot-tau", str(args.hot_tau),
+             "--combine-rows", str(args.combine_rows), "--combine-flush", str(args.combine_flush),
+             "--semantics", args.semantics, "--seed", str(args.seed)]
+    vals = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="smore_pmc_")
+        try:
+            r = subprocess.run([rocprof, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--"]
+                               + child, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=180)
+            path = os.path.join(d, "run_counter_collection.csv")
+            if r.returncode != 0 or not os.path.exists(path):
+                return None, "rocprofv3 --pmc %s exited %d: %s" % (counter, r.returncode,
+                                                                    r.stderr.decode(errors="replace")[-300:])
+            per = {}
+            for row in csv.DictReader(open(path)):
+                for k in PMC_KERNELS:
+                    if k in row["Kernel_Name"] and row["Counter_Name"] == counter:
+                        per.setdefault(k, {}).setdefault(row["Dispatch_Id"], 0.0)
+                        per[k][row["Dispatch_Id"]] += float(row["Counter_Value"])
+            for k in PMC_KERNELS:
+                if not per.get(k):
+                    return None, "no %s dispatches under --pmc %s" % (k, counter)
+                kb = sum(per[k].values()) / len(per[k])
+                vals.setdefault(k, 0.0)
+                vals[k] += kb * 1024.0 * (FETCH_CORRECTION if counter == "FETCH_SIZE" else 1.0)
+        except (OSError, subprocess.SubprocessError, KeyError, ValueError) as e:
+            return None, "rocprofv3 --pmc %s failed: %s" % (counter, e)
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+    return vals, ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) of this config, run by "
+                  "bench.py in 2-step child runs before the timed run; FETCH_SIZE x 2 (gfx950 calibration), KB x 1024")
 
 
 def cgroup_cpu_quota():
@@ -153,6 +211,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # live PMC traffic (N=1): child runs under rocprofv3, before this process
+    # initialises the GPU
+    pmc_live, pmc_note = None, "off"
+    if world == 1 and not args.pmc_child and args.pmc == "auto":
+        pmc_live, pmc_note = pmc_traffic_live(args)
+        print("[bench] pmc: %s" % (pmc_note if pmc_live is None else
+                                   {k: round(v / args.samples, 1) for k, v in pmc_live.items()}),
+              file=sys.stderr, flush=True)
     import torch
     dist = None
     local = local % max(1, torch.cuda.device_count())
@@ -219,6 +285,11 @@ def main():
         if sync is not None and (k + 1) % args.sync_every == 0:
             sync.begin()      # folds the previous exchange in; this one overlaps the next step
 
+    if args.pmc_child:      # the profiled child of pmc_traffic_live: the steps only
+        for k in range(args.steps):
+            step(k)
+        torch.cuda.synchronize()
+        return
     for k in range(args.warmup):
         step(k)
     if sync is not None:
@@ -263,12 +334,17 @@ def main():
     # kernel, one launch each) and per update launch
     traffic = traffic_upd = traffic_src = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
+    if pmc_live is not None and n_launch == 1:
+        traffic = sum(pmc_live.values())
+        traffic_upd = pmc_live["edge_train_kernel"]
+        traffic_src = pmc_note
+    elif os.path.exists(pmc):
         p = json.load(open(pmc))
         if p.get("config") == args.config and p.get("samples") == S and p.get("mode") == args.mode:
             traffic = p.get("hbm_bytes_per_step", p.get("hbm_bytes_per_launch"))
             traffic_upd = p.get("hbm_bytes_per_launch")
-            traffic_src = "profiles/pmc_traffic.json: rocprofv3 --pmc of this config (%s)" % p.get("round", "")
+            traffic_src = ("profiles/pmc_traffic.json: rocprofv3 --pmc of this config (%s)%s"
+                           % (p.get("round", ""), "" if pmc_note == "off" else "; live measurement: " + pmc_note))
     copy_peak = pn.copy_bandwidth(4 << 30, 5) if rank == 0 else 0.0   # membw.hip float4 copy
     Wt = pn.get_table(0)
     assert np.isfinite(Wt).all(), "non-finite embeddings"
