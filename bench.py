@@ -97,6 +97,22 @@ FETCH_CORRECTION = 2.0
 PMC_KERNELS = ("draw_kernel", "edge_train_kernel")
 
 
+def pmc_per_launch(path, counter):
+    """{kernel: bytes per dispatch} of PMC_KERNELS from a rocprofv3 --pmc
+    counter_collection CSV (Counter_Value in KB, summed per dispatch, averaged
+    over dispatches; FETCH_SIZE x FETCH_CORRECTION)."""
+    per = {}
+    for row in csv.DictReader(open(path)):
+        if row["Counter_Name"] != counter:
+            continue
+        for k in PMC_KERNELS:
+            if k in row["Kernel_Name"]:
+                d = per.setdefault(k, {})
+                d[row["Dispatch_Id"]] = d.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
+    scale = 1024.0 * (FETCH_CORRECTION if counter == "FETCH_SIZE" else 1.0)
+    return {k: sum(d.values()) / len(d) * scale for k, d in per.items() if d}
+
+
 def pmc_traffic_live(args):
     """HBM traffic per step of this config, measured now: this script re-run for
     2 steps under `rocprofv3 --pmc FETCH_SIZE` and, separately, `--pmc
@@ -121,18 +137,11 @@ def pmc_traffic_live(args):
             if r.returncode != 0 or not os.path.exists(path):
                 return None, "rocprofv3 --pmc %s exited %d: %s" % (counter, r.returncode,
                                                                     r.stderr.decode(errors="replace")[-300:])
-            per = {}
-            for row in csv.DictReader(open(path)):
-                for k in PMC_KERNELS:
-                    if k in row["Kernel_Name"] and row["Counter_Name"] == counter:
-                        per.setdefault(k, {}).setdefault(row["Dispatch_Id"], 0.0)
-                        per[k][row["Dispatch_Id"]] += float(row["Counter_Value"])
+            per = pmc_per_launch(path, counter)
             for k in PMC_KERNELS:
-                if not per.get(k):
+                if k not in per:
                     return None, "no %s dispatches under --pmc %s" % (k, counter)
-                kb = sum(per[k].values()) / len(per[k])
-                vals.setdefault(k, 0.0)
-                vals[k] += kb * 1024.0 * (FETCH_CORRECTION if counter == "FETCH_SIZE" else 1.0)
+                vals[k] = vals.get(k, 0.0) + per[k]
         except (OSError, subprocess.SubprocessError, KeyError, ValueError) as e:
             return None, "rocprofv3 --pmc %s failed: %s" % (counter, e)
         finally:
