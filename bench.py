@@ -62,7 +62,7 @@ def parse():
     ap.add_argument("--samples", type=int, default=1 << 27, help="edge samples per step per GPU")
     ap.add_argument("--mode", default="hybrid", choices=["hogwild", "atomic", "hybrid"],
                     help="scatter: hybrid (default), atomic (every row), hogwild (plain stores, loses updates)")
-    ap.add_argument("--hot-tau", type=float, default=0.3, help="hybrid: hot-row threshold")
+    ap.add_argument("--hot-tau", type=float, default=None, help="hybrid: hot-row threshold (default: the library's, 1.0)")
     ap.add_argument("--combine-rows", type=int, default=128, help="hybrid: LDS write-combined hottest rows")
     ap.add_argument("--combine-flush", type=int, default=0, help="hybrid: rounds between LDS drains (0: automatic)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
@@ -124,9 +124,11 @@ def pmc_traffic_live(args):
         return None, "rocprofv3 not found"
     child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "2", "--warmup", "0",
              "--config", args.config, "--dim", str(args.dim), "--negative", str(args.negative),
-             "--samples", str(args.samples), "--mode", args.mode, "--hot-tau", str(args.hot_tau),
+             "--samples", str(args.samples), "--mode", args.mode,
              "--combine-rows", str(args.combine_rows), "--combine-flush", str(args.combine_flush),
              "--semantics", args.semantics, "--seed", str(args.seed)]
+    if args.hot_tau is not None:
+        child += ["--hot-tau", str(args.hot_tau)]
     vals = {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="smore_pmc_")
@@ -255,7 +257,8 @@ def main():
     E = pn.MAX_line
     if args.semantics == "go":
         pn.set_semantics("go")
-    pn.set_hot_threshold(args.hot_tau)
+    if args.hot_tau is not None:
+        pn.set_hot_threshold(args.hot_tau)
     pn.set_write_combine(args.combine_rows, args.combine_flush)
     pn.alloc_tables(args.dim, 2)
     pn.init_table_uniform(0, args.seed)     # W ~ (u-0.5)/d, as the reference Init law

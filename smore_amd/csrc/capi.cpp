@@ -432,7 +432,16 @@ constexpr double SH_STALE_MAX = 65536.0;
 // [8, 32] rounds keeps that at the config-4 level (flush 32) on hotter graphs
 constexpr double SH_AUTO_BUDGET = 6144.0;
 
-static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
+// hot-row threshold defaults (smore_set_hot_threshold(ctx, -1)): the edge
+// models' record kernels take 1.0 (C4 / C2 update 4 % / 12 % faster than at
+// 0.3, held-out loss +0.1 / +0.2 % of the atomic scatter's), the walk models'
+// pair kernels 0.3 (on small graphs their runs of W_v updates need the
+// context rows' atomics: Go DeepWalk AUC on the 920-vertex graph 0.881 at 1.0
+// vs 0.900 at 0.3, serial 0.906); DESIGN.md 8, profiles/r03/tau
+constexpr double HOT_TAU_EDGE = 1.0, HOT_TAU_WALK = 0.3;
+
+static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_default) {
+    const double tau = c->hot_tau >= 0 ? c->hot_tau : tau_default;
     char key[128];
     const char* stale_env = getenv("SMORE_SH_STALE");
     // W rows of two-table models stay out of the write-combined set unless
@@ -443,7 +452,7 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
     // it (1338 vs 1342 M/s), DESIGN.md 8
     const char* wrows_env = getenv("SMORE_SH_WROWS");
     const bool wrows = wrows_env && atoi(wrows_env) != 0;
-    snprintf(key, sizeof key, "%d/%d/%lld/%.9g/%d/%d/%s/%d/%d/%d", model, K, (long long)M, c->hot_tau, c->sh_max,
+    snprintf(key, sizeof key, "%d/%d/%lld/%.9g/%d/%d/%s/%d/%d/%d", model, K, (long long)M, tau, c->sh_max,
              c->sh_flush, stale_env ? stale_env : "", (int)wrows, c->part_n, c->part_i);
     if (c->hot_key == key) return SMORE_OK;
     if (c->g->V >= ((int64_t)1 << 30)) return fail(c, SMORE_EINVAL, "hybrid scatter needs V < 2^30");
@@ -464,8 +473,8 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M) {
         double pw, pcx;
         if (model == SMORE_LINE2) { pw = ps[v]; pcx = pc[v] + negs * pn[v]; }
         else { pw = pcx = ps[v] + pc[v] + negs * pn[v]; }
-        if ((double)M * pw > c->hot_tau) { hw[v] = 1; c->hot_rows[0]++; }
-        if ((double)M * pcx > c->hot_tau) { hc[v] = 1; c->hot_rows[1]++; }
+        if ((double)M * pw > tau) { hw[v] = 1; c->hot_rows[0]++; }
+        if ((double)M * pcx > tau) { hc[v] = 1; c->hot_rows[1]++; }
     }
     // super-hot rows: the hottest hot context rows, write-combined per block
     {
@@ -667,7 +676,7 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
         const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
         // Go BPR has two tables (users W, items C): the LINE-2 row roles
         const int hot_model = go && model == SMORE_BPR ? SMORE_LINE2 : model;
-        if ((rc = build_hot_maps(c, hot_model, a.K, M))) return rc;
+        if ((rc = build_hot_maps(c, hot_model, a.K, M, HOT_TAU_EDGE))) return rc;
     }
     a.sh_rows = combine ? c->sh_rows : 0;
     a.sh_hash = c->d_sh_hash;
@@ -798,7 +807,8 @@ int smore_set_semantics(smore_ctx* c, int semantics) {
 }
 
 int smore_set_hot_threshold(smore_ctx* c, double tau) {
-    if (!c || !(tau >= 0)) return SMORE_EINVAL;
+    if (!c || tau != tau) return SMORE_EINVAL;
+    if (tau < 0) tau = -1.0;   // the per-path defaults
     c->hot_tau = tau;
     return SMORE_OK;
 }
@@ -1192,7 +1202,7 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
     const int ugrid = edge_grid(c, ar, false, go ? 2 : 0);
     if (mode == SMORE_HYBRID) {
         const int64_t M = (int64_t)ugrid * (256 / lanes_of(c->dpad));
-        if ((rc = build_hot_maps(c, SMORE_LINE2, K, M))) return rc;
+        if ((rc = build_hot_maps(c, SMORE_LINE2, K, M, HOT_TAU_WALK))) return rc;
     }
     ar.g = dev_graph(c);
     ar.sh_rows = combine ? c->sh_rows : 0;
@@ -1412,7 +1422,7 @@ int smore_train_app_async(smore_ctx* c, uint64_t unit_begin, uint64_t unit_end, 
     const int grid = edge_grid(c, a);
     if (mode == SMORE_HYBRID) {
         const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
-        if ((rc = build_hot_maps(c, SMORE_LINE2, K, M))) return rc;
+        if ((rc = build_hot_maps(c, SMORE_LINE2, K, M, HOT_TAU_WALK))) return rc;
     }
     a.g = dev_graph(c);
     a.sh_rows = combine ? c->sh_rows : 0;
@@ -1488,7 +1498,7 @@ int smore_train_hpe_async(smore_ctx* c, uint64_t begin, uint64_t count, uint64_t
     const int grid = edge_grid(c, a);
     if (mode == SMORE_HYBRID) {
         const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
-        if ((rc = build_hot_maps(c, SMORE_LINE2, K, M))) return rc;
+        if ((rc = build_hot_maps(c, SMORE_LINE2, K, M, HOT_TAU_WALK))) return rc;
     }
     a.g = dev_graph(c);
     a.sh_rows = combine ? c->sh_rows : 0;

@@ -39,7 +39,7 @@ struct smore_ctx {
     float* d_table[2] = {nullptr, nullptr};
     int dim = 0, dpad = 0, ntables = 0;
     // hybrid scatter: hot-row bitmaps (1 bit per row), keyed by what built them
-    double hot_tau = 0.3;
+    double hot_tau = -1.0;               // < 0: the per-path default (HOT_TAU_EDGE / HOT_TAU_WALK)
     std::string hot_key;
     int64_t hot_rows[2] = {0, 0};
     // DeepWalk buffers

@@ -118,8 +118,9 @@ def test_c2_walklets_app_hpe_serial_bit_exact(c2):
 
 def test_c2_full_grid_hybrid_matches_atomic(c2):
     """The bench's default scatter on a full grid (no V/16 cap at V=1M): 2^28
-    samples, hybrid (tau 0.3, 128 LDS write-combined rows, 32-round drain) vs
-    the lossless atomic scatter, held-out LINE-2 loss within 1 %."""
+    samples, hybrid (the defaults: tau 1.0, 128 LDS write-combined rows,
+    automatic drain) vs the lossless atomic scatter, held-out LINE-2 loss
+    within 1.5 % (measured 0.9 %; tau 0.3: 0.7 %, profiles/r03/tau)."""
     g, pn = c2
     dim, K, total = 64, 5, 1 << 28
     heldout = orc.sample_line(g, SEED + 1, 0, 100_000, K)
@@ -128,7 +129,7 @@ def test_c2_full_grid_hybrid_matches_atomic(c2):
         pn.alloc_tables(dim, 2)
         pn.init_table_uniform(0, 5)
         pn.zero_table(1)
-        pn.set_hot_threshold(0.3)
+        pn.set_hot_threshold(1.0)
         pn.set_write_combine(128, 0)     # the defaults: 128 rows, automatic drain interval
         pn.train_edges("line2", 0, total, total, K, 0.025, 0.0, SEED, mode)
         W, C = pn.get_table(0), pn.get_table(1)
@@ -139,7 +140,7 @@ def test_c2_full_grid_hybrid_matches_atomic(c2):
             assert hw > 0 and hc > 0, (hw, hc)
     init = np.log(2.0) * (1 + K)          # C = 0: every logit is 0
     assert res["atomic"] < 0.9 * init, res
-    assert abs(res["hybrid"] - res["atomic"]) <= 0.01 * res["atomic"], res
+    assert abs(res["hybrid"] - res["atomic"]) <= 0.015 * res["atomic"], res
 
 
 # ---------------------------------------------------------------- C4: the north-star graph
@@ -182,8 +183,8 @@ def test_c4_full_grid_hybrid_matches_atomic(c4):
     """The bench's workload and default scatter: full-grid hybrid launches of
     2^27 samples are finite and tag hot rows at V = 10M; after 2^31 samples
     (~215 per vertex) the held-out LINE-2 loss of the hybrid scatter is within
-    1 % of the lossless atomic scatter's (measured at 2e9 samples: 2.593 vs
-    2.587; at 2^30 the gap is still 1.1 %, profiles/quality)."""
+    1 % of the lossless atomic scatter's (measured with the default tau 1.0:
+    2.5585 vs 2.5509, 0.3 %; tau 0.3: 0.2 %, profiles/r03/tau)."""
     g, pn = c4
     dim, K, launch, total = 64, 5, 1 << 27, 1 << 31
     heldout = orc.sample_line(g, SEED + 1, 0, 100_000, K)
@@ -192,7 +193,7 @@ def test_c4_full_grid_hybrid_matches_atomic(c4):
         pn.alloc_tables(dim, 2)
         pn.init_table_uniform(0, 5)
         pn.zero_table(1)
-        pn.set_hot_threshold(0.3)
+        pn.set_hot_threshold(1.0)
         pn.set_write_combine(128, 0)
         for b in range(0, total, launch):
             pn.train_edges("line2", b, launch, total, K, 0.025, 0.0, SEED, mode)
