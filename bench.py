@@ -225,7 +225,9 @@ def main():
     # live PMC traffic (N=1): child runs under rocprofv3, before this process
     # initialises the GPU
     pmc_live, pmc_note = None, "off"
-    if world == 1 and not args.pmc_child and args.pmc == "auto":
+    # (not when this run is itself under a profiler: no nested rocprofv3)
+    profiled = any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ)
+    if world == 1 and not args.pmc_child and args.pmc == "auto" and not profiled:
         pmc_live, pmc_note = pmc_traffic_live(args)
         print("[bench] pmc: %s" % (pmc_note if pmc_live is None else
                                    {k: round(v / args.samples, 1) for k, v in pmc_live.items()}),
