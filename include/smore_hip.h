@@ -174,8 +174,8 @@ int smore_train_edges(smore_ctx* ctx, int model, uint64_t begin, uint64_t count,
                       int mode);
 /* SMORE_HYBRID: a row takes float atomics when (resident sample groups) x
  * (its per-sample touch probability) > tau; tau < 0 (the default) = 1.0 for the
- * edge-record models (LINE, MF, BPR, C++ and Go rules), 0.3 for the pair-record
- * models (DeepWalk, Walklets, APP, HPE, the Go walk models); see DESIGN.md 8 */
+ * C++ rules' edge-record models (LINE, MF, BPR), 0.3 for the Go rules and the
+ * pair-record models (DeepWalk, Walklets, APP, HPE, the Go walks); DESIGN.md 8 */
 int smore_set_hot_threshold(smore_ctx* ctx, double tau);
 /* rows marked hot in W and C by the last hybrid launch */
 /* hybrid scatter: the `rows` hottest hot context rows (default 128; 0 = off; at

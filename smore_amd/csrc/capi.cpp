@@ -432,12 +432,13 @@ constexpr double SH_STALE_MAX = 65536.0;
 // [8, 32] rounds keeps that at the config-4 level (flush 32) on hotter graphs
 constexpr double SH_AUTO_BUDGET = 6144.0;
 
-// hot-row threshold defaults (smore_set_hot_threshold(ctx, -1)): the edge
-// models' record kernels take 1.0 (C4 / C2 update 4 % / 12 % faster than at
-// 0.3, held-out loss +0.1 / +0.2 % of the atomic scatter's), the walk models'
-// pair kernels 0.3 (on small graphs their runs of W_v updates need the
-// context rows' atomics: Go DeepWalk AUC on the 920-vertex graph 0.881 at 1.0
-// vs 0.900 at 0.3, serial 0.906); DESIGN.md 8, profiles/r03/tau
+// hot-row threshold defaults (smore_set_hot_threshold(ctx, -1)): the C++
+// rules' edge-record kernel takes 1.0 (C4 / C2 update 4 % / 12 % faster than
+// at 0.3, held-out loss +0.1 / +0.2 % of the atomic scatter's); the Go edge
+// rules (no faster at 1.0: C4 Go LINE-2 1140 vs 1133 M/s) and the pair-record
+// kernels keep 0.3 (on small graphs the walk models' runs of W_v updates need
+// the context rows' atomics: Go DeepWalk AUC on the 920-vertex graph 0.881 at
+// 1.0 vs 0.900 at 0.3, serial 0.906); DESIGN.md 8, profiles/r03/tau
 constexpr double HOT_TAU_EDGE = 1.0, HOT_TAU_WALK = 0.3;
 
 static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_default) {
@@ -676,7 +677,7 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
         const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
         // Go BPR has two tables (users W, items C): the LINE-2 row roles
         const int hot_model = go && model == SMORE_BPR ? SMORE_LINE2 : model;
-        if ((rc = build_hot_maps(c, hot_model, a.K, M, HOT_TAU_EDGE))) return rc;
+        if ((rc = build_hot_maps(c, hot_model, a.K, M, go ? HOT_TAU_WALK : HOT_TAU_EDGE))) return rc;
     }
     a.sh_rows = combine ? c->sh_rows : 0;
     a.sh_hash = c->d_sh_hash;
