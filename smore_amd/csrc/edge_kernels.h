@@ -662,8 +662,10 @@ edge_train_kernel(EdgeArgs a) {
         for (uint64_t c0 = grab(); c0 < count; c0 = grab()) {
             const uint64_t lim = c0 + span < count ? c0 + span : count;
             if constexpr (SHARED == 2) {
-                // BPR: no row prefetch (a second set of 7 rows would halve the
-                // resident waves); the next record is still loaded one round ahead
+                // BPR: no row prefetch -- gathering the next sample's 7 rows
+                // before this sample's scatter was measured no faster at C3
+                // (639 vs 637 M samples/s, 2 waves/SIMD either way, 221 vs 184
+                // VGPRs); the next record is still loaded one round ahead
                 uint64_t t = c0 + gib;
                 load_rec(t, lim, rr);
                 for (uint64_t r = c0; r < lim; r += gpb) {
