@@ -3,4 +3,4 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 bash tools/gpu_session.sh \
-  "dw_c5_tau 600 python -u tools/dw_quality.py --config c5 --dim 128 --walk-times 1 --walk-steps 40 --window 5 --settings atomic hybrid:0.3:128:0 hybrid:1.0:128:0 hybrid:3.0:128:0"
+  "dw_c5_tau10 900 python -u tools/dw_quality.py --config c5 --dim 128 --walk-times 10 --walk-steps 40 --window 5 --settings atomic hybrid:0.3:128:0 hybrid:1.0:128:0"
