@@ -16,6 +16,8 @@
 // keeps thousands of chains in flight per CU (few registers), and the update
 // kernel sees one streaming 32-B read per sample.  Draws are identical to the
 // fused form (same Philox slots, same compares), so results are unchanged.
+#include <cstdlib>
+
 #include "train_kernels.h"
 
 namespace smore {
@@ -146,7 +148,11 @@ hipError_t launch_pack(const DevGraph& g, uint64_t E, uint4* vt32, uint4* ct16, 
 
 hipError_t launch_draw(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K, int32_t* rec,
                        unsigned long long* skipped, hipStream_t st) {
-    const int block = 256;
+    static const int block = [] {   // tuning knob: SMORE_DRAW_BLOCK (64..256 threads)
+        const char* e = getenv("SMORE_DRAW_BLOCK");
+        const int b = e ? atoi(e) : 256;
+        return (b == 64 || b == 128 || b == 256) ? b : 256;
+    }();
     const dim3 grid((unsigned)((count + block - 1) / block));
 #if SMORE_DRAW_SPLIT
     // negatives first, then source/target (unused record words stay as written by
