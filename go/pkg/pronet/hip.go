@@ -10,7 +10,9 @@
 //	go build -tags smore_hip ./cmd/line ./cmd/bpr ./cmd/deepwalk
 //
 // What stays Go: NewProNet, LoadEdgeList (pkg/pronet/pronet.go:77,112), the
-// models' Init and SaveWeights.  What moves to the GPU: the per-sample loops of
+// models' Init and SaveWeights.  (*ProNet).UpdatePairs (optimizer.go:8-18) also
+// runs on the GPU under this tag (pairs_hook.go + the patch): a caller that
+// builds its own pairs gets one library call per batch.  What moves to the GPU: the per-sample loops of
 // (*LINE).Train (internal/models/line/line.go:73-150), (*BPR).Train
 // (internal/models/bpr/bpr.go:61-135) and (*DeepWalk).Train
 // (internal/models/deepwalk/deepwalk.go:61-141), i.e. SourceSample /
@@ -37,8 +39,10 @@ import "C"
 
 import (
 	"fmt"
+	"math/rand"
 	"os"
 	"strconv"
+	"sync"
 	"unsafe"
 )
 
@@ -454,4 +458,100 @@ func (h *HIP) TrainCTDNE(w, c [][]float64, dim int, order []int64, walkTimes, wa
 			C.int(walkSteps), C.int(window), C.int(K), C.double(alpha), C.double(timeWindow),
 			C.uint64_t(h.cfg.Seed), ord, C.int(h.cfg.Mode), 0, h.mean())
 	}, progress)
+}
+
+// ---- UpdatePairs on the GPU (optimizer.go:8-18; smore_train_pairs) -----------
+
+func init() { hipUpdatePairs = updatePairsHIP }
+
+// one single-GPU context per *ProNet, made on the first UpdatePairs; the
+// library context is not thread-safe, so batches from concurrent goroutines
+// run one after another (each sees the tables the previous one wrote back)
+type pairSession struct {
+	mu  sync.Mutex
+	h   *HIP
+	err error
+}
+
+var pairSessions sync.Map // *ProNet -> *pairSession
+
+func (pn *ProNet) pairSession() *pairSession {
+	v, loaded := pairSessions.LoadOrStore(pn, &pairSession{})
+	s := v.(*pairSession)
+	if !loaded {
+		s.mu.Lock()
+		cfg := HIPConfigFromEnv(1)
+		cfg.GPUs = 1
+		s.h, s.err = pn.NewHIP(cfg)
+		s.mu.Unlock()
+	}
+	return s
+}
+
+// updatePairsHIP is (*ProNet).UpdatePairs under -tags smore_hip: the tables go
+// up (fp64 -> fp32), the library runs Go UpdatePair for each pair in order
+// (negatives drawn on the device from the rng's next word as the Philox unit,
+// duplicates of the context skipped, the context's gradient deferred), and
+// the tables come back.  The copies cost O(MaxVid x dim) per call, so batch the
+// pairs (a chunk of walks per call), or keep the tables on the GPU across
+// batches with (*HIP).BeginPairs / Pairs / EndPairs.  UpdatePairs has no error
+// path (the reference panics on a bad index): failures panic.
+func updatePairsHIP(pn *ProNet, wVertex, wContext [][]float64, vertices, contexts []int64, dim,
+	negativeSamples int, alpha float64, rng *rand.Rand) {
+	if len(vertices) == 0 {
+		return
+	}
+	s := pn.pairSession()
+	s.mu.Lock()
+	defer s.mu.Unlock()
+	if s.err != nil {
+		panic(s.err)
+	}
+	if err := s.h.BeginPairs(wVertex, wContext, dim); err != nil {
+		panic(err)
+	}
+	if err := s.h.Pairs(vertices, contexts, negativeSamples, alpha, rng.Uint64()); err != nil {
+		panic(err)
+	}
+	if err := s.h.EndPairs(wVertex, wContext); err != nil {
+		panic(err)
+	}
+}
+
+// BeginPairs puts w (vertex) and c (context) on the GPU for Pairs calls.
+func (h *HIP) BeginPairs(w, c [][]float64, dim int) error {
+	if err := h.alloc(dim, 2); err != nil {
+		return err
+	}
+	return h.transfer([][][]float64{w, c}, true)
+}
+
+// Pairs runs UpdatePair over (vertices[i], contexts[i]) in order on the
+// resident tables with negativeSamples <= 10 negatives per pair from Philox
+// unit `unit` (smore_train_pairs; pair i uses unit + i/2^20).
+func (h *HIP) Pairs(vertices, contexts []int64, negativeSamples int, alpha float64, unit uint64) error {
+	n := len(vertices)
+	if n != len(contexts) {
+		return fmt.Errorf("Pairs: %d vertices, %d contexts", n, len(contexts))
+	}
+	if n == 0 {
+		return nil
+	}
+	v := (*[1 << 40]C.int32_t)(C.malloc(C.size_t(4 * n)))[:n:n]
+	c := (*[1 << 40]C.int32_t)(C.malloc(C.size_t(4 * n)))[:n:n]
+	defer C.free(unsafe.Pointer(&v[0]))
+	defer C.free(unsafe.Pointer(&c[0]))
+	for i := 0; i < n; i++ {
+		v[i], c[i] = C.int32_t(vertices[i]), C.int32_t(contexts[i])
+	}
+	if rc := C.smore_train_pairs(h.ctx, &v[0], &c[0], C.int64_t(n), C.int(negativeSamples), C.double(alpha),
+		C.uint64_t(h.cfg.Seed), C.uint64_t(unit), C.int(h.cfg.Mode)); rc != C.SMORE_OK {
+		return h.err("smore_train_pairs")
+	}
+	return nil
+}
+
+// EndPairs copies the trained tables back into w and c.
+func (h *HIP) EndPairs(w, c [][]float64) error {
+	return h.transfer([][][]float64{w, c}, false)
 }

@@ -245,6 +245,7 @@ int smore_set_source_partition(smore_ctx* ctx, int nparts, int part);
  * under `model` with K negatives (the sampler marginals of the context's graph;
  * the ranking smore_hot_row_ids sorts by); rate[V] */
 int smore_row_rates(smore_ctx* ctx, int model, int K, int which, int64_t n, double* rate);
+/* (model SMORE_CENSUS: the last census's touches per unit, see smore_census_begin) */
 /* Exchange rules (the `mean` argument of smore_exchange_begin and the group
  * training calls):
  *   SMORE_SYNC_SUM       scale 1: every rank's update lands once on every replica
@@ -260,7 +261,9 @@ int smore_row_rates(smore_ctx* ctx, int model, int K, int which, int64_t n, doub
 #define SMORE_SYNC_ADAPTIVE 2
 /* the row scales of the adaptive rule for `updates` samples of `model` per rank
  * per exchange (smore_exchange_begin with SMORE_SYNC_ADAPTIVE needs them); after
- * smore_comm_init (they depend on the world size) and smore_alloc_tables */
+ * smore_comm_init (they depend on the world size) and smore_alloc_tables;
+ * model SMORE_CENSUS: the census rates, `updates` = units per rank per exchange.
+ * SMORE_ESTATE while an exchange is in flight (call smore_exchange_end first). */
 int smore_exchange_set_adaptive(smore_ctx* ctx, int model, int K, double updates, double c0);
 
 /* ---- multi-GPU replicas over RCCL, in the library (smore_amd/csrc/exchange.cpp) ------
@@ -462,6 +465,35 @@ int smore_train_app_async(smore_ctx* ctx, uint64_t unit_begin, uint64_t unit_end
                           const int64_t* order, int mode);
 int smore_train_hpe_async(smore_ctx* ctx, uint64_t begin, uint64_t count, uint64_t total, int walk_steps,
                           int K, double reg, double alpha0, uint64_t seed, int mode);
+
+/* replaces: proNet::UpdatePairs (src/proNet.cpp:2741-2753) and Go
+ * (*ProNet).UpdatePairs (pkg/pronet/optimizer.go:8-18): UpdatePair for each
+ * caller-supplied pair (v[i], c[i]), i = 0 .. n-1 in order, with K <= 10
+ * negatives and the fixed learning rate alpha, under the context's semantics
+ * (C++: UpdatePair src/proNet.cpp:1784-1809, the context row updated in place;
+ * Go: optimizer.go:21-58, negatives equal to the context skipped, the
+ * context's gradient deferred).  v, c: host arrays of ids < V (copied in).
+ * Draws: pair i takes its K negatives (index, then p) from stream 3, unit
+ * `unit` + i / 2^20, slots 2K (i mod 2^20) + 2j, +1 -- a serial run equals
+ * the reference's UpdatePairs over blocks of 2^20 pairs with the RNG spec
+ * interposed.  mode as the training calls; synchronous. */
+int smore_train_pairs(smore_ctx* ctx, const int32_t* v, const int32_t* c, int64_t n, int K, double alpha,
+                      uint64_t seed, uint64_t unit, int mode);
+
+/* ---- row census (the walk models' multi-GPU exchange rates) ---------------
+ * Between smore_census_begin and smore_census_end the walk-model calls of this
+ * context (DeepWalk, Walklets, APP, HPE, node2vec, metapath2vec, CTDNE,
+ * smore_train_pairs) generate their walks and records as usual but COUNT the
+ * rows each record would update -- W at its vertex, C at its context and at
+ * each negative -- instead of training (the tables are untouched; edge models
+ * have exact marginals and are rejected).  smore_census_end divides the counts
+ * by `units` (the walks / APP units / HPE samples / pairs the calls covered):
+ * expected row touches per unit, which smore_row_rates(ctx, SMORE_CENSUS, ...)
+ * returns and smore_exchange_set_adaptive(ctx, SMORE_CENSUS, K, units per rank
+ * per exchange, c0) scales by.  A new graph clears the census. */
+#define SMORE_CENSUS 16
+int smore_census_begin(smore_ctx* ctx);
+int smore_census_end(smore_ctx* ctx, double units);
 
 /* ---- samplers (parity tests) -------------------------------------------------------- */
 /* replaces: SourceSample/TargetSample/NegativeSample (src/proNet.cpp:623-683):

@@ -113,6 +113,7 @@ def main():
     only = sys.argv[sys.argv.index("--only") + 1:] if "--only" in sys.argv else None
     if only:
         gen_e2e(graphs, 20251015, only)
+        gen_pairs(graphs, 20251015, only)
         return
 
     # ---- G1: AliasMethod on hand-made distributions (src/proNet.cpp:544-620)
@@ -190,6 +191,7 @@ def main():
         np.savez_compressed(os.path.join(GOLD, name + ".npz"), **rec)
 
     gen_e2e(graphs, seed, None)
+    gen_pairs(graphs, seed, None)
     print("golden fixtures written to", GOLD)
 
 
@@ -217,6 +219,36 @@ def gen_e2e(graphs, seed, only):
         run(*(args + [out]))
         o = read_smrf(out)
         o["meta_args"] = np.frombuffer(" ".join(str(a) for a in args[:1] + args[2:]).encode(), np.uint8)
+        np.savez_compressed(os.path.join(GOLD, name + ".npz"), **o)
+
+
+def gen_pairs(graphs, seed, only):
+    # ---- caller-supplied pairs: proNet::UpdatePairs (src/proNet.cpp:2741-2753)
+    # from fixed starting tables; pairs mix runs of one vertex (the pair kernel
+    # keeps W_v in registers over a run), v == c, and uniform ids
+    cases = [("pairs_pl100w", 16, 5, 0.025, 7, 3000, 31), ("pairs_pl100w_d7", 7, 3, 0.05, 1 << 33, 1500, 32)]
+    for name, dim, K, alpha, unit, n, rs in cases:
+        if only and name not in only:
+            continue
+        rng = np.random.default_rng(rs)
+        with open(graphs["pl100w"]) as f:
+            V = len({x for line in f for x in line.split()[:2]})
+        v = np.empty(n, np.int64)
+        c = rng.integers(0, V, n)
+        i = 0
+        while i < n:
+            run_len = int(rng.integers(1, 12))
+            v[i:i + run_len] = rng.integers(0, V)
+            i += run_len
+        same = rng.random(n) < 0.05
+        c[same] = v[same]
+        fn = os.path.join(TMP, name + ".i64")
+        np.stack([v, c], 1).astype(np.int64).tofile(fn)
+        out = os.path.join(TMP, name + ".bin")
+        run("pairs", graphs["pl100w"], 1, dim, K, alpha, seed, unit, fn, out)
+        o = read_smrf(out)
+        o["meta"] = np.array([dim, K, seed, unit], dtype=np.uint64)
+        o["meta_f"] = np.array([alpha])
         np.savez_compressed(os.path.join(GOLD, name + ".npz"), **o)
 
 

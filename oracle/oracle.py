@@ -92,6 +92,10 @@ def _declare(L):
     L.orc_train_hpe_f32.argtypes = [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, dbl, dbl, u64, u64, u64, u64]
     L.orc_app_pairs.restype = None
     L.orc_app_pairs.argtypes = [P, C.c_int, C.c_int, dbl, u64, P, u64, u64, P]
+    L.orc_update_pairs_f64.restype = C.c_int
+    L.orc_update_pairs_f64.argtypes = [P, P, P, C.c_int, P, P, i64, C.c_int, dbl, u64, u64, C.c_int]
+    L.orc_update_pairs_f32.restype = C.c_int
+    L.orc_update_pairs_f32.argtypes = [P, P, P, C.c_int, C.c_int, P, P, i64, C.c_int, dbl, u64, u64, C.c_int]
 
 
 def ptr(a):
@@ -344,6 +348,25 @@ def app_pairs(g, walk_times, sample_times, jump, seed, order, begin, end):
     out = np.zeros((end - begin, 2), np.int32)
     lib().orc_app_pairs(g.ref, walk_times, sample_times, jump, seed, ptr(order), begin, end, ptr(out))
     return out
+
+
+PAIR_BLOCK = 1 << 20
+
+
+def update_pairs_f64(g, W, C_, v, c, K, alpha, seed, unit, go=False):
+    """UpdatePairs (src/proNet.cpp:2741-2753; Go pkg/pronet/optimizer.go:8-18) over
+    caller pairs, fp64; negatives from stream 3, unit + i // PAIR_BLOCK."""
+    v = np.ascontiguousarray(v, np.int32)
+    c = np.ascontiguousarray(c, np.int32)
+    return lib().orc_update_pairs_f64(g.ref, ptr(W), ptr(C_), W.shape[1], ptr(v), ptr(c), len(v), K, alpha, seed,
+                                      unit, int(go))
+
+
+def update_pairs_f32(g, W, C_, dim, v, c, K, alpha, seed, unit, go=False):
+    v = np.ascontiguousarray(v, np.int32)
+    c = np.ascontiguousarray(c, np.int32)
+    return lib().orc_update_pairs_f32(g.ref, ptr(W), ptr(C_), dim, W.shape[1], ptr(v), ptr(c), len(v), K, alpha,
+                                      seed, unit, int(go))
 
 
 # --------------------------------------------------------------------- Go semantics

@@ -15,6 +15,8 @@
 //                  jumping walk (and its UpdatePair) is one unit
 //   HPE          : proNet::SourceSample is wrapped (HPE mode only): each
 //                  sample is one unit of stream 0, consecutive slots
+//   UpdatePairs  : (caller-supplied pairs) each block of ORC_PAIR_BLOCK pairs
+//                  is one unit of stream 3, consecutive slots
 //   random_gen(0,1)   -> k * 2^-32
 //   random_gen(a,b)   -> a + floor(k * (b-a) / 2^32)
 // Weight init keeps the reference's own glibc rand() calls.
@@ -178,7 +180,8 @@ static void usage() {
             "ref_harness walklets <edges> <undirected> <dim> <walk_times> <walk_steps> <wmin> <wmax> <K> <alpha> <seed> <out>\n"
             "ref_harness app <edges> <undirected> <dim> <walk_times> <sample_times> <jump> <K> <alpha> <seed> <out>\n"
             "ref_harness hpe <edges> <undirected> <dim> <sample_times> <walk_steps> <K> <reg> <alpha> <seed> <out>\n"
-            "ref_harness updates <edges> <undirected> <model:line2|line1|mf|bpr> <dim> <K> <alpha> <reg> <seed> <first> <n> <out>\n");
+            "ref_harness updates <edges> <undirected> <model:line2|line1|mf|bpr> <dim> <K> <alpha> <reg> <seed> <first> <n> <out>\n"
+            "ref_harness pairs <edges> <undirected> <dim> <K> <alpha> <seed> <unit> <pairs.i64> <out>\n");
     exit(1);
 }
 
@@ -365,6 +368,48 @@ int main(int argc, char** argv) {
         o.put("W", 'd', {(uint64_t)n, (uint64_t)V, (uint64_t)dim}, Wout.data(), 8);
         o.put("C", 'd', {(uint64_t)n, (uint64_t)V, (uint64_t)dim}, Cout.data(), 8);
         o.put("trial", 'q', {(uint64_t)n, 3}, ids.data(), 8);
+        dump_graph(o, pn);
+        return 0;
+    }
+    if (mode == "pairs" && argc == 11) {
+        // caller-supplied pairs (smore_train_pairs): proNet::UpdatePairs over
+        // the pairs in <pairs.i64> (v, c interleaved) from fixed starting
+        // tables (the "updates" LCG); block b of ORC_PAIR_BLOCK pairs draws
+        // from stream 3, unit <unit> + b, consecutive slots
+        int dim = atoi(argv[4]), K = atoi(argv[5]);
+        double alpha = atof(argv[6]);
+        g_seed = strtoull(argv[7], 0, 10);
+        uint64_t unit0 = strtoull(argv[8], 0, 10);
+        std::vector<double> raw = read_dist(argv[9]);   // 8-byte records, reinterpreted below
+        std::vector<long> pv, pc;
+        for (size_t i = 0; i + 1 < raw.size(); i += 2) {
+            long a, b;
+            memcpy(&a, &raw[i], 8);
+            memcpy(&b, &raw[i + 1], 8);
+            pv.push_back(a);
+            pc.push_back(b);
+        }
+        proNet pn;
+        pn.LoadEdgeList(argv[2], atoi(argv[3]) != 0);
+        long V = pn.MAX_vid;
+        std::vector<std::vector<double>> W(V, std::vector<double>(dim)), C = W;
+        uint64_t lcg = 0x243F6A8885A308D3ull;
+        auto nxt = [&]() { lcg = lcg * 6364136223846793005ull + 1442695040888963407ull;
+                           return std::ldexp((double)(lcg >> 11), -53) - 0.5; };
+        for (long v = 0; v < V; ++v) for (int d = 0; d < dim; ++d) W[v][d] = nxt();
+        for (long v = 0; v < V; ++v) for (int d = 0; d < dim; ++d) C[v][d] = nxt();
+        Out o(argv[10]);
+        o.table("W0", W, dim); o.table("C0", C, dim);
+        g_walk_mode = 1; g_walk_stream = 3;
+        for (size_t b = 0; b < pv.size(); b += ORC_PAIR_BLOCK) {
+            const size_t e = std::min(pv.size(), b + (size_t)ORC_PAIR_BLOCK);
+            std::vector<long> bv(pv.begin() + b, pv.begin() + e), bc(pc.begin() + b, pc.begin() + e);
+            g_walk_unit = unit0 + b / ORC_PAIR_BLOCK;
+            g_walk_slot = 0;
+            pn.UpdatePairs(W, C, bv, bc, dim, K, alpha);
+        }
+        o.table("W", W, dim); o.table("C", C, dim);
+        o.i64("pv", pv); o.i64("pc", pc);
         dump_graph(o, pn);
         return 0;
     }

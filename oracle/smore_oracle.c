@@ -1573,3 +1573,52 @@ int orc_go_ctdne_f32(const orc_go_graph* g, int64_t E, const int32_t* src, const
     ct_free(&t);
     return rc;
 }
+
+/* ---- caller-supplied pairs: UpdatePairs (src/proNet.cpp:2741-2753; Go
+ * pkg/pronet/optimizer.go:8-18) ----------------------------------------------
+ * UpdatePair for each pair (v[i], c[i]) in order with a fixed alpha.  Pair i
+ * draws its K negatives (NegativeSample: index, then p) from stream 3, unit
+ * unit0 + i / ORC_PAIR_BLOCK, slots 2K (i % ORC_PAIR_BLOCK) + 2j, +1 -- the
+ * reference's UpdatePairs over blocks of ORC_PAIR_BLOCK pairs with the RNG spec
+ * interposed (oracle/ref_harness.cpp "pairs").  go = 0: C++ UpdatePair
+ * (src/proNet.cpp:1784-1809); go = 1: Go UpdatePair (optimizer.go:21-58:
+ * negatives equal to the context skipped, the context's gradient deferred),
+ * both on g's negative table. */
+static void pair_negs(const orc_graph* g, uint64_t seed, uint64_t unit0, int64_t i, int K, int32_t* negs) {
+    const uint64_t unit = unit0 + (uint64_t)i / ORC_PAIR_BLOCK;
+    const uint32_t base = 2u * (uint32_t)K * (uint32_t)((uint64_t)i % ORC_PAIR_BLOCK);
+    for (int j = 0; j < K; ++j)
+        negs[j] = negative_sample(g, orc_word(seed, 3, unit, base + 2u * j), orc_word(seed, 3, unit, base + 2u * j + 1u));
+}
+
+int orc_update_pairs_f64(const orc_graph* g, double* W, double* C, int dim, const int32_t* v, const int32_t* c,
+                         int64_t n, int K, double alpha, uint64_t seed, uint64_t unit0, int go) {
+    sig_init();
+    if (K < 0 || K > MAX_SLOTS) return -1;
+    double* buf = (double*)malloc(sizeof(double) * dim * 3);
+    int32_t negs[MAX_SLOTS];
+    for (int64_t i = 0; i < n; ++i) {
+        pair_negs(g, seed, unit0, i, K, negs);
+        if (go) go_update_pair_f64(W, C, dim, v[i], c[i], negs, K, alpha, buf, buf + dim, buf + 2 * dim);
+        else update_edge_f64(0, W, C, dim, v[i], c[i], negs, K, alpha, 0.0, buf);
+    }
+    free(buf);
+    return 0;
+}
+
+int orc_update_pairs_f32(const orc_graph* g, float* W, float* C, int dim, int dpad, const int32_t* v,
+                         const int32_t* c, int64_t n, int K, double alpha, uint64_t seed, uint64_t unit0, int go) {
+    (void)dim;
+    sig_init();
+    if (K < 0 || K > MAX_SLOTS) return -1;
+    float* buf = (float*)malloc(sizeof(float) * dpad * 2);
+    int32_t negs[MAX_SLOTS];
+    const float a = (float)alpha;
+    for (int64_t i = 0; i < n; ++i) {
+        pair_negs(g, seed, unit0, i, K, negs);
+        if (go) go_update_pair_f32(W, C, dpad, v[i], c[i], negs, K, a, buf, buf + dpad);
+        else update_edge_f32(0, W, C, dpad, v[i], c[i], negs, K, a, 0.0f, buf);
+    }
+    free(buf);
+    return 0;
+}

@@ -14,7 +14,7 @@ VM = {"out_degrees": 0, "no_degrees": 1, "degrees": 2}
 NM = {"degrees": 0, "in_degrees": 1, "no_degrees": 2}
 AT_VERTEX, AT_NEGATIVE, AT_CONTEXT = 0, 1, 2
 W, CTX = 0, 1
-MODEL = {"line2": 0, "line1": 1, "mf": 2, "bpr": 3}
+MODEL = {"line2": 0, "line1": 1, "mf": 2, "bpr": 3, "census": 16}   # census: smore_row_rates of the last census
 # exchange rules of the replica exchange (smore_hip.h SMORE_SYNC_*)
 SYNC = {"sum": 0, "mean": 1, "adaptive": 2}
 
@@ -133,6 +133,9 @@ def _load():
         "smore_group_train_app": (i32, [P, u64, u64, i32, i32, dbl, i32, dbl, u64, P, i32, u64, i32]),
         "smore_group_train_hpe": (i32, [P, u64, u64, u64, i32, i32, dbl, dbl, u64, i32, u64, i32]),
         "smore_sample_edges": (i32, [P, i32, u64, u64, i32, u64, P]),
+        "smore_train_pairs": (i32, [P, P, P, i64, i32, dbl, u64, u64, i32]),
+        "smore_census_begin": (i32, [P]),
+        "smore_census_end": (i32, [P, dbl]),
         "smore_save_weights": (i32, [P, i32, C.c_char_p, i32]),
         "smore_load_pretrain": (i32, [P, i32, C.c_char_p]),
     }

@@ -63,7 +63,7 @@ void smore_destroy(smore_ctx* c) {
 
     dfree(c->d_order); dfree(c->d_walks); dfree(c->d_lens); dfree(c->d_tcum); dfree(c->d_wts); dfree(c->d_nbr_sorted); dfree(c->d_ntype); dfree(c->d_ttargets); dfree(c->d_toff); dfree(c->d_paths); dfree(c->d_path_off); dfree(c->d_t_off); dfree(c->d_t_tgt); dfree(c->d_t_ts); dfree(c->d_t_min); dfree(c->d_t_max); dfree(c->d_sh_hash); dfree(c->d_sh_ids);
     dfree(c->d_rec); dfree(c->d_vt32); dfree(c->d_ct16);
-    dfree(c->d_pcount); dfree(c->d_poff);
+    dfree(c->d_pcount); dfree(c->d_poff); dfree(c->d_pairs); dfree(c->d_census[0]); dfree(c->d_census[1]);
     if (c->d_scan_tmp) (void)hipFree(c->d_scan_tmp);
     for (hipEvent_t e : c->phase_ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -635,6 +635,8 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
     const int need_tables = model == SMORE_LINE2 ? 2 : 1;
     if (c->ntables < need_tables) return fail(c, SMORE_ESTATE, "tables not allocated");
     if (total == 0) return fail(c, SMORE_EINVAL, "total == 0");
+    if (c->census)
+        return fail(c, SMORE_ESTATE, "row census: edge models have exact rates (smore_row_rates with their model)");
     if (count == 0) return SMORE_OK;
     int rc;
     if ((rc = set_device(c))) return rc;
@@ -834,10 +836,17 @@ int smore_write_combine_info(const smore_ctx* c, int* rows, int* flush_rounds) {
 // Go BPR: W = sources, C = contexts + K x negatives; one-table models: the
 // union), highest first -- the rows the replica exchange syncs every launch
 int smore_row_rates(smore_ctx* c, int model, int K, int which, int64_t n, double* rate) {
-    if (!c || !rate || which < 0 || which > 1 || model < 0 || model > 3 || K < 0) return SMORE_EINVAL;
+    if (!c || !rate || which < 0 || which > 1 || ((model < 0 || model > 3) && model != SMORE_CENSUS) || K < 0)
+        return SMORE_EINVAL;
     if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
     const int64_t V = c->g->V;
     if (n != V) return fail(c, SMORE_EINVAL, "row_rates: n must be the vertex count");
+    if (model == SMORE_CENSUS) {
+        if (!c->census_ok || (int64_t)c->census_rate[which].size() != V)
+            return fail(c, SMORE_ESTATE, "row_rates: no census (smore_census_begin / _end)");
+        std::copy(c->census_rate[which].begin(), c->census_rate[which].end(), rate);
+        return SMORE_OK;
+    }
     std::vector<double> ps, pn, pc;
     draw_probabilities(*c->g, ps, pn, pc);
     const bool two = model == SMORE_LINE2 || (model == SMORE_BPR && c->semantics == SMORE_SEM_GO);
@@ -848,7 +857,7 @@ int smore_row_rates(smore_ctx* c, int model, int K, int which, int64_t n, double
 }
 
 int smore_hot_row_ids(smore_ctx* c, int model, int K, int which, int64_t n, int32_t* ids) {
-    if (!c || !ids || n < 0 || which < 0 || which > 1 || model < 0 || model > 3 || K < 0)
+    if (!c || !ids || n < 0 || which < 0 || which > 1 || ((model < 0 || model > 3) && model != SMORE_CENSUS) || K < 0)
         return SMORE_EINVAL;
     if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
     const int64_t V = c->g->V;
@@ -1263,7 +1272,10 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
         ak.rec = c->d_rec;
         HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
         const int g = mode == SMORE_SERIAL ? 1 : ugrid;
-        if (!go) HIPCHK(c, launch_edge_train(ak, g, c->stream));
+        if (c->census)
+            HIPCHK(c, launch_row_census(ak.rec, ak.count, ak.count_dev, RW, K, c->d_census[0], c->d_census[1], c->cus,
+                                        c->stream));
+        else if (!go) HIPCHK(c, launch_edge_train(ak, g, c->stream));
         else if (mode == SMORE_ATOMIC) HIPCHK(c, launch_go_pair_a(ak, g, c->stream));
         else if (mode == SMORE_HYBRID) HIPCHK(c, launch_go_pair_h(ak, g, c->stream));
         else HIPCHK(c, launch_go_pair_s(ak, g, c->stream));
@@ -1446,7 +1458,10 @@ int smore_train_app_async(smore_ctx* c, uint64_t unit_begin, uint64_t unit_end, 
         ak.begin = 0;
         ak.count = p.n;
         HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
-        HIPCHK(c, launch_edge_train(ak, mode == SMORE_SERIAL ? 1 : grid, c->stream));
+        if (c->census)
+            HIPCHK(c, launch_row_census(ak.rec, ak.count, nullptr, RW, K, c->d_census[0], c->d_census[1], c->cus,
+                                        c->stream));
+        else HIPCHK(c, launch_edge_train(ak, mode == SMORE_SERIAL ? 1 : grid, c->stream));
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
@@ -1519,7 +1534,10 @@ int smore_train_hpe_async(smore_ctx* c, uint64_t begin, uint64_t count, uint64_t
         ak.begin = 0;
         ak.count = p.n * nrec;
         HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
-        HIPCHK(c, launch_edge_train(ak, mode == SMORE_SERIAL ? 1 : grid, c->stream));
+        if (c->census)
+            HIPCHK(c, launch_row_census(ak.rec, ak.count, nullptr, RW, K, c->d_census[0], c->d_census[1], c->cus,
+                                        c->stream));
+        else HIPCHK(c, launch_edge_train(ak, mode == SMORE_SERIAL ? 1 : grid, c->stream));
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
@@ -1541,6 +1559,131 @@ int smore_train_deepwalk(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, i
                                         order, mode);
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return SMORE_OK;
+}
+
+// ---------------------------------------------------------------- caller pairs
+// proNet::UpdatePairs (src/proNet.cpp:2741-2753) / Go (*ProNet).UpdatePairs
+// (pkg/pronet/optimizer.go:8-18): the caller's pairs become records
+// (caller_pair_kernel, negatives drawn on the device) for the pair kernels --
+// pair_train_kernel (C++ UpdatePair; serial: edge_train_kernel's in-order
+// path) or go_pair_kernel (Go UpdatePair) -- in chunks of up to 2^24 pairs.
+int smore_train_pairs(smore_ctx* c, const int32_t* v, const int32_t* cc, int64_t n, int K, double alpha,
+                      uint64_t seed, uint64_t unit, int mode) {
+    if (!c) return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    if (c->ntables < 2) return fail(c, SMORE_ESTATE, "UpdatePairs needs W and C tables");
+    if (n < 0 || (n > 0 && (!v || !cc)) || K < 0 || K > 10 || mode < 0 || mode > 3)
+        return fail(c, SMORE_EINVAL, "bad UpdatePairs arguments");
+    if (n == 0) return SMORE_OK;
+    const int64_t V = c->g->V;
+    for (int64_t i = 0; i < n; ++i)
+        if (v[i] < 0 || v[i] >= V || cc[i] < 0 || cc[i] >= V) return fail(c, SMORE_EINVAL, "pair id out of range");
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    const bool go = c->semantics == SMORE_SEM_GO;
+    const int RW = rec_width(kmax_of(K));
+    const uint64_t chunk = std::min<uint64_t>((uint64_t)n, (uint64_t)1 << 24);
+    if (c->pairs_cap < chunk) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        dfree(c->d_pairs);
+        c->pairs_cap = 0;
+        HIPCHK(c, hipMalloc((void**)&c->d_pairs, 2 * chunk * sizeof(int32_t)));
+        c->pairs_cap = chunk;
+    }
+    if (c->rec_cap < chunk * RW) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        dfree(c->d_rec);
+        c->rec_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_rec, chunk * RW * sizeof(int32_t)));
+        c->rec_cap = chunk * RW;
+    }
+    EdgeArgs a{};
+    a.sig = c->d_sig;
+    a.W = c->d_table[0];
+    a.C = c->d_table[1];
+    a.skipped = c->d_skipped;
+    a.total = 1; a.seed = seed; a.alpha0 = alpha; a.reg = 0.0f;
+    a.dpad = c->dpad; a.K = K; a.model = SMORE_LINE2; a.mode = mode;
+    a.tcum = c->d_tcum;
+    a.alpha_rec = 1;
+    a.work = c->d_work;
+    a.count = chunk;
+    const bool combine = mode == SMORE_HYBRID;
+    a.sh_rows = combine ? std::min(c->sh_max, 8192 / std::max(1, c->dpad)) : 0;
+    const int grid = edge_grid(c, a, false, go ? 2 : 0);
+    if (mode == SMORE_HYBRID) {
+        const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
+        if ((rc = build_hot_maps(c, SMORE_LINE2, K, M, HOT_TAU_WALK))) return rc;
+    }
+    a.g = dev_graph(c);
+    a.sh_rows = combine ? c->sh_rows : 0;
+    a.sh_hash = c->d_sh_hash;
+    a.sh_ids = c->d_sh_ids;
+    a.sh_flush = std::max(1, c->sh_flush_eff);
+    a.rec = c->d_rec;
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    for (uint64_t b = 0; b < (uint64_t)n; b += chunk) {
+        const uint64_t m = std::min<uint64_t>(chunk, (uint64_t)n - b);
+        // the previous chunk's kernels read d_pairs / d_rec: the copies are
+        // ordered after them on the stream
+        HIPCHK(c, hipMemcpyAsync(c->d_pairs, v + b, m * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->d_pairs + chunk, cc + b, m * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, launch_caller_pairs(a.g, c->d_pairs, c->d_pairs + chunk, m, b, K, (float)alpha, seed, unit, go ? 1 : 0,
+                                      mode == SMORE_HYBRID, c->d_rec, c->stream));
+        EdgeArgs ak = a;
+        ak.begin = 0;
+        ak.count = m;
+        const int g = mode == SMORE_SERIAL ? 1 : grid;
+        HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
+        if (c->census)
+            HIPCHK(c, launch_row_census(ak.rec, m, nullptr, RW, K, c->d_census[0], c->d_census[1], c->cus, c->stream));
+        else if (!go) HIPCHK(c, launch_edge_train(ak, g, c->stream));
+        else if (mode == SMORE_ATOMIC) HIPCHK(c, launch_go_pair_a(ak, g, c->stream));
+        else if (mode == SMORE_HYBRID) HIPCHK(c, launch_go_pair_h(ak, g, c->stream));
+        else HIPCHK(c, launch_go_pair_s(ak, g, c->stream));
+    }
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
+    c->phase_n = 0;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipGetLastError());
+    return SMORE_OK;
+}
+
+// ---------------------------------------------------------------- row census
+int smore_census_begin(smore_ctx* c) {
+    if (!c) return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    const size_t V = (size_t)std::max<int64_t>(1, c->g->V);
+    for (auto*& p : c->d_census) {
+        if (!p) HIPCHK(c, hipMalloc((void**)&p, V * sizeof(unsigned long long)));
+        HIPCHK(c, hipMemsetAsync(p, 0, V * sizeof(unsigned long long), c->stream));
+    }
+    c->census = true;
+    c->census_ok = false;
+    return SMORE_OK;
+}
+
+int smore_census_end(smore_ctx* c, double units) {
+    if (!c) return SMORE_EINVAL;
+    if (!c->census) return fail(c, SMORE_ESTATE, "no census in progress (smore_census_begin)");
+    c->census = false;
+    if (!(units > 0.0)) return fail(c, SMORE_EINVAL, "census: units must be > 0");
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const size_t V = (size_t)c->g->V;
+    std::vector<unsigned long long> h(V);
+    for (int t = 0; t < 2; ++t) {
+        if (V) HIPCHK(c, hipMemcpy(h.data(), c->d_census[t], V * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        c->census_rate[t].resize(V);
+        for (size_t i = 0; i < V; ++i) c->census_rate[t][i] = (double)h[i] / units;
+    }
+    c->census_ok = true;
+    c->census_gen++;
     return SMORE_OK;
 }
 

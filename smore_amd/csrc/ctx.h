@@ -104,8 +104,9 @@ struct smore_ctx {
     int phase_n = 0;                    // chunks of the last edge launch
     // replica exchange over RCCL (exchange.cpp): snapshot S, own delta D and
     // the all-reduced deltas R per table, a communicator and its stream
-    void* comm = nullptr;               // ncclComm_t
+    void* comm = nullptr;               // ncclComm_t (a same-device group: the group, no RCCL)
     bool own_comm = false;              // created by smore_comm_init (destroyed with the context)
+    bool local_comm = false;            // replica of a same-device group (exchange.cpp local collectives)
     int nranks = 1, rank = 0;
     hipStream_t comm_stream = nullptr;
     hipEvent_t ex_ready = nullptr, ex_done = nullptr;
@@ -132,6 +133,18 @@ struct smore_ctx {
     int part_n = 1, part_i = 0;
     hvec<AliasEntry> part_vtab;
     std::vector<int64_t> part_bounds;   // part_n + 1 bounds of the current partition
+    // row census (smore_census_begin / _end): while `census` is set the record
+    // paths count the rows each record would update (d_census: W, C; V
+    // counters each) instead of training; census_rate = counts per unit
+    bool census = false;
+    unsigned long long* d_census[2] = {nullptr, nullptr};
+    std::vector<double> census_rate[2];
+    bool census_ok = false;
+    uint64_t census_gen = 0;            // bumped by every smore_census_end (the adaptive scales' key)
+    std::string census_key;             // what the group driver censused (exchange.cpp)
+    // caller-supplied pairs (smore_train_pairs): a chunk of (v, c) on the device
+    int32_t* d_pairs = nullptr;
+    size_t pairs_cap = 0;               // pairs
 };
 
 // exchange.cpp: frees the exchange buffers and the communicator
@@ -186,6 +199,17 @@ inline int upload_graph(smore_ctx* c) {
     dfree(c->d_t_min);
     dfree(c->d_t_max);
     c->has_temporal = false;
+    // everything keyed by the previous graph: hub-row ids of the exchange,
+    // the adaptive scales, the census rates
+    c->hot_ex_key.clear();
+    c->ex_scale_key.clear();
+    c->census = false;
+    c->census_ok = false;
+    c->census_key.clear();
+    c->census_rate[0].clear();
+    c->census_rate[1].clear();
+    dfree(c->d_census[0]);
+    dfree(c->d_census[1]);
     if (c->device < 0) {
         c->has_graph = true;
         return SMORE_OK;

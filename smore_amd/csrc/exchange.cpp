@@ -19,10 +19,15 @@
 //     enqueues every replica's work; the collectives of all replicas go out in
 //     one ncclGroupStart/End).
 // RCCL is loaded on first use (dlopen librccl.so.1): single-GPU users and the
-// host-only context never load it.
+// host-only context never load it.  A group whose replicas all sit on ONE
+// device (smore_group_create with a repeated device id) runs the same rounds
+// with its collectives as device passes on that GPU (local_sum_kernel, stream-
+// ordered copies) and no RCCL: the multi-replica path on a one-GPU machine
+// (tests, the replica-quality runs of DESIGN.md 10).
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <initializer_list>
 #include <mutex>
 
 #include "ctx.h"
@@ -228,8 +233,8 @@ int upload_scales(smore_ctx* c, const std::vector<float> (&sc)[2], const std::st
 
 std::string scale_key(int model, int K, double updates, double c0, int nranks, const smore_ctx* c) {
     char key[160];
-    snprintf(key, sizeof key, "%d/%d/%.17g/%.17g/%d/%lld/%d", model, K, updates, c0, nranks, (long long)c->g->V,
-             c->ntables);
+    snprintf(key, sizeof key, "%d/%d/%.17g/%.17g/%d/%lld/%d/%llu", model, K, updates, c0, nranks, (long long)c->g->V,
+             c->ntables, model == SMORE_CENSUS ? (unsigned long long)c->census_gen : 0ull);
     return key;
 }
 
@@ -271,6 +276,11 @@ struct smore_group {
     int launches = 8;
     double c0 = -1.0;   // adaptive exchange (smore_group_set_adaptive); -1: 2048 with the source partition, else 64
     int partition = 1;  // LINE-2: W rows partitioned by source (smore_group_set_partition)
+    // every replica on one device: collectives as device passes, ordered by
+    // events between the replicas' streams (no RCCL)
+    bool local = false;
+    std::vector<hipEvent_t> lev;   // one per replica
+    hipEvent_t ldone = nullptr;
 };
 
 namespace {
@@ -278,6 +288,77 @@ namespace {
 int gfail(smore_group* g, int rank, int rc) {
     if (g && rc != SMORE_OK && rank >= 0) g->err = "replica " + std::to_string(rank) + ": " + g->ctx[rank]->err;
     return rc;
+}
+
+// ---- the group's collectives over per-replica buffers, each replica's part
+// on its own stream (RCCL: one grouped call; local: device passes)
+int coll_allreduce(smore_group* g, const std::vector<float*>& buf, size_t n, const std::vector<hipStream_t>& st,
+                   const char* what) {
+    const size_t R = g->ctx.size();
+    if (g->local) {
+        smore_ctx* c0 = g->ctx[0];
+        int rc;
+        if ((rc = set_device(c0))) return gfail(g, 0, rc);
+        // the sum runs on replica 0's stream after every replica's stream
+        // reached this point; every stream continues after the sum
+        for (size_t r = 1; r < R; ++r) {
+            if (hipEventRecord(g->lev[r], st[r]) != hipSuccess || hipStreamWaitEvent(st[0], g->lev[r], 0) != hipSuccess)
+                return gfail(g, (int)r, fail(g->ctx[r], SMORE_EHIP, std::string(what) + ": event"));
+        }
+        if (launch_local_sum(buf.data(), (int)R, n, c0->cus, st[0]) != hipSuccess)
+            return gfail(g, 0, fail(c0, SMORE_EHIP, std::string(what) + ": local sum"));
+        if (hipEventRecord(g->ldone, st[0]) != hipSuccess) return gfail(g, 0, fail(c0, SMORE_EHIP, what));
+        for (size_t r = 1; r < R; ++r)
+            if (hipStreamWaitEvent(st[r], g->ldone, 0) != hipSuccess)
+                return gfail(g, (int)r, fail(g->ctx[r], SMORE_EHIP, what));
+        return SMORE_OK;
+    }
+    Rccl* L = rccl();
+    ncclResult_t nr = L->group_start();
+    for (size_t r = 0; r < R && nr == ncclSuccess; ++r) {
+        (void)hipSetDevice(g->ctx[r]->device);
+        nr = L->all_reduce(buf[r], buf[r], n, ncclFloat32, ncclSum, (ncclComm_t)g->ctx[r]->comm, st[r]);
+    }
+    ncclResult_t ne = L->group_end();
+    if (nr == ncclSuccess) nr = ne;
+    if (nr != ncclSuccess) return gfail(g, 0, nccl_fail(g->ctx[0], what, nr));
+    return SMORE_OK;
+}
+
+int coll_broadcast(smore_group* g, const std::vector<float*>& buf, size_t n, int root,
+                   const std::vector<hipStream_t>& st, const char* what) {
+    const size_t R = g->ctx.size();
+    if (g->local) {
+        int rc;
+        if ((rc = set_device(g->ctx[0]))) return gfail(g, 0, rc);
+        if (hipEventRecord(g->ldone, st[root]) != hipSuccess) return gfail(g, root, fail(g->ctx[root], SMORE_EHIP, what));
+        for (size_t r = 0; r < R; ++r) {
+            if ((int)r == root) continue;
+            // the copy waits for the root's stream; the root's stream waits
+            // for the copy before it writes the rows again
+            if (hipStreamWaitEvent(st[r], g->ldone, 0) != hipSuccess ||
+                hipMemcpyAsync(buf[r], buf[root], n * sizeof(float), hipMemcpyDeviceToDevice, st[r]) != hipSuccess ||
+                hipEventRecord(g->lev[r], st[r]) != hipSuccess || hipStreamWaitEvent(st[root], g->lev[r], 0) != hipSuccess)
+                return gfail(g, (int)r, fail(g->ctx[r], SMORE_EHIP, std::string(what) + ": local copy"));
+        }
+        return SMORE_OK;
+    }
+    Rccl* L = rccl();
+    ncclResult_t nr = L->group_start();
+    for (size_t r = 0; r < R && nr == ncclSuccess; ++r) {
+        (void)hipSetDevice(g->ctx[r]->device);
+        nr = L->broadcast(buf[r], buf[r], n, ncclFloat32, root, (ncclComm_t)g->ctx[r]->comm, st[r]);
+    }
+    ncclResult_t ne = L->group_end();
+    if (nr == ncclSuccess) nr = ne;
+    if (nr != ncclSuccess) return gfail(g, 0, nccl_fail(g->ctx[0], what, nr));
+    return SMORE_OK;
+}
+
+std::vector<hipStream_t> compute_streams(const smore_group* g) {
+    std::vector<hipStream_t> st;
+    for (smore_ctx* c : g->ctx) st.push_back(c->stream);
+    return st;
 }
 
 // every replica adopts replica 0's (shared) host graph and uploads it
@@ -296,32 +377,35 @@ int replicate_graph(smore_group* g) {
 
 int group_exchange_begin(smore_group* g, int rule) {
     int rc;
-    for (size_t r = 0; r < g->ctx.size(); ++r)
+    const size_t R = g->ctx.size();
+    for (size_t r = 0; r < R; ++r)
         if ((rc = exchange_passes(g->ctx[r], rule))) return gfail(g, (int)r, rc);
-    Rccl* L = rccl();
-    ncclResult_t nr = L->group_start();
-    for (size_t r = 0; r < g->ctx.size() && nr == ncclSuccess; ++r) {
-        (void)hipSetDevice(g->ctx[r]->device);
-        if ((rc = exchange_collective(g->ctx[r]))) {
-            (void)L->group_end();
-            return gfail(g, (int)r, rc);
-        }
+    std::vector<hipStream_t> st;
+    for (smore_ctx* c : g->ctx) st.push_back(c->comm_stream);
+    for (int t = g->ctx[0]->ex_t0; t < g->ctx[0]->ntables; ++t) {
+        std::vector<float*> buf;
+        for (smore_ctx* c : g->ctx) buf.push_back(c->ex_buf[t][2]);
+        if ((rc = coll_allreduce(g, buf, g->ctx[0]->ex_n, st, "ncclAllReduce"))) return rc;
     }
-    if (nr == ncclSuccess) nr = L->group_end();
-    if (nr != ncclSuccess) return gfail(g, 0, nccl_fail(g->ctx[0], "ncclGroupEnd", nr));
-    for (size_t r = 0; r < g->ctx.size(); ++r)
+    for (size_t r = 0; r < R; ++r)
         if ((rc = exchange_posted(g->ctx[r]))) return gfail(g, (int)r, rc);
     return SMORE_OK;
 }
 
-// the hub rows of every replica (replica 0's host graph: all replicas share it)
+// the hub rows of every exchanged table of every replica (replica 0's host
+// graph: all replicas share it); keyed by the rows' law and the tables (the
+// key is cleared with the graph, upload_graph)
 int ensure_hot(smore_group* g, int model, int K, int64_t rows) {
     smore_ctx* c0 = g->ctx[0];
     const std::string key = std::to_string(model) + "/" + std::to_string(K) + "/" + std::to_string(rows) + "/" +
-                            std::to_string(c0->dpad) + "/" + std::to_string(c0->ntables);
-    if (c0->hot_ex_key == key) return SMORE_OK;
+                            std::to_string(c0->dpad) + "/" + std::to_string(c0->ntables) + "/" +
+                            std::to_string(c0->ex_t0) + "/" + std::to_string(c0->g->V) + "/" +
+                            std::to_string(c0->g->E) + "/" + c0->census_key;
+    bool same = true;
+    for (smore_ctx* c : g->ctx) same = same && c->hot_ex_key == key;
+    if (same) return SMORE_OK;
     std::vector<int32_t> ids[2];
-    for (int t = 0; t < c0->ntables; ++t) {
+    for (int t = c0->ex_t0; t < c0->ntables; ++t) {
         ids[t].resize((size_t)rows);
         int rc = smore_hot_row_ids(c0, model, K, t, rows, ids[t].data());
         if (rc) return gfail(g, 0, rc);
@@ -335,7 +419,7 @@ int ensure_hot(smore_group* g, int model, int K, int64_t rows) {
             dfree(c->hot_buf[t][0]);
             dfree(c->hot_buf[t][1]);
         }
-        for (int t = 0; t < c->ntables; ++t) {
+        for (int t = c->ex_t0; t < c->ntables; ++t) {
             if ((rc = upload(c, c->hot_idx[t], ids[t].data(), ids[t].size()))) return gfail(g, (int)r, rc);
             for (float*& p : c->hot_buf[t])
                 if (hipMalloc((void**)&p, (size_t)rows * c->dpad * sizeof(float)) != hipSuccess)
@@ -347,33 +431,30 @@ int ensure_hot(smore_group* g, int model, int K, int64_t rows) {
     return SMORE_OK;
 }
 
-// the synchronous hub-row exchange on every replica's compute stream
+// the synchronous hub-row exchange of the exchanged tables on every replica's
+// compute stream (a table outside [ex_t0, ntables) has no snapshot to pack against)
 int group_hot_exchange(smore_group* g) {
     int rc;
+    const int t0 = g->ctx[0]->ex_t0;
     for (size_t r = 0; r < g->ctx.size(); ++r) {
         smore_ctx* c = g->ctx[r];
         if ((rc = set_device(c))) return gfail(g, (int)r, rc);
-        for (int t = 0; t < c->ntables; ++t)
+        for (int t = t0; t < c->ntables; ++t)
             if (launch_hot_pack(c->d_table[t], c->ex_buf[t][0], c->hot_idx[t], (uint64_t)c->hot_n, c->dpad,
                                 c->hot_buf[t][0], c->hot_buf[t][1], c->cus, c->stream) != hipSuccess)
                 return gfail(g, (int)r, fail(c, SMORE_EHIP, "hot_pack"));
     }
-    Rccl* L = rccl();
-    ncclResult_t nr = L->group_start();
-    for (size_t r = 0; r < g->ctx.size() && nr == ncclSuccess; ++r) {
-        smore_ctx* c = g->ctx[r];
-        (void)hipSetDevice(c->device);
-        for (int t = 0; t < c->ntables && nr == ncclSuccess; ++t)
-            nr = L->all_reduce(c->hot_buf[t][1], c->hot_buf[t][1], (size_t)c->hot_n * c->dpad, ncclFloat32, ncclSum,
-                               (ncclComm_t)c->comm, c->stream);
+    const std::vector<hipStream_t> st = compute_streams(g);
+    for (int t = t0; t < g->ctx[0]->ntables; ++t) {
+        std::vector<float*> buf;
+        for (smore_ctx* c : g->ctx) buf.push_back(c->hot_buf[t][1]);
+        if ((rc = coll_allreduce(g, buf, (size_t)g->ctx[0]->hot_n * g->ctx[0]->dpad, st, "hub-row ncclAllReduce")))
+            return rc;
     }
-    ncclResult_t ne = L->group_end();
-    if (nr == ncclSuccess) nr = ne;
-    if (nr != ncclSuccess) return gfail(g, 0, nccl_fail(g->ctx[0], "hub-row ncclAllReduce", nr));
     for (size_t r = 0; r < g->ctx.size(); ++r) {
         smore_ctx* c = g->ctx[r];
         if ((rc = set_device(c))) return gfail(g, (int)r, rc);
-        for (int t = 0; t < c->ntables; ++t)
+        for (int t = t0; t < c->ntables; ++t)
             if (launch_hot_unpack(c->d_table[t], c->ex_buf[t][0], c->hot_idx[t], (uint64_t)c->hot_n, c->dpad,
                                   c->hot_buf[t][0], c->hot_buf[t][1], c->cus, c->stream) != hipSuccess)
                 return gfail(g, (int)r, fail(c, SMORE_EHIP, "hot_unpack"));
@@ -388,20 +469,14 @@ int gather_sources(smore_group* g) {
     std::vector<int64_t> b(n + 1);
     int rc;
     if ((rc = smore_source_parts(g->ctx[0], (int)n, b.data()))) return gfail(g, 0, rc);
-    Rccl* L = rccl();
+    const std::vector<hipStream_t> st = compute_streams(g);
     for (size_t p = 0; p < n; ++p) {
         if (b[p + 1] <= b[p]) continue;
-        ncclResult_t nr = L->group_start();
-        for (size_t r = 0; r < n && nr == ncclSuccess; ++r) {
-            smore_ctx* c = g->ctx[r];
-            (void)hipSetDevice(c->device);
-            float* rows = c->d_table[0] + (size_t)b[p] * c->dpad;
-            nr = L->broadcast(rows, rows, (size_t)(b[p + 1] - b[p]) * c->dpad, ncclFloat32, (int)p,
-                              (ncclComm_t)c->comm, c->stream);
-        }
-        ncclResult_t ne = L->group_end();
-        if (nr == ncclSuccess) nr = ne;
-        if (nr != ncclSuccess) return gfail(g, 0, nccl_fail(g->ctx[0], "W gather ncclBroadcast", nr));
+        std::vector<float*> rows;
+        for (smore_ctx* c : g->ctx) rows.push_back(c->d_table[0] + (size_t)b[p] * c->dpad);
+        if ((rc = coll_broadcast(g, rows, (size_t)(b[p + 1] - b[p]) * g->ctx[0]->dpad, (int)p, st,
+                                 "W gather ncclBroadcast")))
+            return rc;
     }
     return SMORE_OK;
 }
@@ -415,22 +490,31 @@ int group_sync(smore_group* g) {
 
 }  // namespace
 
-// The group training round structure: round k, replica r queues units
-// [begin + (k n + r) per, + per) of the global range on its stream (run(ctx, b, e)
-// must not synchronize), then the group folds the previous exchange in and
-// starts this round's all-reduce, which overlaps round k+1.  rule: SMORE_SYNC_*;
-// the adaptive rule's row scales are made for `model` with K negatives at per
-// * upu updates per replica per exchange (upu: updates per unit, e.g. the
-// expected pairs of a walk).  With the hub-row exchange on (sum rule), each
-// replica's share of a round runs as g->launches launches and the hub rows
-// are synced after each.
+// The group training round structure.  The range [begin, end) is cut into
+// R = ceil(count / (per * N)) rounds of equal size (+-1); round k's units are
+// split evenly over the N replicas (replica r gets the r-th of N equal
+// slices, so every replica trains a share of every call -- with the source
+// partition a replica that got nothing would leave its part's W rows
+// untrained).  Replica r queues its slice on its stream (run(ctx, b, e) must
+// not synchronize), then the group folds the previous exchange in and starts
+// this round's all-reduce, which overlaps round k+1.  rule: SMORE_SYNC_*; the
+// adaptive rule's row scales are made for `model` with K negatives at the
+// replicas' actual units per round (count / (R N)) * upu updates per replica
+// per exchange (upu: updates per unit).  model SMORE_CENSUS (the walk models):
+// the rows' touches per unit come from a census of the call's first round on
+// replica 0 (run in census mode: records generated, rows counted, nothing
+// trained; smore_census_begin), redone only when census_key changes.  With
+// the hub-row exchange on (sum rule), each replica's slice runs as
+// g->launches launches and the hub rows are synced after each.
 template <class F>
 static int group_rounds(smore_group* g, uint64_t begin, uint64_t end, uint64_t per, int rule, F&& run,
-                        int model = SMORE_LINE2, int K = 5, double upu = 1.0, bool part = false) {
+                        int model = SMORE_LINE2, int K = 5, double upu = 1.0, bool part = false,
+                        const std::string& census_key = std::string()) {
     const size_t n = g->ctx.size();
     int rc;
     if (end <= begin) return SMORE_OK;
     if (rule < SMORE_SYNC_SUM || rule > SMORE_SYNC_ADAPTIVE) return gfail(g, 0, fail(g->ctx[0], SMORE_EINVAL, "bad exchange rule"));
+    if (per == 0) return gfail(g, 0, fail(g->ctx[0], SMORE_EINVAL, "per == 0"));
     // LINE-2 with the source partition: replica r draws its sources from part
     // r, owns those W rows, and only C is exchanged (W gathered at the end)
     part = part && g->partition && n > 1;
@@ -440,31 +524,52 @@ static int group_rounds(smore_group* g, uint64_t begin, uint64_t end, uint64_t p
         c->ex_t0 = part ? 1 : 0;
         if ((rc = exchange_reset(c))) return gfail(g, (int)r, rc);
     }
-    const double c0 = g->c0 > 0 ? g->c0 : (part ? 2048.0 : 64.0);
+    const uint64_t count = end - begin;
+    const uint64_t round_units = per > count / n ? count : per * (uint64_t)n;   // no overflow: per * n <= count
+    const uint64_t rounds = (count + round_units - 1) / round_units;
+    auto round_lo = [&](uint64_t k) { return (uint64_t)(((unsigned __int128)count * k) / rounds); };
+    const double share = (double)count / ((double)rounds * (double)n);   // units per replica per exchange
+    int64_t rows = g->hot_rows < 0 ? std::min<int64_t>(65536, g->ctx[0]->g->V / 8) : g->hot_rows;
+    rows = std::min<int64_t>(rows, g->ctx[0]->g->V);
+    const bool hot = rule == SMORE_SYNC_SUM && rows > 0 && g->launches > 1;
+    if (model == SMORE_CENSUS && (rule == SMORE_SYNC_ADAPTIVE || hot)) {
+        smore_ctx* c0 = g->ctx[0];
+        const std::string key = census_key + "/" + std::to_string(c0->semantics);
+        if (c0->census_key != key || !c0->census_ok) {
+            // at least 2^16 units (or the call) so that the hub rows' rates are
+            // well measured on small rounds
+            const uint64_t m = std::min<uint64_t>(count, std::max<uint64_t>(round_lo(1), (uint64_t)1 << 16));
+            if ((rc = smore_census_begin(c0))) return gfail(g, 0, rc);
+            rc = run(c0, begin, begin + m);
+            const int rc2 = smore_census_end(c0, (double)m);
+            if (rc || rc2) return gfail(g, 0, rc ? rc : rc2);
+            c0->census_key = key;
+            for (size_t r = 1; r < n; ++r) g->ctx[r]->census_key.clear();
+        }
+    }
+    const double c0v = g->c0 > 0 ? g->c0 : (part ? 2048.0 : 64.0);
     if (rule == SMORE_SYNC_ADAPTIVE) {
-        const double updates = (double)per * upu;
-        const std::string key = scale_key(model, K, updates, c0, (int)n, g->ctx[0]);
-        if (g->ctx[0]->ex_scale_key != key) {
+        const double updates = share * upu;
+        const std::string key = scale_key(model, K, updates, c0v, (int)n, g->ctx[0]) + "/" + g->ctx[0]->census_key;
+        bool same = true;
+        for (smore_ctx* c : g->ctx) same = same && c->ex_scale_key == key;
+        if (!same) {
             std::vector<float> sc[2];
-            if ((rc = adaptive_scales(g->ctx[0], model, K, updates, c0, (int)n, sc))) return gfail(g, 0, rc);
+            if ((rc = adaptive_scales(g->ctx[0], model, K, updates, c0v, (int)n, sc))) return gfail(g, 0, rc);
             for (size_t r = 0; r < n; ++r)
                 if ((rc = upload_scales(g->ctx[r], sc, key))) return gfail(g, (int)r, rc);
         }
     }
-    int64_t rows = g->hot_rows < 0 ? std::min<int64_t>(65536, g->ctx[0]->g->V / 8) : g->hot_rows;
-    rows = std::min<int64_t>(rows, g->ctx[0]->g->V);
-    const bool hot = rule == SMORE_SYNC_SUM && rows > 0 && g->launches > 1;
     if (hot && (rc = ensure_hot(g, model, K, rows))) return rc;
     const int sub = hot ? g->launches : 1;
-    const uint64_t count = end - begin;
-    for (uint64_t base = 0; base < count; base += per * n) {
+    for (uint64_t k = 0; k < rounds; ++k) {
+        const uint64_t lo = round_lo(k), m = round_lo(k + 1) - lo;
         for (int j = 0; j < sub; ++j) {
             for (size_t r = 0; r < n; ++r) {
-                const uint64_t b = base + r * per;
-                if (b >= count) break;
-                const uint64_t m = std::min<uint64_t>(per, count - b);
-                const uint64_t lo = b + m * (uint64_t)j / sub, hi = b + m * (uint64_t)(j + 1) / sub;
-                if (hi > lo && (rc = run(g->ctx[r], begin + lo, begin + hi))) return gfail(g, (int)r, rc);
+                const uint64_t b = lo + (uint64_t)(((unsigned __int128)m * r) / n);
+                const uint64_t e = lo + (uint64_t)(((unsigned __int128)m * (r + 1)) / n);
+                const uint64_t bj = b + (e - b) * (uint64_t)j / sub, ej = b + (e - b) * (uint64_t)(j + 1) / sub;
+                if (ej > bj && (rc = run(g->ctx[r], begin + bj, begin + ej))) return gfail(g, (int)r, rc);
             }
             if (hot && (rc = group_hot_exchange(g))) return rc;
         }
@@ -476,12 +581,16 @@ static int group_rounds(smore_group* g, uint64_t begin, uint64_t end, uint64_t p
     return group_sync(g);
 }
 
-// expected skip-gram pairs of one walk (the adaptive rule's updates per walk):
-// C++ DeepWalk shrinks the window uniformly (window + 1 pairs per position on
-// average), Go's is fixed (2 window)
-static double walk_pairs(const smore_ctx* c, int steps, int window) {
-    const double L = (double)steps + 1.0, w = std::max(1, window);
-    return L * (c->semantics == SMORE_SEM_GO ? std::min(2.0 * w, L - 1.0) : std::min(w + 1.0, L - 1.0));
+// the census key of a walk-model call: the model and every argument that
+// changes which rows its records touch (walk law, window, K, seed)
+static std::string census_key(const char* model, std::initializer_list<double> args) {
+    std::string k = model;
+    char b[40];
+    for (double a : args) {
+        snprintf(b, sizeof b, "/%.17g", a);
+        k += b;
+    }
+    return k;
 }
 
 extern "C" {
@@ -519,6 +628,7 @@ int smore_exchange_reset(smore_ctx* c) { return exchange_reset(c); }
 int smore_exchange_begin(smore_ctx* c, int mean) {
     int rc;
     if ((rc = check_comm(c))) return rc;
+    if (c->local_comm) return fail(c, SMORE_ESTATE, "a same-device group's replica: use the smore_group_* calls");
     if ((rc = exchange_passes(c, mean))) return rc;
     if ((rc = exchange_collective(c))) return rc;
     return exchange_posted(c);
@@ -532,6 +642,8 @@ int smore_exchange_set_adaptive(smore_ctx* c, int model, int K, double updates, 
     if (c->ntables < 1) return fail(c, SMORE_ESTATE, "tables not allocated");
     // the scales depend on the world size: only after smore_comm_init
     if (!c->comm) return fail(c, SMORE_ESTATE, "adaptive exchange before smore_comm_init");
+    // an in-flight exchange's end applies the scales it was begun with
+    if (c->ex_pending) return fail(c, SMORE_ESTATE, "adaptive scales changed while an exchange is in flight");
     const std::string key = scale_key(model, K, updates, c0, c->nranks, c);
     if (c->ex_scale_key == key) return SMORE_OK;
     std::vector<float> sc[2];
@@ -544,6 +656,13 @@ int smore_exchange_set_adaptive(smore_ctx* c, int model, int K, double updates, 
 int smore_group_create(const int* devices, int n, smore_group** out) {
     if (!out || !devices || n < 1 || n > 64) return SMORE_EINVAL;
     *out = nullptr;
+    // all replicas on one device (a repeated id): local collectives, no RCCL;
+    // otherwise every device must be distinct (one RCCL rank per GPU)
+    bool local = n > 1, distinct = true;
+    for (int r = 1; r < n; ++r) local = local && devices[r] == devices[0];
+    for (int r = 0; r < n; ++r)
+        for (int q = 0; q < r; ++q) distinct = distinct && devices[q] != devices[r];
+    if (n > 1 && !local && !distinct) return SMORE_EINVAL;
     smore_group* g = new smore_group();
     for (int r = 0; r < n; ++r) {
         smore_ctx* c = nullptr;
@@ -554,7 +673,24 @@ int smore_group_create(const int* devices, int n, smore_group** out) {
         }
         g->ctx.push_back(c);
     }
-    if (n > 1) {
+    if (local) {
+        g->local = true;
+        g->lev.assign((size_t)n, nullptr);
+        bool ok = hipSetDevice(devices[0]) == hipSuccess &&
+                  hipEventCreateWithFlags(&g->ldone, hipEventDisableTiming) == hipSuccess;
+        for (int r = 0; r < n && ok; ++r) ok = hipEventCreateWithFlags(&g->lev[r], hipEventDisableTiming) == hipSuccess;
+        if (!ok) {
+            smore_group_destroy(g);
+            return SMORE_EHIP;
+        }
+        for (int r = 0; r < n; ++r) {
+            g->ctx[r]->comm = g;   // non-null: the exchange buffers are usable; never passed to RCCL
+            g->ctx[r]->own_comm = false;
+            g->ctx[r]->local_comm = true;
+            g->ctx[r]->nranks = n;
+            g->ctx[r]->rank = r;
+        }
+    } else if (n > 1) {
         Rccl* L = rccl();
         if (!L) {
             smore_group_destroy(g);
@@ -586,6 +722,9 @@ void smore_group_destroy(smore_group* g) {
     if (Rccl* L = g->comms.empty() ? nullptr : rccl())
         for (ncclComm_t cm : g->comms)
             if (cm) (void)L->destroy(cm);
+    for (hipEvent_t e : g->lev)
+        if (e) (void)hipEventDestroy(e);
+    if (g->ldone) (void)hipEventDestroy(g->ldone);
     delete g;
 }
 
@@ -689,18 +828,12 @@ int smore_group_broadcast_tables(smore_group* g) {
         if (c->ntables < 1 || !c->d_table[0]) return gfail(g, (int)r, fail(c, SMORE_ESTATE, "tables not allocated"));
         if ((rc = smore_synchronize(c))) return gfail(g, (int)r, rc);
     }
-    Rccl* L = rccl();
     const size_t n = table_floats(g->ctx[0]);
+    const std::vector<hipStream_t> st = compute_streams(g);
     for (int t = 0; t < g->ctx[0]->ntables; ++t) {
-        ncclResult_t nr = L->group_start();
-        for (size_t r = 0; r < g->ctx.size() && nr == ncclSuccess; ++r) {
-            smore_ctx* c = g->ctx[r];
-            (void)hipSetDevice(c->device);
-            nr = L->broadcast(c->d_table[t], c->d_table[t], n, ncclFloat32, 0, (ncclComm_t)c->comm, c->stream);
-        }
-        ncclResult_t ne = L->group_end();
-        if (nr == ncclSuccess) nr = ne;
-        if (nr != ncclSuccess) return gfail(g, 0, nccl_fail(g->ctx[0], "ncclBroadcast", nr));
+        std::vector<float*> buf;
+        for (smore_ctx* c : g->ctx) buf.push_back(c->d_table[t]);
+        if ((rc = coll_broadcast(g, buf, n, 0, st, "ncclBroadcast"))) return rc;
     }
     return group_sync(g);
 }
@@ -729,7 +862,8 @@ int smore_group_train_deepwalk(smore_group* g, uint64_t walk_begin, uint64_t wal
                             return smore_train_deepwalk_async(c, b, e, walk_times, walk_steps, window, K, alpha0,
                                                               seed, order, mode);
                         },
-                        SMORE_LINE2, K, walk_pairs(g->ctx[0], walk_steps, window));
+                        SMORE_CENSUS, K, 1.0, false,
+                        census_key("deepwalk", {(double)walk_times, (double)walk_steps, (double)window, (double)K, (double)seed}));
 }
 
 int smore_group_train_node2vec(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
@@ -744,7 +878,8 @@ int smore_group_train_node2vec(smore_group* g, uint64_t walk_begin, uint64_t wal
                             return smore_train_node2vec_async(c, b, e, walk_times, walk_steps, window, K, alpha0, p,
                                                               q, seed, order, mode);
                         },
-                        SMORE_LINE2, K, walk_pairs(g->ctx[0], walk_steps, window));
+                        SMORE_CENSUS, K, 1.0, false,
+                        census_key("node2vec", {(double)walk_times, (double)walk_steps, (double)window, (double)K, p, q, (double)seed}));
 }
 
 int smore_group_train_metapath2vec(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
@@ -761,7 +896,8 @@ int smore_group_train_metapath2vec(smore_group* g, uint64_t walk_begin, uint64_t
                                                                   alpha0, paths, path_lens, npaths, seed, order,
                                                                   mode);
                         },
-                        SMORE_LINE2, K, walk_pairs(g->ctx[0], walk_steps, window));
+                        SMORE_CENSUS, K, 1.0, false,
+                        census_key("metapath2vec", {(double)walk_times, (double)walk_steps, (double)window, (double)K, (double)npaths, (double)seed}));
 }
 
 int smore_group_train_ctdne(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
@@ -776,7 +912,8 @@ int smore_group_train_ctdne(smore_group* g, uint64_t walk_begin, uint64_t walk_e
                             return smore_train_ctdne_async(c, b, e, walk_times, walk_steps, window, K, alpha0,
                                                            time_window, seed, order, mode);
                         },
-                        SMORE_LINE2, K, walk_pairs(g->ctx[0], walk_steps, window));
+                        SMORE_CENSUS, K, 1.0, false,
+                        census_key("ctdne", {(double)walk_times, (double)walk_steps, (double)window, (double)K, time_window, (double)seed}));
 }
 
 int smore_group_train_walklets(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
@@ -791,7 +928,8 @@ int smore_group_train_walklets(smore_group* g, uint64_t walk_begin, uint64_t wal
                             return smore_train_walklets_async(c, b, e, walk_times, walk_steps, window_min,
                                                               window_max, K, alpha0, seed, mode);
                         },
-                        SMORE_LINE2, K, 2.0 * walk_pairs(g->ctx[0], walk_steps, window_max - window_min));
+                        SMORE_CENSUS, K, 1.0, false,
+                        census_key("walklets", {(double)walk_times, (double)walk_steps, (double)window_min, (double)window_max, (double)K, (double)seed}));
 }
 
 int smore_group_train_app(smore_group* g, uint64_t unit_begin, uint64_t unit_end, int walk_times, int sample_times,
@@ -806,7 +944,8 @@ int smore_group_train_app(smore_group* g, uint64_t unit_begin, uint64_t unit_end
                             return smore_train_app_async(c, b, e, walk_times, sample_times, jump, K, alpha0, seed,
                                                          order, mode);
                         },
-                        SMORE_LINE2, K, (double)sample_times);
+                        SMORE_CENSUS, K, 1.0, false,
+                        census_key("app", {(double)walk_times, (double)sample_times, jump, (double)K, (double)seed}));
 }
 
 int smore_group_train_hpe(smore_group* g, uint64_t begin, uint64_t count, uint64_t total, int walk_steps, int K,
@@ -818,7 +957,8 @@ int smore_group_train_hpe(smore_group* g, uint64_t begin, uint64_t count, uint64
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_hpe_async(c, b, e - b, total, walk_steps, K, reg, alpha0, seed, mode);
                         },
-                        SMORE_LINE2, K, (double)walk_steps);
+                        SMORE_CENSUS, K, 1.0, false,
+                        census_key("hpe", {(double)walk_steps, (double)K, (double)total, (double)seed}));
 }
 
 }  // extern "C"

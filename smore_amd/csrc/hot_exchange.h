@@ -21,4 +21,9 @@ hipError_t launch_delta_cycle_rows(float* T, float* S, float* D, float* R, const
                                    int dpad, int cus, hipStream_t st);
 hipError_t launch_hot_unpack(float* T, float* S, const int32_t* idx, uint64_t n, int dpad, const float* P,
                              const float* R, int cus, hipStream_t st);
+// the all-reduce of a group whose replicas share one device (exchange.cpp
+// local collectives): every bufs[r] (n floats, n % 4 == 0, 16-B aligned)
+// becomes sum_r bufs[r], added in replica order; nrep <= LOCAL_MAX
+constexpr int LOCAL_MAX = 64;
+hipError_t launch_local_sum(float* const* bufs, int nrep, uint64_t n, int cus, hipStream_t st);
 }  // namespace smore

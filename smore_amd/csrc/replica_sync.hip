@@ -135,6 +135,33 @@ static unsigned stream_grid(uint64_t n4, int cus) {
     return (unsigned)(want < cap ? (want ? want : 1) : cap);
 }
 
+// row census: the rows each record would update (smore_census_begin; the walk
+// models' adaptive exchange scales).  One record per thread.
+__global__ void __launch_bounds__(256) row_census_kernel(const int32_t* __restrict__ rec, uint64_t n,
+                                                         const uint64_t* count_dev, int RW, int K,
+                                                         unsigned long long* cw, unsigned long long* cc) {
+    const uint64_t cnt = count_dev ? *count_dev : n;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const int32_t* r = rec + i * (uint64_t)RW;
+        const int32_t w0 = r[0], w1 = r[1];
+        if (w1 < 0) continue;
+        atomicAdd(cw + untag(w0), 1ull);
+        atomicAdd(cc + untag(w1), 1ull);
+        for (int k = 0; k < K; ++k) {
+            const int32_t x = r[2 + k];
+            if (x >= 0) atomicAdd(cc + untag(x), 1ull);
+        }
+    }
+}
+
+hipError_t launch_row_census(const int32_t* rec, uint64_t n, const uint64_t* count_dev, int RW, int K,
+                             unsigned long long* cw, unsigned long long* cc, int cus, hipStream_t st) {
+    hipLaunchKernelGGL(row_census_kernel, dim3(stream_grid(n, cus)), dim3(256), 0, st, rec, n, count_dev, RW, K, cw,
+                       cc);
+    return hipGetLastError();
+}
+
 hipError_t launch_delta_begin(const float* T, float* S, float* D, float* R, uint64_t n, int cus, hipStream_t st) {
     const uint64_t n4 = n / 4;
     hipLaunchKernelGGL(delta_begin_kernel, dim3(stream_grid(n4, cus)), dim3(256), 0, st,
@@ -180,6 +207,32 @@ hipError_t launch_hot_unpack(float* T, float* S, const int32_t* idx, uint64_t n,
     hipLaunchKernelGGL(hot_unpack_kernel, dim3(stream_grid(n4, cus)), dim3(256), 0, st, reinterpret_cast<float4*>(T),
                        reinterpret_cast<float4*>(S), idx, n4, dpad / 4, reinterpret_cast<const float4*>(P),
                        reinterpret_cast<const float4*>(R));
+    return hipGetLastError();
+}
+
+// the all-reduce of a same-device group: out = sum over the replicas' buffers
+// in replica order, written back to every buffer (16 B per lane)
+struct LocalBufs {
+    float4* p[LOCAL_MAX];
+    int n;
+};
+
+__global__ void __launch_bounds__(256) local_sum_kernel(LocalBufs b, uint64_t n4) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        float4 s = b.p[0][i];
+        for (int r = 1; r < b.n; ++r) s = add4(s, b.p[r][i]);
+        for (int r = 0; r < b.n; ++r) b.p[r][i] = s;
+    }
+}
+
+hipError_t launch_local_sum(float* const* bufs, int nrep, uint64_t n, int cus, hipStream_t st) {
+    if (nrep < 1 || nrep > LOCAL_MAX || (n & 3)) return hipErrorInvalidValue;
+    LocalBufs b{};
+    for (int r = 0; r < nrep; ++r) b.p[r] = reinterpret_cast<float4*>(bufs[r]);
+    b.n = nrep;
+    const uint64_t n4 = n / 4;
+    hipLaunchKernelGGL(local_sum_kernel, dim3(stream_grid(n4, cus)), dim3(256), 0, st, b, n4);
     return hipGetLastError();
 }
 

@@ -138,6 +138,16 @@ hipError_t launch_hpe_records(const DevGraph& g, const HpeArgs& p, uint64_t seed
 hipError_t launch_app_records(const DevGraph& g, const AppArgs& p, uint64_t seed, int K, double alpha0, int32_t* rec,
                               hipStream_t st);
 constexpr int APP_MAX_STEPS = 1 << 24;   // jumping-walk bound (oracle APP_MAX_STEPS)
+// caller-supplied pairs (smore_train_pairs): pairs per RNG unit (oracle ORC_PAIR_BLOCK)
+constexpr uint64_t PAIR_BLOCK = (uint64_t)1 << 20;
+hipError_t launch_caller_pairs(const DevGraph& g, const int32_t* pv, const int32_t* pc, uint64_t n, uint64_t first,
+                               int K, float alpha, uint64_t seed, uint64_t unit0, int go, int tagged, int32_t* rec,
+                               hipStream_t st);
+// row census (smore_census_begin): per record +1 at W[word 0] and at C[word 1]
+// and C[each negative >= 0]; records whose word 1 is negative (HPE's skipped
+// samples and finished walks) count nothing.  count_dev: the count on the device
+hipError_t launch_row_census(const int32_t* rec, uint64_t n, const uint64_t* count_dev, int RW, int K,
+                             unsigned long long* cw, unsigned long long* cc, int cus, hipStream_t st);
 // edge kernel instantiations, one per (scatter mode s/a/h, KMAX) (train_edge_*.hip)
 #define SMORE_DECL_EDGE(name)                                                   \
     hipError_t launch_edge_##name(const EdgeArgs& a, int grid, hipStream_t st); \

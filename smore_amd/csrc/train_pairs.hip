@@ -328,4 +328,68 @@ hipError_t launch_hpe_records(const DevGraph& g, const HpeArgs& p, uint64_t seed
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- caller pairs
+// proNet::UpdatePairs (src/proNet.cpp:2741-2753) / Go (*ProNet).UpdatePairs
+// (pkg/pronet/optimizer.go:8-18) over caller-supplied pairs: one record per
+// pair, {v | W tag, c | C tag, n_1 .. n_K, -1 .., alpha bits at 2 + KMAX}, for
+// the pair kernels.  Pair i (of the call; this launch holds pairs first ..
+// first + n) draws its K negatives (index, then p) from stream 3, unit
+// unit0 + i / PAIR_BLOCK, slots 2K (i % PAIR_BLOCK) + 2j, +1 (the oracle's
+// orc_update_pairs).  go: the Go record form (go_pair_emit_kernel: untagged W
+// row, the C tag only when `tagged`).
+template <int KMAX>
+__global__ void __launch_bounds__(256) caller_pair_kernel(DevGraph g, const int32_t* __restrict__ pv,
+                                                          const int32_t* __restrict__ pc, uint64_t n, uint64_t first,
+                                                          int K, float alpha, uint64_t seed, uint64_t unit0, int go,
+                                                          int tagged, int32_t* rec) {
+    constexpr int RW = rec_width(KMAX);
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const uint64_t i = first + t;
+    WalkWords wd{seed, unit0 + i / PAIR_BLOCK};
+    wd.stream = 3;
+    const uint32_t base = 2u * (uint32_t)K * (uint32_t)(i % PAIR_BLOCK);
+    const int32_t v = pv[t], c = pc[t];
+    int32_t x[RW];
+    if (go) {
+        x[0] = v;
+        x[1] = tagged ? (int32_t)(c | ((g.ntab[c].y >> 31) << 30)) : c;
+    } else {
+        x[0] = v | (int32_t)((g.vtab[v].y >> 31) << 30);
+        x[1] = c | (int32_t)((g.ntab[c].y >> 31) << 30);
+    }
+#pragma unroll
+    for (int q = 0; q < RW - 2; ++q) x[2 + q] = -1;
+#pragma unroll
+    for (int q = 0; q < KMAX; ++q) {
+        if (q < K) {
+            const uint32_t ki = wd(base + 2u * (uint32_t)q), kp = wd(base + 2u * (uint32_t)q + 1u);
+            const uint32_t ni = draw_index(ki, g.V);
+            const int32_t id = alias_pick(ni, g.ntab[ni], kp);
+            x[2 + q] = go && !tagged ? untag(id) : id;
+        }
+    }
+    x[2 + KMAX] = __float_as_int(alpha);
+    i32x4* o = reinterpret_cast<i32x4*>(rec + t * RW);
+#pragma unroll
+    for (int q = 0; q < RW / 4; ++q) {
+        const i32x4 y = {x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]};
+        __builtin_nontemporal_store(y, o + q);
+    }
+}
+
+hipError_t launch_caller_pairs(const DevGraph& g, const int32_t* pv, const int32_t* pc, uint64_t n, uint64_t first,
+                               int K, float alpha, uint64_t seed, uint64_t unit0, int go, int tagged, int32_t* rec,
+                               hipStream_t st) {
+    const int block = 256;
+    const dim3 grid((unsigned)((n + block - 1) / block));
+    if (kmax_of(K) == 5)
+        hipLaunchKernelGGL(caller_pair_kernel<5>, grid, dim3(block), 0, st, g, pv, pc, n, first, K, alpha, seed, unit0,
+                           go, tagged, rec);
+    else
+        hipLaunchKernelGGL(caller_pair_kernel<10>, grid, dim3(block), 0, st, g, pv, pc, n, first, K, alpha, seed,
+                           unit0, go, tagged, rec);
+    return hipGetLastError();
+}
+
 }  // namespace smore

@@ -193,6 +193,26 @@ class ProNet:
                                            int(walk_steps), int(window), int(K), float(alpha0), int(seed),
                                            ptr(order), _lib.MODE[mode]), "train_deepwalk")
 
+    def train_pairs(self, v, c, K, alpha, seed, unit=0, mode="hogwild"):
+        """UpdatePairs (src/proNet.cpp:2741-2753; Go pkg/pronet/optimizer.go:8-18)
+        over caller-supplied pairs (v[i], c[i]) in order, fixed alpha; pair i's
+        negatives from stream 3, unit `unit` + i // 2^20 (smore_train_pairs)."""
+        v = np.ascontiguousarray(v, np.int32)
+        c = np.ascontiguousarray(c, np.int32)
+        if v.shape != c.shape:
+            raise ValueError("v and c must have the same length")
+        self._chk(lib.smore_train_pairs(self.ctx, ptr(v), ptr(c), len(v), int(K), float(alpha), int(seed), int(unit),
+                                        _lib.MODE[mode]), "train_pairs")
+
+    def census_begin(self):
+        """Row census: the following walk-model calls count the rows their
+        records would update instead of training (smore_census_begin)."""
+        self._chk(lib.smore_census_begin(self.ctx), "census_begin")
+
+    def census_end(self, units):
+        """End the census: counts / units = row_rates("census", ...)."""
+        self._chk(lib.smore_census_end(self.ctx, float(units)), "census_end")
+
     def set_temporal_edges(self, src, dst, ts):
         """Timestamped edges (pkg/temporal OutEdges) for CTDNE."""
         src = np.ascontiguousarray(src, np.int32)

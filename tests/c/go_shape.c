@@ -12,7 +12,9 @@
  * int64 ntypes, int32 type[V], int64 npaths, total, int32 lens[npaths],
  * paths[total]; CTDNE (model -4, ctdne_hip.go: NewHIPEdges, SetTemporalEdges,
  * TrainCTDNE): double time_window, int64 Et, int32 tsrc[Et], tdst[Et], double
- * ts[Et].  output: double W[V*dim], C[V*dim] (C = C0 when not trained). */
+ * ts[Et]; UpdatePairs (model -5, hip.go updatePairsHIP: NewHIP on one GPU,
+ * BeginPairs, Pairs, EndPairs): int64 n, uint64 unit, int32 v[n], c[n].
+ * output: double W[V*dim], C[V*dim] (C = C0 when not trained). */
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -64,7 +66,7 @@ int main(int argc, char** argv) {
     double* T[2] = {rd(f, 8 * V * dim), rd(f, 8 * V * dim)};
     int64_t walk_times = 0, walk_steps = 0, window = 0, n_order = 0;
     int64_t* order = NULL;
-    if (model < 0) {
+    if (model < 0 && model != -5) {
         walk_times = rd64(f);
         walk_steps = rd64(f);
         window = rd64(f);
@@ -83,6 +85,15 @@ int main(int argc, char** argv) {
         ptotal = rd64(f);
         plens = rd(f, 4 * npaths);
         paths = rd(f, 4 * ptotal);
+    }
+    int64_t npairs = 0;
+    uint64_t unit = 0;
+    int32_t *pv = NULL, *pc = NULL;
+    if (model == -5) {
+        npairs = rd64(f);
+        if (fread(&unit, 8, 1, f) != 1) return 3;
+        pv = rd(f, 4 * npairs);
+        pc = rd(f, 4 * npairs);
     }
     if (model == -4) {
         if (fread(&twin, 8, 1, f) != 1) return 3;
@@ -113,7 +124,9 @@ int main(int argc, char** argv) {
         CHECK("set_table", smore_set_table(c0, t, buf, V, (int)dim));
     }
     CHECK("broadcast", smore_group_broadcast_tables(G));
-    if (model >= 0) {
+    if (model == -5) {   /* Pairs: smore_train_pairs on replica 0 with the session's seed and mode */
+        CHECK("train_pairs", smore_train_pairs(c0, pv, pc, npairs, (int)K, ad[0], seed, unit, (int)mode));
+    } else if (model >= 0) {
         const uint64_t step = ((uint64_t)1 << 27) * (uint64_t)gpus;
         for (uint64_t done = 0; done < (uint64_t)total;) {
             uint64_t n = (uint64_t)total - done;

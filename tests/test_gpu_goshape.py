@@ -21,7 +21,8 @@ pytestmark = pytest.mark.gpu
 BIN = os.path.join(ROOT, "tests", "c", "go_shape")
 SEED = 4242
 SERIAL, ATOMIC = 2, 1
-MODEL = {"line2": 0, "line1": 1, "bpr": 3, "deepwalk": -1, "node2vec": -2, "metapath2vec": -3, "ctdne": -4}
+MODEL = {"line2": 0, "line1": 1, "bpr": 3, "deepwalk": -1, "node2vec": -2, "metapath2vec": -3, "ctdne": -4,
+         "pairs": -5}
 
 
 def _shim_inputs(g):
@@ -180,3 +181,30 @@ def test_go_shim_ctdne_serial_bit_exact(tmp_path):
     orc.go_ctdne_f32(g, s, d, ts, twin, Wr, Cr, dim, times, steps, window, K, 0.025, SEED, order)
     np.testing.assert_array_equal(W.astype(np.float32), Wr[:, :dim])
     np.testing.assert_array_equal(C.astype(np.float32), Cr[:, :dim])
+
+
+@pytest.mark.parametrize("mode", [SERIAL, ATOMIC])
+def test_go_shim_update_pairs(tmp_path, mode):
+    """(*ProNet).UpdatePairs under -tags smore_hip (hip.go updatePairsHIP ->
+    BeginPairs, Pairs = smore_train_pairs, EndPairs): in serial mode bit-exact
+    with the oracle's Go UpdatePair over the caller's pairs (negatives skipped
+    when equal to the context, deferred context); atomic mode (Hogwild order)
+    finite and within 5 % of it (relative Frobenius norm of the tables)."""
+    g = orc.GoGraph.from_file(os.path.join(GOLDEN, "pl100w.txt"), 1)
+    dim, K, unit = 24, 5, 1 << 40
+    rng = np.random.default_rng(5)
+    v = np.repeat(rng.integers(0, g.V, 1000), 4).astype(np.int32)
+    c = rng.integers(0, g.V, 4000).astype(np.int32)
+    c[::17] = v[::17]
+    W0, C0 = _tables(g.V, dim, 77)
+    extra = struct.pack("<qQ", len(v), unit) + v.tobytes() + c.tobytes()
+    W, C = _run(tmp_path, g, "pairs", dim, K, 0, mode, 0.025, 0.0, W0, C0, extra=extra)
+    Wo, Co = _padded(W0, dim), _padded(C0, dim)
+    orc.update_pairs_f32(g, Wo, Co, dim, v, c, K, 0.025, SEED, unit, go=True)
+    if mode == SERIAL:
+        np.testing.assert_array_equal(W.astype(np.float32), Wo[:, :dim])
+        np.testing.assert_array_equal(C.astype(np.float32), Co[:, :dim])
+    else:
+        assert np.isfinite(W).all() and np.isfinite(C).all()
+        for T, R in ((W, Wo[:, :dim]), (C, Co[:, :dim])):
+            assert np.linalg.norm(T - R) <= 0.05 * np.linalg.norm(R), np.linalg.norm(T - R) / np.linalg.norm(R)

@@ -271,3 +271,80 @@ def test_source_partition_draws(smore):
         assert (np.abs(got - expect) < 5.5 * sigma + 1e-5).all(), p
     pn.set_source_partition(1, 0)
     np.testing.assert_array_equal(pn.sample_edges("line2", 0, 200_000, 5, SEED), draws0)
+
+
+def _local_group(smore, n, dim=32, path=PL1K):
+    g = smore.Group([0] * n)
+    g.LoadEdgeList(path, 1)
+    g.alloc_tables(dim, 2)
+    g.primary.init_table_glibc(0, 0)
+    g.primary.zero_table(1)
+    g.broadcast_tables()
+    return g
+
+
+def test_local_group_rejects_mixed_devices(smore):
+    """A group is either one RCCL rank per distinct GPU or N replicas on one
+    GPU (local collectives); a partly repeated device list is refused."""
+    with pytest.raises(smore._lib.SmoreError):
+        smore.Group([0, 0, 1])
+
+
+@pytest.mark.parametrize("rule", ["adaptive", "sum"])
+def test_local_group_partition_every_replica_trains(smore, rule):
+    """a group call whose count is below per * N (the CLIs
+    call 2^26 per GPU against the default per of 2^27) must give every replica
+    a share -- with the source partition a replica without samples leaves its
+    part's W rows untrained.  And the sum rule's hub-row exchange must only
+    touch the exchanged table (C): W is not snapshotted under the partition.
+    Four replicas on cuda:0 (the group's local collectives): every part's W
+    rows move, the replicas agree, and the held-out loss is within 3 % of one
+    context that ran all samples."""
+    n, total = 4, 400_000
+    g = _local_group(smore, n)
+    W0 = g.primary.get_table(0)
+    g.train_edges("line2", 0, total, total, 5, 0.025, 0.0, SEED, "atomic", mean=rule)
+    Ws = [r.get_table(0) for r in g.replicas]
+    Cs = [r.get_table(1) for r in g.replicas]
+    for r in range(1, n):
+        np.testing.assert_array_equal(Ws[r], Ws[0])          # W gathered from the owners
+        np.testing.assert_allclose(Cs[r], Cs[0], atol=2e-5, rtol=0)
+    b = g.primary.source_parts(n)
+    off, _ = g.primary.csr()
+    moved = np.any(Ws[0] != W0, axis=1) | (np.diff(off) == 0)
+    for p in range(n):
+        assert moved[b[p]:b[p + 1]].mean() > 0.95, (p, moved[b[p]:b[p + 1]].mean())
+    g.close()
+    one = _fresh(smore)
+    one.alloc_tables(32, 2)
+    one.init_table_glibc(0, 0)
+    one.zero_table(1)
+    one.train_edges("line2", 0, total, total, 5, 0.025, 0.0, SEED, "atomic")
+    held = orc.sample_line(orc.Graph.from_file(PL1K, 1), SEED + 7, 0, 50_000, 5)
+    l1 = _heldout_loss(one.get_table(0), one.get_table(1), held)
+    ln = _heldout_loss(Ws[0], Cs[0], held)
+    assert np.isfinite(ln) and ln <= 1.03 * l1, (l1, ln)
+
+
+def test_local_group_rounds_split_the_range(smore):
+    """The rounds cover [begin, end) exactly once: a serial-mode group of one
+    replica equals one context (unchanged), and with N replicas the union of
+    the slices is the call's range -- checked through the census, which
+    counts exactly the records the calls generate."""
+    g = _local_group(smore, 3)
+    V = g.primary.MAX_vid
+    order = smore.deepwalk_order(V, 2, 0)
+    one = _fresh(smore)
+    one.alloc_tables(32, 2)
+    one.census_begin()
+    one.train_deepwalk(0, 2 * V, 2, 10, 3, 2, 0.025, SEED, order, "atomic")
+    one.census_end(2 * V)
+    ref_w = one.row_rates("census", 2, 0)
+    # the group's own census (first round of the call) and the call itself
+    g.train_deepwalk(0, 2 * V, 2, 10, 3, 2, 0.025, SEED, order, "atomic", per=100)
+    for r in g.replicas[1:]:
+        np.testing.assert_allclose(r.get_table(0), g.primary.get_table(0), atol=2e-5, rtol=0)
+    got = g.primary.row_rates("census", 2, 0)
+    # the group censused its first 2^16 walks (here: the whole call)
+    np.testing.assert_allclose(got, ref_w, rtol=0, atol=1e-12)
+    g.close()
