@@ -672,7 +672,10 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
             a.K = K;
         }
     }
-    const bool combine = mode == SMORE_HYBRID && (go || model != SMORE_BPR);
+    // C++ BPR combines its hub rows only with SMORE_BPR_COMBINE=1 (measured in
+    // the hub items are positives, the negatives are uniform)
+    const char* bpr_comb = getenv("SMORE_BPR_COMBINE");
+    const bool combine = mode == SMORE_HYBRID && (go || model != SMORE_BPR || (bpr_comb && atoi(bpr_comb) != 0));
     a.sh_rows = combine ? std::min(c->sh_max, 8192 / std::max(1, c->dpad)) : 0;   // LDS bound for the grid
     const int grid = edge_grid(c, a, false, go ? 1 : 0);
     if (mode == SMORE_HYBRID) {

@@ -355,11 +355,14 @@ __device__ __forceinline__ void sgd_update(const EdgeArgs& a, const float* s_sig
 // ------------------------------------------------------------------ BPR update
 // UpdateBPRPair (src/proNet.cpp:1406-1455), one shared table, 5 rounds, on
 // rows gathered by gather_rows: wv = W[u], rows[0] = W[i], rows[1+n] = W[j_n].
+// Hybrid: rows in the block's write-combined set (sh, the hottest hot rows)
+// are read as HBM value + this block's pending delta and add their delta in
+// LDS; the block drains them every sh_flush rounds (sh_drain).
 template <int G, int M, int KMAX, int MODE>
 __device__ __forceinline__ void bpr_update_rows(const EdgeArgs& a, const float* s_sig, int lane,
                                                 const bool (&ev)[M], int32_t u, const int32_t (&idc)[KMAX + 1],
                                                 bool hotu, const bool (&hotc)[KMAX + 1], float alpha,
-                                                float (&wv)[M], float (&rows)[KMAX + 1][M]) {
+                                                float (&wv)[M], float (&rows)[KMAX + 1][M], const ShState& sh) {
     static_assert(KMAX == 5, "BPR: 5 rounds");
     constexpr int NS = 7;
     const int dpad = a.dpad;
@@ -377,6 +380,23 @@ __device__ __forceinline__ void bpr_update_rows(const EdgeArgs& a, const float* 
         hot[1 + k] = hotc[k];
 #pragma unroll
         for (int m = 0; m < M; ++m) row[1 + k][m] = rows[k][m];
+    }
+    int slot[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) slot[k] = -1;
+    if constexpr (MODE == MODE_HYBRID) {
+        if (sh.n > 0) {
+#pragma unroll
+            for (int k = 0; k < NS; ++k) {
+                if (hot[k]) slot[k] = sh_lookup(sh.hash, id[k]);
+                if (slot[k] >= 0) {
+                    const float* pp = sh.pend + slot[k] * dpad;
+#pragma unroll
+                    for (int m = 0; m < M; ++m)
+                        if (ev[m]) row[k][m] += pp[elem_off<G>(lane, m)];
+                }
+            }
+        }
     }
 #pragma unroll
     for (int k = 1; k < NS; ++k)
@@ -452,7 +472,18 @@ _Pragma("unroll") for (int k2 = 0; k2 < NS; ++k2) if (k2 != (K_) && id[k2] == id
                 float dd[M];
 #pragma unroll
                 for (int m = 0; m < M; ++m) dd[m] = row[k][m] - orig[DELTA ? k : 0][m];
-                atomic_row<G, M>(q, dd, lane, dpad);
+                int sk = -1;
+#pragma unroll
+                for (int k2 = 0; k2 < NS; ++k2)
+                    if (id[k2] == id[k] && slot[k2] >= 0) sk = slot[k2];
+                if (MODE == MODE_HYBRID && sk >= 0) {
+                    float* pq = sh.pend + sk * dpad;
+#pragma unroll
+                    for (int m = 0; m < M; ++m)
+                        if (ev[m]) atomicAdd(pq + elem_off<G>(lane, m), dd[m]);
+                } else {
+                    atomic_row<G, M>(q, dd, lane, dpad);
+                }
             } else {
                 st_row<G, M>(q, row[k], lane, ev);
             }
@@ -545,7 +576,7 @@ edge_train_kernel(EdgeArgs a) {
     auto update_rows = [&](int32_t v, const int32_t (&id)[KMAX + 1], bool hotw, const bool (&hot)[KMAX + 1],
                            float alpha, float (&wv)[M], float (&rows)[KMAX + 1][M], bool reg) {
         if constexpr (SHARED == 2) {
-            if constexpr (KMAX == 5) bpr_update_rows<G, M, KMAX, MODE>(a, s_sig, lane, ev, v, id, hotw, hot, alpha, wv, rows);
+            if constexpr (KMAX == 5) bpr_update_rows<G, M, KMAX, MODE>(a, s_sig, lane, ev, v, id, hotw, hot, alpha, wv, rows, sh);
         } else {
             sgd_update_rows<G, M, KMAX, MODE, SHARED, true, true>(a, s_sig, lane, ev, v, id, hotw, hot, alpha, shared,
                                                                   mf, sh, wv, rows, reg);
@@ -680,7 +711,8 @@ edge_train_kernel(EdgeArgs a) {
                         gather_rows<G, M, KMAX>(a, lane, ev, xa.v(), id, shared, wva, rowsa);
                         if constexpr (KMAX == 5)
                             bpr_update_rows<G, M, KMAX, MODE>(a, s_sig, lane, ev, xa.v(), id,
-                                                              scatter_atomic<MODE>(xa.w[0]), hot, xa.alpha, wva, rowsa);
+                                                              scatter_atomic<MODE>(xa.w[0]), hot, xa.alpha, wva, rowsa,
+                                                              sh);
                     }
                     maybe_flush();
                 }

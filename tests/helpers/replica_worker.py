@@ -9,6 +9,12 @@ TEST INFRASTRUCTURE.
 HOT_ROWS > 0 (sum rule): the hub-row exchange after each of LAUNCHES
 launches per step (ReplicaSync.hot).  SYNC: sum (default), mean, adaptive or
 adaptive:C0 (bench.py's N > 1 default is adaptive:64); 0 / 1 = sum / mean.
+
+MODEL deepwalk (argv 10): TOTAL walks of DeepWalk (walk_times = TOTAL / V,
+40 steps, window 5, K 5) in STEPS exchanges per rank; the adaptive rule's row
+rates come from a row census (smore_census_begin / _end) of the first
+round's walks, ReplicaSync(model="census", updates = walks per rank per
+exchange) -- DESIGN.md 10.
 """
 import os
 import sys
@@ -23,6 +29,7 @@ def main():
     hot_rows = int(sys.argv[7]) if len(sys.argv) > 7 else 0
     launches = int(sys.argv[8]) if len(sys.argv) > 8 else 1
     spec = sys.argv[9] if len(sys.argv) > 9 else "sum"
+    model = sys.argv[10] if len(sys.argv) > 10 else "line2"
     spec = {"0": "sum", "1": "mean"}.get(spec, spec)
     # "+part": W partitioned by source (ReplicaSync partition=True: each rank
     # draws sources from its own part of the vertex law, only C is exchanged,
@@ -45,6 +52,30 @@ def main():
     pn.init_table_glibc(0, 0)
     pn.zero_table(1)
     per = total // world // steps
+    if model == "deepwalk":
+        V = pn.MAX_vid
+        wt = total // V
+        order = smore_amd.deepwalk_order(V, wt, 0)
+        sync = None
+        if world > 1:
+            units = min(total, max(per * world, 1 << 12))
+            pn.census_begin()
+            pn.train_deepwalk(0, units, wt, 40, 5, 5, 0.025, 20251015, order, "atomic")
+            pn.census_end(units)
+            sync = ReplicaSync(pn, sync=rule, model="census", K=5, updates=per, c0=c0)
+        for k in range(steps):
+            b = (k * world + rank) * per
+            pn.train_deepwalk(b, min(total, b + per), wt, 40, 5, 5, 0.025, 20251015, order, "atomic")
+            if sync is not None:
+                sync.begin()
+        if sync is not None:
+            sync.end()
+        torch.cuda.synchronize()
+        np.savez(out, W=pn.get_table(0), C=pn.get_table(1))
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     sync = (ReplicaSync(pn, sync=rule, hot_rows=hot_rows, model="line2", K=5, updates=per, c0=c0,
                         partition=part)
             if world > 1 else None)
