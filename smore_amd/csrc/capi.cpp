@@ -441,8 +441,28 @@ constexpr double SH_AUTO_BUDGET = 6144.0;
 // 1.0 vs 0.900 at 0.3, serial 0.906); DESIGN.md 8, profiles/r03/tau
 constexpr double HOT_TAU_EDGE = 1.0, HOT_TAU_WALK = 0.3;
 
-static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_default) {
-    const double tau = c->hot_tau >= 0 ? c->hot_tau : tau_default;
+// PAIR_FLUSH_MAX: the pair-record kernels' automatic drain interval (8 rounds,
+// the floor, instead of up to 32): a group runs a walk's consecutive records,
+// so a combined context row gathers its pending deltas in bursts; C5 DeepWalk
+// (d=128, 10 walks per vertex) held-out loss / AUC: drain 32 rounds (the edge
+// rule's choice there) 0.5648 / 0.9835 in 2.99 s, 16: 0.5444 / 0.9840 in 3.02
+// s, 8: 0.5376 / 0.9847 in 3.20 s, no combining 0.5312 / 0.9843 in 4.28 s,
+// atomic 0.5276 / 0.9844 in 6.98 s (profiles/r04/walk_combine.jsonl)
+constexpr int EDGE_FLUSH_MAX = 32, PAIR_FLUSH_MAX = 8;
+
+static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_default,
+                          int flush_max = EDGE_FLUSH_MAX) {
+    // Small graphs (the V/16 concurrency cap binds: 16 M >= V, e.g. the test
+    // graphs, never C2-C5): with the default threshold every touched row is
+    // hot and nothing is write-combined, i.e. the hybrid is the lossless
+    // atomic scatter.  There every row is a hub (920 vertices: M p ~ 0.3-3 for
+    // most rows), plain stores lose updates at any threshold (caller pairs,
+    // C++ rules: held-out loss +2.6 % at tau 0.3, +16 % at 1.0, atomic +0.06 %;
+    // profiles/r04/pairs_probe.jsonl), and the tables sit in L2, so the
+    // memory-side traffic the hybrid saves does not exist.  An explicit
+    // smore_set_hot_threshold keeps its meaning.
+    const bool small = c->hot_tau < 0 && 16.0 * (double)M >= (double)c->g->V;
+    const double tau = c->hot_tau >= 0 ? c->hot_tau : small ? 0.0 : tau_default;
     char key[128];
     const char* stale_env = getenv("SMORE_SH_STALE");
     // W rows of two-table models stay out of the write-combined set unless
@@ -453,8 +473,8 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_
     // it (1338 vs 1342 M/s), DESIGN.md 8
     const char* wrows_env = getenv("SMORE_SH_WROWS");
     const bool wrows = wrows_env && atoi(wrows_env) != 0;
-    snprintf(key, sizeof key, "%d/%d/%lld/%.9g/%d/%d/%s/%d/%d/%d", model, K, (long long)M, tau, c->sh_max,
-             c->sh_flush, stale_env ? stale_env : "", (int)wrows, c->part_n, c->part_i);
+    snprintf(key, sizeof key, "%d/%d/%lld/%.9g/%d/%d/%s/%d/%d/%d/%d", model, K, (long long)M, tau, c->sh_max,
+             c->sh_flush, stale_env ? stale_env : "", (int)wrows, c->part_n, c->part_i, flush_max);
     if (c->hot_key == key) return SMORE_OK;
     if (c->g->V >= ((int64_t)1 << 30)) return fail(c, SMORE_EINVAL, "hybrid scatter needs V < 2^30");
     std::vector<double> ps, pn, pc;
@@ -482,7 +502,7 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_
         double stale_max = SH_STALE_MAX;   // SMORE_SH_STALE overrides (tuning)
         if (const char* e = getenv("SMORE_SH_STALE")) stale_max = atof(e);
         std::vector<std::pair<double, int32_t>> r;
-        const int flush_cap = c->sh_flush > 0 ? c->sh_flush : 32;
+        const int flush_cap = c->sh_flush > 0 ? c->sh_flush : flush_max;
         for (int64_t v = 0; v < V; ++v) {
             const double p = model == SMORE_LINE2 ? pc[v] + negs * pn[v] : ps[v] + pc[v] + negs * pn[v];
             // bounded staleness: a combined row's pending deltas are invisible to
@@ -495,7 +515,8 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_
             if (wrows && model == SMORE_LINE2 && hw[v] && (double)M * ps[v] * flush_cap <= stale_max)
                 r.push_back({ps[v], (int32_t)(v | SH_WKEY)});
         }
-        const int64_t cap = std::max<int64_t>(0, std::min<int64_t>(c->sh_max, 8192 / std::max(1, c->dpad)));
+        const int64_t cap =
+            small ? 0 : std::max<int64_t>(0, std::min<int64_t>(c->sh_max, 8192 / std::max(1, c->dpad)));
         const int64_t n = std::min<int64_t>(cap, (int64_t)r.size());
         std::partial_sort(r.begin(), r.begin() + n, r.end(), [](const auto& x, const auto& y) {
             return x.first > y.first || (x.first == y.first && x.second < y.second);
@@ -1215,7 +1236,7 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
     const int ugrid = edge_grid(c, ar, false, go ? 2 : 0);
     if (mode == SMORE_HYBRID) {
         const int64_t M = (int64_t)ugrid * (256 / lanes_of(c->dpad));
-        if ((rc = build_hot_maps(c, SMORE_LINE2, K, M, HOT_TAU_WALK))) return rc;
+        if ((rc = build_hot_maps(c, SMORE_LINE2, K, M, HOT_TAU_WALK, PAIR_FLUSH_MAX))) return rc;
     }
     ar.g = dev_graph(c);
     ar.sh_rows = combine ? c->sh_rows : 0;
@@ -1438,7 +1459,7 @@ int smore_train_app_async(smore_ctx* c, uint64_t unit_begin, uint64_t unit_end, 
     const int grid = edge_grid(c, a);
     if (mode == SMORE_HYBRID) {
         const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
-        if ((rc = build_hot_maps(c, SMORE_LINE2, K, M, HOT_TAU_WALK))) return rc;
+        if ((rc = build_hot_maps(c, SMORE_LINE2, K, M, HOT_TAU_WALK, PAIR_FLUSH_MAX))) return rc;
     }
     a.g = dev_graph(c);
     a.sh_rows = combine ? c->sh_rows : 0;
@@ -1517,7 +1538,7 @@ int smore_train_hpe_async(smore_ctx* c, uint64_t begin, uint64_t count, uint64_t
     const int grid = edge_grid(c, a);
     if (mode == SMORE_HYBRID) {
         const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
-        if ((rc = build_hot_maps(c, SMORE_LINE2, K, M, HOT_TAU_WALK))) return rc;
+        if ((rc = build_hot_maps(c, SMORE_LINE2, K, M, HOT_TAU_WALK, PAIR_FLUSH_MAX))) return rc;
     }
     a.g = dev_graph(c);
     a.sh_rows = combine ? c->sh_rows : 0;
@@ -1617,7 +1638,7 @@ int smore_train_pairs(smore_ctx* c, const int32_t* v, const int32_t* cc, int64_t
     const int grid = edge_grid(c, a, false, go ? 2 : 0);
     if (mode == SMORE_HYBRID) {
         const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
-        if ((rc = build_hot_maps(c, SMORE_LINE2, K, M, HOT_TAU_WALK))) return rc;
+        if ((rc = build_hot_maps(c, SMORE_LINE2, K, M, HOT_TAU_WALK, PAIR_FLUSH_MAX))) return rc;
     }
     a.g = dev_graph(c);
     a.sh_rows = combine ? c->sh_rows : 0;

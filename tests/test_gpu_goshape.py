@@ -188,8 +188,11 @@ def test_go_shim_update_pairs(tmp_path, mode):
     """(*ProNet).UpdatePairs under -tags smore_hip (hip.go updatePairsHIP ->
     BeginPairs, Pairs = smore_train_pairs, EndPairs): in serial mode bit-exact
     with the oracle's Go UpdatePair over the caller's pairs (negatives skipped
-    when equal to the context, deferred context); atomic mode (Hogwild order)
-    finite and within 5 % of it (relative Frobenius norm of the tables)."""
+    when equal to the context, deferred context); atomic mode (Hogwild order,
+    ~240 updates per row of a 98-vertex graph, so the tables themselves differ
+    from the serial order's by tens of %) finite and training like it: the
+    pairs' logistic loss against fixed uniform negatives within 3 % of the
+    serial run's, and below the initial tables'."""
     g = orc.GoGraph.from_file(os.path.join(GOLDEN, "pl100w.txt"), 1)
     dim, K, unit = 24, 5, 1 << 40
     rng = np.random.default_rng(5)
@@ -206,5 +209,14 @@ def test_go_shim_update_pairs(tmp_path, mode):
         np.testing.assert_array_equal(C.astype(np.float32), Co[:, :dim])
     else:
         assert np.isfinite(W).all() and np.isfinite(C).all()
-        for T, R in ((W, Wo[:, :dim]), (C, Co[:, :dim])):
-            assert np.linalg.norm(T - R) <= 0.05 * np.linalg.norm(R), np.linalg.norm(T - R) / np.linalg.norm(R)
+        negs = np.random.default_rng(6).integers(0, g.V, (len(v), K))
+
+        def loss(Wt, Ct):
+            Wv = Wt[v].astype(np.float64)
+            out = np.logaddexp(0.0, -np.einsum("ij,ij->i", Wv, Ct[c].astype(np.float64)))
+            for k in range(K):
+                out += np.logaddexp(0.0, np.einsum("ij,ij->i", Wv, Ct[negs[:, k]].astype(np.float64)))
+            return float(out.mean())
+
+        l_par, l_ser, l_0 = loss(W, C), loss(Wo[:, :dim], Co[:, :dim]), loss(W0, C0)
+        assert l_ser < l_0 and l_par <= 1.03 * l_ser, (l_par, l_ser, l_0)

@@ -297,33 +297,40 @@ def test_local_group_partition_every_replica_trains(smore, rule):
     a share -- with the source partition a replica without samples leaves its
     part's W rows untrained.  And the sum rule's hub-row exchange must only
     touch the exchanged table (C): W is not snapshotted under the partition.
-    Four replicas on cuda:0 (the group's local collectives): every part's W
-    rows move, the replicas agree, and the held-out loss is within 3 % of one
-    context that ran all samples."""
-    n, total = 4, 400_000
-    g = _local_group(smore, n)
-    W0 = g.primary.get_table(0)
-    g.train_edges("line2", 0, total, total, 5, 0.025, 0.0, SEED, "atomic", mean=rule)
-    Ws = [r.get_table(0) for r in g.replicas]
-    Cs = [r.get_table(1) for r in g.replicas]
-    for r in range(1, n):
-        np.testing.assert_array_equal(Ws[r], Ws[0])          # W gathered from the owners
-        np.testing.assert_allclose(Cs[r], Cs[0], atol=2e-5, rtol=0)
-    b = g.primary.source_parts(n)
-    off, _ = g.primary.csr()
-    moved = np.any(Ws[0] != W0, axis=1) | (np.diff(off) == 0)
-    for p in range(n):
-        assert moved[b[p]:b[p + 1]].mean() > 0.95, (p, moved[b[p]:b[p + 1]].mean())
-    g.close()
+    Four replicas on cuda:0 (the group's local collectives), one call of 400k
+    samples at the default per (one round): every part's W rows move and the
+    replicas agree.  At 12k samples per replica per exchange (13 per row, the
+    C4 bench's rate) over 4 * 10^6 samples (83 rounds, the regime of
+    tools/replica_quality.py) the held-out loss is within 3 % of one context
+    that ran all samples (one round of 100k samples per replica over 920 rows,
+    or 8 such rounds, is a different regime: 1.44x / 1.16x, profiles/r04)."""
+    n = 4
+    held = orc.sample_line(orc.Graph.from_file(PL1K, 1), SEED + 7, 0, 50_000, 5)
     one = _fresh(smore)
     one.alloc_tables(32, 2)
     one.init_table_glibc(0, 0)
     one.zero_table(1)
-    one.train_edges("line2", 0, total, total, 5, 0.025, 0.0, SEED, "atomic")
-    held = orc.sample_line(orc.Graph.from_file(PL1K, 1), SEED + 7, 0, 50_000, 5)
+    one.train_edges("line2", 0, 4_000_000, 4_000_000, 5, 0.025, 0.0, SEED, "atomic")
     l1 = _heldout_loss(one.get_table(0), one.get_table(1), held)
-    ln = _heldout_loss(Ws[0], Cs[0], held)
-    assert np.isfinite(ln) and ln <= 1.03 * l1, (l1, ln)
+    for per, total in ((0, 400_000), (12_000, 4_000_000)):
+        g = _local_group(smore, n)
+        W0 = g.primary.get_table(0)
+        g.train_edges("line2", 0, total, total, 5, 0.025, 0.0, SEED, "atomic", per=per, mean=rule)
+        Ws = [r.get_table(0) for r in g.replicas]
+        Cs = [r.get_table(1) for r in g.replicas]
+        for r in range(1, n):
+            np.testing.assert_array_equal(Ws[r], Ws[0])          # W gathered from the owners
+            np.testing.assert_allclose(Cs[r], Cs[0], atol=2e-5, rtol=0)
+        b = g.primary.source_parts(n)
+        off, _ = g.primary.csr()
+        moved = np.any(Ws[0] != W0, axis=1) | (np.diff(off) == 0)
+        for p in range(n):
+            assert moved[b[p]:b[p + 1]].mean() > 0.95, (p, moved[b[p]:b[p + 1]].mean())
+        g.close()
+        ln = _heldout_loss(Ws[0], Cs[0], held)
+        assert np.isfinite(ln)
+        if per:
+            assert ln <= 1.03 * l1, (l1, ln)
 
 
 def test_local_group_rounds_split_the_range(smore):
@@ -348,3 +355,73 @@ def test_local_group_rounds_split_the_range(smore):
     # the group censused its first 2^16 walks (here: the whole call)
     np.testing.assert_allclose(got, ref_w, rtol=0, atol=1e-12)
     g.close()
+
+
+def _emulate_group_walks(g, n, per, rule, W0, C0, dim, wt, steps, window, K, alpha0, order):
+    """The group driver's rounds and one-late exchange (exchange.cpp
+    group_rounds, replica_sync.hip delta_begin / delta_cycle / delta_end,
+    local_sum) restated in fp32 numpy around the oracle's serial DeepWalk."""
+    count = wt * g.V
+    round_units = count if per > count // n else per * n
+    rounds = -(-count // round_units)
+    lo = [count * k // rounds for k in range(rounds + 1)]
+    T = [[W0.copy(), C0.copy()] for _ in range(n)]
+    S = [[W0.copy(), C0.copy()] for _ in range(n)]
+    D = [[None, None] for _ in range(n)]
+    R = [[None, None] for _ in range(n)]
+    sc = np.float32(1.0) / np.float32(n) if rule == "mean" else np.float32(1.0)
+    for k in range(rounds):
+        m = lo[k + 1] - lo[k]
+        for r in range(n):
+            b, e = lo[k] + m * r // n, lo[k] + m * (r + 1) // n
+            if e > b:
+                orc.train_deepwalk_f32(g, T[r][0], T[r][1], dim, wt, steps, window, K, alpha0, SEED, order, b, e)
+        for r in range(n):
+            for t in range(2):
+                if k > 0:                                   # end of exchange k-1 fused with begin k
+                    x = sc * R[r][t] - D[r][t]
+                    tn, sn = T[r][t] + x, S[r][t] + x
+                    T[r][t] = tn
+                    D[r][t] = tn - sn
+                else:
+                    D[r][t] = T[r][t] - S[r][t]
+                R[r][t] = D[r][t].copy()
+                S[r][t] = T[r][t].copy()
+        for t in range(2):
+            s = R[0][t].copy()
+            for r in range(1, n):
+                s = s + R[r][t]
+            for r in range(n):
+                R[r][t] = s.copy()
+    for r in range(n):
+        for t in range(2):
+            x = sc * R[r][t] - D[r][t]
+            T[r][t] = T[r][t] + x
+    return T
+
+
+@pytest.mark.parametrize("rule", ["mean", "sum"])
+def test_local_group_deepwalk_matches_emulation(smore, rule):
+    """The walk-model group path end to end in serial mode (3 replicas of
+    DeepWalk on cuda:0, 100 walks per replica per exchange, 7 rounds, the
+    hub-row exchange off): every
+    replica's tables equal an fp32 numpy restatement of the rounds, the
+    one-late exchange passes and the local all-reduce around the oracle's
+    serial DeepWalk, bit for bit."""
+    g = orc.Graph.from_file(PL1K, 1)
+    n, dim, wt, steps, window, K, alpha0 = 3, 16, 2, 10, 2, 3, 0.025
+    grp = smore.Group([0] * n)
+    grp.LoadEdgeList(PL1K, 1)
+    grp.alloc_tables(dim, 2)
+    grp.primary.init_table_glibc(0, 0)
+    grp.primary.init_table_glibc(1, g.V * dim)
+    grp.broadcast_tables()
+    grp.set_hot_exchange(0)
+    W0, C0 = grp.primary.get_table(0), grp.primary.get_table(1)
+    order = orc.deepwalk_order(g.V, wt, 0)
+    grp.train_deepwalk(0, wt * g.V, wt, steps, window, K, alpha0, SEED, order, "serial", per=100, mean=rule)
+    T = _emulate_group_walks(g, n, 100, rule, W0, C0, dim, wt, steps, window, K, alpha0, order)
+    for r in range(n):
+        np.testing.assert_array_equal(grp.replicas[r].get_table(0), T[r][0])
+        np.testing.assert_array_equal(grp.replicas[r].get_table(1), T[r][1])
+    grp.close()

@@ -76,6 +76,9 @@ def main():
     ap.add_argument("--dim", type=int, default=None)
     ap.add_argument("--seed", type=int, default=20251015)
     ap.add_argument("--no-partition", action="store_true")
+    ap.add_argument("--combine-rows", type=int, default=None, help="hybrid: LDS write-combined rows on every replica")
+    ap.add_argument("--hot-exchange", type=int, default=None, help="sum rule: hub rows synced per launch (0: off)")
+    ap.add_argument("--hot-tau", type=float, default=None, help="hybrid: hot-row threshold on every replica")
     args = ap.parse_args()
 
     import smore_amd
@@ -99,6 +102,13 @@ def main():
                 g.set_graph_edges(V, src, dst, w)
             g.alloc_tables(dim, 2)
             g.set_partition(not args.no_partition)
+            if args.hot_exchange is not None:
+                g.set_hot_exchange(args.hot_exchange)
+            for r in g.replicas:
+                if args.combine_rows is not None:
+                    r.set_write_combine(args.combine_rows)
+                if args.hot_tau is not None:
+                    r.set_hot_threshold(args.hot_tau)
             groups[n] = g
         return groups[n]
 
@@ -145,6 +155,7 @@ def main():
             spread = float(np.abs(Cl - C).max() / max(1e-30, np.abs(C).max()))
         row.update({"config": args.graph or args.config, "ranks": n, "rule": rule if n > 1 else "one",
                     "c0": c0, "period": period, "per_row": args.per_row, "mode": args.mode,
+                    "combine_rows": args.combine_rows, "hot_tau": args.hot_tau, "hot_exchange": args.hot_exchange,
                     "finite": bool(np.isfinite(W).all() and np.isfinite(C).all()),
                     "loss": round(heldout_loss(W, C, held), 5), "auc": round(edge_auc(W, C, off, tgt), 5),
                     "replica_spread_rel": spread, "wall_s": round(el, 2)})
