@@ -67,6 +67,10 @@ def parse():
     ap.add_argument("--combine-flush", type=int, default=0, help="hybrid: rounds between LDS drains (0: automatic)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
     ap.add_argument("--sync-every", type=int, default=1)
+    ap.add_argument("--exchanges-per-step", type=int, default=2,
+                    help="N > 1: the step's samples in this many launches, an exchange after each (default 2: "
+                         "6.7 samples per row per rank per exchange at C4, the best effective 8-GPU speed-up of "
+                         "the C2-scale samples-to-loss study, DESIGN.md 10)")
     ap.add_argument("--sync", default="adaptive", choices=["sum", "mean", "adaptive"],
                     help="N > 1 exchange rule: adaptive (default: per row the sum for rows with few updates per "
                          "exchange, towards the mean for the hubs), mean (model averaging) or sum (every update "
@@ -273,10 +277,11 @@ def main():
     # adaptive rule scales C's summed deltas per row
     partition = world > 1 and not args.no_partition
     c0 = args.sync_c0 if args.sync_c0 is not None else (2048.0 if partition else 64.0)
+    n_ex = max(1, args.exchanges_per_step) if world > 1 and args.sync != "sum" else 1
     sync = (ReplicaSync(pn, sync=args.sync, hot_rows=args.hot_rows, model="line2", K=args.negative,
-                        updates=args.samples * args.sync_every, c0=c0, partition=partition)
+                        updates=args.samples * args.sync_every // n_ex, c0=c0, partition=partition)
             if world > 1 else None)
-    n_launch = max(1, args.launches) if (sync is not None and sync.hot_idx) else 1
+    n_launch = max(1, args.launches) if (sync is not None and sync.hot_idx) else n_ex
     phase = [0.0, 0.0, 0]     # exposed draw ms, update ms, update launches (timed steps)
 
     S, K = args.samples, args.negative
@@ -294,8 +299,10 @@ def main():
                     phase[0] += ph[0]
                     phase[1] += ph[1]
                     phase[2] += ph[2]
-            if n_launch > 1:
+            if n_launch > 1 and sync.hot_idx:
                 sync.hot()    # the hub rows of every rank, synchronously
+            elif n_ex > 1 and j + 1 < n_launch:
+                sync.begin()  # exchanges inside the step (--exchanges-per-step)
         if sync is not None and (k + 1) % args.sync_every == 0:
             sync.begin()      # folds the previous exchange in; this one overlaps the next step
 
@@ -384,11 +391,12 @@ def main():
                                    % (args.config, "" if args.semantics == "cpp" else ", Go rules (pkg/pronet)"),
                        "vertices": V, "edge_slots": E, "dim": args.dim, "negative": K,
                        "samples_per_step_per_gpu": S, "scatter": args.mode,
-                       "sync": ("%s%s every %d steps%s%s" % (
-                           args.sync, " c0=%g" % c0 if args.sync == "adaptive" else "", args.sync_every,
+                       "sync": ("%s%s every %s%s%s" % (
+                           args.sync, " c0=%g" % c0 if args.sync == "adaptive" else "",
+                           "%d steps" % args.sync_every if n_ex == 1 else "1/%d step" % n_ex,
                            ", W partitioned by source (C exchanged, W gathered at the end)" if partition else "",
                            ", %d hub rows per table after each of %d launches per step"
-                           % (args.hot_rows, n_launch) if n_launch > 1 else ""))
+                           % (args.hot_rows, n_launch) if sync is not None and sync.hot_idx else ""))
                                if world > 1 else "none",
                        "parallelism": "replicas%d" % world},
             # achieved = updates/s x 1868 B (the whole path's algorithmic

@@ -312,8 +312,15 @@ int smore_group_set_adaptive(smore_group* g, double c0);
 /* LINE-2 group training partitions the W rows by source (default on): replica
  * r draws its sources from part r (smore_set_source_partition, left set after
  * the call), only C is exchanged, and the W parts are broadcast from their
- * owners before the call returns */
+ * owners before the call returns. */
 int smore_group_set_partition(smore_group* g, int on);
+/* the walk models (DeepWalk, Walklets, node2vec, metapath2vec, CTDNE) with
+ * W partitioned by walk center (default off: measured worse than replicated
+ * tables): every replica runs every walk of a round and trains
+ * the pairs whose center it owns (smore_walk_parts of the call's first-round
+ * census, smore_set_walk_owner; reset after the call), only C is exchanged, W
+ * is gathered from the owners.  APP and HPE always replicate both tables. */
+int smore_group_set_walk_partition(smore_group* g, int on);
 smore_ctx* smore_group_ctx(smore_group* g, int rank);
 const char* smore_group_last_error(const smore_group* g);
 int smore_group_load_edgelist(smore_group* g, const char* path, int undirected, int vertex_method,
@@ -328,14 +335,17 @@ int smore_group_set_temporal_edges(smore_group* g, int64_t E, const int32_t* src
                                    const double* ts);
 int smore_group_alloc_tables(smore_group* g, int dim, int ntables);
 int smore_group_broadcast_tables(smore_group* g);
-/* per = samples per replica per exchange (0: 2^27); mean = SMORE_SYNC_* */
+/* per = samples per replica per exchange (0: the default, 6.71 x V clamped to
+ * [2^12, 2^27]: 6.7 samples per row per replica per exchange); mean = SMORE_SYNC_* */
 int smore_group_train_edges(smore_group* g, int model, uint64_t begin, uint64_t count, uint64_t total, int K,
                             double alpha0, double reg, uint64_t seed, int mode, uint64_t per, int mean);
-/* per = walks per replica per exchange (0: 2^18) */
+/* per = walks per replica per exchange (0: the default, 4 pair updates per row
+ * per replica per exchange: 4 V / the pairs per walk of the call's row census) */
 int smore_group_train_deepwalk(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
                                int walk_steps, int window, int K, double alpha0, uint64_t seed,
                                const int64_t* order, int mode, uint64_t per, int mean);
-/* per = walks / APP units / HPE samples per replica per exchange (0: 2^18 / 2^24 / 2^24) */
+/* per = walks / APP units / HPE samples per replica per exchange (0: 4 W updates
+ * per row per replica per exchange, from the call's row census) */
 int smore_group_train_node2vec(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
                                int walk_steps, int window, int K, double alpha0, double p, double q,
                                uint64_t seed, const int64_t* order, int mode, uint64_t per, int mean);
@@ -494,6 +504,20 @@ int smore_train_pairs(smore_ctx* ctx, const int32_t* v, const int32_t* c, int64_
 #define SMORE_CENSUS 16
 int smore_census_begin(smore_ctx* ctx);
 int smore_census_end(smore_ctx* ctx, double units);
+
+/* ---- walk partition (the walk models' multi-GPU W ownership) ---------------
+ * new in this build (the reference's walk models run on one shared table:
+ * DeepWalk::Train src/model/DeepWalk.cpp:128-155).  A skip-gram pair updates
+ * W only at its center walk[i].  smore_set_walk_owner(ctx, lo, hi): the
+ * context's DeepWalk / Walklets / node2vec / metapath2vec / CTDNE calls emit
+ * only the pairs whose center is in [lo, hi) -- every pair still takes its
+ * draws, so N contexts with disjoint ranges covering [0, V) that all run the
+ * same walks train exactly the one-context records between them, each W row
+ * on one context only.  hi < 0: every pair (the default); a new graph resets.
+ * smore_walk_parts: nparts contiguous ranges of equal W-touch mass from the
+ * last row census (bounds[nparts + 1], as smore_source_parts). */
+int smore_set_walk_owner(smore_ctx* ctx, int64_t lo, int64_t hi);
+int smore_walk_parts(smore_ctx* ctx, int nparts, int64_t* bounds);
 
 /* ---- samplers (parity tests) -------------------------------------------------------- */
 /* replaces: SourceSample/TargetSample/NegativeSample (src/proNet.cpp:623-683):

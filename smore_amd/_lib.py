@@ -88,6 +88,7 @@ def _load():
         "smore_exchange_set_adaptive": (i32, [P, i32, i32, dbl, dbl]),
         "smore_group_set_adaptive": (i32, [P, dbl]),
         "smore_group_set_partition": (i32, [P, i32]),
+        "smore_group_set_walk_partition": (i32, [P, i32]),
         "smore_train_deepwalk": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, u64, P, i32]),
         "smore_train_deepwalk_async": (i32, [P, u64, u64, i32, i32, i32, i32, dbl, u64, P, i32]),
         "smore_set_temporal_edges": (i32, [P, i64, P, P, P]),
@@ -136,6 +137,8 @@ def _load():
         "smore_train_pairs": (i32, [P, P, P, i64, i32, dbl, u64, u64, i32]),
         "smore_census_begin": (i32, [P]),
         "smore_census_end": (i32, [P, dbl]),
+        "smore_set_walk_owner": (i32, [P, i64, i64]),
+        "smore_walk_parts": (i32, [P, i32, P]),
         "smore_save_weights": (i32, [P, i32, C.c_char_p, i32]),
         "smore_load_pretrain": (i32, [P, i32, C.c_char_p]),
     }

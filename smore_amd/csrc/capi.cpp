@@ -1269,6 +1269,10 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
         w.ntypes = c->ntypes;
         w.npaths = npaths;
         w.slot_extra = rule >= 3 ? 1 : 0;   // metapath2vec: the path pick; CTDNE: the start time
+        if (c->own_hi >= 0) {
+            w.own_lo = (int32_t)c->own_lo;
+            w.own_hi = (int32_t)c->own_hi;
+        }
         // walks, then their pair counts plus a zero at n: the exclusive scan's
         // entry n is the chunk's pair total, which the update kernel reads on
         // the device (no host round trip between chunks)
@@ -1708,6 +1712,32 @@ int smore_census_end(smore_ctx* c, double units) {
     }
     c->census_ok = true;
     c->census_gen++;
+    return SMORE_OK;
+}
+
+// ---------------------------------------------------------------- walk partition
+int smore_set_walk_owner(smore_ctx* c, int64_t lo, int64_t hi) {
+    if (!c) return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    if (hi < 0) {
+        c->own_lo = 0;
+        c->own_hi = -1;
+        return SMORE_OK;
+    }
+    if (lo < 0 || lo > hi || hi > c->g->V) return fail(c, SMORE_EINVAL, "walk owner range outside [0, V]");
+    c->own_lo = lo;
+    c->own_hi = hi;
+    return SMORE_OK;
+}
+
+int smore_walk_parts(smore_ctx* c, int nparts, int64_t* bounds) {
+    if (!c || !bounds || nparts < 1) return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    if (nparts > c->g->V) return fail(c, SMORE_EINVAL, "more parts than vertices");
+    if (!c->census_ok) return fail(c, SMORE_ESTATE, "walk parts need a row census (smore_census_begin / _end)");
+    std::vector<int64_t> bound;
+    source_bounds(c->census_rate[0], nparts, bound);
+    std::copy(bound.begin(), bound.end(), bounds);
     return SMORE_OK;
 }
 

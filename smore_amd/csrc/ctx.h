@@ -136,6 +136,9 @@ struct smore_ctx {
     // row census (smore_census_begin / _end): while `census` is set the record
     // paths count the rows each record would update (d_census: W, C; V
     // counters each) instead of training; census_rate = counts per unit
+    // walk partition (smore_set_walk_owner): W rows [own_lo, own_hi) owned;
+    // the walk models emit only pairs of owned centers.  own_hi < 0: all
+    int64_t own_lo = 0, own_hi = -1;
     bool census = false;
     unsigned long long* d_census[2] = {nullptr, nullptr};
     std::vector<double> census_rate[2];
@@ -203,6 +206,8 @@ inline int upload_graph(smore_ctx* c) {
     // the adaptive scales, the census rates
     c->hot_ex_key.clear();
     c->ex_scale_key.clear();
+    c->own_lo = 0;
+    c->own_hi = -1;
     c->census = false;
     c->census_ok = false;
     c->census_key.clear();

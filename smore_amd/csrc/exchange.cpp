@@ -276,6 +276,7 @@ struct smore_group {
     int launches = 8;
     double c0 = -1.0;   // adaptive exchange (smore_group_set_adaptive); -1: 2048 with the source partition, else 64
     int partition = 1;  // LINE-2: W rows partitioned by source (smore_group_set_partition)
+    int walk_partition = 0;   // walk models: W rows partitioned by walk center (smore_group_set_walk_partition)
     // every replica on one device: collectives as device passes, ordered by
     // events between the replicas' streams (no RCCL)
     bool local = false;
@@ -463,12 +464,11 @@ int group_hot_exchange(smore_group* g) {
 }
 
 // every replica gets every part's W rows from the part's owner (replica p
-// owns part p of the source partition): one in-place broadcast per part
-int gather_sources(smore_group* g) {
+// owns rows [b[p], b[p+1]): the source partition's or the walk partition's
+// parts): one in-place broadcast per part
+int gather_sources(smore_group* g, const std::vector<int64_t>& b) {
     const size_t n = g->ctx.size();
-    std::vector<int64_t> b(n + 1);
     int rc;
-    if ((rc = smore_source_parts(g->ctx[0], (int)n, b.data()))) return gfail(g, 0, rc);
     const std::vector<hipStream_t> st = compute_streams(g);
     for (size_t p = 0; p < n; ++p) {
         if (b[p + 1] <= b[p]) continue;
@@ -506,39 +506,52 @@ int group_sync(smore_group* g) {
 // trained; smore_census_begin), redone only when census_key changes.  With
 // the hub-row exchange on (sum rule), each replica's slice runs as
 // g->launches launches and the hub rows are synced after each.
+//
+// part (LINE-2): the source partition.  walkpart (the walk models whose pairs
+// come from pair_emit / go_pair_emit): the walk partition -- every replica
+// runs the whole round and trains the pairs whose center it owns
+// (smore_set_walk_owner over smore_walk_parts of the census), only C is
+// exchanged, W is gathered from the owners at the end.
+// Default exchange periods (per = 0): measured on config 2's graph for LINE-2
+// (tools/replica_study.py + tools/samples_to_loss.py: 6.7 samples per row per
+// replica per exchange gives the best effective 8-GPU speed-up, 4.4-5.4x
+// counting the exchange passes; 13.4: 3.7-5.1x) and on config 5's for
+// DeepWalk (4 pair updates per row per replica, c0 64: 1.02 / 1.07 / 1.35x
+// one replica's held-out loss at 2 / 4 / 8 replicas; 54, about the old 2^18
+// walks, drain 32: 1.09 / 1.79 / 3.75x), profiles/r04/replica
+constexpr double EDGE_PER_ROW = 6.71, EDGE_PER_MIN = 4096.0, EDGE_PER_MAX = 134217728.0, WALK_PER_ROW = 4.0;
+
 template <class F>
 static int group_rounds(smore_group* g, uint64_t begin, uint64_t end, uint64_t per, int rule, F&& run,
                         int model = SMORE_LINE2, int K = 5, double upu = 1.0, bool part = false,
-                        const std::string& census_key = std::string()) {
+                        const std::string& census_key = std::string(), bool walkpart = false) {
     const size_t n = g->ctx.size();
     int rc;
     if (end <= begin) return SMORE_OK;
     if (rule < SMORE_SYNC_SUM || rule > SMORE_SYNC_ADAPTIVE) return gfail(g, 0, fail(g->ctx[0], SMORE_EINVAL, "bad exchange rule"));
-    if (per == 0) return gfail(g, 0, fail(g->ctx[0], SMORE_EINVAL, "per == 0"));
     // LINE-2 with the source partition: replica r draws its sources from part
     // r, owns those W rows, and only C is exchanged (W gathered at the end)
     part = part && g->partition && n > 1;
+    walkpart = walkpart && !part && g->walk_partition && n > 1;
     for (size_t r = 0; r < n; ++r) {
         smore_ctx* c = g->ctx[r];
         if ((rc = smore_set_source_partition(c, part ? (int)n : 1, part ? (int)r : 0))) return gfail(g, (int)r, rc);
-        c->ex_t0 = part ? 1 : 0;
+        if ((rc = smore_set_walk_owner(c, 0, -1))) return gfail(g, (int)r, rc);
+        c->ex_t0 = part || walkpart ? 1 : 0;
         if ((rc = exchange_reset(c))) return gfail(g, (int)r, rc);
     }
     const uint64_t count = end - begin;
-    const uint64_t round_units = per > count / n ? count : per * (uint64_t)n;   // no overflow: per * n <= count
-    const uint64_t rounds = (count + round_units - 1) / round_units;
-    auto round_lo = [&](uint64_t k) { return (uint64_t)(((unsigned __int128)count * k) / rounds); };
-    const double share = (double)count / ((double)rounds * (double)n);   // units per replica per exchange
     int64_t rows = g->hot_rows < 0 ? std::min<int64_t>(65536, g->ctx[0]->g->V / 8) : g->hot_rows;
     rows = std::min<int64_t>(rows, g->ctx[0]->g->V);
     const bool hot = rule == SMORE_SYNC_SUM && rows > 0 && g->launches > 1;
-    if (model == SMORE_CENSUS && (rule == SMORE_SYNC_ADAPTIVE || hot)) {
+    const int64_t V = g->ctx[0]->g->V;
+    if (model == SMORE_CENSUS && (rule == SMORE_SYNC_ADAPTIVE || hot || walkpart || per == 0)) {
         smore_ctx* c0 = g->ctx[0];
         const std::string key = census_key + "/" + std::to_string(c0->semantics);
         if (c0->census_key != key || !c0->census_ok) {
-            // at least 2^16 units (or the call) so that the hub rows' rates are
-            // well measured on small rounds
-            const uint64_t m = std::min<uint64_t>(count, std::max<uint64_t>(round_lo(1), (uint64_t)1 << 16));
+            // the first round (or 2^16 units at least, so that the hub rows'
+            // rates are well measured on small rounds, or the call)
+            const uint64_t m = std::min<uint64_t>(count, std::max<uint64_t>(per * (uint64_t)n, (uint64_t)1 << 16));
             if ((rc = smore_census_begin(c0))) return gfail(g, 0, rc);
             rc = run(c0, begin, begin + m);
             const int rc2 = smore_census_end(c0, (double)m);
@@ -546,6 +559,29 @@ static int group_rounds(smore_group* g, uint64_t begin, uint64_t end, uint64_t p
             c0->census_key = key;
             for (size_t r = 1; r < n; ++r) g->ctx[r]->census_key.clear();
         }
+    }
+    if (per == 0) {
+        // the default exchange period, relative to the graph:
+        // edge models EDGE_PER_ROW samples per row per replica, walk models
+        // WALK_PER_ROW W updates (pairs) per row per replica, from the census
+        if (model == SMORE_CENSUS) {
+            double upr = 0.0;   // W touches (pairs) per unit
+            for (double x : g->ctx[0]->census_rate[0]) upr += x;
+            per = (uint64_t)std::max(1.0, std::round(WALK_PER_ROW * (double)V / std::max(upr, 1e-30)));
+        } else {
+            per = (uint64_t)std::min(EDGE_PER_MAX, std::max(EDGE_PER_MIN, std::round(EDGE_PER_ROW * (double)V)));
+        }
+    }
+    const uint64_t round_units = per > count / n ? count : per * (uint64_t)n;   // no overflow: per * n <= count
+    const uint64_t rounds = (count + round_units - 1) / round_units;
+    auto round_lo = [&](uint64_t k) { return (uint64_t)(((unsigned __int128)count * k) / rounds); };
+    const double share = (double)count / ((double)rounds * (double)n);   // units per replica per exchange
+    std::vector<int64_t> bounds((size_t)n + 1);
+    if (part && (rc = smore_source_parts(g->ctx[0], (int)n, bounds.data()))) return gfail(g, 0, rc);
+    if (walkpart) {
+        if ((rc = smore_walk_parts(g->ctx[0], (int)n, bounds.data()))) return gfail(g, 0, rc);
+        for (size_t r = 0; r < n; ++r)
+            if ((rc = smore_set_walk_owner(g->ctx[r], bounds[r], bounds[r + 1]))) return gfail(g, (int)r, rc);
     }
     const double c0v = g->c0 > 0 ? g->c0 : (part ? 2048.0 : 64.0);
     if (rule == SMORE_SYNC_ADAPTIVE) {
@@ -566,8 +602,9 @@ static int group_rounds(smore_group* g, uint64_t begin, uint64_t end, uint64_t p
         const uint64_t lo = round_lo(k), m = round_lo(k + 1) - lo;
         for (int j = 0; j < sub; ++j) {
             for (size_t r = 0; r < n; ++r) {
-                const uint64_t b = lo + (uint64_t)(((unsigned __int128)m * r) / n);
-                const uint64_t e = lo + (uint64_t)(((unsigned __int128)m * (r + 1)) / n);
+                // the walk partition: every replica runs the whole round (its pairs)
+                const uint64_t b = walkpart ? lo : lo + (uint64_t)(((unsigned __int128)m * r) / n);
+                const uint64_t e = walkpart ? lo + m : lo + (uint64_t)(((unsigned __int128)m * (r + 1)) / n);
                 const uint64_t bj = b + (e - b) * (uint64_t)j / sub, ej = b + (e - b) * (uint64_t)(j + 1) / sub;
                 if (ej > bj && (rc = run(g->ctx[r], begin + bj, begin + ej))) return gfail(g, (int)r, rc);
             }
@@ -577,8 +614,11 @@ static int group_rounds(smore_group* g, uint64_t begin, uint64_t end, uint64_t p
     }
     for (size_t r = 0; r < n; ++r)
         if ((rc = exchange_end(g->ctx[r]))) return gfail(g, (int)r, rc);
-    if (part && (rc = gather_sources(g))) return rc;
-    return group_sync(g);
+    if ((part || walkpart) && (rc = gather_sources(g, bounds))) return rc;
+    if ((rc = group_sync(g))) return rc;
+    for (size_t r = 0; walkpart && r < n; ++r)
+        if ((rc = smore_set_walk_owner(g->ctx[r], 0, -1))) return gfail(g, (int)r, rc);
+    return SMORE_OK;
 }
 
 // the census key of a walk-model call: the model and every argument that
@@ -742,6 +782,12 @@ int smore_group_set_partition(smore_group* g, int on) {
     return SMORE_OK;
 }
 
+int smore_group_set_walk_partition(smore_group* g, int on) {
+    if (!g) return SMORE_EINVAL;
+    g->walk_partition = on != 0;
+    return SMORE_OK;
+}
+
 int smore_group_set_hot_exchange(smore_group* g, int64_t rows, int launches) {
     if (!g || launches < 1) return SMORE_EINVAL;
     g->hot_rows = rows < 0 ? -1 : rows;
@@ -843,7 +889,7 @@ int smore_group_train_edges(smore_group* g, int model, uint64_t begin, uint64_t 
     if (!g) return SMORE_EINVAL;
     if (g->ctx.size() == 1)
         return gfail(g, 0, smore_train_edges(g->ctx[0], model, begin, count, total, K, alpha0, reg, seed, mode));
-    return group_rounds(g, begin, begin + count, sync_samples ? sync_samples : (uint64_t)1 << 27, mean,
+    return group_rounds(g, begin, begin + count, sync_samples, mean,
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_edges_async(c, model, b, e - b, total, K, alpha0, reg, seed, mode);
                         },
@@ -857,13 +903,13 @@ int smore_group_train_deepwalk(smore_group* g, uint64_t walk_begin, uint64_t wal
     if (g->ctx.size() == 1)
         return gfail(g, 0, smore_train_deepwalk(g->ctx[0], walk_begin, walk_end, walk_times, walk_steps, window, K,
                                                 alpha0, seed, order, mode));
-    return group_rounds(g, walk_begin, walk_end, sync_walks ? sync_walks : (uint64_t)1 << 18, mean,
+    return group_rounds(g, walk_begin, walk_end, sync_walks, mean,
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_deepwalk_async(c, b, e, walk_times, walk_steps, window, K, alpha0,
                                                               seed, order, mode);
                         },
                         SMORE_CENSUS, K, 1.0, false,
-                        census_key("deepwalk", {(double)walk_times, (double)walk_steps, (double)window, (double)K, (double)seed}));
+                        census_key("deepwalk", {(double)walk_times, (double)walk_steps, (double)window, (double)K, (double)seed}), true);
 }
 
 int smore_group_train_node2vec(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
@@ -873,13 +919,13 @@ int smore_group_train_node2vec(smore_group* g, uint64_t walk_begin, uint64_t wal
     if (g->ctx.size() == 1)
         return gfail(g, 0, smore_train_node2vec(g->ctx[0], walk_begin, walk_end, walk_times, walk_steps, window, K,
                                                 alpha0, p, q, seed, order, mode));
-    return group_rounds(g, walk_begin, walk_end, sync_walks ? sync_walks : (uint64_t)1 << 18, mean,
+    return group_rounds(g, walk_begin, walk_end, sync_walks, mean,
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_node2vec_async(c, b, e, walk_times, walk_steps, window, K, alpha0, p,
                                                               q, seed, order, mode);
                         },
                         SMORE_CENSUS, K, 1.0, false,
-                        census_key("node2vec", {(double)walk_times, (double)walk_steps, (double)window, (double)K, p, q, (double)seed}));
+                        census_key("node2vec", {(double)walk_times, (double)walk_steps, (double)window, (double)K, p, q, (double)seed}), true);
 }
 
 int smore_group_train_metapath2vec(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times,
@@ -890,14 +936,14 @@ int smore_group_train_metapath2vec(smore_group* g, uint64_t walk_begin, uint64_t
     if (g->ctx.size() == 1)
         return gfail(g, 0, smore_train_metapath2vec(g->ctx[0], walk_begin, walk_end, walk_times, walk_steps, window,
                                                     K, alpha0, paths, path_lens, npaths, seed, order, mode));
-    return group_rounds(g, walk_begin, walk_end, sync_walks ? sync_walks : (uint64_t)1 << 18, mean,
+    return group_rounds(g, walk_begin, walk_end, sync_walks, mean,
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_metapath2vec_async(c, b, e, walk_times, walk_steps, window, K,
                                                                   alpha0, paths, path_lens, npaths, seed, order,
                                                                   mode);
                         },
                         SMORE_CENSUS, K, 1.0, false,
-                        census_key("metapath2vec", {(double)walk_times, (double)walk_steps, (double)window, (double)K, (double)npaths, (double)seed}));
+                        census_key("metapath2vec", {(double)walk_times, (double)walk_steps, (double)window, (double)K, (double)npaths, (double)seed}), true);
 }
 
 int smore_group_train_ctdne(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
@@ -907,13 +953,13 @@ int smore_group_train_ctdne(smore_group* g, uint64_t walk_begin, uint64_t walk_e
     if (g->ctx.size() == 1)
         return gfail(g, 0, smore_train_ctdne(g->ctx[0], walk_begin, walk_end, walk_times, walk_steps, window, K,
                                              alpha0, time_window, seed, order, mode));
-    return group_rounds(g, walk_begin, walk_end, sync_walks ? sync_walks : (uint64_t)1 << 18, mean,
+    return group_rounds(g, walk_begin, walk_end, sync_walks, mean,
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_ctdne_async(c, b, e, walk_times, walk_steps, window, K, alpha0,
                                                            time_window, seed, order, mode);
                         },
                         SMORE_CENSUS, K, 1.0, false,
-                        census_key("ctdne", {(double)walk_times, (double)walk_steps, (double)window, (double)K, time_window, (double)seed}));
+                        census_key("ctdne", {(double)walk_times, (double)walk_steps, (double)window, (double)K, time_window, (double)seed}), true);
 }
 
 int smore_group_train_walklets(smore_group* g, uint64_t walk_begin, uint64_t walk_end, int walk_times, int walk_steps,
@@ -923,13 +969,13 @@ int smore_group_train_walklets(smore_group* g, uint64_t walk_begin, uint64_t wal
     if (g->ctx.size() == 1)
         return gfail(g, 0, smore_train_walklets(g->ctx[0], walk_begin, walk_end, walk_times, walk_steps, window_min,
                                                 window_max, K, alpha0, seed, mode));
-    return group_rounds(g, walk_begin, walk_end, sync_walks ? sync_walks : (uint64_t)1 << 18, mean,
+    return group_rounds(g, walk_begin, walk_end, sync_walks, mean,
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_walklets_async(c, b, e, walk_times, walk_steps, window_min,
                                                               window_max, K, alpha0, seed, mode);
                         },
                         SMORE_CENSUS, K, 1.0, false,
-                        census_key("walklets", {(double)walk_times, (double)walk_steps, (double)window_min, (double)window_max, (double)K, (double)seed}));
+                        census_key("walklets", {(double)walk_times, (double)walk_steps, (double)window_min, (double)window_max, (double)K, (double)seed}), true);
 }
 
 int smore_group_train_app(smore_group* g, uint64_t unit_begin, uint64_t unit_end, int walk_times, int sample_times,
@@ -939,7 +985,7 @@ int smore_group_train_app(smore_group* g, uint64_t unit_begin, uint64_t unit_end
     if (g->ctx.size() == 1)
         return gfail(g, 0, smore_train_app(g->ctx[0], unit_begin, unit_end, walk_times, sample_times, jump, K, alpha0,
                                            seed, order, mode));
-    return group_rounds(g, unit_begin, unit_end, sync_units ? sync_units : (uint64_t)1 << 24, mean,
+    return group_rounds(g, unit_begin, unit_end, sync_units, mean,
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_app_async(c, b, e, walk_times, sample_times, jump, K, alpha0, seed,
                                                          order, mode);
@@ -953,7 +999,7 @@ int smore_group_train_hpe(smore_group* g, uint64_t begin, uint64_t count, uint64
     if (!g) return SMORE_EINVAL;
     if (g->ctx.size() == 1)
         return gfail(g, 0, smore_train_hpe(g->ctx[0], begin, count, total, walk_steps, K, reg, alpha0, seed, mode));
-    return group_rounds(g, begin, begin + count, sync_samples ? sync_samples : (uint64_t)1 << 24, mean,
+    return group_rounds(g, begin, begin + count, sync_samples, mean,
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_hpe_async(c, b, e - b, total, walk_steps, K, reg, alpha0, seed, mode);
                         },

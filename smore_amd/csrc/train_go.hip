@@ -420,7 +420,21 @@ __device__ __forceinline__ uint32_t go_pair_count(int L, int window) {
 __global__ void __launch_bounds__(256) go_pair_count_kernel(WalkArgs w, uint32_t* count) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= w.nwalks) return;
-    count[t] = go_pair_count(w.lens[t], w.window);
+    const int L = w.lens[t];
+    if (w.own_lo <= 0 && w.own_hi == 0x7FFFFFFF) {
+        count[t] = go_pair_count(L, w.window);
+        return;
+    }
+    // the walk partition (smore_set_walk_owner): pairs of owned centers only
+    const int32_t* walk = w.walks + t * (uint64_t)(w.steps + 1);
+    uint32_t n = 0;
+    for (int i = 0; i < L; ++i) {
+        if (walk[i] < w.own_lo || walk[i] >= w.own_hi) continue;
+        const int lo = i - w.window < 0 ? 0 : i - w.window;
+        const int hi = i + w.window + 1 > L ? L : i + w.window + 1;
+        n += (uint32_t)(hi - lo - 1);
+    }
+    count[t] = n;
 }
 
 template <int KMAX>
@@ -448,8 +462,13 @@ __global__ void __launch_bounds__(256) go_pair_emit_kernel(DevGraph g, WalkArgs 
     for (int i = 0; i < L; ++i) {
         const int lo = i - w.window < 0 ? 0 : i - w.window;
         const int hi = i + w.window + 1 > L ? L : i + w.window + 1;
+        const bool own = walk[i] >= w.own_lo && walk[i] < w.own_hi;
         for (int j = lo; j < hi; ++j) {
             if (j == i) continue;
+            if (!own) {                     // another part's pair: its draws only
+                slot += 2u * (uint32_t)K;
+                continue;
+            }
             int32_t x[RW];
             x[0] = walk[i];
             // hybrid: the context's C hot bit is bit 31 of its own negative

@@ -58,6 +58,10 @@ struct WalkArgs {
     const int32_t* path_off;
     int ntypes, npaths;
     int slot_extra;                // draws before the step draws (metapath2vec: the path choice)
+    // walk partition (smore_set_walk_owner): only pairs whose center (W row)
+    // walk[i] is in [own_lo, own_hi) become records; every pair still takes
+    // its draws, so the records are the one-context records restricted
+    int32_t own_lo = 0, own_hi = 0x7FFFFFFF;
 };
 
 // APP: units [unit_begin, unit_begin + n) of walk_times * V * sample_times; unit

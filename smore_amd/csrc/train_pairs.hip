@@ -51,13 +51,22 @@ struct ScaleRanges {
     }
 };
 
+// the walk partition's filter: is walk position i's center (W row) owned?
+__device__ __forceinline__ bool center_owned(const WalkArgs& w, const int32_t* walk, int i) {
+    const int32_t v = walk[i] & ID_MASK;
+    return v >= w.own_lo && v < w.own_hi;
+}
+
 __global__ void __launch_bounds__(256) pair_count_kernel(WalkArgs w, uint64_t seed, uint32_t* count) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= w.nwalks) return;
     const int L = w.lens[t];
+    const bool all = w.own_lo <= 0 && w.own_hi == 0x7FFFFFFF;
+    const int32_t* walk = w.walks + t * (uint64_t)(w.steps + 1);
     uint32_t n = 0;
     if (w.rule == 1) {
         for (int i = 0; i < L; ++i) {
+            if (!all && !center_owned(w, walk, i)) continue;
             const ScaleRanges q(i, L, w.window_min, w.window);
             n += ScaleRanges::span(q.l0, q.r0, i) + ScaleRanges::span(q.l1, q.r1, i);
         }
@@ -67,7 +76,7 @@ __global__ void __launch_bounds__(256) pair_count_kernel(WalkArgs w, uint64_t se
         for (int i = 0; i < L; ++i) {
             const int r = (int)draw_index(wd(win_base + (uint32_t)i), (uint32_t)w.window) + 1;
             const int left = i - r < 0 ? 0 : i - r, right = i + r >= L ? L - 1 : i + r;
-            n += (uint32_t)(right - left);   // [left, right] minus i itself
+            if (all || center_owned(w, walk, i)) n += (uint32_t)(right - left);   // [left, right] minus i itself
         }
     }
     count[t] = n;
@@ -102,9 +111,14 @@ __global__ void __launch_bounds__(256) pair_emit_kernel(DevGraph g, WalkArgs w, 
             ranges[0][1] = i + r >= L ? L - 1 : i + r;
         }
         const int32_t vi = walk[i];
+        const bool own = center_owned(w, walk, i);
         for (int q = 0; q < nr; ++q)
         for (int j = ranges[q][0]; j <= ranges[q][1]; ++j) {
             if (j == i) continue;
+            if (!own) {                     // another part's pair: its draws only
+                slot += 2u * (uint32_t)K;
+                continue;
+            }
             int32_t x[RW];
             // W row walk[i] with its W tag, C row walk[j] with its C tag
             x[0] = (vi & ID_MASK) | (int32_t)((((uint32_t)vi >> 31) & 1u) << 30);

@@ -220,7 +220,13 @@ class ReplicaSync(OverlapSync):
     vertex ids (contiguous ranges of equal source mass,
     smore_set_source_partition), so each W row is updated by one rank only
     and only C is exchanged; end() then gathers W (each part broadcast from
-    its owner).  The adaptive scales come from the global law."""
+    its owner).  The adaptive scales come from the global law.
+    partition=True with model="census" (DeepWalk, Walklets, node2vec,
+    metapath2vec, CTDNE after a row census): the walk partition -- this rank
+    trains only the pairs whose center (W row) lies in its part of
+    smore_walk_parts (smore_set_walk_owner), so EVERY rank runs EVERY walk of a
+    step (the walks and draws are deterministic per walk index); only C is
+    exchanged and W is gathered the same way."""
 
     def __init__(self, pn, mean=False, tables=(0, 1), group=None, hot_rows=0, model="line2", K=5, sync=None,
                  updates=None, c0=64.0, partition=False):
@@ -232,8 +238,8 @@ class ReplicaSync(OverlapSync):
             torch.cuda.set_stream(torch.cuda.Stream())
         pn.set_stream(torch.cuda.current_stream().cuda_stream)
         if partition:
-            if model != "line2":
-                raise ValueError("source partition: LINE-2 (W rows are sources only)")
+            if model not in ("line2", "census"):
+                raise ValueError("partition: LINE-2 (sources) or a censused walk model (walk centers)")
             tables = (1,)
         T = [table_tensor(pn, w) for w in tables]
         if sync is None:
@@ -258,9 +264,13 @@ class ReplicaSync(OverlapSync):
         self.bounds = None
         if partition:
             world, rank = dist.get_world_size(group), dist.get_rank(group)
-            self.bounds = [int(b) for b in pn.source_parts(world)]
             self.W = table_tensor(pn, 0)
-            pn.set_source_partition(world, rank)
+            if model == "census":
+                self.bounds = [int(b) for b in pn.walk_parts(world)]
+                pn.set_walk_owner(self.bounds[rank], self.bounds[rank + 1])
+            else:
+                self.bounds = [int(b) for b in pn.source_parts(world)]
+                pn.set_source_partition(world, rank)
 
     def gather_sources(self):
         """Every rank gets every part's W rows from the part's owner."""

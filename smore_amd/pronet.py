@@ -325,6 +325,18 @@ class ProNet:
         """Draw sources from part `part` of `nparts` only (1 = the global law)."""
         self._chk(lib.smore_set_source_partition(self.ctx, int(nparts), int(part)), "set_source_partition")
 
+    def walk_parts(self, nparts):
+        """Bounds (nparts + 1, int64) of contiguous vertex parts of equal W-touch
+        mass under the last row census (smore_walk_parts)."""
+        b = np.zeros(int(nparts) + 1, np.int64)
+        self._chk(lib.smore_walk_parts(self.ctx, int(nparts), b.ctypes.data_as(C.c_void_p)), "walk_parts")
+        return b
+
+    def set_walk_owner(self, lo, hi=-1):
+        """Walk models train only the pairs whose center is in [lo, hi)
+        (smore_set_walk_owner; hi < 0: every pair)."""
+        self._chk(lib.smore_set_walk_owner(self.ctx, int(lo), int(hi)), "set_walk_owner")
+
     def synchronize(self):
         self._chk(lib.smore_synchronize(self.ctx), "synchronize")
 
@@ -473,6 +485,11 @@ class Group:
     def set_partition(self, on=True):
         """smore_group_set_partition: LINE-2 W rows partitioned by source (default on)."""
         self._chk(lib.smore_group_set_partition(self.g, int(bool(on))), "set_partition")
+
+    def set_walk_partition(self, on=True):
+        """smore_group_set_walk_partition: walk-model W rows partitioned by walk
+        center (default off)."""
+        self._chk(lib.smore_group_set_walk_partition(self.g, int(bool(on))), "set_walk_partition")
 
     def set_hot_exchange(self, rows=-1, launches=8):
         """smore_group_set_hot_exchange: hub rows per table synced after every

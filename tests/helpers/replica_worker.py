@@ -14,7 +14,8 @@ MODEL deepwalk (argv 10): TOTAL walks of DeepWalk (walk_times = TOTAL / V,
 40 steps, window 5, K 5) in STEPS exchanges per rank; the adaptive rule's row
 rates come from a row census (smore_census_begin / _end) of the first
 round's walks, ReplicaSync(model="census", updates = walks per rank per
-exchange) -- DESIGN.md 10.
+exchange) -- DESIGN.md 10.  SYNC "...+part": the walk partition (every rank
+runs every walk, trains the pairs of its own centers; only C exchanged).
 """
 import os
 import sys
@@ -62,10 +63,12 @@ def main():
             pn.census_begin()
             pn.train_deepwalk(0, units, wt, 40, 5, 5, 0.025, 20251015, order, "atomic")
             pn.census_end(units)
-            sync = ReplicaSync(pn, sync=rule, model="census", K=5, updates=per, c0=c0)
+            sync = ReplicaSync(pn, sync=rule, model="census", K=5, updates=per, c0=c0, partition=part)
         for k in range(steps):
-            b = (k * world + rank) * per
-            pn.train_deepwalk(b, min(total, b + per), wt, 40, 5, 5, 0.025, 20251015, order, "atomic")
+            # walk partition: every rank runs the step's walks (its pairs only)
+            b = k * world * per if part else (k * world + rank) * per
+            e = b + per * world if part else b + per
+            pn.train_deepwalk(b, min(total, e), wt, 40, 5, 5, 0.025, 20251015, order, "atomic")
             if sync is not None:
                 sync.begin()
         if sync is not None:

@@ -425,3 +425,132 @@ def test_local_group_deepwalk_matches_emulation(smore, rule):
         np.testing.assert_array_equal(grp.replicas[r].get_table(0), T[r][0])
         np.testing.assert_array_equal(grp.replicas[r].get_table(1), T[r][1])
     grp.close()
+
+
+@pytest.mark.parametrize("sem", ["cpp", "go"])
+def test_walk_owner_splits_the_records(smore, sem):
+    """smore_set_walk_owner: the pairs of N disjoint center ranges covering
+    [0, V) are exactly the one-context pairs -- the row census of each part
+    (W at the center, C at the context and every negative) sums to the
+    unfiltered census, and a part's W counts vanish outside its range."""
+    pn = smore.ProNet(0)
+    pn.LoadEdgeList(PL1K, 1)
+    if sem == "go":
+        pn.set_semantics("go")
+    pn.alloc_tables(16, 2)
+    V = pn.MAX_vid
+    wt, units = 2, 2 * pn.MAX_vid
+    order = smore.deepwalk_order(V, wt, 0)
+
+    def census(lo, hi):
+        pn.set_walk_owner(lo, hi)
+        pn.census_begin()
+        pn.train_deepwalk(0, units, wt, 10, 3, 2, 0.025, SEED, order, "atomic")
+        pn.census_end(1.0)                   # raw counts
+        return pn.row_rates("census", 2, 0), pn.row_rates("census", 2, 1)
+
+    w_all, c_all = census(0, -1)
+    b = pn.walk_parts(3)
+    assert b[0] == 0 and b[-1] == V and np.all(np.diff(b) > 0)
+    w_sum, c_sum = np.zeros(V), np.zeros(V)
+    for r in range(3):
+        w, c = census(b[r], b[r + 1])
+        assert w[:b[r]].sum() == 0 and w[b[r + 1]:].sum() == 0
+        np.testing.assert_array_equal(w[b[r]:b[r + 1]], w_all[b[r]:b[r + 1]])
+        w_sum += w
+        c_sum += c
+    np.testing.assert_array_equal(w_sum, w_all)
+    np.testing.assert_array_equal(c_sum, c_all)
+    pn.set_walk_owner(0, -1)
+
+
+def test_local_group_walk_partition(smore):
+    """The group's walk partition (DeepWalk, 4 replicas on cuda:0, opt-in):
+    every replica ends with identical W (gathered from the owners) and C
+    within float rounding, and the held-out LINE objective is within 10 % of
+    one context that ran every walk (the partition trains worse than
+    replicated tables; measured 1.08x here)."""
+    g = orc.Graph.from_file(PL1K, 1)
+    dim, wt, K = 32, 10, 5
+    order = orc.deepwalk_order(g.V, wt, 0)
+    held = orc.sample_line(g, SEED + 7, 0, 50_000, 5)
+
+    def init(p):
+        p.alloc_tables(dim, 2)
+        p.init_table_glibc(0, 0)
+        p.init_table_glibc(1, g.V * dim)
+
+    one = smore.ProNet(0)
+    one.LoadEdgeList(PL1K, 1)
+    init(one)
+    one.train_deepwalk(0, wt * g.V, wt, 40, 5, K, 0.025, SEED, order, "atomic")
+    l1 = _heldout_loss(one.get_table(0), one.get_table(1), held)
+    grp = smore.Group([0] * 4)
+    grp.LoadEdgeList(PL1K, 1)
+    grp.alloc_tables(dim, 2)
+    grp.primary.init_table_glibc(0, 0)
+    grp.primary.init_table_glibc(1, g.V * dim)
+    grp.broadcast_tables()
+    grp.set_walk_partition(True)
+    grp.train_deepwalk(0, wt * g.V, wt, 40, 5, K, 0.025, SEED, order, "atomic", per=64)
+    W, C = grp.primary.get_table(0), grp.primary.get_table(1)
+    for r in grp.replicas[1:]:
+        np.testing.assert_array_equal(r.get_table(0), W)
+        np.testing.assert_allclose(r.get_table(1), C, atol=2e-5, rtol=0)
+    grp.close()
+    ln = _heldout_loss(W, C, held)
+    assert np.isfinite(ln) and ln <= 1.10 * l1, (l1, ln)
+
+
+def _edge_auc(W, C, off, tgt, seed=3):
+    rng = np.random.default_rng(seed)
+    V = len(off) - 1
+    srcv = np.repeat(np.arange(V), np.diff(off))
+    pick = rng.integers(0, len(tgt), 20000)
+    nv, nc = rng.integers(0, V, 2000), rng.integers(0, V, 2000)
+    pos = np.einsum("ij,ij->i", W[srcv[pick]].astype(np.float64), C[tgt[pick]].astype(np.float64))
+    neg = np.einsum("ij,ij->i", W[nv].astype(np.float64), C[nc].astype(np.float64))
+    return float((pos[:, None] > neg[None, :]).mean())
+
+
+def test_c5_deepwalk_group_defaults(smore):
+    """Config 5's DeepWalk (the Youtube-sized stand-in, d=128, 10 walks per
+    vertex, 40 steps, window 5, K 5, hybrid) on 2, 4 and 8 replicas with the
+    group's defaults (replicated tables, the adaptive rule at c0 64 from a row
+    census of the walks, 4 pair updates per row per replica per exchange)
+    against one context that walked everything: held-out LINE objective
+    within 10 % / 12 % / 45 % and edge AUC within 0.012 / 0.01 / 0.02
+    (measured 1.035-1.06 / 1.066 / 1.345x and -0.009 / -0.0003 / -0.004,
+    DESIGN.md 10)."""
+    from smore_amd import graphgen
+    V, (src, dst, w) = graphgen.config_edges("c5")
+    dim, wt, K = 128, 10, 5
+    order = smore.deepwalk_order(V, wt, 0)
+    one = smore.ProNet(0)
+    one.set_graph_edges(V, src, dst, w)
+    held = one.sample_edges("line2", (1 << 40) + 17, 100_000, K, SEED + 1)
+    off, tgt = one.csr()
+    one.alloc_tables(dim, 2)
+    one.init_table_glibc(0, 0)
+    one.init_table_glibc(1, V * dim)
+    one.train_deepwalk(0, wt * V, wt, 40, 5, K, 0.025, SEED, order, "hybrid")
+    l1, a1 = _heldout_loss(one.get_table(0), one.get_table(1), held), _edge_auc(one.get_table(0), one.get_table(1),
+                                                                               off, tgt)
+    one.close()
+    res = {1: (l1, a1)}
+    bounds = ((2, 1.10, 0.012), (4, 1.12, 0.01), (8, 1.45, 0.02))
+    for n, _, _ in bounds:
+        g = smore.Group([0] * n)
+        g.set_graph_edges(V, src, dst, w)
+        g.alloc_tables(dim, 2)
+        g.primary.init_table_glibc(0, 0)
+        g.primary.init_table_glibc(1, V * dim)
+        g.broadcast_tables()
+        g.train_deepwalk(0, wt * V, wt, 40, 5, K, 0.025, SEED, order, "hybrid")
+        W, C = g.primary.get_table(0), g.primary.get_table(1)
+        g.close()
+        res[n] = (_heldout_loss(W, C, held), _edge_auc(W, C, off, tgt))
+        print("C5 DeepWalk group", n, res[n], "one", res[1], flush=True)
+    for n, lb, ab in bounds:
+        assert np.isfinite(res[n][0]) and res[n][0] <= lb * l1, res
+        assert res[n][1] >= a1 - ab, res

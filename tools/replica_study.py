@@ -76,8 +76,10 @@ def main():
     ap.add_argument("--dim", type=int, default=None)
     ap.add_argument("--seed", type=int, default=20251015)
     ap.add_argument("--no-partition", action="store_true")
+    ap.add_argument("--walk-partition", action="store_true", help="walk models: W partitioned by walk center")
     ap.add_argument("--combine-rows", type=int, default=None, help="hybrid: LDS write-combined rows on every replica")
     ap.add_argument("--hot-exchange", type=int, default=None, help="sum rule: hub rows synced per launch (0: off)")
+    ap.add_argument("--diag", action="store_true", help="largest rows of each table and their census rate rank")
     ap.add_argument("--hot-tau", type=float, default=None, help="hybrid: hot-row threshold on every replica")
     args = ap.parse_args()
 
@@ -102,6 +104,7 @@ def main():
                 g.set_graph_edges(V, src, dst, w)
             g.alloc_tables(dim, 2)
             g.set_partition(not args.no_partition)
+            g.set_walk_partition(args.walk_partition)
             if args.hot_exchange is not None:
                 g.set_hot_exchange(args.hot_exchange)
             for r in g.replicas:
@@ -132,7 +135,7 @@ def main():
         t0 = time.perf_counter()
         if line:
             T = int(2 ** tot)
-            per = max(1, int(args.per_row * Vn * period))
+            per = max(1, int(args.per_row * Vn * period)) if args.per_row > 0 else 0   # 0: the group default
             g.train_edges("line2", 0, T, T, K, 0.025, 0.0, args.seed, args.mode, per=per, mean=rule)
             row = {"model": "line2", "total": T, "log2_total": tot, "samples_per_exchange": per}
         else:
@@ -143,7 +146,7 @@ def main():
                 p.train_deepwalk(0, min(Vn, 1 << 16), wt, 40, 5, K, 0.025, args.seed, order, args.mode)
                 p.census_end(min(Vn, 1 << 16))
                 pairs_per_walk = float(p.row_rates("census", K, 0).sum())
-            per = max(1, int(args.per_row * Vn * period / pairs_per_walk))
+            per = max(1, int(args.per_row * Vn * period / pairs_per_walk)) if args.per_row > 0 else 0
             g.train_deepwalk(0, wt * Vn, wt, 40, 5, K, 0.025, args.seed, order, args.mode, per=per, mean=rule)
             row = {"model": "deepwalk", "walk_times": wt, "walks_per_exchange": per,
                    "pairs_per_walk": round(pairs_per_walk, 2)}
@@ -153,9 +156,24 @@ def main():
         if n > 1:
             Cl = g.replicas[n - 1].get_table(1)
             spread = float(np.abs(Cl - C).max() / max(1e-30, np.abs(C).max()))
+        if args.diag and (line or n > 1):
+            # where a run went wrong: the largest rows of each table and their
+            # rank in the census's touch rates (0 = the hottest row)
+            for t, T in (("W", W), ("C", C)):
+                nrm = np.sqrt((T.astype(np.float64) ** 2).sum(1))
+                rate = p.row_rates("census", K, 0 if t == "W" else 1) if not line else p.row_rates("line2", K,
+                                                                                                   0 if t == "W" else 1)
+                rank = np.empty(len(rate), np.int64)
+                rank[np.argsort(-rate)] = np.arange(len(rate))
+                top = np.argsort(-nrm)[:8]
+                row["diag_" + t] = {"norm_p50": float(np.median(nrm)), "norm_p99": float(np.quantile(nrm, 0.99)),
+                                    "top_norm": [round(float(nrm[i]), 3) for i in top],
+                                    "top_rate_rank": [int(rank[i]) for i in top],
+                                    "rows_norm_gt_10": int((nrm > 10).sum())}
         row.update({"config": args.graph or args.config, "ranks": n, "rule": rule if n > 1 else "one",
                     "c0": c0, "period": period, "per_row": args.per_row, "mode": args.mode,
                     "combine_rows": args.combine_rows, "hot_tau": args.hot_tau, "hot_exchange": args.hot_exchange,
+                    "walk_partition": args.walk_partition,
                     "finite": bool(np.isfinite(W).all() and np.isfinite(C).all()),
                     "loss": round(heldout_loss(W, C, held), 5), "auc": round(edge_auc(W, C, off, tgt), 5),
                     "replica_spread_rel": spread, "wall_s": round(el, 2)})
