@@ -32,3 +32,25 @@ def test_pmc_per_launch_ignores_other_counters(tmp_path):
     got = bench.pmc_per_launch(str(p), "FETCH_SIZE")
     assert list(got) == ["draw_kernel"]
     assert got["draw_kernel"] == (16 + 12) / 2 * 1024 * bench.FETCH_CORRECTION
+
+
+def test_samples_to_loss_interpolation(tmp_path):
+    """tools/samples_to_loss.py: the N-replica total that reaches one
+    replica's loss, by log-linear interpolation, and the effective speed-up
+    N x sample efficiency x exchange time efficiency."""
+    import json
+    import subprocess
+    import sys
+    rows = [{"ranks": 1, "c0": 1.0, "period": 1.0, "log2_total": t, "loss": l} for t, l in ((29, 3.0), (30, 2.0))]
+    rows += [{"ranks": 4, "c0": 1.0, "period": 0.5, "log2_total": t, "loss": l}
+             for t, l in ((29, 4.0), (30, 3.0), (31, 2.0))]
+    p = tmp_path / "s.jsonl"
+    p.write_text("".join(json.dumps(r) + "\n" for r in rows))
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "samples_to_loss.py"), str(p),
+                          "--step-ms", "100", "--exchange-ms", "5"], capture_output=True, text=True, check=True)
+    got = {r["target_log2_total"]: r for r in map(json.loads, out.stdout.split("\n")[:-1])}
+    # one replica reaches 3.0 at 2^29 and 2.0 at 2^30; four do at 2^30 and 2^31
+    assert got[29]["n_ranks_log2_total"] == 30.0 and got[29]["sample_eff"] == 0.5
+    assert got[30]["n_ranks_log2_total"] == 31.0
+    assert abs(got[29]["time_eff"] - 100 / 110) < 1e-3
+    assert abs(got[29]["effective_speedup"] - 4 * 0.5 * 100 / 110) < 0.01

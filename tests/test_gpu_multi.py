@@ -427,12 +427,13 @@ def test_local_group_deepwalk_matches_emulation(smore, rule):
     grp.close()
 
 
-@pytest.mark.parametrize("sem", ["cpp", "go"])
+@pytest.mark.parametrize("sem", ["cpp", "go", "walklets"])
 def test_walk_owner_splits_the_records(smore, sem):
     """smore_set_walk_owner: the pairs of N disjoint center ranges covering
     [0, V) are exactly the one-context pairs -- the row census of each part
     (W at the center, C at the context and every negative) sums to the
-    unfiltered census, and a part's W counts vanish outside its range."""
+    unfiltered census, and a part's W counts vanish outside its range
+    (DeepWalk under the C++ and the Go rules, Walklets)."""
     pn = smore.ProNet(0)
     pn.LoadEdgeList(PL1K, 1)
     if sem == "go":
@@ -445,7 +446,10 @@ def test_walk_owner_splits_the_records(smore, sem):
     def census(lo, hi):
         pn.set_walk_owner(lo, hi)
         pn.census_begin()
-        pn.train_deepwalk(0, units, wt, 10, 3, 2, 0.025, SEED, order, "atomic")
+        if sem == "walklets":                # ScaleSkipGrams pairs (rule 1)
+            pn.train_walklets(0, units, wt, 10, 1, 3, 2, 0.025, SEED, "atomic")
+        else:
+            pn.train_deepwalk(0, units, wt, 10, 3, 2, 0.025, SEED, order, "atomic")
         pn.census_end(1.0)                   # raw counts
         return pn.row_rates("census", 2, 0), pn.row_rates("census", 2, 1)
 
