@@ -473,8 +473,12 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_
     // it (1338 vs 1342 M/s), DESIGN.md 8
     const char* wrows_env = getenv("SMORE_SH_WROWS");
     const bool wrows = wrows_env && atoi(wrows_env) != 0;
-    snprintf(key, sizeof key, "%d/%d/%lld/%.9g/%d/%d/%s/%d/%d/%d/%d", model, K, (long long)M, tau, c->sh_max,
-             c->sh_flush, stale_env ? stale_env : "", (int)wrows, c->part_n, c->part_i, flush_max);
+    // combined W rows drain on their own interval (SMORE_SH_WFLUSH rounds,
+    // default 8; 0 = with the context rows)
+    const char* wflush_env = getenv("SMORE_SH_WFLUSH");
+    const int wflush = wrows ? (wflush_env ? std::max(0, atoi(wflush_env)) : 8) : 0;
+    snprintf(key, sizeof key, "%d/%d/%lld/%.9g/%d/%d/%s/%d/%d/%d/%d/%d", model, K, (long long)M, tau, c->sh_max,
+             c->sh_flush, stale_env ? stale_env : "", (int)wrows, c->part_n, c->part_i, flush_max, wflush);
     if (c->hot_key == key) return SMORE_OK;
     if (c->g->V >= ((int64_t)1 << 30)) return fail(c, SMORE_EINVAL, "hybrid scatter needs V < 2^30");
     std::vector<double> ps, pn, pc;
@@ -512,7 +516,7 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_
             if (hc[v] && (double)M * p * flush_cap <= stale_max) r.push_back({p, (int32_t)v});
             // two tables (SMORE_SH_WROWS=1 only): the hub W rows compete for
             // the same slots (key v | SH_WKEY)
-            if (wrows && model == SMORE_LINE2 && hw[v] && (double)M * ps[v] * flush_cap <= stale_max)
+            if (wrows && model == SMORE_LINE2 && hw[v] && (double)M * ps[v] * (wflush ? wflush : flush_cap) <= stale_max)
                 r.push_back({ps[v], (int32_t)(v | SH_WKEY)});
         }
         const int64_t cap =
@@ -536,8 +540,13 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_
         if ((rc2 = upload(c, c->d_sh_ids, ids.data(), ids.size()))) return rc2;
         c->sh_rows = (int)n;
         c->sh_flush_eff = flush_cap;
-        if (c->sh_flush <= 0 && n > 0) {
-            const double f = SH_AUTO_BUDGET / ((double)M * r[0].first);
+        c->sh_flush_w_eff = wflush;
+        // the automatic interval follows the hottest row drained on it (with
+        // their own interval, W rows do not count)
+        int64_t top = 0;
+        while (top < n && wflush && (r[top].second & SH_WKEY)) ++top;
+        if (c->sh_flush <= 0 && top < n) {
+            const double f = SH_AUTO_BUDGET / ((double)M * r[top].first);
             c->sh_flush_eff = (int)std::max(8.0, std::min((double)flush_cap, std::floor(f)));
         }
     }
@@ -709,6 +718,7 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
     a.sh_hash = c->d_sh_hash;
     a.sh_ids = c->d_sh_ids;
     a.sh_flush = std::max(1, c->sh_flush_eff);
+    a.sh_flush_w = c->sh_flush_w_eff;
     // edge models: draw kernel -> update kernel per chunk of samples.  With
     // several chunks the draws of chunk k+1 run on a second stream while
     // chunk k updates (two record buffers; the update kernel leaves one block
@@ -1243,6 +1253,7 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
     ar.sh_hash = c->d_sh_hash;
     ar.sh_ids = c->d_sh_ids;
     ar.sh_flush = std::max(1, c->sh_flush_eff);
+    ar.sh_flush_w = c->sh_flush_w_eff;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     for (uint64_t b = walk_begin; b < walk_end; b += chunk) {
         WalkArgs w;
@@ -1470,6 +1481,7 @@ int smore_train_app_async(smore_ctx* c, uint64_t unit_begin, uint64_t unit_end, 
     a.sh_hash = c->d_sh_hash;
     a.sh_ids = c->d_sh_ids;
     a.sh_flush = std::max(1, c->sh_flush_eff);
+    a.sh_flush_w = c->sh_flush_w_eff;
     a.rec = c->d_rec;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     for (uint64_t b = unit_begin; b < unit_end; b += chunk) {
@@ -1549,6 +1561,7 @@ int smore_train_hpe_async(smore_ctx* c, uint64_t begin, uint64_t count, uint64_t
     a.sh_hash = c->d_sh_hash;
     a.sh_ids = c->d_sh_ids;
     a.sh_flush = std::max(1, c->sh_flush_eff);
+    a.sh_flush_w = c->sh_flush_w_eff;
     a.rec = c->d_rec;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     for (uint64_t b = begin; b < begin + count; b += chunk) {
@@ -1649,6 +1662,7 @@ int smore_train_pairs(smore_ctx* c, const int32_t* v, const int32_t* cc, int64_t
     a.sh_hash = c->d_sh_hash;
     a.sh_ids = c->d_sh_ids;
     a.sh_flush = std::max(1, c->sh_flush_eff);
+    a.sh_flush_w = c->sh_flush_w_eff;
     a.rec = c->d_rec;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     for (uint64_t b = 0; b < (uint64_t)n; b += chunk) {

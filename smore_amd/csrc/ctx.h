@@ -87,6 +87,7 @@ struct smore_ctx {
     int sh_rows = 0;
     int sh_max = 128, sh_flush = 0;      // flush 0: automatic drain interval (capi build_hot_maps)
     int sh_flush_eff = 32;               // the interval of the last hybrid launch
+    int sh_flush_w_eff = 0;              // its W-key slots' own interval (0: none)
     // pre-drawn edge-sample records (train_draw.hip) and per-phase timing
     int32_t* d_rec = nullptr;
     // DeepWalk pair records: per-walk pair counts, their exclusive scan, scan scratch

@@ -537,6 +537,22 @@ __device__ __forceinline__ void sh_drain(const ShState& sh, const int32_t* sh_id
     }
 }
 
+// sh_drain of the W-key slots only (the combined hub W rows of a two-table
+// model, drained on their own shorter interval: EdgeArgs::sh_flush_w)
+__device__ __forceinline__ void sh_drain_w(const ShState& sh, const int32_t* sh_ids, float* Tw, int dpad) {
+    const int nwaves = blockDim.x / 64, wave = threadIdx.x / 64;
+    const int n = sh.n * dpad;
+    const int per = (n + nwaves - 1) / nwaves;
+    const int lo = wave * per, hi = n < lo + per ? n : lo + per;
+    for (int i = lo + (threadIdx.x & 63); i < hi; i += 64) {
+        const int s = i / dpad;
+        const int32_t key = sh_ids[s];
+        if (!(key & SH_WKEY)) continue;
+        const float x = atomicExch(&sh.pend[i], 0.0f);
+        if (x != 0.0f) unsafeAtomicAdd(Tw + (int64_t)(key & ~SH_WKEY) * dpad + (i - s * dpad), x);
+    }
+}
+
 // ------------------------------------------------------------------ edge kernel
 // LINE-2 (W,C; SHARED 0), LINE-1 / MF (W,W; SHARED 1, Opt_SGD for MF at run
 // time) and BPR (W,W; SHARED 2, UpdateBPRPair); the scatter MODE is
@@ -605,6 +621,8 @@ edge_train_kernel(EdgeArgs a) {
             if (sh.n > 0 && ++round == (uint32_t)a.sh_flush) {
                 drain();
                 round = 0;
+            } else if (sh.n > 0 && a.sh_flush_w > 0 && round % (uint32_t)a.sh_flush_w == 0) {
+                sh_drain_w(sh, sh_ids, a.W, a.dpad);
             }
         }
     };

@@ -270,6 +270,8 @@ go_rec_kernel(EdgeArgs a) {
             if (sh.n > 0 && ++round == (uint32_t)a.sh_flush) {
                 sh_drain(sh, sh_ids, a.W, Tc, a.dpad);
                 round = 0;
+            } else if (sh.n > 0 && a.sh_flush_w > 0 && round % (uint32_t)a.sh_flush_w == 0) {
+                sh_drain_w(sh, sh_ids, a.W, a.dpad);
             }
         }
     };

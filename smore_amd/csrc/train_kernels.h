@@ -21,6 +21,7 @@ struct EdgeArgs {
     const int2* sh_hash;
     const int32_t* sh_ids;
     int sh_rows, sh_flush;
+    int sh_flush_w;                // W-key slots (SMORE_SH_WROWS) drained every sh_flush_w rounds too (0: off)
     // edge kernels: the pre-drawn sample records of samples [begin, begin+count)
     // (draw_kernel), rec_width(KMAX) int32 each
     const int32_t* rec;

@@ -187,3 +187,21 @@ def test_source_parts_are_contiguous_equal_mass(nparts):
         assert abs(ps[b[p]:b[p + 1]].sum() - 1.0 / nparts) <= ps.max() + 1e-12
     with pytest.raises(_lib.SmoreError):
         pn.source_parts(V + 1)
+
+
+def test_walk_owner_arguments():
+    """smore_set_walk_owner / smore_walk_parts host checks (no GPU): ranges
+    inside [0, V], hi < 0 = every pair, and parts only after a row census."""
+    from smore_amd import ProNet
+    from smore_amd import _lib
+    pn = ProNet(device=-1)
+    pn.LoadEdgeList(os.path.join(GOLDEN, "pl1k.txt"), 1)
+    V = pn.MAX_vid
+    pn.set_walk_owner(0, V)
+    pn.set_walk_owner(V // 3, V // 2)
+    pn.set_walk_owner(0, -1)
+    for lo, hi in ((5, 3), (-1, 4), (0, V + 1)):
+        with pytest.raises(_lib.SmoreError):
+            pn.set_walk_owner(lo, hi)
+    with pytest.raises(_lib.SmoreError):
+        pn.walk_parts(4)                      # no census yet
