@@ -595,8 +595,8 @@ static int ensure_packed(smore_ctx* c) {
     if (c->packed_ok) return SMORE_OK;
     const int64_t V = c->g->V, E = c->g->E;
     if (E >= ((int64_t)1 << 32)) return SMORE_OK;
-    if (!c->d_vt32) HIPCHK(c, hipMalloc(&c->d_vt32, (size_t)std::max<int64_t>(V, 1) * 2 * sizeof(uint4)));
-    if (!c->d_ct16) HIPCHK(c, hipMalloc(&c->d_ct16, (size_t)std::max<int64_t>(E, 1) * sizeof(uint4)));
+    if (!c->d_vt32) HIPCHK(c, draw_malloc((void**)&c->d_vt32, (size_t)std::max<int64_t>(V, 1) * 2 * sizeof(uint4)));
+    if (!c->d_ct16) HIPCHK(c, draw_malloc((void**)&c->d_ct16, (size_t)std::max<int64_t>(E, 1) * sizeof(uint4)));
     HIPCHK(c, launch_pack(dev_graph(c), (uint64_t)E, c->d_vt32, c->d_ct16, c->stream));
     c->packed_ok = true;
     return SMORE_OK;
@@ -834,7 +834,7 @@ int smore_set_semantics(smore_ctx* c, int semantics) {
     int rc;
     if ((rc = set_device(c))) return rc;
     if ((rc = upload(c, c->d_vtab, c->g->vtab.data(), c->g->vtab.size()))) return rc;
-    if ((rc = upload(c, c->d_ntab, c->g->ntab.data(), c->g->ntab.size()))) return rc;
+    if ((rc = upload(c, c->d_ntab, c->g->ntab.data(), c->g->ntab.size(), true))) return rc;
     if (semantics == SMORE_SEM_GO) {
         if ((rc = upload(c, c->d_tcum, tcum.data(), tcum.size()))) return rc;
     } else {

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -174,11 +175,23 @@ inline void dfree(T*& p) {
     p = nullptr;
 }
 
+// the draw kernel's random-read tables (packed vertex / context tables, the
+// negative alias table): default device memory; SMORE_DRAW_MEM=uncached
+// allocates them uncached (memory-side reads sized to the access instead of
+// 128-B L2 lines; an experiment knob)
+inline hipError_t draw_malloc(void** p, size_t n) {
+    static const bool unc = [] {
+        const char* e = getenv("SMORE_DRAW_MEM");
+        return e && !strcmp(e, "uncached");
+    }();
+    return unc ? hipExtMallocWithFlags(p, n, hipDeviceMallocUncached) : hipMalloc(p, n);
+}
+
 template <class T>
-int upload(smore_ctx* c, T*& d, const T* h, size_t n) {
+int upload(smore_ctx* c, T*& d, const T* h, size_t n, bool draw_table = false) {
     dfree(d);
     if (n == 0) n = 1;
-    HIPCHK(c, hipMalloc((void**)&d, n * sizeof(T)));
+    HIPCHK(c, draw_table ? draw_malloc((void**)&d, n * sizeof(T)) : hipMalloc((void**)&d, n * sizeof(T)));
     if (h) HIPCHK(c, hipMemcpy(d, h, n * sizeof(T), hipMemcpyHostToDevice));
     return SMORE_OK;
 }
@@ -232,7 +245,7 @@ inline int upload_graph(smore_ctx* c) {
     if ((rc = upload(c, c->d_offsets, g.offsets.data(), g.offsets.size()))) return rc;
     if ((rc = upload(c, c->d_targets, g.targets.data(), g.targets.size()))) return rc;
     if ((rc = upload(c, c->d_vtab, g.vtab.data(), g.vtab.size()))) return rc;
-    if ((rc = upload(c, c->d_ntab, g.ntab.data(), g.ntab.size()))) return rc;
+    if ((rc = upload(c, c->d_ntab, g.ntab.data(), g.ntab.size(), true))) return rc;
     if ((rc = upload(c, c->d_ctab, g.ctab.data(), g.ctab.size()))) return rc;
     // fastSigmoid table, 1001 entries (src/proNet.cpp:52-60; the reference
     // sizes it 1000 and writes 1001 -- the build keeps all 1001)

@@ -155,6 +155,7 @@ struct Zipf {   // inverse CDF of p(r) ~ (r+1)^-s over [0, V)
 static void* alloc(size_t n, int kind) {
     void* p = nullptr;
     if (kind == 0) CHK(hipMalloc(&p, n));
+    else if (kind == 2) CHK(hipExtMallocWithFlags(&p, n, hipDeviceMallocFinegrained));
     else CHK(hipExtMallocWithFlags(&p, n, hipDeviceMallocUncached));
     CHK(hipMemset(p, 0, n));
     return p;
@@ -178,15 +179,17 @@ int main(int argc, char** argv) {
         }
         const size_t Fs[] = {(size_t)2 << 20, (size_t)16 << 20, (size_t)80000000, (size_t)192 << 20,
                              (size_t)320000000, (size_t)1280000000, (size_t)6400000000ull};
-        void* tab = alloc(Fs[6], 0);
+        // PROBE_MEM: 0 hipMalloc (default), 1 uncached, 2 fine-grained
+        const int kind = getenv("PROBE_MEM") ? atoi(getenv("PROBE_MEM")) : 0;
+        void* tab = alloc(Fs[6], kind);
         CHK(hipMemset(tab, 0x5a, Fs[6]));
         for (size_t F : Fs)
             for (int W : {8, 16, 32}) {
                 const float ms = run_rand(F, W, threads, tab, out, 3);
                 const double reads = (double)threads * 5;
-                printf("{\"probe\": \"rand\", \"footprint\": %zu, \"width\": %d, \"reads_per_thread\": 5, "
+                printf("{\"probe\": \"rand\", \"mem\": %d, \"footprint\": %zu, \"width\": %d, \"reads_per_thread\": 5, "
                        "\"threads\": %llu, \"ms\": %.3f, \"Greads_per_s\": %.2f, \"GBs_payload\": %.1f}\n",
-                       F, W, (unsigned long long)threads, ms, reads / ms / 1e6, reads * W / ms / 1e6);
+                       kind, F, W, (unsigned long long)threads, ms, reads / ms / 1e6, reads * W / ms / 1e6);
                 fflush(stdout);
             }
         return 0;
