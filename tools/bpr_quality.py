@@ -5,7 +5,7 @@ samples, per scatter: atomic, hybrid (no LDS combining, the default), hybrid
 with the hub rows write-combined (SMORE_BPR_COMBINE=1).  TEST
 INFRASTRUCTURE (reads the oracle's sampler).  DESIGN.md 8.
 
-    python tools/bpr_quality.py --log2-total 28
+    python tools/bpr_quality.py --log2-total 28 [--variants atomic hybrid hybrid@3]
 """
 import argparse
 import json
@@ -51,6 +51,9 @@ def main():
     total = 1 << args.log2_total
     step = 1 << 27
     for var in args.variants:
+        # variant: mode[+combine][@tau] (tau: the hot-row threshold; default the library's)
+        var, _, tau = var.partition("@")
+        pn.set_hot_threshold(float(tau) if tau else -1.0)
         mode = var.split("+")[0]
         os.environ["SMORE_BPR_COMBINE"] = "1" if var.endswith("+combine") else "0"
         pn.alloc_tables(args.dim, 1)
@@ -62,9 +65,10 @@ def main():
             ms.append(pn.last_kernel_ms())
         el = time.perf_counter() - t0
         loss, acc = bpr_objective(pn.get_table(0), held, args.dim)
-        print(json.dumps({"config": "c3", "variant": var, "total": total, "loss": round(loss, 6),
+        print(json.dumps({"config": "c3", "variant": var + ("@" + tau if tau else ""), "total": total, "loss": round(loss, 6),
                           "rank_acc": round(acc, 5), "call_ms_per_2^27": round(float(np.median(ms)), 2),
-                          "wall_s": round(el, 2), "combine_info": pn.write_combine_info()}), flush=True)
+                          "wall_s": round(el, 2), "combine_info": pn.write_combine_info(),
+                          "hot_rows": pn.hot_rows() if mode == "hybrid" else None}), flush=True)
     os.environ.pop("SMORE_BPR_COMBINE", None)
 
 
