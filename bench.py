@@ -221,6 +221,27 @@ def cpu_baseline(V, src, dst, w, dim, K, seconds, config):
                       % (dim, K, config, n_all, mine, quota, machine, t_all, n_one, t_one)}
 
 
+def run_step(pn, sync, k, world, rank, S, n_launch, n_ex, total, K, seed, mode, sync_every, on_launch=None):
+    """One bench step of rank `rank`: its global samples [(k*world + rank)*S, +S)
+    in n_launch launches; with a replica exchange (N > 1) the hub-row exchange
+    after every launch (sum rule), or an exchange begun after every launch but
+    the last (--exchanges-per-step), and one begun at the end of every
+    sync_every-th step, which overlaps the next step (dist.OverlapSync)."""
+    begin = (k * world + rank) * S
+    sub = S // n_launch
+    for j in range(n_launch):
+        n = sub if j + 1 < n_launch else S - j * sub
+        pn.train_edges("line2", begin + j * sub, n, total, K, 0.025, 0.0, seed, mode, sync=False)
+        if on_launch is not None:
+            on_launch()
+        if n_launch > 1 and sync.hot_idx:
+            sync.hot()    # the hub rows of every rank, synchronously
+        elif n_ex > 1 and j + 1 < n_launch:
+            sync.begin()  # exchanges inside the step (--exchanges-per-step)
+    if sync is not None and (k + 1) % sync_every == 0:
+        sync.begin()      # folds the previous exchange in; this one overlaps the next step
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -288,23 +309,15 @@ def main():
     total = (args.warmup + args.steps) * S * world     # alpha schedule over the whole job
 
     def step(k, timed=False):
-        begin = (k * world + rank) * S
-        sub = S // n_launch
-        for j in range(n_launch):
-            n = sub if j + 1 < n_launch else S - j * sub
-            pn.train_edges("line2", begin + j * sub, n, total, K, 0.025, 0.0, args.seed, args.mode, sync=False)
+        def on_launch():
             if timed:
                 ph = pn.last_phase_ms()      # waits for this launch's events (a few us of host gap)
                 if ph is not None:
                     phase[0] += ph[0]
                     phase[1] += ph[1]
                     phase[2] += ph[2]
-            if n_launch > 1 and sync.hot_idx:
-                sync.hot()    # the hub rows of every rank, synchronously
-            elif n_ex > 1 and j + 1 < n_launch:
-                sync.begin()  # exchanges inside the step (--exchanges-per-step)
-        if sync is not None and (k + 1) % args.sync_every == 0:
-            sync.begin()      # folds the previous exchange in; this one overlaps the next step
+        run_step(pn, sync, k, world, rank, S, n_launch, n_ex, total, K, args.seed, args.mode, args.sync_every,
+                 on_launch)
 
     if args.pmc_child:      # the profiled child of pmc_traffic_live: the steps only
         for k in range(args.steps):
