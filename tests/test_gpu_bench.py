@@ -1,0 +1,61 @@
+"""bench.py end to end on the GPU at a small config: the one JSON line the
+driver reads (its keys, units and roofline object), at N = 1 and at N = 2
+(torchrun, gloo ranks sharing the one GPU: the N > 1 step schedule, the
+adaptive exchange and the max-over-ranks timing; the 2..8-GPU RCCL runs are
+the driver's)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SMALL = ["--config", "small", "--samples", str(1 << 22), "--steps", "2", "--warmup", "1", "--pmc", "off"]
+
+pytestmark = pytest.mark.gpu
+
+
+def _json_line(out):
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out[-2000:]
+    return json.loads(lines[0])
+
+
+def _check_contract(d, n):
+    assert d["metric"] == "M edge-updates/sec (d=64, neg=5)" and d["unit"] == "M edge-updates/s"
+    assert d["n_gpus"] == n and d["steps"] == 2 and d["warmup"] == 1
+    assert d["value"] > 0 and d["ms_per_step"] > 0 and d["higher_is_better"] is True
+    assert d["scaling"] == "weak" and d["dtype"] == "f32" and d["vs_baseline"] is None
+    assert d["config"]["parallelism"] == "replicas%d" % n and "workload" in d["config"]
+    r = d["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in r
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    assert d["skipped_samples"] == 0
+
+
+def test_bench_json_line_n1():
+    p = subprocess.run([sys.executable, "bench.py", "--no-cpu-baseline"] + SMALL, cwd=ROOT,
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = _json_line(p.stdout)
+    _check_contract(d, 1)
+    assert d["cpu_baseline"] is None and d["config"]["sync"] == "none"
+
+
+def test_bench_json_line_n2_gloo_ranks():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+                        "--dist-backend", "gloo"] + SMALL, cwd=ROOT, capture_output=True, text=True, timeout=300,
+                       env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = _json_line(p.stdout)
+    _check_contract(d, 2)
+    assert d["config"]["sync"].startswith("adaptive") and "1/2 step" in d["config"]["sync"]
