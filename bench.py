@@ -92,7 +92,13 @@ def parse():
                     help="N=1: measure roofline.traffic with rocprofv3 --pmc in child runs of this config "
                          "before the timed run (off: the committed profiles/pmc_traffic.json)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
-    return ap.parse_args()
+    a = ap.parse_args()
+    # exchanges inside a step assume one exchange period of S / n_ex samples;
+    # with --sync-every > 1 the period would alternate between S / n_ex and S
+    # while the adaptive scales assume one: not a valid combination
+    if a.sync_every > 1 and a.exchanges_per_step > 1:
+        ap.error("--sync-every > 1 needs --exchanges-per-step 1")
+    return a
 
 
 # gfx950: FETCH_SIZE counts half the bytes of these kernels' reads (calibrated on

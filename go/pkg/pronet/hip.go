@@ -468,23 +468,25 @@ func init() { hipUpdatePairs = updatePairsHIP }
 // library context is not thread-safe, so batches from concurrent goroutines
 // run one after another (each sees the tables the previous one wrote back)
 type pairSession struct {
-	mu  sync.Mutex
-	h   *HIP
-	err error
+	once sync.Once // the context is made exactly once, before any caller uses it
+	mu   sync.Mutex
+	h    *HIP
+	err  error
 }
 
 var pairSessions sync.Map // *ProNet -> *pairSession
 
+// pairSession returns pn's session with its context made: every goroutine,
+// including ones that lost the LoadOrStore race, waits in once.Do until the
+// winner's NewHIP returned, so none can see an unset h (ADVICE r4).
 func (pn *ProNet) pairSession() *pairSession {
-	v, loaded := pairSessions.LoadOrStore(pn, &pairSession{})
+	v, _ := pairSessions.LoadOrStore(pn, &pairSession{})
 	s := v.(*pairSession)
-	if !loaded {
-		s.mu.Lock()
+	s.once.Do(func() {
 		cfg := HIPConfigFromEnv(1)
 		cfg.GPUs = 1
 		s.h, s.err = pn.NewHIP(cfg)
-		s.mu.Unlock()
-	}
+	})
 	return s
 }
 
@@ -542,6 +544,10 @@ func (h *HIP) Pairs(vertices, contexts []int64, negativeSamples int, alpha float
 	defer C.free(unsafe.Pointer(&v[0]))
 	defer C.free(unsafe.Pointer(&c[0]))
 	for i := 0; i < n; i++ {
+		// range-check before narrowing: an id >= 2^31 must not wrap to a small valid one
+		if vertices[i] < 0 || vertices[i] >= h.maxVid || contexts[i] < 0 || contexts[i] >= h.maxVid {
+			return fmt.Errorf("Pairs: pair %d (%d, %d) out of range [0, %d)", i, vertices[i], contexts[i], h.maxVid)
+		}
 		v[i], c[i] = C.int32_t(vertices[i]), C.int32_t(contexts[i])
 	}
 	if rc := C.smore_train_pairs(h.ctx, &v[0], &c[0], C.int64_t(n), C.int(negativeSamples), C.double(alpha),

@@ -118,8 +118,10 @@ static int64_t print_graph(smore_ctx* ctx) {
     return V;
 }
 
-// run samples [0, n) of a run of `total` in launches of 2^26 per GPU with progress
-static void train_chunks(Run& r, int model, unsigned long long total, unsigned long long n, int K, double alpha,
+// run samples [0, n) of a run of `total` in launches of 2^26 per GPU with
+// progress (the edge-model CLIs line / mf / bpr; inline: the walk-model CLIs
+// include this header without calling it)
+inline void train_chunks(Run& r, int model, unsigned long long total, unsigned long long n, int K, double alpha,
                          double reg, unsigned long long seed, int mode) {
     const int gpus = r.g ? smore_group_size(r.g) : 1;
     const unsigned long long chunk = (1ull << 26) * (unsigned long long)gpus;

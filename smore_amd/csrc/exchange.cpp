@@ -553,7 +553,17 @@ static int group_rounds(smore_group* g, uint64_t begin, uint64_t end, uint64_t p
             // rates are well measured on small rounds, or the call)
             const uint64_t m = std::min<uint64_t>(count, std::max<uint64_t>(per * (uint64_t)n, (uint64_t)1 << 16));
             if ((rc = smore_census_begin(c0))) return gfail(g, 0, rc);
-            rc = run(c0, begin, begin + m);
+            // m units in 16 slices spread evenly over [begin, end), not the
+            // leading m: walks without a start order begin at walk mod V, so a
+            // prefix would census one contiguous id block's neighbourhood only
+            // 
+            const uint64_t ns = std::min<uint64_t>(16, m);
+            rc = SMORE_OK;
+            for (uint64_t k = 0; k < ns && !rc; ++k) {
+                const uint64_t lo = begin + (uint64_t)(((unsigned __int128)count * k) / ns);
+                const uint64_t len = m * (k + 1) / ns - m * k / ns;
+                if (len) rc = run(c0, lo, lo + len);
+            }
             const int rc2 = smore_census_end(c0, (double)m);
             if (rc || rc2) return gfail(g, 0, rc ? rc : rc2);
             c0->census_key = key;

@@ -196,11 +196,17 @@ class ProNet:
     def train_pairs(self, v, c, K, alpha, seed, unit=0, mode="hogwild"):
         """UpdatePairs (src/proNet.cpp:2741-2753; Go pkg/pronet/optimizer.go:8-18)
         over caller-supplied pairs (v[i], c[i]) in order, fixed alpha; pair i's
-        negatives from stream 3, unit `unit` + i // 2^20 (smore_train_pairs)."""
-        v = np.ascontiguousarray(v, np.int32)
-        c = np.ascontiguousarray(c, np.int32)
+        negatives from stream 3, unit `unit` + i // 2^20 (smore_train_pairs).
+        Ids are range-checked before they are narrowed to int32 (an id of 2^31
+        or more must not wrap to a valid small one; the reference panics)."""
+        v, c = np.asarray(v), np.asarray(c)
         if v.shape != c.shape:
             raise ValueError("v and c must have the same length")
+        for a in (v, c):
+            if a.size and (a.min() < 0 or a.max() >= self.MAX_vid):
+                raise IndexError("train_pairs: vertex id out of range [0, %d)" % self.MAX_vid)
+        v = np.ascontiguousarray(v, np.int32)
+        c = np.ascontiguousarray(c, np.int32)
         self._chk(lib.smore_train_pairs(self.ctx, ptr(v), ptr(c), len(v), int(K), float(alpha), int(seed), int(unit),
                                         _lib.MODE[mode]), "train_pairs")
 
