@@ -23,7 +23,7 @@ all: lib cli goshape
 
 lib: $(LIB)
 
-HOST_SRCS := host_graph loader capi exchange graphgen
+HOST_SRCS := host_graph loader capi exchange graphgen blocks
 $(OBJ)/%.o: $(SRC)/%.cpp $(HOST_HDRS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(CXXFLAGS) -c -o $@ $<

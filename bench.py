@@ -66,6 +66,10 @@ def parse():
     ap.add_argument("--combine-rows", type=int, default=128, help="hybrid: LDS write-combined hottest rows")
     ap.add_argument("--combine-flush", type=int, default=0, help="hybrid: rounds between LDS drains (0: automatic)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal)")
+    ap.add_argument("--schedule", default="blocks", choices=["blocks", "replicas"],
+                    help="N > 1: blocks (default: the 2-D block schedule -- rank r owns W part r, the C table in 2N "
+                         "blocks rotating around the ring by send/recv, one epoch of 2N sub-rounds per step, nothing "
+                         "all-reduced; DESIGN.md 10) or replicas (replicated C, deltas all-reduced)")
     ap.add_argument("--sync-every", type=int, default=1)
     ap.add_argument("--exchanges-per-step", type=int, default=2,
                     help="N > 1: the step's samples in this many launches, an exchange after each (default 2: "
@@ -227,6 +231,50 @@ def cpu_baseline(V, src, dst, w, dim, K, seconds, config):
                       % (dim, K, config, n_all, mine, quota, machine, t_all, n_one, t_one)}
 
 
+def largest_remainder(samples, mass):
+    """smore_block_counts restated: samples split by mass, largest remainder
+    first (ties to the lower block)."""
+    x = [samples * m for m in mass]
+    c = [int(np.floor(v)) for v in x]
+    rem = sorted(range(len(x)), key=lambda k: -(x[k] - np.floor(x[k])))
+    for k in rem[:samples - sum(c)]:
+        c[k] += 1
+    return c
+
+
+def block_schedule(count, per, world, rank, counts):
+    """exchange.cpp group_block_edges' split of samples [0, count) for replica
+    `rank`: rounds (epochs) of per * world samples, the rank's slice of each
+    split over its 2N cells by counts(slice) in sub-round order.  Yields
+    (sub-round, block, first sample, samples) -- zero-sample cells too: their
+    rotation still happens."""
+    nb = 2 * world
+    rounds = 1 if per > count // world else -(-count // (per * world))
+    for k in range(rounds):
+        lo = count * k // rounds
+        m = count * (k + 1) // rounds - lo
+        cur = lo + m * rank // world
+        cnt = counts(lo + m * (rank + 1) // world - cur)
+        for s in range(nb):
+            b = (2 * rank + s) % nb
+            yield k * nb + s, b, cur, int(cnt[b])
+            cur += int(cnt[b])
+
+
+def run_block_step(pn, bsync, k, world, rank, S, total, K, seed, mode):
+    """One bench step in the block schedule: one epoch (2N sub-rounds) of the
+    rank's samples [(k*world + rank)*S, +S), each sub-round one cell launch
+    followed by its C block's rotation (dist.BlockSync)."""
+    base = k * world * S
+    for s, b, lo, n in block_schedule(world * S, S, world, rank, pn.block_counts):
+        assert bsync.block() == b
+
+        def train(blk, lo=lo, n=n):
+            if n:
+                pn.block_train_edges(blk, base + lo, n, total, K, 0.025, seed, mode, sync=False)
+        bsync.sub_round(train)
+
+
 def run_step(pn, sync, k, world, rank, S, n_launch, n_ex, total, K, seed, mode, sync_every, on_launch=None):
     """One bench step of rank `rank`: its global samples [(k*world + rank)*S, +S)
     in n_launch launches; with a replica exchange (N > 1) the hub-row exchange
@@ -276,7 +324,7 @@ def main():
 
     import smore_amd
     from smore_amd import graphgen
-    from smore_amd.dist import ReplicaSync
+    from smore_amd.dist import BlockSync, ReplicaSync, table_tensor
 
     t_gen = time.perf_counter()
     V, (src, dst, w) = graphgen.config_edges(args.config)
@@ -302,12 +350,24 @@ def main():
     # N > 1: each rank draws its sources from its own part of the vertex ids
     # (equal source mass), so W rows are owned and only C is exchanged; the
     # adaptive rule scales C's summed deltas per row
-    partition = world > 1 and not args.no_partition
+    blocks = world > 1 and args.schedule == "blocks"
+    partition = world > 1 and not args.no_partition and not blocks
     c0 = args.sync_c0 if args.sync_c0 is not None else (2048.0 if partition else 64.0)
-    n_ex = max(1, args.exchanges_per_step) if world > 1 and args.sync != "sum" else 1
+    n_ex = max(1, args.exchanges_per_step) if world > 1 and args.sync != "sum" and not blocks else 1
     sync = (ReplicaSync(pn, sync=args.sync, hot_rows=args.hot_rows, model="line2", K=args.negative,
                         updates=args.samples * args.sync_every // n_ex, c0=c0, partition=partition)
-            if world > 1 else None)
+            if world > 1 and not blocks else None)
+    bsync = None
+    if blocks:
+        # the 2-D block schedule: this rank's cells' draw tables (W part r,
+        # 2N C blocks), the rotation over torch.distributed
+        t_bs = time.perf_counter()
+        pn.block_setup("line2", world, rank, args.negative, args.mode)
+        wb, cb = pn.block_bounds()
+        bsync = BlockSync(table_tensor(pn, 0), table_tensor(pn, 1), wb, cb)
+        if rank == 0:
+            print("[bench] block schedule set up in %.1f s" % (time.perf_counter() - t_bs), file=sys.stderr,
+                  flush=True)
     n_launch = max(1, args.launches) if (sync is not None and sync.hot_idx) else n_ex
     phase = [0.0, 0.0, 0]     # exposed draw ms, update ms, update launches (timed steps)
 
@@ -315,6 +375,10 @@ def main():
     total = (args.warmup + args.steps) * S * world     # alpha schedule over the whole job
 
     def step(k, timed=False):
+        if bsync is not None:
+            run_block_step(pn, bsync, k, world, rank, S, total, K, args.seed, args.mode)
+            return
+
         def on_launch():
             if timed:
                 ph = pn.last_phase_ms()      # waits for this launch's events (a few us of host gap)
@@ -334,6 +398,8 @@ def main():
         step(k)
     if sync is not None:
         sync.end()
+    if bsync is not None:
+        bsync.finish(gather=False)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -346,6 +412,8 @@ def main():
     draw_ms, upd_ms, launches = phase
     if sync is not None:
         sync.end()            # the last exchange lands inside the timed region
+    if bsync is not None:
+        bsync.finish(gather=True)   # the last rotations and the W / C gather inside the timed region
     ev1.record(stream)
     torch.cuda.synchronize()
     if dist:
@@ -410,14 +478,17 @@ def main():
                                    % (args.config, "" if args.semantics == "cpp" else ", Go rules (pkg/pronet)"),
                        "vertices": V, "edge_slots": E, "dim": args.dim, "negative": K,
                        "samples_per_step_per_gpu": S, "scatter": args.mode,
-                       "sync": ("%s%s every %s%s%s" % (
+                       "sync": (("blocks: 2-D block schedule, rank r owns W part r, C in %d blocks rotated to "
+                                 "rank r-1 (send/recv) after each of %d sub-rounds per step, nothing all-reduced; "
+                                 "W parts and C blocks gathered at the end" % (2 * world, 2 * world)) if blocks else
+                                "%s%s every %s%s%s" % (
                            args.sync, " c0=%g" % c0 if args.sync == "adaptive" else "",
                            "%d steps" % args.sync_every if n_ex == 1 else "1/%d step" % n_ex,
                            ", W partitioned by source (C exchanged, W gathered at the end)" if partition else "",
                            ", %d hub rows per table after each of %d launches per step"
                            % (args.hot_rows, n_launch) if sync is not None and sync.hot_idx else ""))
                                if world > 1 else "none",
-                       "parallelism": "replicas%d" % world},
+                       "parallelism": ("blocks%d" if blocks else "replicas%d") % world},
             # achieved = updates/s x 1868 B (the whole path's algorithmic
             # reads) over the 8 TB/s HBM read roofline; the dominant kernel's own
             # figure (its per-launch time, as rocprof reports it) is "kernel"

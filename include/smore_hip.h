@@ -321,6 +321,18 @@ int smore_group_set_partition(smore_group* g, int on);
  * census, smore_set_walk_owner; reset after the call), only C is exchanged, W
  * is gathered from the owners.  APP and HPE always replicate both tables. */
 int smore_group_set_walk_partition(smore_group* g, int on);
+/* The multi-GPU schedule of LINE-2, DeepWalk and Walklets (C++ rules):
+ *   SMORE_SCHED_REPLICAS  replicated tables, deltas exchanged (the rules above);
+ *   SMORE_SCHED_BLOCKS    the 2-D block schedule (smore_block_setup below): no
+ *                         row is replicated while it trains, C blocks rotate
+ *                         between the replicas (ncclSend / ncclRecv), nothing is
+ *                         all-reduced.  `per` of the training calls = samples
+ *                         (walks) per replica per epoch (nb sub-rounds); 0 = the
+ *                         default.  The other models keep the replicas.
+ * Default: SMORE_SCHED_BLOCKS. */
+#define SMORE_SCHED_REPLICAS 0
+#define SMORE_SCHED_BLOCKS 1
+int smore_group_set_schedule(smore_group* g, int schedule);
 smore_ctx* smore_group_ctx(smore_group* g, int rank);
 const char* smore_group_last_error(const smore_group* g);
 int smore_group_load_edgelist(smore_group* g, const char* path, int undirected, int vertex_method,
@@ -518,6 +530,47 @@ int smore_census_end(smore_ctx* ctx, double units);
  * last row census (bounds[nparts + 1], as smore_source_parts). */
 int smore_set_walk_owner(smore_ctx* ctx, int64_t lo, int64_t hi);
 int smore_walk_parts(smore_ctx* ctx, int nparts, int64_t* bounds);
+
+/* ---- 2-D block schedule (one replica's side) ------------------------------
+ * new in this build: SURVEY.md 8e's conflict-free multi-GPU layout for the
+ * reference's one shared table pair (src/model/LINE.cpp:160-191,
+ * src/model/DeepWalk.cpp:128-155).  Context `part` of `nparts` (N <= 16) owns
+ * the W rows of part r (smore_block_bounds wb: N + 1 bounds of equal source
+ * mass); the C table is cut into nb = 2N blocks (cb: nb + 1 bounds of equal
+ * negative mass).  Sub-round s trains cell (r, b = (2r + s) mod nb) on every
+ * replica; then replica r hands block b to replica r - 1 (which trains it at
+ * sub-round s + 2) -- the drivers: smore_group_set_schedule, smore_amd/dist.py
+ * BlockSync.  A cell draws the one-context law restricted to the cell: LINE-2
+ * (v, c) from an alias table over the part's TargetSample outcomes whose
+ * context is in block b, negatives from the negative law restricted to block b;
+ * walk models: every replica runs every walk of a round and keeps its centers'
+ * pairs, bucketed by the context's block (negatives likewise in the block).
+ * model: SMORE_LINE2 or SMORE_CENSUS (the C++ walk models DeepWalk /
+ * Walklets); K and mode must match the training calls.  nparts 1 = off. */
+int smore_block_setup(smore_ctx* ctx, int model, int nparts, int part, int K, int mode);
+int smore_block_info(const smore_ctx* ctx, int* nparts, int* part, int* nblocks);
+int smore_block_bounds(const smore_ctx* ctx, int64_t* wb, int64_t* cb);
+/* LINE-2: this part's sample mass per C block (nb doubles, sum 1), and
+ * `samples` split over the blocks by it (largest remainder; nb counts) */
+int smore_block_mass(const smore_ctx* ctx, double* mass);
+int smore_block_counts(const smore_ctx* ctx, uint64_t samples, uint64_t* counts);
+/* LINE-2: samples [begin, begin + count) (Philox units; LINE's learning rate
+ * from the global index as smore_train_edges) drawn from cell (part, block) and
+ * trained, asynchronously on the context stream */
+int smore_block_train_edges_async(smore_ctx* ctx, int block, uint64_t begin, uint64_t count, uint64_t total, int K,
+                                  double alpha0, uint64_t seed, int mode);
+/* the draws of a cell: out count x (2 + K) {v, c, n1..nK} (parity tests) */
+int smore_block_sample_edges(smore_ctx* ctx, int block, uint64_t seed, uint64_t begin, uint64_t count, int K,
+                             int32_t* out);
+/* walk models: a round of walks [walk_begin, walk_end) (<= 2^18; rule 0
+ * DeepWalk with its start order, 1 Walklets with window_min) -> this part's
+ * pair records bucketed by block; then smore_block_train_walks_async per
+ * block; smore_block_walk_records: a bucket's record count (synchronises) */
+int smore_block_prepare_walks(smore_ctx* ctx, int rule, uint64_t walk_begin, uint64_t walk_end, int walk_times,
+                              int walk_steps, int window, int window_min, int K, double alpha0, uint64_t seed,
+                              const int64_t* order, uint64_t order_base, int mode);
+int smore_block_train_walks_async(smore_ctx* ctx, int block);
+int smore_block_walk_records(smore_ctx* ctx, int block, uint64_t* n);
 
 /* ---- samplers (parity tests) -------------------------------------------------------- */
 /* replaces: SourceSample/TargetSample/NegativeSample (src/proNet.cpp:623-683):

@@ -733,6 +733,30 @@ int orc_train_edge_f32(const orc_graph* g, int model, float* W, float* C, int di
     return skipped;
 }
 
+/* LINE-2 / LINE-1 / MF over explicit sample records {v, c, n_1 .. n_K} (count
+ * x (2 + K), ids masked to 30 bits) in order: the update of
+ * orc_train_edge_f32 with record i taking the learning rate of global sample
+ * begin + i.  The records of the block schedule's cells (smore_block_sample_edges)
+ * are checked through it. */
+int orc_train_records_f32(int model, float* W, float* C, int dpad, const int32_t* rec, int64_t count, int K,
+                          double alpha0, double reg, uint64_t total, uint64_t begin) {
+    sig_init();
+    uint64_t base = (model == 2) ? 0 : 1;
+    float* e = (float*)malloc(sizeof(float) * dpad);
+    int32_t negs[MAX_SLOTS];
+    for (int64_t i = 0; i < count; ++i) {
+        const int32_t* r = rec + i * (2 + K);
+        int32_t v = r[0] & 0x3FFFFFFF, c = r[1];
+        if (c < 0) continue;
+        c &= 0x3FFFFFFF;
+        for (int j = 0; j < K; ++j) negs[j] = r[2 + j] & 0x3FFFFFFF;
+        float alpha = (float)orc_alpha_line(begin + (uint64_t)i + base, alpha0, total);
+        update_edge_f32(model, W, C, dpad, v, c, negs, K, alpha, (float)reg, e);
+    }
+    free(e);
+    return 0;
+}
+
 /* fp32 BPR (UpdateBPRPair, src/proNet.cpp:1406-1455).  Per round n, element
  * order as the reference's d-loop:
  *   x = wi - wj;  f = dot(wu, x);  g = sig(0 - f) * alpha   (0-f in fp64 == -f)

@@ -27,6 +27,8 @@ def sync_rule(sync):
 
 
 MODE = {"hogwild": 0, "atomic": 1, "serial": 2, "hybrid": 3}
+# multi-GPU schedules of the group (smore_hip.h SMORE_SCHED_*)
+SCHED = {"replicas": 0, "blocks": 1}
 SEM = {"cpp": 0, "go": 1}
 
 
@@ -139,6 +141,17 @@ def _load():
         "smore_census_end": (i32, [P, dbl]),
         "smore_set_walk_owner": (i32, [P, i64, i64]),
         "smore_walk_parts": (i32, [P, i32, P]),
+        "smore_group_set_schedule": (i32, [P, i32]),
+        "smore_block_setup": (i32, [P, i32, i32, i32, i32, i32]),
+        "smore_block_info": (i32, [P, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
+        "smore_block_bounds": (i32, [P, P, P]),
+        "smore_block_mass": (i32, [P, P]),
+        "smore_block_counts": (i32, [P, u64, P]),
+        "smore_block_train_edges_async": (i32, [P, i32, u64, u64, u64, i32, dbl, u64, i32]),
+        "smore_block_sample_edges": (i32, [P, i32, u64, u64, u64, i32, P]),
+        "smore_block_prepare_walks": (i32, [P, i32, u64, u64, i32, i32, i32, i32, i32, dbl, u64, P, u64, i32]),
+        "smore_block_train_walks_async": (i32, [P, i32]),
+        "smore_block_walk_records": (i32, [P, i32, C.POINTER(u64)]),
         "smore_save_weights": (i32, [P, i32, C.c_char_p, i32]),
         "smore_load_pretrain": (i32, [P, i32, C.c_char_p]),
     }

@@ -1,0 +1,579 @@
+// blocks.cpp -- the 2-D block schedule of the multi-GPU path (SURVEY.md 8e's
+// conflict-free fallback), one context's side: its draw tables,
+// its cell launches and, for the walk models, its bucketed round records.
+//
+// The reference trains one shared table pair with Hogwild threads
+// (src/model/LINE.cpp:160-191, src/model/DeepWalk.cpp:128-155).  Replicated
+// tables over N GPUs need an exchange that either loses samples' worth
+// (averaging) or overshoots (summing stale deltas).  Here no
+// row is ever replicated while it trains: GPU r owns the W rows of part r
+// (equal source mass), the C table is cut into nb = 2N blocks (equal negative
+// mass), and sub-round s trains cell (r, b = (2r + s) mod nb) on every GPU at
+// once -- disjoint W rows, disjoint C rows.  After a sub-round GPU r passes
+// block b to GPU r - 1, which trains it two sub-rounds later, so the transfer
+// has a whole sub-round to overlap (exchange.cpp group_rotate, dist.py
+// BlockSync).  The samples of a cell follow the one-GPU law restricted to the
+// cell (train_blocks.hip); a call's samples are spread over the cells in
+// proportion to their mass, so an epoch (nb sub-rounds) draws the one-GPU
+// law.  What changes is the order (cell by cell) and the negatives (drawn in
+// the context's block: the law restricted to the block; blocks have equal
+// negative mass).
+#include <cmath>
+#include <numeric>
+#include <thread>
+
+#include "ctx.h"
+
+using namespace smore_host;
+
+namespace {
+
+constexpr uint64_t WALK_ROUND_MAX = (uint64_t)1 << 18;   // walks per prepared block round
+
+int check_ctx(smore_ctx* c) {
+    if (!c) return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    if (c->device < 0) return fail(c, SMORE_ESTATE, "host-only context");
+    return SMORE_OK;
+}
+
+BlockArgs block_args(const smore_ctx* c) {
+    BlockArgs b{};
+    b.atoms = c->blk.d_atoms;
+    b.ntab = c->blk.d_ntab;
+    b.nb = c->blk.nb;
+    for (int k = 0; k <= c->blk.nb; ++k) b.cb[k] = (int32_t)c->blk.cb[k];
+    return b;
+}
+
+// the resident sample groups of this context's update launches (the hot
+// tags' M): the same grid the training calls use
+int64_t resident_groups(smore_ctx* c, bool walk, int K, int mode) {
+    EdgeArgs a{};
+    a.g = dev_graph(c);
+    a.dpad = c->dpad;
+    a.K = K;
+    a.model = SMORE_LINE2;
+    a.mode = mode;
+    a.count = (uint64_t)1 << 30;
+    a.alpha_rec = walk ? 1 : 0;
+    a.sh_rows = mode == SMORE_HYBRID ? std::min(c->sh_max, 8192 / std::max(1, c->dpad)) : 0;
+    return (int64_t)launch_grid(c, a) * (256 / lanes_of(c->dpad));
+}
+
+// per-block write-combined rows: the hottest hot C rows of each block under
+// the scaled C-row law (hot_pc), with the edge rule's staleness bound and
+// automatic drain interval (capi build_hot_maps)
+void block_sh_sets(smore_ctx* c, bool walk, std::vector<int2>& hash, std::vector<int32_t>& ids) {
+    auto& B = c->blk;
+    const int cap = B.mode == SMORE_HYBRID && !c->hot_small && !c->hot_c.empty()
+                        ? std::max(0, std::min(c->sh_max, 8192 / std::max(1, c->dpad)))
+                        : 0;
+    B.sh_cap = std::max(cap, 1);
+    B.sh_n.assign((size_t)B.nb, 0);
+    B.sh_flush.assign((size_t)B.nb, 8);
+    hash.assign((size_t)B.nb * SH_HASH, make_int2(-1, -1));
+    ids.assign((size_t)B.nb * B.sh_cap, -1);
+    if (cap == 0) return;
+    const double M = (double)c->hot_M, stale = sh_stale_max();
+    const int flush_cap = c->sh_flush > 0 ? c->sh_flush : sh_flush_max(walk);
+    for (int k = 0; k < B.nb; ++k) {
+        std::vector<std::pair<double, int32_t>> r;
+        for (int64_t x = B.cb[k]; x < B.cb[k + 1]; ++x)
+            if (c->hot_c[x] && M * c->hot_pc[x] * flush_cap <= stale) r.push_back({c->hot_pc[x], (int32_t)x});
+        const int64_t n = std::min<int64_t>(cap, (int64_t)r.size());
+        std::partial_sort(r.begin(), r.begin() + n, r.end(), [](const auto& x, const auto& y) {
+            return x.first > y.first || (x.first == y.first && x.second < y.second);
+        });
+        int2* h = hash.data() + (size_t)k * SH_HASH;
+        for (int64_t i = 0; i < n; ++i) {
+            ids[(size_t)k * B.sh_cap + i] = r[i].second;
+            uint32_t p = sh_hash_of(r[i].second);
+            while (h[p & (SH_HASH - 1)].x >= 0) ++p;
+            h[p & (SH_HASH - 1)] = make_int2(r[i].second, (int)i);
+        }
+        B.sh_n[k] = (int)n;
+        B.sh_flush[k] = c->sh_flush > 0 ? c->sh_flush : flush_cap;
+        if (c->sh_flush <= 0 && n > 0)
+            B.sh_flush[k] = (int)std::max(8.0, std::min((double)flush_cap, std::floor(sh_auto_budget() / (M * r[0].first))));
+    }
+}
+
+// the update-kernel arguments shared by a context's cell launches
+EdgeArgs cell_args(smore_ctx* c, int k, bool walk) {
+    const auto& B = c->blk;
+    EdgeArgs a{};
+    a.g = dev_graph(c);
+    a.sig = c->d_sig;
+    a.W = c->d_table[0];
+    a.C = c->d_table[1];
+    a.skipped = c->d_skipped;
+    a.dpad = c->dpad;
+    a.K = B.K;
+    a.model = SMORE_LINE2;
+    a.mode = B.mode;
+    a.alpha_rec = walk ? 1 : 0;
+    a.work = c->d_work;
+    const bool on = B.mode == SMORE_HYBRID && B.sh_n[k] > 0;
+    a.sh_rows = on ? B.sh_n[k] : 0;
+    a.sh_hash = B.d_sh_hash + (size_t)k * SH_HASH;
+    a.sh_ids = B.d_sh_ids + (size_t)k * B.sh_cap;
+    a.sh_flush = std::max(1, B.sh_flush[k]);
+    a.sh_flush_w = 0;
+    return a;
+}
+
+int grow_events(smore_ctx* c, std::vector<hipEvent_t>& v, size_t n) {
+    while (v.size() < n) {
+        hipEvent_t e;
+        HIPCHK(c, hipEventCreate(&e));
+        v.push_back(e);
+    }
+    return SMORE_OK;
+}
+
+}  // namespace
+
+namespace smore_host {
+void blocks_release(smore_ctx* c) {
+    auto& B = c->blk;
+    dfree(B.d_atoms);
+    dfree(B.d_ntab);
+    dfree(B.d_sh_hash);
+    dfree(B.d_sh_ids);
+    dfree(B.d_count);
+    dfree(B.d_off);
+    B = smore_ctx::Blocks{};
+}
+}  // namespace smore_host
+
+extern "C" {
+
+int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int mode) {
+    int rc;
+    if ((rc = check_ctx(c))) return rc;
+    if (model != SMORE_LINE2 && model != SMORE_CENSUS)
+        return fail(c, SMORE_EINVAL, "block schedule: LINE-2 (SMORE_LINE2) or the C++ walk models (SMORE_CENSUS)");
+    if (nparts < 1 || 2 * nparts > BLOCK_MAX || part < 0 || part >= nparts)
+        return fail(c, SMORE_EINVAL, "block schedule: 1 <= nparts <= 16, 0 <= part < nparts");
+    if (K < 0 || K > (model == SMORE_LINE2 ? 20 : 10) || mode < 0 || mode > 3)
+        return fail(c, SMORE_EINVAL, "block schedule: bad K / mode");
+    if (c->semantics != SMORE_SEM_CPP) return fail(c, SMORE_EINVAL, "block schedule: C++ rules only");
+    if (c->ntables < 2) return fail(c, SMORE_ESTATE, "block schedule: W and C tables needed");
+    if ((rc = set_device(c))) return rc;
+    const bool walk = model == SMORE_CENSUS;
+    if (nparts == 1) {
+        blocks_release(c);
+        return model == SMORE_LINE2 ? smore_set_source_partition(c, 1, 0) : SMORE_OK;
+    }
+    const HostGraph& g = *c->g;
+    const int64_t V = g.V;
+    const int nb = 2 * nparts;
+    if (V < nb) return fail(c, SMORE_EINVAL, "block schedule: fewer vertices than blocks");
+    char key[256];
+    snprintf(key, sizeof key, "%d/%d/%d/%d/%d/%lld/%lld/%d/%d/%d/%.9g/%s", model, nparts, part, K, mode, (long long)V,
+             (long long)g.E, c->dpad, c->sh_max, c->sh_flush, c->hot_tau, getenv("SMORE_SH_STALE") ? getenv("SMORE_SH_STALE") : "");
+    if (c->blk.key == key) return SMORE_OK;
+    blocks_release(c);
+    auto& B = c->blk;
+    B.n = nparts;
+    B.r = part;
+    B.nb = nb;
+    B.model = model;
+    B.K = K;
+    B.mode = mode;
+    std::vector<double> ps, pn, pc;
+    draw_probabilities(g, ps, pn, pc);
+    part_bounds(ps, nparts, B.wb);
+    part_bounds(pn, nb, B.cb);
+    for (int p = 0; p < nparts; ++p)
+        if (B.wb[p + 1] <= B.wb[p]) return fail(c, SMORE_EINVAL, "block schedule: an empty W part");
+    for (int k = 0; k < nb; ++k)
+        if (B.cb[k + 1] <= B.cb[k]) return fail(c, SMORE_EINVAL, "block schedule: an empty C block");
+    // LINE-2: this context's sources are its part's (the hot W tags follow the
+    // restricted law); walks: the walk ids carry the scaled global tags
+    if (!walk && (rc = smore_set_source_partition(c, nparts, part))) return rc;
+    if (mode == SMORE_HYBRID) {
+        const int64_t M = resident_groups(c, walk, K, mode);
+        if ((rc = hot_maps(c, SMORE_LINE2, K, M, walk, walk ? (double)nparts : 1.0, (double)nb))) return rc;
+    } else {
+        c->hot_c.clear();
+        c->hot_w.clear();
+        c->hot_pc.clear();
+        c->hot_small = false;
+    }
+    const bool tags = mode == SMORE_HYBRID && !c->hot_c.empty();
+    auto hc = [&](int64_t x) -> uint32_t { return tags ? c->hot_c[x] : 0u; };
+    auto hw = [&](int64_t x) -> uint32_t { return tags ? c->hot_w[x] : 0u; };
+    // negative tables: block k's law restricted to [cb[k], cb[k+1]) (Go alias
+    // rule, power 1: any exact encoding of the law), ids absolute
+    {
+        hvec<AliasEntry> nt((size_t)V);
+        std::vector<std::thread> th;
+        const int T = (int)std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), (unsigned)nb);
+        for (int t = 0; t < T; ++t)
+            th.emplace_back([&, t] {
+                for (int k = t; k < nb; k += T) {
+                    const int64_t lo = B.cb[k], n = B.cb[k + 1] - lo;
+                    std::vector<double> prob((size_t)n);
+                    std::vector<int64_t> alias((size_t)n);
+                    std::vector<int32_t> self((size_t)n);
+                    alias_go(pn.data() + lo, n, 1.0, prob.data(), alias.data());
+                    for (int64_t i = 0; i < n; ++i) {
+                        alias[i] += lo;
+                        self[i] = (int32_t)(lo + i);
+                    }
+                    alias_encode(prob.data(), alias.data(), n, self.data(), nt.data() + lo);
+                    for (int64_t i = 0; i < n; ++i) {
+                        const uint32_t al = (uint32_t)nt[lo + i].alias;
+                        nt[lo + i].alias = (int32_t)(al | (hc(al) << 30) | (hc(lo + i) << 31));
+                    }
+                }
+            });
+        for (auto& x : th) x.join();
+        if ((rc = upload(c, B.d_ntab, reinterpret_cast<const uint2*>(nt.data()), (size_t)V, true))) return rc;
+    }
+    // LINE-2 atoms of this part: the TargetSample outcomes of its sources,
+    // bucketed by the context's block, one alias table per block
+    B.mass.assign((size_t)nb, 0.0);
+    B.atom_off.assign((size_t)nb + 1, 0);
+    if (!walk) {
+        const int64_t lo = B.wb[part], hi = B.wb[part + 1];
+        auto blk_of = [&](int64_t x) {
+            return (int)(std::upper_bound(B.cb.begin(), B.cb.end(), x) - B.cb.begin()) - 1;
+        };
+        auto each_atom = [&](auto&& f) {
+            for (int64_t v = lo; v < hi; ++v) {
+                const int64_t off = g.offsets[v], br = g.offsets[v + 1] - off;
+                if (br == 0 || ps[v] <= 0) continue;
+                const double s = ps[v] / (double)br;
+                for (int64_t i = 0; i < br; ++i) {
+                    const double pr = g.cprob[off + i];
+                    f(v, (int64_t)g.targets[off + i], s * pr);
+                    if (g.calias[off + i] >= 0 && pr < 1.0) f(v, g.calias[off + i], s * (1.0 - pr));
+                }
+            }
+        };
+        std::vector<uint64_t> cnt((size_t)nb, 0);
+        each_atom([&](int64_t, int64_t x, double w) {
+            if (w > 0) cnt[blk_of(x)]++;
+        });
+        for (int k = 0; k < nb; ++k) B.atom_off[k + 1] = B.atom_off[k] + cnt[k];
+        const uint64_t A = B.atom_off[nb];
+        if (A == 0) return fail(c, SMORE_EINVAL, "block schedule: a part without edges");
+        std::vector<int32_t> av(A), ac(A);
+        std::vector<double> aw(A);
+        std::vector<uint64_t> pos(B.atom_off.begin(), B.atom_off.end() - 1);
+        each_atom([&](int64_t v, int64_t x, double w) {
+            if (w <= 0) return;
+            const uint64_t p = pos[blk_of(x)]++;
+            av[p] = (int32_t)v;
+            ac[p] = (int32_t)x;
+            aw[p] = w;
+        });
+        double tot = 0.0;
+        for (int k = 0; k < nb; ++k) {
+            double m = 0.0;
+            for (uint64_t p = B.atom_off[k]; p < B.atom_off[k + 1]; ++p) m += aw[p];
+            B.mass[k] = m;
+            tot += m;
+        }
+        for (double& m : B.mass) m /= tot;
+        hvec<uint4> at((size_t)A * 2);
+        std::vector<std::thread> th;
+        const int T = (int)std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), (unsigned)nb);
+        for (int t = 0; t < T; ++t)
+            th.emplace_back([&, t] {
+                for (int k = t; k < nb; k += T) {
+                    const uint64_t a0 = B.atom_off[k], n = B.atom_off[k + 1] - a0;
+                    if (n == 0) continue;
+                    std::vector<double> prob(n);
+                    std::vector<int64_t> alias(n);
+                    std::vector<AliasEntry> e(n);
+                    alias_go(aw.data() + a0, (int64_t)n, 1.0, prob.data(), alias.data());
+                    alias_encode(prob.data(), alias.data(), (int64_t)n, nullptr, e.data());
+                    for (uint64_t i = 0; i < n; ++i) {
+                        const uint64_t s = a0 + i, a = a0 + (uint64_t)e[i].alias;
+                        at[2 * s] = make_uint4(e[i].thresh, (uint32_t)av[s] | (hw(av[s]) << 30),
+                                               (uint32_t)ac[s] | (hc(ac[s]) << 30), 0u);
+                        at[2 * s + 1] = make_uint4((uint32_t)av[a] | (hw(av[a]) << 30),
+                                                   (uint32_t)ac[a] | (hc(ac[a]) << 30), 0u, 0u);
+                    }
+                }
+            });
+        for (auto& x : th) x.join();
+        if ((rc = upload(c, B.d_atoms, at.data(), at.size(), true))) return rc;
+    }
+    std::vector<int2> hash;
+    std::vector<int32_t> ids;
+    block_sh_sets(c, walk, hash, ids);
+    if ((rc = upload(c, B.d_sh_hash, hash.data(), hash.size()))) return rc;
+    if ((rc = upload(c, B.d_sh_ids, ids.data(), ids.size()))) return rc;
+    B.key = key;
+    return SMORE_OK;
+}
+
+int smore_block_info(const smore_ctx* c, int* nparts, int* part, int* nblocks) {
+    if (!c) return SMORE_EINVAL;
+    if (nparts) *nparts = c->blk.nb ? c->blk.n : 1;
+    if (part) *part = c->blk.nb ? c->blk.r : 0;
+    if (nblocks) *nblocks = c->blk.nb;
+    return SMORE_OK;
+}
+
+int smore_block_bounds(const smore_ctx* c, int64_t* wb, int64_t* cb) {
+    if (!c) return SMORE_EINVAL;
+    if (!c->blk.nb) return SMORE_ESTATE;
+    if (wb) std::copy(c->blk.wb.begin(), c->blk.wb.end(), wb);
+    if (cb) std::copy(c->blk.cb.begin(), c->blk.cb.end(), cb);
+    return SMORE_OK;
+}
+
+int smore_block_mass(const smore_ctx* c, double* mass) {
+    if (!c || !mass) return SMORE_EINVAL;
+    if (!c->blk.nb || c->blk.model != SMORE_LINE2) return SMORE_ESTATE;
+    std::copy(c->blk.mass.begin(), c->blk.mass.end(), mass);
+    return SMORE_OK;
+}
+
+int smore_block_counts(const smore_ctx* c, uint64_t samples, uint64_t* counts) {
+    if (!c || !counts) return SMORE_EINVAL;
+    if (!c->blk.nb || c->blk.model != SMORE_LINE2) return SMORE_ESTATE;
+    // largest remainder of samples * mass (ties to the lower block)
+    const auto& m = c->blk.mass;
+    const int nb = c->blk.nb;
+    std::vector<std::pair<double, int>> rem;
+    uint64_t used = 0;
+    for (int k = 0; k < nb; ++k) {
+        const double x = (double)samples * m[k];
+        counts[k] = (uint64_t)std::floor(x);
+        used += counts[k];
+        rem.push_back({x - std::floor(x), k});
+    }
+    std::stable_sort(rem.begin(), rem.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+    for (size_t i = 0; used < samples && i < rem.size(); ++i, ++used) counts[rem[i].second]++;
+    for (int k = 0; used < samples; k = (k + 1) % nb, ++used) counts[k]++;   // rounding slack (never in practice)
+    return SMORE_OK;
+}
+
+int smore_block_train_edges_async(smore_ctx* c, int block, uint64_t begin, uint64_t count, uint64_t total, int K,
+                                  double alpha0, uint64_t seed, int mode) {
+    int rc;
+    if ((rc = check_ctx(c))) return rc;
+    auto& B = c->blk;
+    if (!B.nb || B.model != SMORE_LINE2) return fail(c, SMORE_ESTATE, "no LINE-2 block setup (smore_block_setup)");
+    if (block < 0 || block >= B.nb) return fail(c, SMORE_EINVAL, "block out of range");
+    if (K != B.K || mode != B.mode) return fail(c, SMORE_EINVAL, "K / mode differ from smore_block_setup's");
+    if (total == 0) return fail(c, SMORE_EINVAL, "total == 0");
+    if (count == 0) return SMORE_OK;
+    if ((rc = set_device(c))) return rc;
+    const uint64_t na = B.atom_off[block + 1] - B.atom_off[block];
+    if (na == 0) return fail(c, SMORE_EINVAL, "block without atoms (mass 0) asked for samples");
+    EdgeArgs a = cell_args(c, block, false);
+    a.total = total;
+    a.seed = seed;
+    a.alpha0 = alpha0;
+    a.count = count;
+    const int grid = launch_grid(c, a);
+    BlockArgs ba = block_args(c);
+    ba.atom_off = B.atom_off[block];
+    ba.natoms = (uint32_t)na;
+    const int RW = rec_width(kmax_of(K));
+    const uint64_t chunk_max = mode == SMORE_SERIAL ? ((uint64_t)1 << 30) / (uint64_t)RW : (uint64_t)1 << 27;
+    const uint64_t chunk = std::min<uint64_t>(count, chunk_max);
+    const int nch = (int)((count + chunk - 1) / chunk);
+    if (c->rec_cap < chunk * RW) {
+        dfree(c->d_rec);
+        c->rec_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_rec, chunk * RW * sizeof(int32_t)));
+        c->rec_cap = chunk * RW;
+    }
+    if ((rc = grow_events(c, c->phase_ev, 2 * (size_t)nch + 1))) return rc;
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream));
+    for (int k = 0; k < nch; ++k) {
+        const uint64_t b = (uint64_t)k * chunk, n = std::min<uint64_t>(chunk, count - b);
+        if (k) HIPCHK(c, hipEventRecord(c->phase_ev[2 * k], c->stream));
+        HIPCHK(c, launch_block_draw(ba, block, seed, begin + b, n, K, c->d_rec, c->stream));
+        HIPCHK(c, hipEventRecord(c->phase_ev[2 * k + 1], c->stream));
+        EdgeArgs ak = a;
+        ak.begin = begin + b;
+        ak.count = n;
+        ak.rec = c->d_rec;
+        HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
+        HIPCHK(c, launch_edge_train(ak, grid, c->stream));
+        HIPCHK(c, hipEventRecord(c->phase_ev[2 * k + 2], c->stream));
+    }
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
+    c->phase_n = nch;
+    return SMORE_OK;
+}
+
+int smore_block_sample_edges(smore_ctx* c, int block, uint64_t seed, uint64_t begin, uint64_t count, int K,
+                             int32_t* out) {
+    int rc;
+    if ((rc = check_ctx(c))) return rc;
+    if (!out) return SMORE_EINVAL;
+    auto& B = c->blk;
+    if (!B.nb || B.model != SMORE_LINE2) return fail(c, SMORE_ESTATE, "no LINE-2 block setup (smore_block_setup)");
+    if (block < 0 || block >= B.nb || K < 0 || K > 20) return fail(c, SMORE_EINVAL, "bad block / K");
+    if (count == 0) return SMORE_OK;
+    if ((rc = set_device(c))) return rc;
+    BlockArgs ba = block_args(c);
+    ba.atom_off = B.atom_off[block];
+    ba.natoms = (uint32_t)(B.atom_off[block + 1] - B.atom_off[block]);
+    if (ba.natoms == 0) return fail(c, SMORE_EINVAL, "block without atoms");
+    const int RW = rec_width(kmax_of(K));
+    int32_t* d = nullptr;
+    HIPCHK(c, hipMalloc((void**)&d, count * RW * sizeof(int32_t)));
+    hipError_t e = launch_block_draw(ba, block, seed, begin, count, K, d, c->stream);
+    std::vector<int32_t> h(count * RW);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(h.data(), d, h.size() * sizeof(int32_t), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(c, SMORE_EHIP, std::string("block sample: ") + hipGetErrorString(e));
+    for (uint64_t t = 0; t < count; ++t)
+        for (int j = 0; j < 2 + K; ++j) out[t * (2 + K) + j] = h[t * RW + j] & ID_MASK;
+    return SMORE_OK;
+}
+
+int smore_block_prepare_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t walk_end, int walk_times,
+                              int walk_steps, int window, int window_min, int K, double alpha0, uint64_t seed,
+                              const int64_t* order, uint64_t order_base, int mode) {
+    int rc;
+    if ((rc = check_ctx(c))) return rc;
+    auto& B = c->blk;
+    if (!B.nb || B.model != SMORE_CENSUS) return fail(c, SMORE_ESTATE, "no walk block setup (smore_block_setup)");
+    if (K != B.K || mode != B.mode) return fail(c, SMORE_EINVAL, "K / mode differ from smore_block_setup's");
+    if (rule != 0 && rule != 1) return fail(c, SMORE_EINVAL, "block rounds: DeepWalk (0) or Walklets (1)");
+    if ((rule == 0 && !order) || walk_times <= 0 || walk_steps < 0 || window <= 0)
+        return fail(c, SMORE_EINVAL, "bad walk arguments");
+    if (rule == 1 && (window_min < 0 || window_min > window)) return fail(c, SMORE_EINVAL, "Walklets: bad window");
+    const uint64_t total = (uint64_t)walk_times * (uint64_t)c->g->V;
+    if (walk_end > total) walk_end = total;
+    B.walks = 0;
+    if (walk_begin >= walk_end) return SMORE_OK;
+    const uint64_t nw = walk_end - walk_begin;
+    if (nw > WALK_ROUND_MAX) return fail(c, SMORE_EINVAL, "a block round holds at most 2^18 walks");
+    if (order) {
+        if (walk_begin < order_base) return fail(c, SMORE_EINVAL, "walk order slice does not cover the range");
+        order -= order_base;
+        for (uint64_t i = walk_begin; i < walk_end; ++i)
+            if (order[i] < 0 || order[i] >= c->g->V) return fail(c, SMORE_EINVAL, "walk start out of range");
+    }
+    if ((rc = set_device(c))) return rc;
+    // the walk ids' tags: the scaled hot maps (a no-op when current)
+    if (mode == SMORE_HYBRID) {
+        const int64_t M = resident_groups(c, true, K, mode);
+        if ((rc = hot_maps(c, SMORE_LINE2, K, M, true, (double)B.n, (double)B.nb))) return rc;
+    }
+    if (order) {
+        if (c->order_cap < nw) {
+            dfree(c->d_order);
+            c->order_cap = 0;
+            HIPCHK(c, hipMalloc((void**)&c->d_order, nw * sizeof(int64_t)));
+            c->order_cap = nw;
+        }
+        HIPCHK(c, hipMemcpyAsync(c->d_order, order + walk_begin, nw * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+    }
+    const int RW = rec_width(kmax_of(K));
+    const uint64_t pb = std::max<uint64_t>(1, pair_bound(walk_steps, window, rule, window_min));
+    const size_t need = nw * (size_t)(walk_steps + 1);
+    if (c->walk_buf_n < need) {
+        dfree(c->d_walks);
+        c->walk_buf_n = 0;
+        HIPCHK(c, hipMalloc((void**)&c->d_walks, need * sizeof(int32_t)));
+        c->walk_buf_n = need;
+    }
+    if (c->walk_lens_n < nw) {
+        dfree(c->d_lens);
+        c->walk_lens_n = 0;
+        HIPCHK(c, hipMalloc((void**)&c->d_lens, nw * sizeof(int32_t)));
+        c->walk_lens_n = nw;
+    }
+    const size_t ncount = (size_t)B.nb * nw + 1;
+    if (B.count_cap < ncount) {
+        dfree(B.d_count);
+        dfree(B.d_off);
+        B.count_cap = 0;
+        HIPCHK(c, hipMalloc((void**)&B.d_count, ncount * sizeof(uint32_t)));
+        HIPCHK(c, hipMalloc((void**)&B.d_off, ncount * sizeof(uint64_t)));
+        B.count_cap = ncount;
+    }
+    if (c->rec_cap < nw * pb * RW) {
+        dfree(c->d_rec);
+        c->rec_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_rec, nw * pb * RW * sizeof(int32_t)));
+        c->rec_cap = nw * pb * RW;
+    }
+    WalkArgs w;
+    w.order = order ? c->d_order : nullptr;
+    w.order_base = walk_begin;
+    w.walks = c->d_walks;
+    w.lens = c->d_lens;
+    w.walk_begin = walk_begin;
+    w.nwalks = nw;
+    w.total_walks = total;
+    w.steps = walk_steps;
+    w.window = window;
+    w.rule = rule;
+    w.window_min = window_min;
+    w.inv_p = w.inv_q = 1.0;
+    w.wts = nullptr;
+    w.nbr_sorted = nullptr;
+    w.ntype = nullptr;
+    w.ttargets = nullptr;
+    w.toff = nullptr;
+    w.paths = nullptr;
+    w.path_off = nullptr;
+    w.ntypes = w.npaths = 0;
+    w.slot_extra = 0;
+    w.own_lo = (int32_t)B.wb[B.r];
+    w.own_hi = (int32_t)B.wb[B.r + 1];
+    const BlockArgs ba = block_args(c);
+    HIPCHK(c, launch_walk_gen(dev_graph(c), w, seed, c->stream));
+    HIPCHK(c, hipMemsetAsync(B.d_count + (ncount - 1), 0, sizeof(uint32_t), c->stream));
+    HIPCHK(c, launch_block_pair_count(w, ba, seed, B.d_count, c->stream));
+    HIPCHK(c, scan_pair_counts(B.d_count, B.d_off, ncount, &c->d_scan_tmp, &c->scan_tmp_bytes, c->stream));
+    HIPCHK(c, launch_block_pair_emit(w, ba, seed, K, alpha0, B.d_off, c->d_rec, c->stream));
+    B.walks = nw;
+    B.rec_bound = nw * pb;
+    return SMORE_OK;
+}
+
+int smore_block_train_walks_async(smore_ctx* c, int block) {
+    int rc;
+    if ((rc = check_ctx(c))) return rc;
+    auto& B = c->blk;
+    if (!B.nb || B.model != SMORE_CENSUS) return fail(c, SMORE_ESTATE, "no walk block setup (smore_block_setup)");
+    if (block < 0 || block >= B.nb) return fail(c, SMORE_EINVAL, "block out of range");
+    if (!B.walks) return SMORE_OK;   // an empty round
+    if ((rc = set_device(c))) return rc;
+    EdgeArgs a = cell_args(c, block, true);
+    a.total = 1;
+    a.rec = c->d_rec;
+    a.count = B.rec_bound;   // the grid's bound; the launch reads its range on the device
+    a.rec_base = B.d_off + (size_t)block * B.walks;
+    a.count_dev = B.d_off + (size_t)(block + 1) * B.walks;
+    const int grid = B.mode == SMORE_SERIAL ? 1 : launch_grid(c, a);
+    HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
+    HIPCHK(c, launch_edge_train(a, grid, c->stream));
+    return SMORE_OK;
+}
+
+int smore_block_walk_records(smore_ctx* c, int block, uint64_t* n) {
+    if (!c || !n) return SMORE_EINVAL;
+    auto& B = c->blk;
+    if (!B.nb || B.model != SMORE_CENSUS || block < 0 || block >= B.nb) return SMORE_EINVAL;
+    *n = 0;
+    if (!B.walks) return SMORE_OK;
+    uint64_t lo = 0, hi = 0;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(&lo, B.d_off + (size_t)block * B.walks, sizeof lo, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(&hi, B.d_off + (size_t)(block + 1) * B.walks, sizeof hi, hipMemcpyDeviceToHost));
+    *n = hi - lo;
+    return SMORE_OK;
+}
+
+}  // extern "C"

@@ -64,6 +64,7 @@ void smore_destroy(smore_ctx* c) {
     dfree(c->d_order); dfree(c->d_walks); dfree(c->d_lens); dfree(c->d_tcum); dfree(c->d_wts); dfree(c->d_nbr_sorted); dfree(c->d_ntype); dfree(c->d_ttargets); dfree(c->d_toff); dfree(c->d_paths); dfree(c->d_path_off); dfree(c->d_t_off); dfree(c->d_t_tgt); dfree(c->d_t_ts); dfree(c->d_t_min); dfree(c->d_t_max); dfree(c->d_sh_hash); dfree(c->d_sh_ids);
     dfree(c->d_rec); dfree(c->d_vt32); dfree(c->d_ct16);
     dfree(c->d_pcount); dfree(c->d_poff); dfree(c->d_pairs); dfree(c->d_census[0]); dfree(c->d_census[1]);
+    blocks_release(c);
     if (c->d_scan_tmp) (void)hipFree(c->d_scan_tmp);
     for (hipEvent_t e : c->phase_ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -450,8 +451,14 @@ constexpr double HOT_TAU_EDGE = 1.0, HOT_TAU_WALK = 0.3;
 // atomic 0.5276 / 0.9844 in 6.98 s (profiles/r04/walk_combine.jsonl)
 constexpr int EDGE_FLUSH_MAX = 32, PAIR_FLUSH_MAX = 8;
 
+// w_scale / c_scale (the 2-D block schedule, blocks.cpp): a launch then
+// draws its W rows from one part of N and its C rows from one block of 2N, so
+// the rows it touches are about N / 2N times as likely per sample as under
+// the global law; the tags and the write-combined set follow the scaled law.
+// The C-row law and the flags are kept on the host (hot_pc, hot_c) for the
+// block tables' own tags and write-combined sets.
 static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_default,
-                          int flush_max = EDGE_FLUSH_MAX) {
+                          int flush_max = EDGE_FLUSH_MAX, double w_scale = 1.0, double c_scale = 1.0) {
     // Small graphs (the V/16 concurrency cap binds: 16 M >= V, e.g. the test
     // graphs, never C2-C5): with the default threshold every touched row is
     // hot and nothing is write-combined, i.e. the hybrid is the lossless
@@ -477,8 +484,9 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_
     // default 8; 0 = with the context rows)
     const char* wflush_env = getenv("SMORE_SH_WFLUSH");
     const int wflush = wrows ? (wflush_env ? std::max(0, atoi(wflush_env)) : 8) : 0;
-    snprintf(key, sizeof key, "%d/%d/%lld/%.9g/%d/%d/%s/%d/%d/%d/%d/%d", model, K, (long long)M, tau, c->sh_max,
-             c->sh_flush, stale_env ? stale_env : "", (int)wrows, c->part_n, c->part_i, flush_max, wflush);
+    snprintf(key, sizeof key, "%d/%d/%lld/%.9g/%d/%d/%s/%d/%d/%d/%d/%d/%g/%g", model, K, (long long)M, tau, c->sh_max,
+             c->sh_flush, stale_env ? stale_env : "", (int)wrows, c->part_n, c->part_i, flush_max, wflush, w_scale,
+             c_scale);
     if (c->hot_key == key) return SMORE_OK;
     if (c->g->V >= ((int64_t)1 << 30)) return fail(c, SMORE_EINVAL, "hybrid scatter needs V < 2^30");
     std::vector<double> ps, pn, pc;
@@ -496,7 +504,7 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_
     c->hot_rows[0] = c->hot_rows[1] = 0;
     for (int64_t v = 0; v < V; ++v) {
         double pw, pcx;
-        if (model == SMORE_LINE2) { pw = ps[v]; pcx = pc[v] + negs * pn[v]; }
+        if (model == SMORE_LINE2) { pw = ps[v] * w_scale; pcx = (pc[v] + negs * pn[v]) * c_scale; }
         else { pw = pcx = ps[v] + pc[v] + negs * pn[v]; }
         if ((double)M * pw > tau) { hw[v] = 1; c->hot_rows[0]++; }
         if ((double)M * pcx > tau) { hc[v] = 1; c->hot_rows[1]++; }
@@ -508,7 +516,7 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_
         std::vector<std::pair<double, int32_t>> r;
         const int flush_cap = c->sh_flush > 0 ? c->sh_flush : flush_max;
         for (int64_t v = 0; v < V; ++v) {
-            const double p = model == SMORE_LINE2 ? pc[v] + negs * pn[v] : ps[v] + pc[v] + negs * pn[v];
+            const double p = model == SMORE_LINE2 ? (pc[v] + negs * pn[v]) * c_scale : ps[v] + pc[v] + negs * pn[v];
             // bounded staleness: a combined row's pending deltas are invisible to
             // other workgroups for up to sh_flush rounds, i.e. about
             // M * p * sh_flush updates; rows above SH_STALE_MAX stay on atomics
@@ -516,8 +524,9 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_
             if (hc[v] && (double)M * p * flush_cap <= stale_max) r.push_back({p, (int32_t)v});
             // two tables (SMORE_SH_WROWS=1 only): the hub W rows compete for
             // the same slots (key v | SH_WKEY)
-            if (wrows && model == SMORE_LINE2 && hw[v] && (double)M * ps[v] * (wflush ? wflush : flush_cap) <= stale_max)
-                r.push_back({ps[v], (int32_t)(v | SH_WKEY)});
+            if (wrows && model == SMORE_LINE2 && hw[v] &&
+                (double)M * ps[v] * w_scale * (wflush ? wflush : flush_cap) <= stale_max)
+                r.push_back({ps[v] * w_scale, (int32_t)(v | SH_WKEY)});
         }
         const int64_t cap =
             small ? 0 : std::max<int64_t>(0, std::min<int64_t>(c->sh_max, 8192 / std::max(1, c->dpad)));
@@ -586,6 +595,14 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_
     }
     c->hot_key = key;
     c->packed_ok = false;
+    // the C-row law and flags for the block tables (blocks.cpp)
+    c->hot_c.assign(hc.begin(), hc.end());
+    c->hot_w.assign(hw.begin(), hw.end());
+    c->hot_pc.resize((size_t)V);
+    for (int64_t v = 0; v < V; ++v)
+        c->hot_pc[v] = model == SMORE_LINE2 ? (pc[v] + negs * pn[v]) * c_scale : ps[v] + pc[v] + negs * pn[v];
+    c->hot_M = M;
+    c->hot_small = small;
     return SMORE_OK;
 }
 
@@ -1812,3 +1829,19 @@ int smore_delta_cycle_rows(smore_ctx* c, void* T, void* S, void* D, void* R, con
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- shared with blocks.cpp
+namespace smore_host {
+void part_bounds(const std::vector<double>& ps, int n, std::vector<int64_t>& bound) { source_bounds(ps, n, bound); }
+int hot_maps(smore_ctx* c, int model, int K, int64_t M, bool walk, double w_scale, double c_scale) {
+    return build_hot_maps(c, model, K, M, walk ? HOT_TAU_WALK : HOT_TAU_EDGE, walk ? PAIR_FLUSH_MAX : EDGE_FLUSH_MAX,
+                          w_scale, c_scale);
+}
+int launch_grid(smore_ctx* c, const EdgeArgs& a) { return edge_grid(c, a, false, 0); }
+int sh_flush_max(bool walk) { return walk ? PAIR_FLUSH_MAX : EDGE_FLUSH_MAX; }
+double sh_stale_max() {
+    const char* e = getenv("SMORE_SH_STALE");
+    return e ? atof(e) : SH_STALE_MAX;
+}
+double sh_auto_budget() { return SH_AUTO_BUDGET; }
+}  // namespace smore_host

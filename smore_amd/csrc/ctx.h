@@ -150,12 +150,45 @@ struct smore_ctx {
     // caller-supplied pairs (smore_train_pairs): a chunk of (v, c) on the device
     int32_t* d_pairs = nullptr;
     size_t pairs_cap = 0;               // pairs
+    // the last hybrid hot maps' host side (capi build_hot_maps): row flags and
+    // the C-row touch law they were made from, for the block tables' own tags
+    std::vector<uint8_t> hot_c, hot_w;
+    std::vector<double> hot_pc;
+    int64_t hot_M = 0;
+    bool hot_small = false;
+    // 2-D block schedule (blocks.cpp): this context is part r of
+    // N W parts; the C table is cut into nb = 2N blocks; a launch trains one
+    // (part r, block b) cell from the cell's own draw tables
+    struct Blocks {
+        int n = 1, r = 0, nb = 0;       // nb 0: off
+        int model = -1, K = 0, mode = -1;
+        std::vector<int64_t> wb, cb;    // W part bounds (n + 1), C block bounds (nb + 1)
+        std::vector<double> mass;       // LINE-2: this part's sample mass per C block (sums to 1)
+        std::vector<uint64_t> atom_off; // LINE-2: first atom of each block (nb + 1)
+        uint4* d_atoms = nullptr;       // LINE-2: 2 uint4 per atom {thr, v, c, 0}, {v', c', 0, 0}
+        uint2* d_ntab = nullptr;        // V entries: block b's negative alias at [cb[b], cb[b+1])
+        int2* d_sh_hash = nullptr;      // nb x SH_HASH: per-block write-combined rows
+        int32_t* d_sh_ids = nullptr;    // nb x sh_cap
+        int sh_cap = 0;
+        std::vector<int> sh_n, sh_flush;
+        std::string key;
+        // walk records of the current round, bucketed by C block: per (block,
+        // walk) counts and their exclusive scan (nb * walks + 1)
+        uint32_t* d_count = nullptr;
+        uint64_t* d_off = nullptr;
+        size_t count_cap = 0;
+        uint64_t walks = 0;             // walks of the prepared round (0: none)
+        uint64_t rec_bound = 0;         // records the prepared round may hold
+    } blk;
 };
 
 // exchange.cpp: frees the exchange buffers and the communicator
 void smore_exchange_release(smore_ctx* c);
 
 namespace smore_host {
+
+// blocks.cpp: frees the block tables (a new graph, smore_destroy)
+void blocks_release(smore_ctx* c);
 
 inline int fail(smore_ctx* c, int code, const std::string& msg) {
     if (c) c->err = msg;
@@ -229,6 +262,7 @@ inline int upload_graph(smore_ctx* c) {
     c->census_rate[1].clear();
     dfree(c->d_census[0]);
     dfree(c->d_census[1]);
+    blocks_release(c);
     if (c->device < 0) {
         c->has_graph = true;
         return SMORE_OK;
@@ -272,6 +306,13 @@ inline DevGraph dev_graph(const smore_ctx* c) {
     return d;
 }
 
+// capi.cpp helpers shared with blocks.cpp
+void part_bounds(const std::vector<double>& ps, int n, std::vector<int64_t>& bound);
+int hot_maps(smore_ctx* c, int model, int K, int64_t M, bool walk, double w_scale, double c_scale);
+int launch_grid(smore_ctx* c, const EdgeArgs& a);
+int sh_flush_max(bool walk);
+double sh_stale_max();
+double sh_auto_budget();
 inline float* table_ptr(smore_ctx* c, int which) {
     if (which < 0 || which > 1) return nullptr;
     return c->d_table[which];

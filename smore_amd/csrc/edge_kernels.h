@@ -566,7 +566,10 @@ edge_train_kernel(EdgeArgs a) {
     const ShState sh = block_setup<MODE>(a, s_sig, s_dyn, sh_ids);
 
     const int lane = threadIdx.x & (G - 1);
-    const uint64_t count = a.count_dev ? *a.count_dev : a.count;   // records of this launch
+    // records of this launch: [0, count) of a.rec, or a block bucket [*rec_base, *count_dev)
+    const uint64_t rb = a.rec_base ? *a.rec_base : 0;
+    const uint64_t count = (a.count_dev ? *a.count_dev : a.count) - rb;
+    const int32_t* const recs = a.rec + rb * (uint64_t)rec_width(KMAX);
     const uint64_t gpb = blockDim.x / G;                 // groups per block
     uint64_t r0 = (uint64_t)blockIdx.x * gpb;            // block-uniform round base
     const uint64_t gib = threadIdx.x / G;
@@ -637,7 +640,7 @@ edge_train_kernel(EdgeArgs a) {
         // serial: records in order, gather after the previous sample's scatter
         constexpr int RW = rec_width(KMAX);
         for (; r0 < count; ++r0) {
-            const i32x4* p = reinterpret_cast<const i32x4*>(a.rec + r0 * RW);
+            const i32x4* p = reinterpret_cast<const i32x4*>(recs + r0 * RW);
             i32x4 r[RW / 4];
 #pragma unroll
             for (int q = 0; q < RW / 4; ++q) r[q] = p[q];
@@ -686,7 +689,7 @@ edge_train_kernel(EdgeArgs a) {
 #pragma unroll
             for (int q = 0; q < RW / 4; ++q) r[q] = i32x4{-1, -1, -1, -1};
             if (t < lim) {
-                const i32x4* p = reinterpret_cast<const i32x4*>(a.rec + t * RW);
+                const i32x4* p = reinterpret_cast<const i32x4*>(recs + t * RW);
 #pragma unroll
                 for (int q = 0; q < RW / 4; ++q) r[q] = __builtin_nontemporal_load(p + q);
             }
@@ -801,11 +804,13 @@ pair_train_kernel(EdgeArgs a) {
     int32_t* sh_ids = nullptr;
     const ShState sh = block_setup<MODE>(a, s_sig, s_dyn, sh_ids);
     const int lane = threadIdx.x & (G - 1);
-    const uint64_t count = a.count_dev ? *a.count_dev : a.count;
+    constexpr int RW = rec_width(KMAX);
+    const uint64_t rb = a.rec_base ? *a.rec_base : 0;   // a block bucket: [*rec_base, *count_dev)
+    const uint64_t count = (a.count_dev ? *a.count_dev : a.count) - rb;
+    const int32_t* const recs = a.rec + rb * (uint64_t)RW;
     const uint64_t gpb = blockDim.x / G, gib = threadIdx.x / G;
     bool ev[M];
     row_valid<G, M>(ev, lane, a.dpad);
-    constexpr int RW = rec_width(KMAX);
     uint32_t round = 0;
     __shared__ uint64_t s_next;
     const uint64_t span = CH_ROUNDS * gpb;
@@ -827,7 +832,7 @@ pair_train_kernel(EdgeArgs a) {
 #pragma unroll
             for (int q = 0; q < RW / 4; ++q) r[q] = i32x4{-1, -1, -1, -1};
             if (t < s1) {
-                const i32x4* p = reinterpret_cast<const i32x4*>(a.rec + t * RW);
+                const i32x4* p = reinterpret_cast<const i32x4*>(recs + t * RW);
 #pragma unroll
                 for (int q = 0; q < RW / 4; ++q) r[q] = __builtin_nontemporal_load(p + q);
             }

@@ -44,6 +44,8 @@ struct Rccl {
     decltype(&ncclCommDestroy) destroy = nullptr;
     decltype(&ncclAllReduce) all_reduce = nullptr;
     decltype(&ncclBroadcast) broadcast = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
     decltype(&ncclGroupStart) group_start = nullptr;
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
@@ -73,6 +75,8 @@ Rccl* rccl() {
         SMORE_SYM(destroy, ncclCommDestroy)
         SMORE_SYM(all_reduce, ncclAllReduce)
         SMORE_SYM(broadcast, ncclBroadcast)
+        SMORE_SYM(send, ncclSend)
+        SMORE_SYM(recv, ncclRecv)
         SMORE_SYM(group_start, ncclGroupStart)
         SMORE_SYM(group_end, ncclGroupEnd)
         SMORE_SYM(error_string, ncclGetErrorString)
@@ -282,6 +286,11 @@ struct smore_group {
     bool local = false;
     std::vector<hipEvent_t> lev;   // one per replica
     hipEvent_t ldone = nullptr;
+    // the 2-D block schedule (smore_group_set_schedule): per replica the
+    // compute-done event of a sub-round and the receive-done events of the
+    // last two rotations (by sub-round parity)
+    int schedule = SMORE_SCHED_REPLICAS;
+    std::vector<hipEvent_t> bdone, brecv;
 };
 
 namespace {
@@ -488,6 +497,208 @@ int group_sync(smore_group* g) {
     return SMORE_OK;
 }
 
+// ---- the 2-D block schedule's group side (blocks.cpp holds one replica's):
+// sub-round s trains cell (r, (2r + s) mod nb) on replica r; after it replica
+// r sends that C block to r - 1, which trains it at sub-round s + 2, and
+// receives the block r + 1 just trained.  Replica r's stream waits for the
+// receive of the rotation two sub-rounds back before its sub-round, so a
+// transfer overlaps one whole sub-round.  No row is replicated while it
+// trains: nothing is all-reduced.
+int ensure_block_events(smore_group* g) {
+    const size_t n = g->ctx.size();
+    if (g->bdone.size() == n) return SMORE_OK;
+    g->bdone.assign(n, nullptr);
+    g->brecv.assign(2 * n, nullptr);
+    for (size_t r = 0; r < n; ++r) {
+        smore_ctx* c = g->ctx[r];
+        int rc;
+        if ((rc = set_device(c))) return gfail(g, (int)r, rc);
+        if (!c->comm_stream && hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking) != hipSuccess)
+            return gfail(g, (int)r, fail(c, SMORE_EHIP, "block schedule: comm stream"));
+        for (hipEvent_t* e : {&g->bdone[r], &g->brecv[2 * r], &g->brecv[2 * r + 1]})
+            if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess)
+                return gfail(g, (int)r, fail(c, SMORE_EHIP, "block schedule: events"));
+    }
+    return SMORE_OK;
+}
+
+float* block_rows(smore_ctx* c, int b) { return c->d_table[1] + (size_t)c->blk.cb[b] * c->dpad; }
+size_t block_floats(const smore_ctx* c, int b) { return (size_t)(c->blk.cb[b + 1] - c->blk.cb[b]) * c->dpad; }
+
+int group_rotate(smore_group* g, uint64_t s) {
+    const size_t n = g->ctx.size();
+    const int nb = 2 * (int)n;
+    for (size_t r = 0; r < n; ++r) {
+        smore_ctx* c = g->ctx[r];
+        (void)hipSetDevice(c->device);
+        if (hipEventRecord(g->bdone[r], c->stream) != hipSuccess)
+            return gfail(g, (int)r, fail(c, SMORE_EHIP, "block rotation: event"));
+    }
+    if (g->local) {
+        for (size_t r = 0; r < n; ++r) {
+            smore_ctx *c = g->ctx[r], *d = g->ctx[(r + n - 1) % n];
+            const int b = (int)((2 * r + s) % (uint64_t)nb);
+            hipEvent_t done = g->brecv[2 * ((r + n - 1) % n) + (s & 1)];
+            if (hipStreamWaitEvent(d->comm_stream, g->bdone[r], 0) != hipSuccess ||
+                hipMemcpyAsync(block_rows(d, b), block_rows(c, b), block_floats(c, b) * sizeof(float),
+                               hipMemcpyDeviceToDevice, d->comm_stream) != hipSuccess ||
+                hipEventRecord(done, d->comm_stream) != hipSuccess)
+                return gfail(g, (int)r, fail(c, SMORE_EHIP, "block rotation: local copy"));
+        }
+        return SMORE_OK;
+    }
+    Rccl* L = rccl();
+    for (size_t r = 0; r < n; ++r) {
+        (void)hipSetDevice(g->ctx[r]->device);
+        if (hipStreamWaitEvent(g->ctx[r]->comm_stream, g->bdone[r], 0) != hipSuccess)
+            return gfail(g, (int)r, fail(g->ctx[r], SMORE_EHIP, "block rotation: wait"));
+    }
+    ncclResult_t nr = L->group_start();
+    for (size_t r = 0; r < n && nr == ncclSuccess; ++r) {
+        smore_ctx* c = g->ctx[r];
+        (void)hipSetDevice(c->device);
+        const int b = (int)((2 * r + s) % (uint64_t)nb), b2 = (b + 2) % nb;
+        nr = L->send(block_rows(c, b), block_floats(c, b), ncclFloat32, (int)((r + n - 1) % n), (ncclComm_t)c->comm,
+                     c->comm_stream);
+        if (nr == ncclSuccess)
+            nr = L->recv(block_rows(c, b2), block_floats(c, b2), ncclFloat32, (int)((r + 1) % n), (ncclComm_t)c->comm,
+                         c->comm_stream);
+    }
+    ncclResult_t ne = L->group_end();
+    if (nr == ncclSuccess) nr = ne;
+    if (nr != ncclSuccess) return gfail(g, 0, nccl_fail(g->ctx[0], "block rotation ncclSend/ncclRecv", nr));
+    for (size_t r = 0; r < n; ++r) {
+        (void)hipSetDevice(g->ctx[r]->device);
+        if (hipEventRecord(g->brecv[2 * r + (s & 1)], g->ctx[r]->comm_stream) != hipSuccess)
+            return gfail(g, (int)r, fail(g->ctx[r], SMORE_EHIP, "block rotation: event"));
+    }
+    return SMORE_OK;
+}
+
+// replica r's stream waits for the block it trains at sub-round s
+int block_wait(smore_group* g, size_t r, uint64_t s) {
+    if (s < 2) return SMORE_OK;
+    smore_ctx* c = g->ctx[r];
+    (void)hipSetDevice(c->device);
+    if (hipStreamWaitEvent(c->stream, g->brecv[2 * r + (s & 1)], 0) != hipSuccess)
+        return gfail(g, (int)r, fail(c, SMORE_EHIP, "block schedule: wait"));
+    return SMORE_OK;
+}
+
+// after the last rotation: every transfer done before the tables are read;
+// then every replica gets the W parts from their owners and the C blocks from
+// their holders (after S sub-rounds block b sits on replica ((b - S) mod nb) / 2)
+int block_finish(smore_group* g, uint64_t S) {
+    const size_t n = g->ctx.size();
+    const int nb = 2 * (int)n;
+    int rc;
+    for (size_t r = 0; r < n; ++r) {
+        smore_ctx* c = g->ctx[r];
+        (void)hipSetDevice(c->device);
+        for (size_t q = 0; q < n; ++q) {
+            if (!g->local && q != r) continue;   // RCCL: own transfers (send and receive) on own comm stream
+            if (hipStreamWaitEvent(c->stream, g->brecv[2 * q], 0) != hipSuccess ||
+                hipStreamWaitEvent(c->stream, g->brecv[2 * q + 1], 0) != hipSuccess)
+                return gfail(g, (int)r, fail(c, SMORE_EHIP, "block schedule: drain"));
+        }
+    }
+    const std::vector<hipStream_t> st = compute_streams(g);
+    smore_ctx* c0 = g->ctx[0];
+    for (size_t p = 0; p < n; ++p) {
+        std::vector<float*> rows;
+        for (smore_ctx* c : g->ctx) rows.push_back(c->d_table[0] + (size_t)c0->blk.wb[p] * c->dpad);
+        if ((rc = coll_broadcast(g, rows, (size_t)(c0->blk.wb[p + 1] - c0->blk.wb[p]) * c0->dpad, (int)p, st,
+                                 "W parts ncclBroadcast")))
+            return rc;
+    }
+    for (int b = 0; b < nb; ++b) {
+        const int holder = (int)(((uint64_t)b + (uint64_t)nb - S % (uint64_t)nb) % (uint64_t)nb) / 2;
+        std::vector<float*> rows;
+        for (smore_ctx* c : g->ctx) rows.push_back(block_rows(c, b));
+        if ((rc = coll_broadcast(g, rows, block_floats(c0, b), holder, st, "C blocks ncclBroadcast"))) return rc;
+    }
+    return group_sync(g);
+}
+
+// samples per row per replica per epoch of the LINE-2 block schedule (the C4
+// bench's one epoch per 2^27-sample step: 13.4 per row)
+constexpr double EDGE_BLOCK_PER_ROW = 13.42;
+constexpr uint64_t WALK_BLOCK_ROUND = (uint64_t)1 << 18;   // walks per epoch (blocks.cpp's round cap)
+
+int group_block_edges(smore_group* g, uint64_t begin, uint64_t count, uint64_t per, uint64_t total, int K,
+                      double alpha0, uint64_t seed, int mode) {
+    const size_t n = g->ctx.size();
+    const int nb = 2 * (int)n;
+    int rc;
+    if (count == 0) return SMORE_OK;
+    for (size_t r = 0; r < n; ++r)
+        if ((rc = smore_block_setup(g->ctx[r], SMORE_LINE2, (int)n, (int)r, K, mode))) return gfail(g, (int)r, rc);
+    if ((rc = ensure_block_events(g))) return rc;
+    const int64_t V = g->ctx[0]->g->V;
+    if (per == 0)
+        per = (uint64_t)std::min(134217728.0, std::max(1024.0 * nb, std::round(EDGE_BLOCK_PER_ROW * (double)V)));
+    const uint64_t round_units = per > count / n ? count : per * (uint64_t)n;
+    const uint64_t rounds = (count + round_units - 1) / round_units;
+    auto round_lo = [&](uint64_t k) { return (uint64_t)(((unsigned __int128)count * k) / rounds); };
+    std::vector<std::vector<uint64_t>> cnt(n, std::vector<uint64_t>((size_t)nb));
+    std::vector<uint64_t> cur(n);
+    uint64_t S = 0;
+    for (uint64_t k = 0; k < rounds; ++k) {
+        const uint64_t lo = round_lo(k), m = round_lo(k + 1) - lo;
+        for (size_t r = 0; r < n; ++r) {
+            const uint64_t b = lo + (uint64_t)(((unsigned __int128)m * r) / n);
+            const uint64_t e = lo + (uint64_t)(((unsigned __int128)m * (r + 1)) / n);
+            if ((rc = smore_block_counts(g->ctx[r], e - b, cnt[r].data()))) return gfail(g, (int)r, rc);
+            cur[r] = b;
+        }
+        for (int s = 0; s < nb; ++s, ++S) {
+            for (size_t r = 0; r < n; ++r) {
+                const int bk = (int)((2 * r + (size_t)s) % (size_t)nb);
+                if ((rc = block_wait(g, r, S))) return rc;
+                const uint64_t x = cnt[r][bk];
+                if (x && (rc = smore_block_train_edges_async(g->ctx[r], bk, begin + cur[r], x, total, K, alpha0,
+                                                             seed, mode)))
+                    return gfail(g, (int)r, rc);
+                cur[r] += x;
+            }
+            if ((rc = group_rotate(g, S))) return rc;
+        }
+    }
+    return block_finish(g, S);
+}
+
+int group_block_walks(smore_group* g, int rule, uint64_t walk_begin, uint64_t walk_end, int walk_times,
+                      int walk_steps, int window, int window_min, int K, double alpha0, uint64_t seed,
+                      const int64_t* order, int mode, uint64_t per) {
+    const size_t n = g->ctx.size();
+    const int nb = 2 * (int)n;
+    int rc;
+    const uint64_t total = (uint64_t)walk_times * (uint64_t)g->ctx[0]->g->V;
+    if (walk_end > total) walk_end = total;
+    if (walk_begin >= walk_end) return SMORE_OK;
+    for (size_t r = 0; r < n; ++r)
+        if ((rc = smore_block_setup(g->ctx[r], SMORE_CENSUS, (int)n, (int)r, K, mode))) return gfail(g, (int)r, rc);
+    if ((rc = ensure_block_events(g))) return rc;
+    if (per == 0 || per > WALK_BLOCK_ROUND) per = WALK_BLOCK_ROUND;
+    uint64_t S = 0;
+    for (uint64_t lo = walk_begin; lo < walk_end; lo += per) {
+        const uint64_t hi = std::min(walk_end, lo + per);
+        for (size_t r = 0; r < n; ++r)
+            if ((rc = smore_block_prepare_walks(g->ctx[r], rule, lo, hi, walk_times, walk_steps, window, window_min, K,
+                                                alpha0, seed, order, 0, mode)))
+                return gfail(g, (int)r, rc);
+        for (int s = 0; s < nb; ++s, ++S) {
+            for (size_t r = 0; r < n; ++r) {
+                if ((rc = block_wait(g, r, S))) return rc;
+                if ((rc = smore_block_train_walks_async(g->ctx[r], (int)((2 * r + (size_t)s) % (size_t)nb))))
+                    return gfail(g, (int)r, rc);
+            }
+            if ((rc = group_rotate(g, S))) return rc;
+        }
+    }
+    return block_finish(g, S);
+}
+
 }  // namespace
 
 // The group training round structure.  The range [begin, end) is cut into
@@ -629,6 +840,12 @@ static int group_rounds(smore_group* g, uint64_t begin, uint64_t end, uint64_t p
     for (size_t r = 0; walkpart && r < n; ++r)
         if ((rc = smore_set_walk_owner(g->ctx[r], 0, -1))) return gfail(g, (int)r, rc);
     return SMORE_OK;
+}
+
+// the block schedule applies: asked for, and the C++ rules (the Go rules keep
+// the replicas)
+static bool blocks_for(const smore_group* g) {
+    return g->schedule == SMORE_SCHED_BLOCKS && g->ctx[0]->semantics == SMORE_SEM_CPP;
 }
 
 // the census key of a walk-model call: the model and every argument that
@@ -774,6 +991,10 @@ void smore_group_destroy(smore_group* g) {
             if (cm) (void)L->destroy(cm);
     for (hipEvent_t e : g->lev)
         if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : g->bdone)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : g->brecv)
+        if (e) (void)hipEventDestroy(e);
     if (g->ldone) (void)hipEventDestroy(g->ldone);
     delete g;
 }
@@ -795,6 +1016,12 @@ int smore_group_set_partition(smore_group* g, int on) {
 int smore_group_set_walk_partition(smore_group* g, int on) {
     if (!g) return SMORE_EINVAL;
     g->walk_partition = on != 0;
+    return SMORE_OK;
+}
+
+int smore_group_set_schedule(smore_group* g, int schedule) {
+    if (!g || (schedule != SMORE_SCHED_REPLICAS && schedule != SMORE_SCHED_BLOCKS)) return SMORE_EINVAL;
+    g->schedule = schedule;
     return SMORE_OK;
 }
 
@@ -899,6 +1126,8 @@ int smore_group_train_edges(smore_group* g, int model, uint64_t begin, uint64_t 
     if (!g) return SMORE_EINVAL;
     if (g->ctx.size() == 1)
         return gfail(g, 0, smore_train_edges(g->ctx[0], model, begin, count, total, K, alpha0, reg, seed, mode));
+    if (blocks_for(g) && model == SMORE_LINE2)
+        return group_block_edges(g, begin, count, sync_samples, total, K, alpha0, seed, mode);
     return group_rounds(g, begin, begin + count, sync_samples, mean,
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_edges_async(c, model, b, e - b, total, K, alpha0, reg, seed, mode);
@@ -913,6 +1142,9 @@ int smore_group_train_deepwalk(smore_group* g, uint64_t walk_begin, uint64_t wal
     if (g->ctx.size() == 1)
         return gfail(g, 0, smore_train_deepwalk(g->ctx[0], walk_begin, walk_end, walk_times, walk_steps, window, K,
                                                 alpha0, seed, order, mode));
+    if (blocks_for(g))
+        return group_block_walks(g, 0, walk_begin, walk_end, walk_times, walk_steps, window, 0, K, alpha0, seed, order,
+                                 mode, sync_walks);
     return group_rounds(g, walk_begin, walk_end, sync_walks, mean,
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_deepwalk_async(c, b, e, walk_times, walk_steps, window, K, alpha0,
@@ -979,6 +1211,9 @@ int smore_group_train_walklets(smore_group* g, uint64_t walk_begin, uint64_t wal
     if (g->ctx.size() == 1)
         return gfail(g, 0, smore_train_walklets(g->ctx[0], walk_begin, walk_end, walk_times, walk_steps, window_min,
                                                 window_max, K, alpha0, seed, mode));
+    if (blocks_for(g))
+        return group_block_walks(g, 1, walk_begin, walk_end, walk_times, walk_steps, window_max, window_min, K, alpha0,
+                                 seed, nullptr, mode, sync_walks);
     return group_rounds(g, walk_begin, walk_end, sync_walks, mean,
                         [&](smore_ctx* c, uint64_t b, uint64_t e) {
                             return smore_train_walklets_async(c, b, e, walk_times, walk_steps, window_min,

@@ -1,0 +1,225 @@
+// train_blocks.hip -- draws and records of the 2-D block schedule (blocks.cpp,
+// DESIGN.md 10; SURVEY.md 8e's conflict-free multi-GPU layout).
+//
+// With N GPUs, GPU r owns the W rows of part r (contiguous ids of equal source
+// mass) and the C table is cut into nb = 2N blocks (contiguous ids of equal
+// negative mass) that rotate around the ring.  A launch trains one cell
+// (part r, block b): every sample's source is in part r and its context and
+// negatives are in block b, so the N GPUs of a sub-round touch disjoint rows
+// of both tables and need no reduction -- the cells' union is one shared table
+// pair, as in the reference (src/model/LINE.cpp:160-191, DeepWalk.cpp:128-155).
+//
+// LINE-2 (block_draw_kernel): the cell's (v, c) pairs are drawn from one alias
+// table over the cell's "atoms" -- per CSR slot i of a source v in part r the
+// reference's TargetSample outcomes (v, target_i) with mass p(v) * prob_i / deg
+// and (v, alias_i) with mass p(v) * (1 - prob_i) / deg (src/proNet.cpp:647-683)
+// whose context falls in block b -- so a cell's samples follow the joint law
+// of SourceSample x TargetSample restricted to the cell; the K negatives come
+// from NegativeSample's law restricted to block b (:623-633).  Philox slots as
+// draw_kernel: word 0 p, word 1 the atom index, negatives from block 1 + j/2.
+//
+// Walk models (block_pair_count / emit): every GPU runs every walk of a round
+// (deterministic per walk index) and keeps the skip-gram pairs whose center is
+// in its part, bucketed by the context's block; a pair's negatives come from
+// its block's restricted law (same slots as pair_emit_kernel, the index drawn
+// over the block).  Buckets keep walk order, so a bucket's records are the
+// one-GPU records restricted to the cell, in order.
+#include "train_kernels.h"
+
+namespace smore {
+
+__device__ __forceinline__ int block_of(const BlockArgs& b, int32_t x) {
+    int lo = 0, hi = b.nb;   // cb[lo] <= x < cb[hi]
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (x >= b.cb[mid]) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// a negative of block k: index over the block, alias entry of vertex cb[k] + i
+__device__ __forceinline__ int32_t block_negative(const BlockArgs& b, int k, uint32_t ki, uint32_t kp) {
+    const int32_t lo = b.cb[k];
+    const uint32_t i = (uint32_t)lo + draw_index(ki, (uint32_t)(b.cb[k + 1] - lo));
+    return alias_pick(i, b.ntab[i], kp);
+}
+
+template <int KMAX>
+__global__ void __launch_bounds__(256) block_draw_kernel(BlockArgs b, int blk, uint64_t seed, uint64_t begin,
+                                                         uint64_t count, int K, int32_t* rec) {
+    constexpr int RW = rec_width(KMAX);
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= count) return;
+    const uint64_t s = begin + t;
+    const uint4 b0 = philox_block(seed, 0, s, 0);
+    const uint64_t ai = b.atom_off + draw_index(b0.y, b.natoms);
+    const uint4 e0 = b.atoms[2 * ai], e1 = b.atoms[2 * ai + 1];
+    const bool acc = b0.x < e0.x;
+    int32_t w[RW];
+    w[0] = (int32_t)(acc ? e0.y : e1.x);
+    w[1] = (int32_t)(acc ? e0.z : e1.y);
+#pragma unroll
+    for (int j = 0; j < RW - 2; ++j) w[2 + j] = -1;
+#pragma unroll
+    for (int j = 0; j < KMAX; j += 2) {
+        if (j < K) {
+            const uint4 q = philox_block(seed, 0, s, 1 + j / 2);
+            w[2 + j] = block_negative(b, blk, q.x, q.y);
+            if (j + 1 < KMAX && j + 1 < K) w[3 + j] = block_negative(b, blk, q.z, q.w);
+        }
+    }
+    i32x4* o = reinterpret_cast<i32x4*>(rec + t * RW);
+#pragma unroll
+    for (int q = 0; q < RW / 4; ++q) {
+        const i32x4 x = {w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
+        __builtin_nontemporal_store(x, o + q);
+    }
+}
+
+hipError_t launch_block_draw(const BlockArgs& b, int blk, uint64_t seed, uint64_t begin, uint64_t count, int K,
+                             int32_t* rec, hipStream_t st) {
+    const int block = 256;
+    const dim3 grid((unsigned)((count + block - 1) / block));
+    switch (kmax_of(K)) {
+        case 5: hipLaunchKernelGGL(block_draw_kernel<5>, grid, dim3(block), 0, st, b, blk, seed, begin, count, K, rec); break;
+        case 10: hipLaunchKernelGGL(block_draw_kernel<10>, grid, dim3(block), 0, st, b, blk, seed, begin, count, K, rec); break;
+        default: hipLaunchKernelGGL(block_draw_kernel<20>, grid, dim3(block), 0, st, b, blk, seed, begin, count, K, rec); break;
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- walk pairs
+struct WalkWordsB {   // consecutive Philox words of one walk (stream 1), as train_pairs.hip
+    uint64_t seed, unit;
+    uint32_t blk = 0xFFFFFFFFu;
+    uint4 q;
+    __device__ uint32_t operator()(uint32_t slot) {
+        if ((slot >> 2) != blk) {
+            blk = slot >> 2;
+            q = philox_block(seed, 1, unit, blk);
+        }
+        return comp(q, (int)(slot & 3));
+    }
+};
+
+// Walklets' ranges (ScaleSkipGrams src/proNet.cpp:928-987, as train_pairs.hip)
+__device__ __forceinline__ void scale_ranges(int i, int L, int wmin, int wmax, int (&rg)[2][2]) {
+    rg[0][0] = i - wmax < 0 ? 0 : i - wmax;
+    rg[0][1] = i - wmin < 0 ? 0 : i - wmin;
+    rg[1][0] = i + wmin >= L ? L - 1 : i + wmin;
+    rg[1][1] = i + wmax >= L ? L - 1 : i + wmax;
+}
+
+// per (block, walk) pair counts of the owned centers: count[k * nwalks + t]
+__global__ void __launch_bounds__(256) block_pair_count_kernel(WalkArgs w, BlockArgs b, uint64_t seed,
+                                                               uint32_t* count) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= w.nwalks) return;
+    uint32_t cnt[BLOCK_MAX];
+    for (int k = 0; k < b.nb; ++k) cnt[k] = 0;
+    const int L = w.lens[t];
+    const int32_t* walk = w.walks + t * (uint64_t)(w.steps + 1);
+    WalkWordsB wd{seed, w.walk_begin + t};
+    const uint32_t win_base = 2u * (uint32_t)(L - 1);
+    for (int i = 0; i < L; ++i) {
+        int rg[2][2];
+        int nr = 1;
+        if (w.rule == 1) {
+            scale_ranges(i, L, w.window_min, w.window, rg);
+            nr = 2;
+        } else {
+            const int r = (int)draw_index(wd(win_base + (uint32_t)i), (uint32_t)w.window) + 1;
+            rg[0][0] = i - r < 0 ? 0 : i - r;
+            rg[0][1] = i + r >= L ? L - 1 : i + r;
+        }
+        const int32_t v = walk[i] & ID_MASK;
+        if (v < w.own_lo || v >= w.own_hi) continue;
+        for (int q = 0; q < nr; ++q)
+            for (int j = rg[q][0]; j <= rg[q][1]; ++j)
+                if (j != i) cnt[block_of(b, walk[j] & ID_MASK)]++;
+    }
+    for (int k = 0; k < b.nb; ++k) count[(uint64_t)k * w.nwalks + t] = cnt[k];
+}
+
+template <int KMAX>
+__global__ void __launch_bounds__(256) block_pair_emit_kernel(WalkArgs w, BlockArgs b, uint64_t seed, int K,
+                                                              double alpha0, const uint64_t* off, int32_t* rec) {
+    constexpr int RW = rec_width(KMAX);
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= w.nwalks) return;
+    uint64_t cur[BLOCK_MAX];
+    for (int k = 0; k < b.nb; ++k) cur[k] = off[(uint64_t)k * w.nwalks + t];
+    const int L = w.lens[t];
+    const int32_t* walk = w.walks + t * (uint64_t)(w.steps + 1);
+    const uint64_t unit = w.walk_begin + t;
+    const float alpha = alpha_walk(unit, alpha0, w.total_walks);
+    WalkWordsB win{seed, unit}, neg{seed, unit};
+    const uint32_t win_base = 2u * (uint32_t)(L - 1);
+    // negatives follow the walk's draws (and DeepWalk's L window draws)
+    uint32_t slot = win_base + (w.rule == 1 ? 0u : (uint32_t)L);
+    for (int i = 0; i < L; ++i) {
+        int rg[2][2];
+        int nr = 1;
+        if (w.rule == 1) {
+            scale_ranges(i, L, w.window_min, w.window, rg);
+            nr = 2;
+        } else {
+            const int r = (int)draw_index(win(win_base + (uint32_t)i), (uint32_t)w.window) + 1;
+            rg[0][0] = i - r < 0 ? 0 : i - r;
+            rg[0][1] = i + r >= L ? L - 1 : i + r;
+        }
+        const int32_t vi = walk[i];
+        const int32_t v = vi & ID_MASK;
+        const bool own = v >= w.own_lo && v < w.own_hi;
+        for (int q = 0; q < nr; ++q)
+            for (int j = rg[q][0]; j <= rg[q][1]; ++j) {
+                if (j == i) continue;
+                if (!own) {   // another part's pair: its draws only
+                    slot += 2u * (uint32_t)K;
+                    continue;
+                }
+                const int32_t cj = walk[j];
+                const int k = block_of(b, cj & ID_MASK);
+                int32_t x[RW];
+                // W row walk[i] with its W tag, C row walk[j] with its C tag
+                x[0] = v | (int32_t)((((uint32_t)vi >> 31) & 1u) << 30);
+                x[1] = cj & (ID_MASK | (1 << 30));
+#pragma unroll
+                for (int n = 0; n < RW - 2; ++n) x[2 + n] = -1;
+#pragma unroll
+                for (int n = 0; n < KMAX; ++n)
+                    if (n < K) x[2 + n] = block_negative(b, k, neg(slot + 2u * (uint32_t)n), neg(slot + 2u * (uint32_t)n + 1u));
+                x[2 + KMAX] = __float_as_int(alpha);
+                slot += 2u * (uint32_t)K;
+                i32x4* o = reinterpret_cast<i32x4*>(rec + cur[k] * RW);
+                cur[k] += 1;
+#pragma unroll
+                for (int qq = 0; qq < RW / 4; ++qq) {
+                    const i32x4 y = {x[4 * qq], x[4 * qq + 1], x[4 * qq + 2], x[4 * qq + 3]};
+                    __builtin_nontemporal_store(y, o + qq);
+                }
+            }
+    }
+}
+
+hipError_t launch_block_pair_count(const WalkArgs& w, const BlockArgs& b, uint64_t seed, uint32_t* count,
+                                   hipStream_t st) {
+    const int block = 256;
+    hipLaunchKernelGGL(block_pair_count_kernel, dim3((unsigned)((w.nwalks + block - 1) / block)), dim3(block), 0, st,
+                       w, b, seed, count);
+    return hipGetLastError();
+}
+
+hipError_t launch_block_pair_emit(const WalkArgs& w, const BlockArgs& b, uint64_t seed, int K, double alpha0,
+                                  const uint64_t* off, int32_t* rec, hipStream_t st) {
+    const int block = 256;
+    const dim3 grid((unsigned)((w.nwalks + block - 1) / block));
+    if (kmax_of(K) == 5)
+        hipLaunchKernelGGL(block_pair_emit_kernel<5>, grid, dim3(block), 0, st, w, b, seed, K, alpha0, off, rec);
+    else
+        hipLaunchKernelGGL(block_pair_emit_kernel<10>, grid, dim3(block), 0, st, w, b, seed, K, alpha0, off, rec);
+    return hipGetLastError();
+}
+
+}  // namespace smore

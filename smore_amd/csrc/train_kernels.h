@@ -26,6 +26,7 @@ struct EdgeArgs {
     // (draw_kernel), rec_width(KMAX) int32 each
     const int32_t* rec;
     const uint64_t* count_dev;     // non-null: the record count is read here (device-side pair totals)
+    const uint64_t* rec_base;      // non-null: the launch's records are [*rec_base, *count_dev) (block buckets)
     unsigned long long* work;      // Hogwild edge kernels: chunk counter, zeroed per launch
     int alpha_rec;                 // 1: learning rate in record word 2 + KMAX (DeepWalk pairs)
     uint64_t begin, count, total, seed;
@@ -174,6 +175,22 @@ hipError_t launch_edge_train(const EdgeArgs& a, int grid, hipStream_t st);
 const void* edge_kernel_symbol(const EdgeArgs& a);
 hipError_t launch_sample(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K,
                          int bpr, int32_t* out, hipStream_t st);
+// 2-D block schedule (train_blocks.hip, blocks.cpp): C blocks <= BLOCK_MAX (N <= 16 W parts)
+constexpr int BLOCK_MAX = 32;
+struct BlockArgs {
+    const uint4* atoms;       // LINE-2: this part's atoms, 2 uint4 each {thr, v, c, 0}, {v', c', 0, 0} (tagged ids)
+    uint64_t atom_off;        // first atom of the launch's block
+    uint32_t natoms;          // atoms of the launch's block
+    const uint2* ntab;        // V entries: block k's negative alias over its vertices [cb[k], cb[k+1])
+    int nb;                   // C blocks
+    int32_t cb[BLOCK_MAX + 1];
+};
+hipError_t launch_block_draw(const BlockArgs& b, int blk, uint64_t seed, uint64_t begin, uint64_t count, int K,
+                             int32_t* rec, hipStream_t st);
+hipError_t launch_block_pair_count(const WalkArgs& w, const BlockArgs& b, uint64_t seed, uint32_t* count,
+                                   hipStream_t st);
+hipError_t launch_block_pair_emit(const WalkArgs& w, const BlockArgs& b, uint64_t seed, int K, double alpha0,
+                                  const uint64_t* off, int32_t* rec, hipStream_t st);
 // streaming copy of n16 16-B words (membw.hip); variant 1 = non-temporal
 hipError_t launch_copy(const void* src, void* dst, uint64_t n16, int blocks, int variant, hipStream_t st);
 hipError_t launch_init_uniform(float* T, int64_t rows, int dim, int dpad, uint64_t seed,

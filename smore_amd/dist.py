@@ -197,6 +197,101 @@ def adaptive_scale(rate, updates, world, c0=64.0):
     return (s + (1.0 - s) / world).astype(np.float32)
 
 
+class BlockSync:
+    """The 2-D block schedule over torch.distributed (one process per GPU;
+    the group driver's twin is exchange.cpp group_block_*).
+
+    Rank r owns the W rows of part r; the C rows are cut into nb = 2N blocks
+    (`c_bounds`, nb + 1 row bounds).  Sub-round s (counted over the whole run)
+    trains cell (r, (2r + s) mod nb) -- `train(block)` queues it on the current
+    stream -- then sends that C block to rank r - 1 and receives block
+    (2r + s + 2) mod nb from rank r + 1, asynchronously (NCCL: on its own
+    stream, ordered after the cell); the cell of sub-round s + 2 waits for that
+    receive, so a transfer overlaps one whole sub-round.  No row trains on two
+    ranks at once: nothing is all-reduced.  finish() drains the transfers and,
+    with gather=True, gives every rank every W part (from its owner) and every
+    C block (from its holder).
+
+    W, C: the table tensors (rows x stride; CPU tensors in the gloo tests).
+    Over gloo, CUDA blocks are staged through host memory (gloo's send/recv
+    take CPU tensors)."""
+
+    def __init__(self, W, C, w_bounds, c_bounds, group=None):
+        self.W, self.C = W, C
+        self.wb = [int(x) for x in w_bounds]
+        self.cb = [int(x) for x in c_bounds]
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.nb = len(self.cb) - 1
+        if self.nb != 2 * self.world or len(self.wb) != self.world + 1:
+            raise ValueError("block schedule: N + 1 W bounds and 2N + 1 C bounds for N ranks")
+        self.ranks = dist.get_process_group_ranks(group) if group is not None else list(range(self.world))
+        self.staged = dist.get_backend(group) == "gloo" and C.is_cuda
+        self.s = 0                 # sub-rounds done
+        self.pending = [None, None]   # (works, post) of the last two rotations, by sub-round parity
+
+    def block(self, s=None):
+        """The C block this rank trains at sub-round s (default: the next)."""
+        s = self.s if s is None else s
+        return (2 * self.rank + s) % self.nb
+
+    def rows(self, b):
+        return self.C[self.cb[b]:self.cb[b + 1]]
+
+    def _wait(self, slot):
+        p = self.pending[slot]
+        if p is not None:
+            works, post = p
+            for w in works:
+                w.wait()
+            if post is not None:
+                post()
+            self.pending[slot] = None
+
+    def sub_round(self, train):
+        """Train this rank's cell of the next sub-round and start its rotation."""
+        s = self.s
+        self._wait(s & 1)               # the block received at sub-round s - 2
+        b = self.block(s)
+        train(b)
+        send, recv = self.rows(b), self.rows((b + 2) % self.nb)
+        dst = self.ranks[(self.rank - 1) % self.world]
+        src = self.ranks[(self.rank + 1) % self.world]
+        post = None
+        if self.staged:
+            send_h = send.cpu()
+            recv_h = torch.empty_like(recv, device="cpu")
+            ops = [dist.P2POp(dist.isend, send_h, dst, self.group), dist.P2POp(dist.irecv, recv_h, src, self.group)]
+
+            def post(recv=recv, recv_h=recv_h):
+                recv.copy_(recv_h)
+        else:
+            ops = [dist.P2POp(dist.isend, send, dst, self.group), dist.P2POp(dist.irecv, recv, src, self.group)]
+        self.pending[s & 1] = (dist.batch_isend_irecv(ops), post)
+        self.s += 1
+
+    def epoch(self, train):
+        """nb sub-rounds: every cell of this rank's W part once."""
+        for _ in range(self.nb):
+            self.sub_round(train)
+
+    def holder(self, b):
+        """The rank holding C block b's latest rows once the transfers drained."""
+        return ((b - self.s) % self.nb) // 2
+
+    def finish(self, gather=True):
+        self._wait(0)
+        self._wait(1)
+        if not gather:
+            return
+        for p in range(self.world):
+            if self.wb[p + 1] > self.wb[p]:
+                dist.broadcast(self.W[self.wb[p]:self.wb[p + 1]], src=self.ranks[p], group=self.group)
+        for b in range(self.nb):
+            dist.broadcast(self.rows(b), src=self.ranks[self.holder(b)], group=self.group)
+
+
 class ReplicaSync(OverlapSync):
     """OverlapSync over a ProNet context's device tables (W and C), with the
     fused HIP passes; the context runs on torch's current stream so the

@@ -210,6 +210,71 @@ class ProNet:
         self._chk(lib.smore_train_pairs(self.ctx, ptr(v), ptr(c), len(v), int(K), float(alpha), int(seed), int(unit),
                                         _lib.MODE[mode]), "train_pairs")
 
+    # ---- 2-D block schedule, one replica's side (smore_block_*)
+    def block_setup(self, model, nparts, part, K, mode="hybrid"):
+        """This context as part `part` of `nparts`: W part bounds, 2 nparts C
+        blocks and the cells' draw tables (smore_block_setup; model "line2" or
+        "census" for the C++ walk models)."""
+        self._chk(lib.smore_block_setup(self.ctx, _lib.MODEL[model], int(nparts), int(part), int(K),
+                                        _lib.MODE[mode]), "block_setup")
+
+    def block_bounds(self):
+        """(W part bounds [N + 1], C block bounds [2N + 1]) of the block setup."""
+        n, r, nb = C.c_int(), C.c_int(), C.c_int()
+        lib.smore_block_info(self.ctx, C.byref(n), C.byref(r), C.byref(nb))
+        wb = np.zeros(n.value + 1, np.int64)
+        cb = np.zeros(nb.value + 1, np.int64)
+        self._chk(lib.smore_block_bounds(self.ctx, ptr(wb), ptr(cb)), "block_bounds")
+        return wb, cb
+
+    def block_mass(self):
+        """LINE-2: this part's sample mass per C block (sums to 1)."""
+        _, cb = self.block_bounds()
+        m = np.zeros(len(cb) - 1, np.float64)
+        self._chk(lib.smore_block_mass(self.ctx, ptr(m)), "block_mass")
+        return m
+
+    def block_counts(self, samples):
+        """LINE-2: `samples` split over the C blocks by mass (largest remainder)."""
+        _, cb = self.block_bounds()
+        out = np.zeros(len(cb) - 1, np.uint64)
+        self._chk(lib.smore_block_counts(self.ctx, int(samples), ptr(out)), "block_counts")
+        return out
+
+    def block_train_edges(self, block, begin, count, total, K, alpha0, seed, mode="hybrid", sync=True):
+        """LINE-2 samples [begin, begin + count) of cell (part, block)."""
+        self._chk(lib.smore_block_train_edges_async(self.ctx, int(block), int(begin), int(count), int(total), int(K),
+                                                    float(alpha0), int(seed), _lib.MODE[mode]), "block_train_edges")
+        if sync:
+            self.synchronize()
+
+    def block_sample_edges(self, block, seed, begin, count, K):
+        out = np.zeros((int(count), 2 + int(K)), np.int32)
+        self._chk(lib.smore_block_sample_edges(self.ctx, int(block), int(seed), int(begin), int(count), int(K),
+                                               ptr(out)), "block_sample_edges")
+        return out
+
+    def block_prepare_walks(self, walk_begin, walk_end, walk_times, walk_steps, window, K, alpha0, seed, order=None,
+                            mode="hybrid", rule="deepwalk", window_min=0):
+        """A round of walks -> this part's pair records bucketed by C block."""
+        if order is not None:
+            order = np.ascontiguousarray(order, np.int64)
+        self._chk(lib.smore_block_prepare_walks(self.ctx, 0 if rule == "deepwalk" else 1, int(walk_begin),
+                                                int(walk_end), int(walk_times), int(walk_steps), int(window),
+                                                int(window_min), int(K), float(alpha0), int(seed),
+                                                ptr(order) if order is not None else None, 0, _lib.MODE[mode]),
+                  "block_prepare_walks")
+
+    def block_train_walks(self, block, sync=True):
+        self._chk(lib.smore_block_train_walks_async(self.ctx, int(block)), "block_train_walks")
+        if sync:
+            self.synchronize()
+
+    def block_walk_records(self, block):
+        n = C.c_uint64()
+        self._chk(lib.smore_block_walk_records(self.ctx, int(block), C.byref(n)), "block_walk_records")
+        return n.value
+
     def census_begin(self):
         """Row census: the following walk-model calls count the rows their
         records would update instead of training (smore_census_begin)."""
@@ -496,6 +561,13 @@ class Group:
         """smore_group_set_walk_partition: walk-model W rows partitioned by walk
         center (default off)."""
         self._chk(lib.smore_group_set_walk_partition(self.g, int(bool(on))), "set_walk_partition")
+
+    def set_schedule(self, schedule):
+        """smore_group_set_schedule: "blocks" (the 2-D block schedule: no row
+        replicated while it trains, C blocks rotating; LINE-2, DeepWalk and
+        Walklets on the C++ rules) or "replicas" (replicated tables, deltas
+        exchanged)."""
+        self._chk(lib.smore_group_set_schedule(self.g, _lib.SCHED[schedule]), "set_schedule")
 
     def set_hot_exchange(self, rows=-1, launches=8):
         """smore_group_set_hot_exchange: hub rows per table synced after every

@@ -1,0 +1,118 @@
+"""The 2-D block schedule's rotation (smore_amd/dist.py BlockSync) on CPU with
+gloo, world size 2 and 3: every rank trains its cells in sub-round order on
+the C blocks it holds, blocks move to rank r - 1 after each sub-round, and
+after finish() every rank holds exactly the tables of ONE shared table pair
+trained cell by cell in the same order -- the schedule is the reference's
+single table (src/model/LINE.cpp:160-191) with the samples grouped by cell.
+Also the group driver's sample split: rounds, replica slices and the
+largest-remainder cell counts (exchange.cpp group_block_edges)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+V, D = 48, 4
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _bounds(world):
+    wb = [V * p // world for p in range(world + 1)]
+    nb = 2 * world
+    cb = [V * b // nb for b in range(nb + 1)]
+    return wb, cb
+
+
+def _cell(W, C, wb, cb, r, b, s):
+    """A deterministic, order-dependent update touching W part r and C block
+    b only (the shape of a LINE-2 cell launch)."""
+    w = W[wb[r]:wb[r + 1]]
+    c = C[cb[b]:cb[b + 1]]
+    g = torch.tanh(w.sum(0) * 0.1 + c.mean(0))
+    c.mul_(0.99).add_(g * (0.01 * (r + 1)) + 0.001 * s)
+    w.add_(c.mean(0) * 0.05 - 0.002 * b)
+
+
+def _reference(world, subrounds):
+    torch.manual_seed(0)
+    W, C = torch.randn(V, D), torch.randn(V, D)
+    wb, cb = _bounds(world)
+    nb = 2 * world
+    for s in range(subrounds):
+        for r in range(world):
+            _cell(W, C, wb, cb, r, (2 * r + s) % nb, s)
+    return W, C
+
+
+def _worker(rank, world, port, subrounds, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from smore_amd.dist import BlockSync
+    torch.manual_seed(0)
+    W, C = torch.randn(V, D), torch.randn(V, D)
+    wb, cb = _bounds(world)
+    # rows this rank must not read stale: poison everything it does not own
+    # at the start except the two blocks it trains first (they are its own)
+    bs = BlockSync(W, C, wb, cb)
+    for b in range(2 * world):
+        if b not in (bs.block(0), bs.block(1)):
+            C[cb[b]:cb[b + 1]] = float("nan")
+    for p in range(world):
+        if p != rank:
+            W[wb[p]:wb[p + 1]] = float("nan")
+    for _ in range(subrounds):
+        s = bs.s
+        bs.sub_round(lambda b: _cell(W, C, wb, cb, rank, b, s))
+    bs.finish(gather=True)
+    RW, RC = _reference(world, subrounds)
+    out[rank] = int(torch.equal(W, RW) and torch.equal(C, RC))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,subrounds", [(2, 4), (2, 11), (3, 6), (3, 17)])
+def test_block_rotation_gloo(world, subrounds):
+    """Whole epochs and a partial one: the holder of every block after the
+    drain is ((b - s) mod 2N) // 2 and no rank ever trains a stale block."""
+    ctx = mp.get_context("spawn")
+    out = ctx.Array("i", [0] * world)
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, subrounds, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert list(out) == [1] * world
+
+
+def test_group_block_split():
+    """exchange.cpp group_block_edges' split restated (bench.py reuses it):
+    the rounds tile [0, count), every replica's slice is split over its cells
+    exactly, in sub-round order, with consecutive sample ranges."""
+    from bench import block_schedule, largest_remainder
+    mass = [[0.1, 0.2, 0.3, 0.15, 0.25, 0.0], [0.5, 0.1, 0.1, 0.1, 0.1, 0.1], [1 / 6] * 6]
+    for count, per in ((10_000, 1000), (9_999, 5000), (7, 100)):
+        seen = []
+        for r, m in enumerate(mass):
+            subs = list(block_schedule(count, per, 3, r, lambda x, m=m: largest_remainder(x, m)))
+            assert [s for s, _, _, _ in subs] == list(range(len(subs))) and len(subs) % 6 == 0
+            for s, b, lo, n in subs:
+                assert b == (2 * r + s) % 6
+                if n:
+                    seen.append((lo, n))
+        seen.sort()
+        pos = 0
+        for lo, n in seen:
+            assert lo == pos
+            pos += n
+        assert pos == count

@@ -1,0 +1,261 @@
+"""The 2-D block schedule of the multi-GPU path (blocks.cpp, train_blocks.hip,
+exchange.cpp group_block_*) on one MI355X:
+  * a cell's draws are bit-exact against the numpy restatement of its tables
+    (tests/block_spec.py: bounds, per-block negative tables, atoms), every
+    source in the part, every context and negative in the block;
+  * a replica's serial cell training equals the oracle's fp32 update over the
+    same records (orc_train_records_f32);
+  * a serial block-schedule group of 2 / 3 replicas on cuda:0 equals the
+    schedule restated around the oracle (cells in sub-round order, C blocks
+    copied to replica r - 1 after each sub-round, W parts / C blocks gathered
+    from their owners) bit for bit;
+  * walk rounds: the bucketed records of all parts and blocks are exactly the
+    one-context pairs (their count), the serial group equals its restatement;
+  * quality: C2 LINE-2 and C5 DeepWalk at 2 / 4 / 8 replicas within 5 % of
+    one context's held-out loss (VERDICT r4's bar).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from tests.block_spec import BlockSpec
+from tests.conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+SEED = 20251015
+PL1K = os.path.join(GOLDEN, "pl1k.txt")
+
+
+@pytest.fixture(scope="module")
+def smore():
+    import smore_amd
+    return smore_amd
+
+
+@pytest.fixture(scope="module")
+def graph():
+    return orc.Graph.from_file(PL1K, 1)
+
+
+def _ctx(smore, dim=32):
+    pn = smore.ProNet(0)
+    pn.LoadEdgeList(PL1K, 1)
+    pn.alloc_tables(dim, 2)
+    pn.init_table_glibc(0, 0)
+    pn.zero_table(1)
+    return pn
+
+
+@pytest.mark.parametrize("n", [2, 3, 4])
+def test_block_draws_match_spec(smore, graph, n):
+    K = 5
+    pn = _ctx(smore)
+    for r in range(n):
+        spec = BlockSpec(graph, n, r)
+        pn.block_setup("line2", n, r, K, "atomic")
+        wb, cb = pn.block_bounds()
+        assert list(wb) == spec.wb and list(cb) == spec.cb
+        np.testing.assert_allclose(pn.block_mass(), spec.mass, rtol=1e-12, atol=0)
+        assert abs(pn.block_mass().sum() - 1.0) < 1e-12
+        for k in range(2 * n):
+            if spec.mass[k] == 0:
+                continue
+            got = pn.block_sample_edges(k, SEED, (1 << 33) + 977 * k, 600, K)
+            want = spec.draw(k, SEED, (1 << 33) + 977 * k, 600, K)
+            np.testing.assert_array_equal(got, want)
+            assert ((got[:, 0] >= wb[r]) & (got[:, 0] < wb[r + 1])).all()
+            assert ((got[:, 1:] >= cb[k]) & (got[:, 1:] < cb[k + 1])).all()
+    pn.close()
+
+
+def test_block_counts_largest_remainder(smore):
+    pn = _ctx(smore)
+    pn.block_setup("line2", 4, 1, 5, "atomic")
+    m = pn.block_mass()
+    for S in (0, 1, 7, 1000, 123457):
+        c = pn.block_counts(S).astype(np.int64)
+        assert c.sum() == S
+        assert (np.abs(c - S * m) < 1.0 + 1e-9).all()
+    pn.close()
+
+
+def test_block_cell_serial_equals_oracle(smore, graph):
+    """One replica's serial cell launches against the oracle's fp32 update
+    over the same records, cell after cell."""
+    K, dim, total = 5, 32, 10 ** 6
+    pn = _ctx(smore, dim)
+    W, C = pn.get_table(0), pn.get_table(1)
+    pn.block_setup("line2", 3, 2, K, "serial")
+    begin = 5000
+    for k in (0, 3, 5, 1):
+        n = 700
+        rec = pn.block_sample_edges(k, SEED, begin, n, K)
+        pn.block_train_edges(k, begin, n, total, K, 0.025, SEED, "serial")
+        orc.train_records_f32("line2", W, C, rec, K, 0.025, 0.0, total, begin)
+        begin += n
+    np.testing.assert_array_equal(pn.get_table(0), W)
+    np.testing.assert_array_equal(pn.get_table(1), C)
+    pn.close()
+
+
+def _schedule_edges(smore, graph, n, begin, count, per, total, K, dim, W0, C0):
+    """exchange.cpp group_block_edges restated: rounds of per * n samples,
+    replica r's slice split over the blocks by its mass, sub-round s trains
+    cell (r, (2r + s) mod 2n), then C block (2r + s) mod 2n moves to replica
+    r - 1; at the end W part p comes from replica p, C block b from b // 2."""
+    nb = 2 * n
+    ctxs, specs = [], []
+    for r in range(n):
+        p = smore.ProNet(0)
+        p.LoadEdgeList(PL1K, 1)
+        p.alloc_tables(dim, 2)
+        p.block_setup("line2", n, r, K, "serial")
+        ctxs.append(p)
+    Ws = [W0.copy() for _ in range(n)]
+    Cs = [C0.copy() for _ in range(n)]
+    wb, cb = ctxs[0].block_bounds()
+    rounds = -(-count // (per * n)) if per * n < count else 1
+    for k in range(rounds):
+        lo, hi = count * k // rounds, count * (k + 1) // rounds
+        m = hi - lo
+        cur = [lo + m * r // n for r in range(n)]
+        cnt = [ctxs[r].block_counts(lo + m * (r + 1) // n - cur[r]) for r in range(n)]
+        for s in range(nb):
+            for r in range(n):
+                b = (2 * r + s) % nb
+                x = int(cnt[r][b])
+                if x:
+                    rec = ctxs[r].block_sample_edges(b, SEED, begin + cur[r], x, K)
+                    orc.train_records_f32("line2", Ws[r], Cs[r], rec, K, 0.025, 0.0, total, begin + cur[r])
+                cur[r] += x
+            moved = [Cs[r][cb[(2 * r + s) % nb]:cb[(2 * r + s) % nb + 1]].copy() for r in range(n)]
+            for r in range(n):
+                b = (2 * r + s) % nb
+                Cs[(r - 1) % n][cb[b]:cb[b + 1]] = moved[r]
+    W, C = W0.copy(), C0.copy()
+    for p in range(n):
+        W[wb[p]:wb[p + 1]] = Ws[p][wb[p]:wb[p + 1]]
+    for b in range(nb):
+        C[cb[b]:cb[b + 1]] = Cs[b // 2][cb[b]:cb[b + 1]]
+    for p in ctxs:
+        p.close()
+    return W, C
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_block_group_serial_equals_schedule(smore, graph, n):
+    K, dim, total = 5, 32, 10 ** 6
+    g = smore.Group([0] * n)
+    g.LoadEdgeList(PL1K, 1)
+    g.alloc_tables(dim, 2)
+    g.primary.init_table_glibc(0, 0)
+    g.primary.init_table_glibc(1, graph.V * dim)
+    g.broadcast_tables()
+    W0, C0 = g.primary.get_table(0), g.primary.get_table(1)
+    g.set_schedule("blocks")
+    begin, count, per = 1000, 9000, 1500
+    g.train_edges("line2", begin, count, total, K, 0.025, 0.0, SEED, "serial", per=per)
+    W, C = _schedule_edges(smore, graph, n, begin, count, per, total, K, dim, W0, C0)
+    for r in g.replicas:
+        np.testing.assert_array_equal(r.get_table(0), W)
+        np.testing.assert_array_equal(r.get_table(1), C)
+    g.close()
+
+
+def test_block_walk_rounds_cover_the_pairs(smore, graph):
+    """Every part's pair records, over all blocks, are the one-context
+    records: for DeepWalk the per-walk pair counts of the oracle's SkipGrams
+    (the window draws are shared), for Walklets the clamped ranges."""
+    K = 5
+    V = graph.V
+    order = orc.deepwalk_order(V, 2, 0)
+    one = _ctx(smore)
+    one.census_begin()
+    one.train_deepwalk(0, 700, 2, 20, 4, K, 0.025, SEED, order, "atomic")
+    one.census_end(1.0)
+    total_pairs = int(round(one.row_rates("census", K, 0).sum()))
+    one.close()
+    for n in (2, 4):
+        got = 0
+        for r in range(n):
+            pn = _ctx(smore)
+            pn.block_setup("census", n, r, K, "atomic")
+            pn.block_prepare_walks(0, 700, 2, 20, 4, K, 0.025, SEED, order, "atomic")
+            got += sum(pn.block_walk_records(b) for b in range(2 * n))
+            pn.close()
+        assert got == total_pairs, (n, got, total_pairs)
+
+
+def test_block_group_walks_serial_replicas_agree(smore, graph):
+    """A serial DeepWalk block group of 3: every replica ends with the same
+    tables (gathered), they moved, and two identical runs agree bit for bit
+    (cells of one sub-round touch disjoint rows: the schedule is
+    deterministic)."""
+    K, dim = 5, 32
+    order = orc.deepwalk_order(graph.V, 2, 0)
+    out = []
+    for _ in range(2):
+        g = smore.Group([0] * 3)
+        g.LoadEdgeList(PL1K, 1)
+        g.alloc_tables(dim, 2)
+        g.primary.init_table_glibc(0, 0)
+        g.primary.zero_table(1)
+        g.broadcast_tables()
+        W0 = g.primary.get_table(0)
+        g.set_schedule("blocks")
+        g.train_deepwalk(0, 2 * graph.V, 2, 20, 4, K, 0.025, SEED, order, "serial", per=500)
+        W, C = g.primary.get_table(0), g.primary.get_table(1)
+        for r in g.replicas[1:]:
+            np.testing.assert_array_equal(r.get_table(0), W)
+            np.testing.assert_array_equal(r.get_table(1), C)
+        assert np.abs(W - W0).max() > 0 and np.abs(C).max() > 0
+        out.append((W, C))
+        g.close()
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+
+
+def _heldout_loss(W, C, draws):
+    v, c, negs = draws[:, 0], draws[:, 1], draws[:, 2:]
+    keep = c >= 0
+    v, c, negs = v[keep], c[keep], negs[keep]
+    Wv = W[v].astype(np.float64)
+    loss = np.logaddexp(0.0, -np.einsum("ij,ij->i", Wv, C[c].astype(np.float64)))
+    for k in range(negs.shape[1]):
+        loss += np.logaddexp(0.0, np.einsum("ij,ij->i", Wv, C[negs[:, k]].astype(np.float64)))
+    return float(loss.mean())
+
+
+def test_c2_line_blocks_quality(smore):
+    """Config 2's LINE-2 (1M vertices / 40M slots, d=64, K 5, hybrid), 2^31
+    samples in total, on 2 / 4 / 8 replicas in the block schedule (the
+    group's default epoch) against one context: held-out loss within 5 %."""
+    from smore_amd import graphgen
+    V, (src, dst, w) = graphgen.config_edges("c2")
+    dim, K, T = 64, 5, 1 << 31
+    one = smore.ProNet(0)
+    one.set_graph_edges(V, src, dst, w)
+    held = one.sample_edges("line2", (1 << 40) + 17, 100_000, K, SEED + 1)
+    one.alloc_tables(dim, 2)
+    one.init_table_glibc(0, 0)
+    one.zero_table(1)
+    one.train_edges("line2", 0, T, T, K, 0.025, 0.0, SEED, "hybrid")
+    l1 = _heldout_loss(one.get_table(0), one.get_table(1), held)
+    one.close()
+    res = {1: l1}
+    for n in (2, 4, 8):
+        g = smore.Group([0] * n)
+        g.set_graph_edges(V, src, dst, w)
+        g.alloc_tables(dim, 2)
+        g.primary.init_table_glibc(0, 0)
+        g.primary.zero_table(1)
+        g.broadcast_tables()
+        g.set_schedule("blocks")
+        g.train_edges("line2", 0, T, T, K, 0.025, 0.0, SEED, "hybrid")
+        res[n] = _heldout_loss(g.primary.get_table(0), g.primary.get_table(1), held)
+        g.close()
+        print("C2 LINE-2 blocks", n, res[n], "one", l1, res[n] / l1, flush=True)
+    for n in (2, 4, 8):
+        assert res[n] <= 1.05 * l1, res

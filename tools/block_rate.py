@@ -1,0 +1,135 @@
+#!/usr/bin/env python3
+"""One replica's compute in the 2-D block schedule, on one GPU.
+
+A context set up as part r of N (smore_block_setup) runs one epoch of its
+cells -- nb = 2N sub-rounds, cell (r, (2r + s) mod nb), the samples split by
+the cells' mass -- back to back (no rotation: on N GPUs the transfers overlap
+the next sub-round), against the one-GPU path over the same number of
+samples.  Prints one JSON line per (config, N, part): the epoch's time, the
+per-cell launch times, and the rate relative to one GPU, i.e. the measured
+per-GPU factor of the predicted N-GPU speed-up.
+
+    python tools/block_rate.py --model line2 --config c4 --nparts 2 4 8 --samples 134217728
+    python tools/block_rate.py --model deepwalk --config c5 --nparts 2 4 8 --walks 262144
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="line2", choices=["line2", "deepwalk"])
+    ap.add_argument("--config", default="c4")
+    ap.add_argument("--nparts", type=int, nargs="+", default=[2, 4, 8])
+    ap.add_argument("--parts", type=int, nargs="+", default=[0], help="which parts to time")
+    ap.add_argument("--samples", type=int, default=1 << 27, help="line2: samples per epoch per GPU")
+    ap.add_argument("--walks", type=int, default=1 << 18, help="deepwalk: walks per epoch")
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--mode", default="hybrid")
+    ap.add_argument("--seed", type=int, default=20251015)
+    args = ap.parse_args()
+
+    import torch  # noqa: F401  (one HIP runtime with torch, as bench.py)
+    import smore_amd
+    from smore_amd import graphgen
+
+    V, (src, dst, w) = graphgen.config_edges(args.config)
+    line = args.model == "line2"
+    dim, K = (64, 5) if line else (128, 5)
+    pn = smore_amd.ProNet(0)
+    pn.set_graph_edges(V, src, dst, w)
+    pn.alloc_tables(dim, 2)
+    pn.init_table_glibc(0, 0)
+    pn.zero_table(1)
+    S = args.samples
+    total = S * 100
+    wt, steps, window = 10, 40, 5
+    order = smore_amd.deepwalk_order(V, wt, 0) if not line else None
+
+    def timed(f):
+        best = 1e30
+        for _ in range(args.reps):
+            pn.synchronize()
+            t0 = time.perf_counter()
+            f()
+            pn.synchronize()
+            best = min(best, time.perf_counter() - t0)
+        return best
+
+    # the one-GPU path over the same work
+    if line:
+        one = timed(lambda: pn.train_edges("line2", 0, S, total, K, 0.025, 0.0, args.seed, args.mode, sync=False))
+        units = S
+    else:
+        one = timed(lambda: pn.train_deepwalk(0, args.walks, wt, steps, window, K, 0.025, args.seed, order,
+                                              args.mode))
+        pn.census_begin()
+        pn.train_deepwalk(0, args.walks, wt, steps, window, K, 0.025, args.seed, order, args.mode)
+        pn.census_end(1.0)
+        units = float(pn.row_rates("census", K, 0).sum())   # pairs of the walks
+    print(json.dumps({"config": args.config, "model": args.model, "nparts": 1, "epoch_ms": round(one * 1e3, 3),
+                      "units": units, "rate_M_per_s": round(units / one / 1e6, 2)}), flush=True)
+    for n in args.nparts:
+        nb = 2 * n
+        for r in args.parts:
+            if r >= n:
+                continue
+            t0 = time.perf_counter()
+            pn.block_setup("line2" if line else "census", n, r, K, args.mode)
+            setup_s = time.perf_counter() - t0
+            cells = []
+            if line:
+                cnt = pn.block_counts(S // n)
+                mine = S // n
+
+                def epoch():
+                    b0 = 0
+                    for s in range(nb):
+                        b = (2 * r + s) % nb
+                        if cnt[b]:
+                            pn.block_train_edges(b, b0, int(cnt[b]), total, K, 0.025, args.seed, args.mode, sync=False)
+                        b0 += int(cnt[b])
+                ep = timed(epoch)
+                for s in range(nb):      # per-cell launch times (one pass, synchronised per cell)
+                    b = (2 * r + s) % nb
+                    if cnt[b]:
+                        t1 = time.perf_counter()
+                        pn.block_train_edges(b, 0, int(cnt[b]), total, K, 0.025, args.seed, args.mode)
+                        cells.append(round((time.perf_counter() - t1) * 1e3, 3))
+                units_r = mine
+            else:
+                prep = timed(lambda: pn.block_prepare_walks(0, args.walks, wt, steps, window, K, 0.025, args.seed,
+                                                            order, args.mode))
+                recs = [pn.block_walk_records(b) for b in range(nb)]
+
+                def epoch():
+                    for s in range(nb):
+                        pn.block_train_walks((2 * r + s) % nb, sync=False)
+                ep = timed(epoch)
+                units_r = sum(recs)
+                cells = recs
+            row = {"config": args.config, "model": args.model, "nparts": n, "part": r, "setup_s": round(setup_s, 2),
+                   "epoch_ms": round(ep * 1e3, 3), "units": units_r,
+                   "rate_M_per_s": round(units_r / ep / 1e6, 2),
+                   "per_gpu_factor": round((units_r / ep) / (units / one), 4),
+                   "cells": cells}
+            if not line:
+                row["prepare_ms"] = round(prep * 1e3, 3)
+                row["per_gpu_factor_with_prepare"] = round((units_r / (ep + prep)) / (units / one), 4)
+            # the C block a rotation moves: its bytes (xGMI time is estimated in DESIGN.md 10)
+            _, cb = pn.block_bounds()
+            row["block_bytes_max"] = int(np.diff(cb).max()) * dim * 4
+            print(json.dumps(row), flush=True)
+    pn.block_setup("line2" if line else "census", 1, 0, K, args.mode)
+
+
+if __name__ == "__main__":
+    main()

@@ -81,6 +81,10 @@ def main():
     ap.add_argument("--hot-exchange", type=int, default=None, help="sum rule: hub rows synced per launch (0: off)")
     ap.add_argument("--diag", action="store_true", help="largest rows of each table and their census rate rank")
     ap.add_argument("--hot-tau", type=float, default=None, help="hybrid: hot-row threshold on every replica")
+    ap.add_argument("--schedule", default="replicas", choices=["replicas", "blocks"],
+                    help="group schedule (blocks: --per-row = samples per row per replica per epoch for line2; "
+                         "deepwalk: --walks-per-epoch)")
+    ap.add_argument("--walks-per-epoch", type=int, default=0, help="blocks, deepwalk: walks per epoch (0: default)")
     args = ap.parse_args()
 
     import smore_amd
@@ -105,6 +109,7 @@ def main():
             g.alloc_tables(dim, 2)
             g.set_partition(not args.no_partition)
             g.set_walk_partition(args.walk_partition)
+            g.set_schedule(args.schedule)
             if args.hot_exchange is not None:
                 g.set_hot_exchange(args.hot_exchange)
             for r in g.replicas:
@@ -147,6 +152,8 @@ def main():
                 p.census_end(min(Vn, 1 << 16))
                 pairs_per_walk = float(p.row_rates("census", K, 0).sum())
             per = max(1, int(args.per_row * Vn * period / pairs_per_walk)) if args.per_row > 0 else 0
+            if args.schedule == "blocks":
+                per = args.walks_per_epoch
             g.train_deepwalk(0, wt * Vn, wt, 40, 5, K, 0.025, args.seed, order, args.mode, per=per, mean=rule)
             row = {"model": "deepwalk", "walk_times": wt, "walks_per_exchange": per,
                    "pairs_per_walk": round(pairs_per_walk, 2)}
@@ -171,6 +178,7 @@ def main():
                                     "top_rate_rank": [int(rank[i]) for i in top],
                                     "rows_norm_gt_10": int((nrm > 10).sum())}
         row.update({"config": args.graph or args.config, "ranks": n, "rule": rule if n > 1 else "one",
+                    "schedule": args.schedule if n > 1 else "one",
                     "c0": c0, "period": period, "per_row": args.per_row, "mode": args.mode,
                     "combine_rows": args.combine_rows, "hot_tau": args.hot_tau, "hot_exchange": args.hot_exchange,
                     "walk_partition": args.walk_partition,
