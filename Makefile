@@ -16,7 +16,7 @@ BIN      := smore_amd/bin
 # kernels depend on the device headers only; host objects on the host headers
 DEV_HDRS := $(SRC)/device_common.h $(SRC)/train_kernels.h $(SRC)/edge_kernels.h $(SRC)/edge_inst.h
 HOST_HDRS := $(SRC)/host_graph.h $(SRC)/ctx.h $(SRC)/train_kernels.h $(SRC)/device_common.h $(SRC)/go_walks.h \
-             $(SRC)/hot_exchange.h include/smore_hip.h
+             $(SRC)/hot_exchange.h $(SRC)/comm_watch.h include/smore_hip.h
 
 .PHONY: all lib cli goshape oracle ref clean
 all: lib cli goshape

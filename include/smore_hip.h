@@ -287,6 +287,15 @@ int smore_comm_init(smore_ctx* ctx, int nranks, int rank, const unsigned char* i
 int smore_exchange_reset(smore_ctx* ctx);
 int smore_exchange_begin(smore_ctx* ctx, int mean /* SMORE_SYNC_* */);
 int smore_exchange_end(smore_ctx* ctx);
+/* RCCL failure detection (new -- the reference has no failure
+ * path): where the host waits on work behind a collective -- smore_synchronize
+ * of a context with its own communicator, the end of every group call over
+ * RCCL -- it polls ncclCommGetAsyncError between completion checks and bounds
+ * the wait (`seconds`; -1 = the default, $SMORE_COMM_TIMEOUT or 1800 s).  On an
+ * asynchronous error, a failed stream or the deadline the communicators are
+ * aborted (ncclCommAbort) and the call returns SMORE_EHIP with the reason in
+ * smore_last_error / smore_group_last_error.  No in-process restart. */
+int smore_set_comm_timeout(double seconds);
 
 /* One process driving N GPUs (`smore_create(dev_ids, n_dev)` with
  * internal fan-out): a group of N contexts with one communicator each

@@ -142,6 +142,7 @@ def _load():
         "smore_set_walk_owner": (i32, [P, i64, i64]),
         "smore_walk_parts": (i32, [P, i32, P]),
         "smore_group_set_schedule": (i32, [P, i32]),
+        "smore_set_comm_timeout": (i32, [dbl]),
         "smore_block_setup": (i32, [P, i32, i32, i32, i32, i32]),
         "smore_block_info": (i32, [P, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
         "smore_block_bounds": (i32, [P, P, P]),

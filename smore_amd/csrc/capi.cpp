@@ -87,6 +87,8 @@ int smore_synchronize(smore_ctx* c) {
     if (!c) return SMORE_EINVAL;
     if (c->device < 0) return SMORE_OK;
     HIPCHK(c, hipSetDevice(c->device));
+    int rc;
+    if ((rc = comm_sync(c))) return rc;   // own communicator: the RCCL failure watch first
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return SMORE_OK;
 }

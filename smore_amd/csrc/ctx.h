@@ -189,6 +189,9 @@ namespace smore_host {
 
 // blocks.cpp: frees the block tables (a new graph, smore_destroy)
 void blocks_release(smore_ctx* c);
+// exchange.cpp: the stream's completion under the RCCL failure watch (a
+// context with its own communicator; SMORE_OK otherwise)
+int comm_sync(smore_ctx* c);
 
 inline int fail(smore_ctx* c, int code, const std::string& msg) {
     if (c) c->err = msg;

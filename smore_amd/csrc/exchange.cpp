@@ -30,6 +30,7 @@
 #include <initializer_list>
 #include <mutex>
 
+#include "comm_watch.h"
 #include "ctx.h"
 #include "hot_exchange.h"
 
@@ -37,20 +38,12 @@ using namespace smore_host;
 
 namespace {
 
-struct Rccl {
-    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
-    decltype(&ncclCommInitRank) init_rank = nullptr;
-    decltype(&ncclCommInitAll) init_all = nullptr;
-    decltype(&ncclCommDestroy) destroy = nullptr;
-    decltype(&ncclAllReduce) all_reduce = nullptr;
-    decltype(&ncclBroadcast) broadcast = nullptr;
-    decltype(&ncclSend) send = nullptr;
-    decltype(&ncclRecv) recv = nullptr;
-    decltype(&ncclGroupStart) group_start = nullptr;
-    decltype(&ncclGroupEnd) group_end = nullptr;
-    decltype(&ncclGetErrorString) error_string = nullptr;
-    std::string err;
-};
+// the RCCL table (comm_watch.h): loaded on first use
+
+
+double g_comm_timeout = -1.0;   // smore_set_comm_timeout; < 0: comm_timeout_default()
+
+double comm_timeout() { return g_comm_timeout > 0 ? g_comm_timeout : comm_timeout_default(); }
 
 Rccl* rccl() {
     static Rccl r;
@@ -73,6 +66,8 @@ Rccl* rccl() {
         SMORE_SYM(init_rank, ncclCommInitRank)
         SMORE_SYM(init_all, ncclCommInitAll)
         SMORE_SYM(destroy, ncclCommDestroy)
+        SMORE_SYM(abort, ncclCommAbort)
+        SMORE_SYM(async_error, ncclCommGetAsyncError)
         SMORE_SYM(all_reduce, ncclAllReduce)
         SMORE_SYM(broadcast, ncclBroadcast)
         SMORE_SYM(send, ncclSend)
@@ -490,8 +485,29 @@ int gather_sources(smore_group* g, const std::vector<int64_t>& b) {
     return SMORE_OK;
 }
 
+// the end of a group call: with RCCL communicators the host waits for every
+// replica's stream under the failure watch (comm_watch.h: async errors
+// polled, the wait bounded, communicators aborted on failure)
 int group_sync(smore_group* g) {
     int rc;
+    if (!g->local && !g->comms.empty()) {
+        std::string why;
+        int bad = -1;
+        auto ready = [&]() -> int {
+            for (size_t r = 0; r < g->ctx.size(); ++r) {
+                (void)hipSetDevice(g->ctx[r]->device);
+                const hipError_t e = hipStreamQuery(g->ctx[r]->stream);
+                if (e == hipErrorNotReady) return 0;
+                if (e != hipSuccess) {
+                    bad = (int)r;
+                    return -1;
+                }
+            }
+            return 1;
+        };
+        if (comm_watch(rccl(), g->comms.data(), (int)g->comms.size(), ready, comm_timeout(), why))
+            return gfail(g, bad < 0 ? 0 : bad, fail(g->ctx[bad < 0 ? 0 : bad], SMORE_EHIP, why));
+    }
     for (size_t r = 0; r < g->ctx.size(); ++r)
         if ((rc = smore_synchronize(g->ctx[r]))) return gfail(g, (int)r, rc);
     return SMORE_OK;
@@ -860,7 +876,29 @@ static std::string census_key(const char* model, std::initializer_list<double> a
     return k;
 }
 
+namespace smore_host {
+// smore_synchronize of a context with its own communicator (one process per
+// GPU): the stream's completion under the failure watch
+int comm_sync(smore_ctx* c) {
+    if (!c->comm || !c->own_comm) return SMORE_OK;
+    ncclComm_t cm = (ncclComm_t)c->comm;
+    std::string why;
+    auto ready = [&]() -> int {
+        const hipError_t e = hipStreamQuery(c->stream);
+        return e == hipSuccess ? 1 : e == hipErrorNotReady ? 0 : -1;
+    };
+    if (comm_watch(rccl(), &cm, 1, ready, comm_timeout(), why)) return fail(c, SMORE_EHIP, why);
+    return SMORE_OK;
+}
+}  // namespace smore_host
+
 extern "C" {
+
+int smore_set_comm_timeout(double seconds) {
+    if (!(seconds > 0.0) && seconds != -1.0) return SMORE_EINVAL;
+    g_comm_timeout = seconds;
+    return SMORE_OK;
+}
 
 int smore_comm_unique_id(unsigned char* id) {
     if (!id) return SMORE_EINVAL;
