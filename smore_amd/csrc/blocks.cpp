@@ -62,25 +62,37 @@ int64_t resident_groups(smore_ctx* c, bool walk, int K, int mode) {
 }
 
 // per-block write-combined rows: the hottest hot C rows of each block under
-// the scaled C-row law (hot_pc), with the edge rule's staleness bound and
-// automatic drain interval (capi build_hot_maps)
-void block_sh_sets(smore_ctx* c, bool walk, std::vector<int2>& hash, std::vector<int32_t>& ids) {
+// its cell's C-row law (pcb, flags hcb), with the edge rule's staleness bound
+// and a two-tier drain (capi build_hot_maps)
+void block_sh_sets(smore_ctx* c, bool walk, bool on, int64_t Mg, const std::vector<std::vector<double>>& pcb,
+                   const std::vector<std::vector<uint8_t>>& hcb, std::vector<int2>& hash, std::vector<int32_t>& ids) {
     auto& B = c->blk;
-    const int cap = B.mode == SMORE_HYBRID && !c->hot_small && !c->hot_c.empty()
-                        ? std::max(0, std::min(c->sh_max, 8192 / std::max(1, c->dpad)))
-                        : 0;
+    const int cap = on ? std::max(0, std::min(c->sh_max, 8192 / std::max(1, c->dpad))) : 0;
     B.sh_cap = std::max(cap, 1);
     B.sh_n.assign((size_t)B.nb, 0);
-    B.sh_flush.assign((size_t)B.nb, 8);
+    B.sh_lvl.assign((size_t)B.nb, std::array<int, 8>{});
     hash.assign((size_t)B.nb * SH_HASH, make_int2(-1, -1));
     ids.assign((size_t)B.nb * B.sh_cap, -1);
-    if (cap == 0) return;
-    const double M = (double)c->hot_M, stale = sh_stale_max();
     const int flush_cap = c->sh_flush > 0 ? c->sh_flush : sh_flush_max(walk);
+    B.sh_flush = flush_cap;
+    if (cap == 0) return;
+    const double M = (double)Mg, stale = sh_stale_max();
+    const bool two_tier = c->sh_flush <= 0;
     for (int k = 0; k < B.nb; ++k) {
+        // A cell concentrates its samples on 1/nb of the C rows, so a hub row
+        // takes about nb times its one-GPU share of a launch's updates (C4,
+        // 8 GPUs: the top row ~18 % of a cell's C touches).  Each combined row
+        // gets its own drain interval from its rate (power-of-two levels:
+        // every slot every flush_cap rounds, each faster level's prefix at
+        // its own interval), so the hubs stay within the staleness bound
+        // without draining every other row as often.
         std::vector<std::pair<double, int32_t>> r;
-        for (int64_t x = B.cb[k]; x < B.cb[k + 1]; ++x)
-            if (c->hot_c[x] && M * c->hot_pc[x] * flush_cap <= stale) r.push_back({c->hot_pc[x], (int32_t)x});
+        for (size_t i = 0; i < pcb[k].size(); ++i) {
+            if (!hcb[k][i]) continue;
+            const double p = pcb[k][i];
+            const double f = two_tier ? (double)sh_slot_interval(M * p, flush_cap) : (double)flush_cap;
+            if (M * p * f <= stale) r.push_back({p, (int32_t)(B.cb[k] + (int64_t)i)});
+        }
         const int64_t n = std::min<int64_t>(cap, (int64_t)r.size());
         std::partial_sort(r.begin(), r.begin() + n, r.end(), [](const auto& x, const auto& y) {
             return x.first > y.first || (x.first == y.first && x.second < y.second);
@@ -93,9 +105,11 @@ void block_sh_sets(smore_ctx* c, bool walk, std::vector<int2>& hash, std::vector
             h[p & (SH_HASH - 1)] = make_int2(r[i].second, (int)i);
         }
         B.sh_n[k] = (int)n;
-        B.sh_flush[k] = c->sh_flush > 0 ? c->sh_flush : flush_cap;
-        if (c->sh_flush <= 0 && n > 0)
-            B.sh_flush[k] = (int)std::max(8.0, std::min((double)flush_cap, std::floor(sh_auto_budget() / (M * r[0].first))));
+        if (two_tier && n > 0) {
+            int lv[8];
+            sh_slot_levels(Mg, flush_cap, r.data(), n, lv);
+            std::copy(lv, lv + 8, B.sh_lvl[k].begin());
+        }
     }
 }
 
@@ -118,8 +132,9 @@ EdgeArgs cell_args(smore_ctx* c, int k, bool walk) {
     a.sh_rows = on ? B.sh_n[k] : 0;
     a.sh_hash = B.d_sh_hash + (size_t)k * SH_HASH;
     a.sh_ids = B.d_sh_ids + (size_t)k * B.sh_cap;
-    a.sh_flush = std::max(1, B.sh_flush[k]);
+    a.sh_flush = std::max(1, B.sh_flush);
     a.sh_flush_w = 0;
+    std::copy(B.sh_lvl[k].begin(), B.sh_lvl[k].end(), a.sh_lvl);
     return a;
 }
 
@@ -164,7 +179,7 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
     const bool walk = model == SMORE_CENSUS;
     if (nparts == 1) {
         blocks_release(c);
-        return model == SMORE_LINE2 ? smore_set_source_partition(c, 1, 0) : SMORE_OK;
+        return SMORE_OK;
     }
     const HostGraph& g = *c->g;
     const int64_t V = g.V;
@@ -190,60 +205,45 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
         if (B.wb[p + 1] <= B.wb[p]) return fail(c, SMORE_EINVAL, "block schedule: an empty W part");
     for (int k = 0; k < nb; ++k)
         if (B.cb[k + 1] <= B.cb[k]) return fail(c, SMORE_EINVAL, "block schedule: an empty C block");
-    // LINE-2: this context's sources are its part's (the hot W tags follow the
-    // restricted law); walks: the walk ids carry the scaled global tags
-    if (!walk && (rc = smore_set_source_partition(c, nparts, part))) return rc;
-    if (mode == SMORE_HYBRID) {
-        const int64_t M = resident_groups(c, walk, K, mode);
-        if ((rc = hot_maps(c, SMORE_LINE2, K, M, walk, walk ? (double)nparts : 1.0, (double)nb))) return rc;
-    } else {
-        c->hot_c.clear();
-        c->hot_w.clear();
-        c->hot_pc.clear();
-        c->hot_small = false;
+    // Hot tags (hybrid scatter) and the write-combined sets.  LINE-2: exact
+    // per cell from its atoms -- W row v: its atoms' share of the cell's mass;
+    // C row x: its atoms' share plus K times its share of the block's negative
+    // law -- so a row is atomic iff M * p > tau in the launch that trains it
+    // (a scaled global law misses the sources whose contexts crowd one block:
+    // up to nb times hotter in that cell).  Walks: the scaled global law
+    // (capi build_hot_maps), whose tags the walk ids carry.
+    const bool hyb = mode == SMORE_HYBRID;
+    int64_t M = 0;
+    double tau = 0.0;
+    bool small = false;
+    if (hyb) {
+        M = resident_groups(c, walk, K, mode);
+        small = c->hot_tau < 0 && 16.0 * (double)M >= (double)V;
+        tau = c->hot_tau >= 0 ? c->hot_tau : small ? 0.0 : hot_tau_default(walk);
+        if (walk && (rc = hot_maps(c, SMORE_LINE2, K, M, true, (double)nparts, (double)nb))) return rc;
     }
-    const bool tags = mode == SMORE_HYBRID && !c->hot_c.empty();
-    auto hc = [&](int64_t x) -> uint32_t { return tags ? c->hot_c[x] : 0u; };
-    auto hw = [&](int64_t x) -> uint32_t { return tags ? c->hot_w[x] : 0u; };
-    // negative tables: block k's law restricted to [cb[k], cb[k+1]) (Go alias
-    // rule, power 1: any exact encoding of the law), ids absolute
-    {
-        hvec<AliasEntry> nt((size_t)V);
+    const int T = (int)std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), (unsigned)nb);
+    auto par_blocks = [&](auto&& f) {
         std::vector<std::thread> th;
-        const int T = (int)std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), (unsigned)nb);
         for (int t = 0; t < T; ++t)
             th.emplace_back([&, t] {
-                for (int k = t; k < nb; k += T) {
-                    const int64_t lo = B.cb[k], n = B.cb[k + 1] - lo;
-                    std::vector<double> prob((size_t)n);
-                    std::vector<int64_t> alias((size_t)n);
-                    std::vector<int32_t> self((size_t)n);
-                    alias_go(pn.data() + lo, n, 1.0, prob.data(), alias.data());
-                    for (int64_t i = 0; i < n; ++i) {
-                        alias[i] += lo;
-                        self[i] = (int32_t)(lo + i);
-                    }
-                    alias_encode(prob.data(), alias.data(), n, self.data(), nt.data() + lo);
-                    for (int64_t i = 0; i < n; ++i) {
-                        const uint32_t al = (uint32_t)nt[lo + i].alias;
-                        nt[lo + i].alias = (int32_t)(al | (hc(al) << 30) | (hc(lo + i) << 31));
-                    }
-                }
+                for (int k = t; k < nb; k += T) f(k);
             });
         for (auto& x : th) x.join();
-        if ((rc = upload(c, B.d_ntab, reinterpret_cast<const uint2*>(nt.data()), (size_t)V, true))) return rc;
-    }
+    };
     // LINE-2 atoms of this part: the TargetSample outcomes of its sources,
-    // bucketed by the context's block, one alias table per block
+    // bucketed by the context's block
     B.mass.assign((size_t)nb, 0.0);
     B.atom_off.assign((size_t)nb + 1, 0);
+    std::vector<int32_t> av, ac;
+    std::vector<double> aw;
+    const int64_t wlo = B.wb[part], whi = B.wb[part + 1];
     if (!walk) {
-        const int64_t lo = B.wb[part], hi = B.wb[part + 1];
         auto blk_of = [&](int64_t x) {
             return (int)(std::upper_bound(B.cb.begin(), B.cb.end(), x) - B.cb.begin()) - 1;
         };
         auto each_atom = [&](auto&& f) {
-            for (int64_t v = lo; v < hi; ++v) {
+            for (int64_t v = wlo; v < whi; ++v) {
                 const int64_t off = g.offsets[v], br = g.offsets[v + 1] - off;
                 if (br == 0 || ps[v] <= 0) continue;
                 const double s = ps[v] / (double)br;
@@ -261,8 +261,9 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
         for (int k = 0; k < nb; ++k) B.atom_off[k + 1] = B.atom_off[k] + cnt[k];
         const uint64_t A = B.atom_off[nb];
         if (A == 0) return fail(c, SMORE_EINVAL, "block schedule: a part without edges");
-        std::vector<int32_t> av(A), ac(A);
-        std::vector<double> aw(A);
+        av.resize(A);
+        ac.resize(A);
+        aw.resize(A);
         std::vector<uint64_t> pos(B.atom_off.begin(), B.atom_off.end() - 1);
         each_atom([&](int64_t v, int64_t x, double w) {
             if (w <= 0) return;
@@ -279,34 +280,89 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
             tot += m;
         }
         for (double& m : B.mass) m /= tot;
-        hvec<uint4> at((size_t)A * 2);
-        std::vector<std::thread> th;
-        const int T = (int)std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), (unsigned)nb);
-        for (int t = 0; t < T; ++t)
-            th.emplace_back([&, t] {
-                for (int k = t; k < nb; k += T) {
-                    const uint64_t a0 = B.atom_off[k], n = B.atom_off[k + 1] - a0;
-                    if (n == 0) continue;
-                    std::vector<double> prob(n);
-                    std::vector<int64_t> alias(n);
-                    std::vector<AliasEntry> e(n);
-                    alias_go(aw.data() + a0, (int64_t)n, 1.0, prob.data(), alias.data());
-                    alias_encode(prob.data(), alias.data(), (int64_t)n, nullptr, e.data());
-                    for (uint64_t i = 0; i < n; ++i) {
-                        const uint64_t s = a0 + i, a = a0 + (uint64_t)e[i].alias;
-                        at[2 * s] = make_uint4(e[i].thresh, (uint32_t)av[s] | (hw(av[s]) << 30),
-                                               (uint32_t)ac[s] | (hc(ac[s]) << 30), 0u);
-                        at[2 * s + 1] = make_uint4((uint32_t)av[a] | (hw(av[a]) << 30),
-                                                   (uint32_t)ac[a] | (hc(ac[a]) << 30), 0u, 0u);
-                    }
+    }
+    // per block: the C-row law of its cell (over [cb[k], cb[k+1])) and the
+    // flags of its C rows and (LINE-2) of this part's W rows
+    std::vector<std::vector<double>> pcb((size_t)nb);
+    std::vector<std::vector<uint8_t>> hcb((size_t)nb), hwb((size_t)nb);
+    if (hyb) {
+        par_blocks([&](int k) {
+            const int64_t lo = B.cb[k], n = B.cb[k + 1] - lo;
+            auto& pcx = pcb[k];
+            pcx.assign((size_t)n, 0.0);
+            hcb[k].assign((size_t)n, 0);
+            if (walk) {
+                for (int64_t i = 0; i < n; ++i) {
+                    pcx[i] = c->hot_pc[lo + i];
+                    hcb[k][i] = c->hot_c[lo + i];
                 }
-            });
-        for (auto& x : th) x.join();
+                return;
+            }
+            std::vector<double> pw((size_t)(whi - wlo), 0.0);
+            double m = 0.0, pnb = 0.0;
+            for (uint64_t p = B.atom_off[k]; p < B.atom_off[k + 1]; ++p) {
+                pw[av[p] - wlo] += aw[p];
+                pcx[ac[p] - lo] += aw[p];
+                m += aw[p];
+            }
+            for (int64_t i = 0; i < n; ++i) pnb += pn[lo + i];
+            hwb[k].assign(pw.size(), 0);
+            for (size_t i = 0; i < pw.size(); ++i) hwb[k][i] = m > 0 && (double)M * pw[i] / m > tau;
+            for (int64_t i = 0; i < n; ++i) {
+                pcx[i] = (m > 0 ? pcx[i] / m : 0.0) + (pnb > 0 ? K * pn[lo + i] / pnb : 0.0);
+                hcb[k][i] = (double)M * pcx[i] > tau;
+            }
+        });
+    }
+    auto hc = [&](int k, int64_t x) -> uint32_t { return hyb ? hcb[k][x - B.cb[k]] : 0u; };
+    auto hw = [&](int k, int64_t v) -> uint32_t { return hyb && !walk ? hwb[k][v - wlo] : 0u; };
+    // negative tables: block k's law restricted to [cb[k], cb[k+1]) (Go alias
+    // rule, power 1: any exact encoding of the law), ids absolute
+    {
+        hvec<AliasEntry> nt((size_t)V);
+        par_blocks([&](int k) {
+            const int64_t lo = B.cb[k], n = B.cb[k + 1] - lo;
+            std::vector<double> prob((size_t)n);
+            std::vector<int64_t> alias((size_t)n);
+            std::vector<int32_t> self((size_t)n);
+            alias_go(pn.data() + lo, n, 1.0, prob.data(), alias.data());
+            for (int64_t i = 0; i < n; ++i) {
+                alias[i] += lo;
+                self[i] = (int32_t)(lo + i);
+            }
+            alias_encode(prob.data(), alias.data(), n, self.data(), nt.data() + lo);
+            for (int64_t i = 0; i < n; ++i) {
+                const uint32_t al = (uint32_t)nt[lo + i].alias;
+                nt[lo + i].alias = (int32_t)(al | (hc(k, al) << 30) | (hc(k, lo + i) << 31));
+            }
+        });
+        if ((rc = upload(c, B.d_ntab, reinterpret_cast<const uint2*>(nt.data()), (size_t)V, true))) return rc;
+    }
+    // LINE-2: one alias table per block over its atoms, tagged per cell
+    if (!walk) {
+        hvec<uint4> at((size_t)B.atom_off[nb] * 2);
+        par_blocks([&](int k) {
+            const uint64_t a0 = B.atom_off[k], n = B.atom_off[k + 1] - a0;
+            if (n == 0) return;
+            std::vector<double> prob(n);
+            std::vector<int64_t> alias(n);
+            std::vector<AliasEntry> e(n);
+            alias_go(aw.data() + a0, (int64_t)n, 1.0, prob.data(), alias.data());
+            alias_encode(prob.data(), alias.data(), (int64_t)n, nullptr, e.data());
+            for (uint64_t i = 0; i < n; ++i) {
+                const uint64_t s = a0 + i, a = a0 + (uint64_t)e[i].alias;
+                at[2 * s] = make_uint4(e[i].thresh, (uint32_t)av[s] | (hw(k, av[s]) << 30),
+                                       (uint32_t)ac[s] | (hc(k, ac[s]) << 30), 0u);
+                at[2 * s + 1] = make_uint4((uint32_t)av[a] | (hw(k, av[a]) << 30),
+                                           (uint32_t)ac[a] | (hc(k, ac[a]) << 30), 0u, 0u);
+            }
+        });
         if ((rc = upload(c, B.d_atoms, at.data(), at.size(), true))) return rc;
     }
+    c->hot_M = M;
     std::vector<int2> hash;
     std::vector<int32_t> ids;
-    block_sh_sets(c, walk, hash, ids);
+    block_sh_sets(c, walk, hyb && !small, M, pcb, hcb, hash, ids);
     if ((rc = upload(c, B.d_sh_hash, hash.data(), hash.size()))) return rc;
     if ((rc = upload(c, B.d_sh_ids, ids.data(), ids.size()))) return rc;
     B.key = key;

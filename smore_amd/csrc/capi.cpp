@@ -459,6 +459,25 @@ constexpr int EDGE_FLUSH_MAX = 32, PAIR_FLUSH_MAX = 8;
 // the global law; the tags and the write-combined set follow the scaled law.
 // The C-row law and the flags are kept on the host (hot_pc, hot_c) for the
 // block tables' own tags and write-combined sets.
+// drain interval of one write-combined row with M * p expected updates per
+// round: the budget of hidden updates over that rate, a power of two in
+// [1, cap] (cap a power of two) -- the two-tier drain's unit
+static int slot_interval(double Mp, int cap) {
+    int f = 1;
+    while (2 * f <= cap && (double)(2 * f) * Mp <= SH_AUTO_BUDGET) f *= 2;
+    return f;
+}
+
+// EdgeArgs::sh_lvl of n slots sorted by rate: lvl[j] = the slots whose own
+// interval is at most 2^j (and below cap, which every slot drains at)
+static void sh_levels(int64_t M, int cap, const std::pair<double, int32_t>* r, int64_t n, int (&lvl)[8]) {
+    for (int j = 0; j < 8; ++j) {
+        int64_t k = 0;
+        while (k < n && slot_interval((double)M * r[k].first, cap) <= (1 << j) && (1 << j) < cap) ++k;
+        lvl[j] = (int)k;
+    }
+}
+
 static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_default,
                           int flush_max = EDGE_FLUSH_MAX, double w_scale = 1.0, double c_scale = 1.0) {
     // Small graphs (the V/16 concurrency cap binds: 16 M >= V, e.g. the test
@@ -486,9 +505,12 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_
     // default 8; 0 = with the context rows)
     const char* wflush_env = getenv("SMORE_SH_WFLUSH");
     const int wflush = wrows ? (wflush_env ? std::max(0, atoi(wflush_env)) : 8) : 0;
-    snprintf(key, sizeof key, "%d/%d/%lld/%.9g/%d/%d/%s/%d/%d/%d/%d/%d/%g/%g", model, K, (long long)M, tau, c->sh_max,
-             c->sh_flush, stale_env ? stale_env : "", (int)wrows, c->part_n, c->part_i, flush_max, wflush, w_scale,
-             c_scale);
+    // per-slot drain levels (EdgeArgs::sh_lvl): the C++ rules' edge and pair
+    // kernels; the Go record kernels drain on one interval
+    const bool two_tier = c->semantics != SMORE_SEM_GO && c->sh_flush <= 0 && !wrows;
+    snprintf(key, sizeof key, "%d/%d/%lld/%.9g/%d/%d/%s/%d/%d/%d/%d/%d/%g/%g/%d", model, K, (long long)M, tau,
+             c->sh_max, c->sh_flush, stale_env ? stale_env : "", (int)wrows, c->part_n, c->part_i, flush_max, wflush,
+             w_scale, c_scale, (int)two_tier);
     if (c->hot_key == key) return SMORE_OK;
     if (c->g->V >= ((int64_t)1 << 30)) return fail(c, SMORE_EINVAL, "hybrid scatter needs V < 2^30");
     std::vector<double> ps, pn, pc;
@@ -523,7 +545,9 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_
             // other workgroups for up to sh_flush rounds, i.e. about
             // M * p * sh_flush updates; rows above SH_STALE_MAX stay on atomics
             // (on small graphs that is every hot row)
-            if (hc[v] && (double)M * p * flush_cap <= stale_max) r.push_back({p, (int32_t)v});
+            // (two tiers: each row at its own interval, slot_interval)
+            const double f = two_tier ? (double)slot_interval((double)M * p, flush_cap) : (double)flush_cap;
+            if (hc[v] && (double)M * p * f <= stale_max) r.push_back({p, (int32_t)v});
             // two tables (SMORE_SH_WROWS=1 only): the hub W rows compete for
             // the same slots (key v | SH_WKEY)
             if (wrows && model == SMORE_LINE2 && hw[v] &&
@@ -552,11 +576,16 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_
         c->sh_rows = (int)n;
         c->sh_flush_eff = flush_cap;
         c->sh_flush_w_eff = wflush;
+        // every slot drains every flush_cap rounds; a slot whose own interval
+        // (slot_interval) is shorter also at its own (a prefix per level: r is
+        // sorted by rate)
+        for (int& x : c->sh_lvl_eff) x = 0;
+        if (two_tier) sh_levels(M, flush_cap, r.data(), n, c->sh_lvl_eff);
         // the automatic interval follows the hottest row drained on it (with
         // their own interval, W rows do not count)
         int64_t top = 0;
         while (top < n && wflush && (r[top].second & SH_WKEY)) ++top;
-        if (c->sh_flush <= 0 && top < n) {
+        if (c->sh_flush <= 0 && top < n && !two_tier) {
             const double f = SH_AUTO_BUDGET / ((double)M * r[top].first);
             c->sh_flush_eff = (int)std::max(8.0, std::min((double)flush_cap, std::floor(f)));
         }
@@ -738,6 +767,7 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
     a.sh_ids = c->d_sh_ids;
     a.sh_flush = std::max(1, c->sh_flush_eff);
     a.sh_flush_w = c->sh_flush_w_eff;
+    std::copy(std::begin(c->sh_lvl_eff), std::end(c->sh_lvl_eff), a.sh_lvl);
     // edge models: draw kernel -> update kernel per chunk of samples.  With
     // several chunks the draws of chunk k+1 run on a second stream while
     // chunk k updates (two record buffers; the update kernel leaves one block
@@ -1273,6 +1303,7 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
     ar.sh_ids = c->d_sh_ids;
     ar.sh_flush = std::max(1, c->sh_flush_eff);
     ar.sh_flush_w = c->sh_flush_w_eff;
+    std::copy(std::begin(c->sh_lvl_eff), std::end(c->sh_lvl_eff), ar.sh_lvl);
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     for (uint64_t b = walk_begin; b < walk_end; b += chunk) {
         WalkArgs w;
@@ -1501,6 +1532,7 @@ int smore_train_app_async(smore_ctx* c, uint64_t unit_begin, uint64_t unit_end, 
     a.sh_ids = c->d_sh_ids;
     a.sh_flush = std::max(1, c->sh_flush_eff);
     a.sh_flush_w = c->sh_flush_w_eff;
+    std::copy(std::begin(c->sh_lvl_eff), std::end(c->sh_lvl_eff), a.sh_lvl);
     a.rec = c->d_rec;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     for (uint64_t b = unit_begin; b < unit_end; b += chunk) {
@@ -1581,6 +1613,7 @@ int smore_train_hpe_async(smore_ctx* c, uint64_t begin, uint64_t count, uint64_t
     a.sh_ids = c->d_sh_ids;
     a.sh_flush = std::max(1, c->sh_flush_eff);
     a.sh_flush_w = c->sh_flush_w_eff;
+    std::copy(std::begin(c->sh_lvl_eff), std::end(c->sh_lvl_eff), a.sh_lvl);
     a.rec = c->d_rec;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     for (uint64_t b = begin; b < begin + count; b += chunk) {
@@ -1682,6 +1715,7 @@ int smore_train_pairs(smore_ctx* c, const int32_t* v, const int32_t* cc, int64_t
     a.sh_ids = c->d_sh_ids;
     a.sh_flush = std::max(1, c->sh_flush_eff);
     a.sh_flush_w = c->sh_flush_w_eff;
+    std::copy(std::begin(c->sh_lvl_eff), std::end(c->sh_lvl_eff), a.sh_lvl);
     a.rec = c->d_rec;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     for (uint64_t b = 0; b < (uint64_t)n; b += chunk) {
@@ -1841,6 +1875,11 @@ int hot_maps(smore_ctx* c, int model, int K, int64_t M, bool walk, double w_scal
 }
 int launch_grid(smore_ctx* c, const EdgeArgs& a) { return edge_grid(c, a, false, 0); }
 int sh_flush_max(bool walk) { return walk ? PAIR_FLUSH_MAX : EDGE_FLUSH_MAX; }
+int sh_slot_interval(double Mp, int cap) { return slot_interval(Mp, cap); }
+void sh_slot_levels(int64_t M, int cap, const std::pair<double, int32_t>* r, int64_t n, int (&lvl)[8]) {
+    sh_levels(M, cap, r, n, lvl);
+}
+double hot_tau_default(bool walk) { return walk ? HOT_TAU_WALK : HOT_TAU_EDGE; }
 double sh_stale_max() {
     const char* e = getenv("SMORE_SH_STALE");
     return e ? atof(e) : SH_STALE_MAX;

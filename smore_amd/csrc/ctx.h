@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -89,6 +90,7 @@ struct smore_ctx {
     int sh_max = 128, sh_flush = 0;      // flush 0: automatic drain interval (capi build_hot_maps)
     int sh_flush_eff = 32;               // the interval of the last hybrid launch
     int sh_flush_w_eff = 0;              // its W-key slots' own interval (0: none)
+    int sh_lvl_eff[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // its per-slot drain levels (EdgeArgs::sh_lvl)
     // pre-drawn edge-sample records (train_draw.hip) and per-phase timing
     int32_t* d_rec = nullptr;
     // DeepWalk pair records: per-walk pair counts, their exclusive scan, scan scratch
@@ -170,7 +172,9 @@ struct smore_ctx {
         int2* d_sh_hash = nullptr;      // nb x SH_HASH: per-block write-combined rows
         int32_t* d_sh_ids = nullptr;    // nb x sh_cap
         int sh_cap = 0;
-        std::vector<int> sh_n, sh_flush;
+        std::vector<int> sh_n;
+        std::vector<std::array<int, 8>> sh_lvl;   // per block: EdgeArgs::sh_lvl
+        int sh_flush = 32;              // every slot's drain interval
         std::string key;
         // walk records of the current round, bucketed by C block: per (block,
         // walk) counts and their exclusive scan (nb * walks + 1)
@@ -314,6 +318,9 @@ void part_bounds(const std::vector<double>& ps, int n, std::vector<int64_t>& bou
 int hot_maps(smore_ctx* c, int model, int K, int64_t M, bool walk, double w_scale, double c_scale);
 int launch_grid(smore_ctx* c, const EdgeArgs& a);
 int sh_flush_max(bool walk);
+int sh_slot_interval(double Mp, int cap);
+void sh_slot_levels(int64_t M, int cap, const std::pair<double, int32_t>* r, int64_t n, int (&lvl)[8]);
+double hot_tau_default(bool walk);
 double sh_stale_max();
 double sh_auto_budget();
 inline float* table_ptr(smore_ctx* c, int which) {

@@ -521,9 +521,10 @@ __device__ __forceinline__ ShState block_setup(const EdgeArgs& a, float* s_sig, 
 // an LDS add racing with the drain lands either in this drain or in the
 // wave's next one, never lost.  A slot's key is a Tc row id, or (two-table
 // models) a Tw row id | SH_WKEY.
-__device__ __forceinline__ void sh_drain(const ShState& sh, const int32_t* sh_ids, float* Tw, float* Tc, int dpad) {
+__device__ __forceinline__ void sh_drain_n(const ShState& sh, const int32_t* sh_ids, float* Tw, float* Tc, int dpad,
+                                           int slots) {
     const int nwaves = blockDim.x / 64, wave = threadIdx.x / 64;
-    const int n = sh.n * dpad;
+    const int n = slots * dpad;
     const int per = (n + nwaves - 1) / nwaves;
     const int lo = wave * per, hi = n < lo + per ? n : lo + per;
     for (int i = lo + (threadIdx.x & 63); i < hi; i += 64) {
@@ -535,6 +536,28 @@ __device__ __forceinline__ void sh_drain(const ShState& sh, const int32_t* sh_id
             unsafeAtomicAdd(T + (int64_t)(key & ~SH_WKEY) * dpad + e, x);
         }
     }
+}
+
+__device__ __forceinline__ void sh_drain(const ShState& sh, const int32_t* sh_ids, float* Tw, float* Tc, int dpad) {
+    sh_drain_n(sh, sh_ids, Tw, Tc, dpad, sh.n);
+}
+
+// the drain schedule of a hybrid launch, called once per round: every slot
+// every sh_flush rounds, and at round t the slots whose own interval 2^j
+// divides t -- a prefix of sh_lvl[j] slots (sorted by rate) -- in between
+__device__ __forceinline__ void sh_tick(const EdgeArgs& a, const ShState& sh, const int32_t* sh_ids, float* Tw,
+                                        float* Tc, uint32_t& round) {
+    if (sh.n <= 0) return;
+    if (++round == (uint32_t)a.sh_flush) {
+        sh_drain(sh, sh_ids, Tw, Tc, a.dpad);
+        round = 0;
+        return;
+    }
+    int ns = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if ((round & ((1u << j) - 1u)) == 0u) ns = a.sh_lvl[j];
+    if (ns > 0) sh_drain_n(sh, sh_ids, Tw, Tc, a.dpad, ns < sh.n ? ns : sh.n);
 }
 
 // sh_drain of the W-key slots only (the combined hub W rows of a two-table
@@ -621,11 +644,15 @@ edge_train_kernel(EdgeArgs a) {
     };
     auto maybe_flush = [&]() {
         if constexpr (MODE == MODE_HYBRID) {
-            if (sh.n > 0 && ++round == (uint32_t)a.sh_flush) {
-                drain();
-                round = 0;
-            } else if (sh.n > 0 && a.sh_flush_w > 0 && round % (uint32_t)a.sh_flush_w == 0) {
-                sh_drain_w(sh, sh_ids, a.W, a.dpad);
+            if (a.sh_flush_w > 0) {   // W-key slots on their own interval (SMORE_SH_WROWS)
+                if (sh.n > 0 && ++round == (uint32_t)a.sh_flush) {
+                    drain();
+                    round = 0;
+                } else if (sh.n > 0 && round % (uint32_t)a.sh_flush_w == 0) {
+                    sh_drain_w(sh, sh_ids, a.W, a.dpad);
+                }
+            } else {
+                sh_tick(a, sh, sh_ids, a.W, Tc, round);
             }
         }
     };
@@ -871,12 +898,7 @@ pair_train_kernel(EdgeArgs a) {
             // word 0 bit 31: HPE community record (Opt_SigmoidRegSGD)
             sgd_update_rows<G, M, KMAX, MODE, 0, false, true>(a, s_sig, lane, ev, v, id, false, hot, alpha, false,
                                                               false, sh, wv, rows, tv < 0);
-            if constexpr (MODE == MODE_HYBRID) {
-                if (sh.n > 0 && ++round == (uint32_t)a.sh_flush) {
-                    sh_drain(sh, sh_ids, a.W, a.C, a.dpad);
-                    round = 0;
-                }
-            }
+            if constexpr (MODE == MODE_HYBRID) sh_tick(a, sh, sh_ids, a.W, a.C, round);
         }
         flush_w();
     }

@@ -22,6 +22,11 @@ struct EdgeArgs {
     const int32_t* sh_ids;
     int sh_rows, sh_flush;
     int sh_flush_w;                // W-key slots (SMORE_SH_WROWS) drained every sh_flush_w rounds too (0: off)
+    // per-slot drain intervals: every slot drains every sh_flush rounds (a
+    // power of two); slot i also every 2^j rounds when i < sh_lvl[j] (the slot
+    // list is sorted by rate, so the slots due at a round are a prefix;
+    // all-zero sh_lvl: one interval for all)
+    int sh_lvl[8];
     // edge kernels: the pre-drawn sample records of samples [begin, begin+count)
     // (draw_kernel), rec_width(KMAX) int32 each
     const int32_t* rec;

@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--mode", default="hybrid")
     ap.add_argument("--seed", type=int, default=20251015)
+    ap.add_argument("--hot-tau", type=float, default=None, help="hybrid: hot-row threshold")
     args = ap.parse_args()
 
     import torch  # noqa: F401  (one HIP runtime with torch, as bench.py)
@@ -47,6 +48,8 @@ def main():
     pn = smore_amd.ProNet(0)
     pn.set_graph_edges(V, src, dst, w)
     pn.alloc_tables(dim, 2)
+    if args.hot_tau is not None:
+        pn.set_hot_threshold(args.hot_tau)
     pn.init_table_glibc(0, 0)
     pn.zero_table(1)
     S = args.samples
@@ -87,8 +90,8 @@ def main():
             setup_s = time.perf_counter() - t0
             cells = []
             if line:
-                cnt = pn.block_counts(S // n)
-                mine = S // n
+                cnt = pn.block_counts(S)      # weak scaling: S samples per GPU per epoch, as bench.py
+                mine = S
 
                 def epoch():
                     b0 = 0
@@ -103,7 +106,7 @@ def main():
                     if cnt[b]:
                         t1 = time.perf_counter()
                         pn.block_train_edges(b, 0, int(cnt[b]), total, K, 0.025, args.seed, args.mode)
-                        cells.append(round((time.perf_counter() - t1) * 1e3, 3))
+                        cells.append([b, int(cnt[b]), round((time.perf_counter() - t1) * 1e3, 3)])
                 units_r = mine
             else:
                 prep = timed(lambda: pn.block_prepare_walks(0, args.walks, wt, steps, window, K, 0.025, args.seed,
