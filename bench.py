@@ -231,6 +231,20 @@ def cpu_baseline(V, src, dst, w, dim, K, seconds, config):
                       % (dim, K, config, n_all, mine, quota, machine, t_all, n_one, t_one)}
 
 
+def graph_file(config):
+    """Where rank 0 of a node leaves the built graph for the others: host
+    memory (/dev/shm) when present; one name per job (the rendezvous port)."""
+    d = "/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir()
+    return os.path.join(d, "smore_bench_%s_%s_%s.graph" % (config, os.environ.get("MASTER_PORT", "0"),
+                                                            os.environ.get("TORCHELASTIC_RUN_ID", "x")))
+
+
+def peak_rss_gb():
+    """This process's peak resident host memory (GB)."""
+    import resource
+    return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0 ** 2
+
+
 def largest_remainder(samples, mass):
     """smore_block_counts restated: samples split by mass, largest remainder
     first (ties to the lower block)."""
@@ -327,14 +341,37 @@ def main():
     from smore_amd.dist import BlockSync, ReplicaSync, table_tensor
 
     t_gen = time.perf_counter()
-    V, (src, dst, w) = graphgen.config_edges(args.config)
-    t_build = time.perf_counter()
     pn = smore_amd.ProNet(local)
-    pn.set_graph_edges(V, src, dst, w)
+    src = dst = w = None
+    if world == 1:
+        V, (src, dst, w) = graphgen.config_edges(args.config)
+        t_build = time.perf_counter()
+        pn.set_graph_edges(V, src, dst, w)
+    else:
+        # one process per node generates and builds the graph and writes it
+        # (smore_save_graph); the others read it (smore_load_graph) instead of
+        # generating and building 400M slots each under a shared CPU quota
+        path = graph_file(args.config)
+        if local == 0:
+            V, (src, dst, w) = graphgen.config_edges(args.config)
+            t_build = time.perf_counter()
+            pn.set_graph_edges(V, src, dst, w)
+            pn.save_graph(path)
+            src = dst = w = None
+        dist.barrier()
+        t_build = time.perf_counter() if local != 0 else t_build
+        if local != 0:
+            pn.load_graph(path)
+        V = pn.MAX_vid
+        dist.barrier()
+        if local == 0:
+            os.remove(path)
     t_ready = time.perf_counter()
+    setup = {"rank": rank, "setup_s": round(t_ready - t_gen, 2), "graph_s": round(t_ready - t_build, 2),
+             "peak_rss_gb": round(peak_rss_gb(), 2)}
     if rank == 0:
-        print("[bench] %s: generated in %.1f s, graph built + uploaded in %.1f s"
-              % (args.config, t_build - t_gen, t_ready - t_build), file=sys.stderr, flush=True)
+        print("[bench] %s: graph ready in %.1f s (generated %.1f s, built / read + uploaded %.1f s)"
+              % (args.config, t_ready - t_gen, t_build - t_gen, t_ready - t_build), file=sys.stderr, flush=True)
     E = pn.MAX_line
     if args.semantics == "go":
         pn.set_semantics("go")
@@ -363,6 +400,7 @@ def main():
         # 2N C blocks), the rotation over torch.distributed
         t_bs = time.perf_counter()
         pn.block_setup("line2", world, rank, args.negative, args.mode)
+        setup["block_setup_s"] = round(time.perf_counter() - t_bs, 2)
         wb, cb = pn.block_bounds()
         bsync = BlockSync(table_tensor(pn, 0), table_tensor(pn, 1), wb, cb)
         if rank == 0:
@@ -426,6 +464,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     skipped = pn.skipped()
+    setup["peak_rss_gb"] = round(peak_rss_gb(), 2)
+    setups = [setup]
+    if dist:
+        setups = [None] * world
+        dist.all_gather_object(setups, setup)
 
     updates = S * args.steps * world
     R, Wb = algorithmic_bytes(args.dim, K)
@@ -515,6 +558,10 @@ def main():
                                     "traffic": traffic_upd}},
             "cpu_baseline": cpu,
             "skipped_samples": int(skipped),
+            # per rank: graph generation / build (local rank 0) or read (the
+            # others), block-table setup, peak host RSS
+            "setup": {"max_setup_s": max(x["setup_s"] for x in setups),
+                      "max_peak_rss_gb": max(x["peak_rss_gb"] for x in setups), "ranks": setups},
         }
         print(json.dumps(out), flush=True)
     if dist:

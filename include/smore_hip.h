@@ -99,6 +99,12 @@ int smore_last_load_info(const smore_ctx* ctx, double* seconds, int* threads, in
 int smore_set_graph_edges(smore_ctx* ctx, int64_t V, int64_t E, const int32_t* src,
                           const int32_t* dst, const double* w, int vertex_method,
                           int negative_method);
+/* new (multi-GPU start-up): the built graph -- CSR, degrees, the three alias
+ * tables -- to a binary file and back (the edge-list loader's graph-cache
+ * format), so one process of an N-GPU job builds it and the others read it;
+ * smore_load_graph fails (SMORE_EIO) on another format or sampling methods. */
+int smore_save_graph(const smore_ctx* ctx, const char* path);
+int smore_load_graph(smore_ctx* ctx, const char* path, int vertex_method, int negative_method);
 /* graph sizes (MAX_vid, MAX_line) */
 int smore_graph_info(const smore_ctx* ctx, int64_t* V, int64_t* E);
 /* vertex name of id (proNet::vertex_hash.keys / Go GetVertexName
@@ -510,6 +516,23 @@ int smore_train_hpe_async(smore_ctx* ctx, uint64_t begin, uint64_t count, uint64
  * interposed.  mode as the training calls; synchronous. */
 int smore_train_pairs(smore_ctx* ctx, const int32_t* v, const int32_t* c, int64_t n, int K, double alpha,
                       uint64_t seed, uint64_t unit, int mode);
+/* new (the Go UpdatePairs hook, go/pkg/pronet/hip.go): a batch costs
+ * O(pairs x dim) instead of O(MaxVid x dim) when only the rows it touches
+ * move.  smore_pairs_rows: the sorted unique W rows (the vertices) and C rows
+ * (the contexts and the K negatives smore_train_pairs will draw for this
+ * batch with this seed / unit -- stream 3, computed on the host) of a batch;
+ * w_ids holds n, c_ids n (K + 1) entries.  smore_set_rows / smore_get_rows:
+ * rows `ids` of a table from / to a dense host buffer [n][dim]. */
+int smore_pairs_rows(smore_ctx* ctx, const int32_t* v, const int32_t* c, int64_t n, int K, uint64_t seed,
+                     uint64_t unit, int32_t* w_ids, int64_t* nw, int32_t* c_ids, int64_t* nc);
+int smore_set_rows(smore_ctx* ctx, int which, const int32_t* ids, int64_t n, const float* rows);
+int smore_get_rows(smore_ctx* ctx, int which, const int32_t* ids, int64_t n, float* rows);
+/* the three in one synchronisation: W rows w_ids (nw x dim, w_rows) and C rows
+ * c_ids (c_rows) up, smore_train_pairs, the same rows back into w_rows /
+ * c_rows (ids from smore_pairs_rows) */
+int smore_train_pairs_rows(smore_ctx* ctx, const int32_t* v, const int32_t* c, int64_t n, int K, double alpha,
+                           uint64_t seed, uint64_t unit, int mode, const int32_t* w_ids, int64_t nw, float* w_rows,
+                           const int32_t* c_ids, int64_t nc, float* c_rows);
 
 /* ---- row census (the walk models' multi-GPU exchange rates) ---------------
  * Between smore_census_begin and smore_census_end the walk-model calls of this

@@ -50,6 +50,8 @@ def _load():
         "smore_version": (C.c_char_p, []),
         "smore_load_edgelist": (i32, [P, C.c_char_p, i32, i32, i32]),
         "smore_set_load_cache": (i32, [P, C.c_char_p]),
+        "smore_save_graph": (i32, [P, C.c_char_p]),
+        "smore_load_graph": (i32, [P, C.c_char_p, i32, i32]),
         "smore_last_load_info": (i32, [P, C.POINTER(dbl), C.POINTER(i32), C.POINTER(i32)]),
         "smore_set_graph_edges": (i32, [P, i64, i64, P, P, P, i32, i32]),
         "smore_graph_info": (i32, [P, C.POINTER(i64), C.POINTER(i64)]),
@@ -137,6 +139,10 @@ def _load():
         "smore_group_train_hpe": (i32, [P, u64, u64, u64, i32, i32, dbl, dbl, u64, i32, u64, i32]),
         "smore_sample_edges": (i32, [P, i32, u64, u64, i32, u64, P]),
         "smore_train_pairs": (i32, [P, P, P, i64, i32, dbl, u64, u64, i32]),
+        "smore_pairs_rows": (i32, [P, P, P, i64, i32, u64, u64, P, C.POINTER(i64), P, C.POINTER(i64)]),
+        "smore_set_rows": (i32, [P, i32, P, i64, P]),
+        "smore_get_rows": (i32, [P, i32, P, i64, P]),
+        "smore_train_pairs_rows": (i32, [P, P, P, i64, i32, dbl, u64, u64, i32, P, i64, P, P, i64, P]),
         "smore_census_begin": (i32, [P]),
         "smore_census_end": (i32, [P, dbl]),
         "smore_set_walk_owner": (i32, [P, i64, i64]),

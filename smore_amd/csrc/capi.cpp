@@ -62,8 +62,9 @@ void smore_destroy(smore_ctx* c) {
     dfree(c->d_sig); dfree(c->d_skipped); dfree(c->d_work); dfree(c->d_table[0]); dfree(c->d_table[1]);
 
     dfree(c->d_order); dfree(c->d_walks); dfree(c->d_lens); dfree(c->d_tcum); dfree(c->d_wts); dfree(c->d_nbr_sorted); dfree(c->d_ntype); dfree(c->d_ttargets); dfree(c->d_toff); dfree(c->d_paths); dfree(c->d_path_off); dfree(c->d_t_off); dfree(c->d_t_tgt); dfree(c->d_t_ts); dfree(c->d_t_min); dfree(c->d_t_max); dfree(c->d_sh_hash); dfree(c->d_sh_ids);
-    dfree(c->d_rec); dfree(c->d_vt32); dfree(c->d_ct16);
+    dfree(c->d_rec); dfree(c->d_vt32); dfree(c->d_ct16); dfree(c->d_split);
     dfree(c->d_pcount); dfree(c->d_poff); dfree(c->d_pairs); dfree(c->d_census[0]); dfree(c->d_census[1]);
+    dfree(c->d_io_ids[0]); dfree(c->d_io_rows[0]); dfree(c->d_io_ids[1]); dfree(c->d_io_rows[1]);
     blocks_release(c);
     if (c->d_scan_tmp) (void)hipFree(c->d_scan_tmp);
     for (hipEvent_t e : c->phase_ev) (void)hipEventDestroy(e);
@@ -141,6 +142,28 @@ int smore_load_edgelist(smore_ctx* c, const char* path, int undirected, int vm, 
     if (rc == SMORE_OK) c->g->names = std::move(names);
     if (rc == SMORE_OK && !gfile.empty()) (void)save_graph_cache(gfile, key, *c->g);
     return rc;
+}
+
+// the built graph (CSR, degrees, alias tables) to / from a binary file: one
+// process of a multi-GPU job builds it, the others read it (bench.py at N > 1;
+// the same format as the edge-list loader's graph cache, loader.cpp)
+static constexpr uint64_t GRAPH_FILE_KEY = 0x534d4f5245475246ull;   // "SMOREGRF"
+
+int smore_save_graph(const smore_ctx* c, const char* path) {
+    if (!c || !path) return SMORE_EINVAL;
+    if (!c->has_graph) return SMORE_ESTATE;
+    return save_graph_cache(path, GRAPH_FILE_KEY, *c->g) ? SMORE_OK : SMORE_EIO;
+}
+
+int smore_load_graph(smore_ctx* c, const char* path, int vm, int nm) {
+    if (!c || !path || vm < 0 || vm > 2 || nm < 0 || nm > 2) return SMORE_EINVAL;
+    auto g = std::make_shared<HostGraph>();
+    if (!load_graph_cache(path, GRAPH_FILE_KEY, vm, nm, *g))
+        return fail(c, SMORE_EIO, std::string("cannot read a graph file (or other sampling methods): ") + path);
+    c->g = g;
+    c->hot_key.clear();
+    c->semantics = SMORE_SEM_CPP;
+    return upload_graph(c);
 }
 
 int smore_set_load_cache(smore_ctx* c, const char* dir) {
@@ -704,6 +727,18 @@ static int edge_grid(smore_ctx* c, const EdgeArgs& a, bool leave_slot = false, i
     return (int)(grid < 1 ? 1 : grid);
 }
 
+// the hot/cold record split of the C++ edge models' hybrid scatter (train_draw.hip
+// draw_split_kernel): SMORE_SPLIT=1 / 0 overrides the per-model default
+static bool split_on(int model) {
+    static const int env = [] {
+        const char* e = getenv("SMORE_SPLIT");
+        return e ? atoi(e) : -1;
+    }();
+    if (env >= 0) return env != 0;
+    (void)model;
+    return false;
+}
+
 int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t count, uint64_t total, int K,
                             double alpha0, double reg, uint64_t seed, int mode) {
     if (!c) return SMORE_EINVAL;
@@ -800,6 +835,11 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
     if ((rc = grow(c->sync_ev, 2 * (size_t)nch))) return rc;
     if ((rc = ensure_packed(c))) return rc;
     const DevGraph dg = dev_graph(c);
+    // hot/cold record split (C++ rules, hybrid): records touching no hot row
+    // run through the plain-store kernel (train_draw.hip draw_split_kernel);
+    // SMORE_SPLIT=1/0 forces it on / off, default split_default()
+    const bool split = mode == SMORE_HYBRID && !go && dg.vt32 && split_on(model);
+    if (split && !c->d_split) HIPCHK(c, hipMalloc((void**)&c->d_split, 4 * sizeof(unsigned long long)));
     // tuning knob: SMORE_DRAW_LEAVE=0 keeps the update kernel's full grid
     // while the next chunk's draws run beside it
     const char* leave_env = getenv("SMORE_DRAW_LEAVE");
@@ -811,7 +851,13 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
         const uint64_t b = (uint64_t)k * chunk, n = std::min<uint64_t>(chunk, count - b);
         if (k >= 2) HIPCHK(c, hipStreamWaitEvent(ds, c->sync_ev[2 * (k - 2) + 1], 0));   // buffer free
         if (go) HIPCHK(c, launch_go_draw(dg, c->d_tcum, c->go_unit_w, seed, begin + b, n, a.K, recbuf(k), c->d_skipped, ds));
-        else HIPCHK(c, launch_draw(dg, seed, begin + b, n, a.K, recbuf(k), c->d_skipped, ds));
+        else if (split) {
+            unsigned long long* cnt = c->d_split + 2 * (k % nbuf);
+            HIPCHK(c, hipMemsetAsync(cnt, 0, 2 * sizeof(unsigned long long), ds));
+            HIPCHK(c, launch_draw_split(dg, seed, begin + b, n, a.K, alpha0, total,
+                                        model == SMORE_MF || model == SMORE_BPR ? 0 : 1, recbuf(k), c->d_skipped, cnt,
+                                        ds));
+        } else HIPCHK(c, launch_draw(dg, seed, begin + b, n, a.K, recbuf(k), c->d_skipped, ds));
         HIPCHK(c, hipEventRecord(c->sync_ev[2 * k], ds));
         return SMORE_OK;
     };
@@ -831,7 +877,21 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
         ak.work = c->d_work;
         HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
         if (go) HIPCHK(c, launch_go_rec(ak, ugrid, c->stream));
-        else HIPCHK(c, launch_edge_train(ak, ugrid, c->stream));
+        else if (split) {
+            // hot records [0, h) on the hybrid kernel, cold [h, n) on the
+            // plain-store kernel; both read their rate from the record
+            unsigned long long* cnt = c->d_split + 2 * (k % nbuf);
+            ak.alpha_rec = 2;
+            ak.count_dev = reinterpret_cast<const uint64_t*>(cnt);
+            HIPCHK(c, launch_edge_train(ak, ugrid, c->stream));
+            EdgeArgs ac = ak;
+            ac.mode = SMORE_HOGWILD;
+            ac.sh_rows = 0;
+            ac.count_dev = nullptr;
+            ac.rec_base = reinterpret_cast<const uint64_t*>(cnt);
+            HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
+            HIPCHK(c, launch_edge_train(ac, edge_grid(c, ac), c->stream));
+        } else HIPCHK(c, launch_edge_train(ak, ugrid, c->stream));
         HIPCHK(c, hipEventRecord(c->phase_ev[2 * k + 2], c->stream));
         HIPCHK(c, hipEventRecord(c->sync_ev[2 * k + 1], c->stream));
     }
@@ -1661,8 +1721,21 @@ int smore_train_deepwalk(smore_ctx* c, uint64_t walk_begin, uint64_t walk_end, i
 // (caller_pair_kernel, negatives drawn on the device) for the pair kernels --
 // pair_train_kernel (C++ UpdatePair; serial: edge_train_kernel's in-order
 // path) or go_pair_kernel (Go UpdatePair) -- in chunks of up to 2^24 pairs.
+static int train_pairs_core(smore_ctx* c, const int32_t* v, const int32_t* cc, int64_t n, int K, double alpha,
+                            uint64_t seed, uint64_t unit, int mode);
+
 int smore_train_pairs(smore_ctx* c, const int32_t* v, const int32_t* cc, int64_t n, int K, double alpha,
                       uint64_t seed, uint64_t unit, int mode) {
+    int rc = train_pairs_core(c, v, cc, n, K, alpha, seed, unit, mode);
+    if (rc || !c || n == 0) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipGetLastError());
+    return SMORE_OK;
+}
+
+// smore_train_pairs queued on the stream (the caller synchronizes)
+static int train_pairs_core(smore_ctx* c, const int32_t* v, const int32_t* cc, int64_t n, int K, double alpha,
+                            uint64_t seed, uint64_t unit, int mode) {
     if (!c) return SMORE_EINVAL;
     if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
     if (c->ntables < 2) return fail(c, SMORE_ESTATE, "UpdatePairs needs W and C tables");
@@ -1729,6 +1802,11 @@ int smore_train_pairs(smore_ctx* c, const int32_t* v, const int32_t* cc, int64_t
         EdgeArgs ak = a;
         ak.begin = 0;
         ak.count = m;
+        // a small batch (one walk's pairs, the Go callers' unit): short
+        // slices so that every pair gets a group of its own; the
+        // CH_ROUNDS-record slices keep W_v in registers over a long batch
+        const uint64_t groups = (uint64_t)grid * (uint64_t)(256 / lanes_of(c->dpad));
+        if (m < groups * CH_ROUNDS) ak.pair_slice = (uint32_t)std::max<uint64_t>(1, (m + groups - 1) / groups);
         const int g = mode == SMORE_SERIAL ? 1 : grid;
         HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
         if (c->census)
@@ -1741,6 +1819,120 @@ int smore_train_pairs(smore_ctx* c, const int32_t* v, const int32_t* cc, int64_t
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
     c->phase_n = 0;
+    return SMORE_OK;
+}
+
+// ---------------------------------------------------------------- touched rows
+// The Philox spec on the host (device_common.h philox_block):
+// the negatives smore_train_pairs will draw, without a device round trip.
+static uint32_t philox_word(uint64_t seed, uint32_t stream, uint64_t unit, uint32_t slot) {
+    uint32_t c0 = (uint32_t)unit, c1 = (uint32_t)(unit >> 32), c2 = slot >> 2, c3 = stream;
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    for (int r = 0; r < 10; ++r) {
+        if (r) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0, hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        c0 = hi1 ^ c1 ^ k0;
+        c1 = lo1;
+        c2 = hi0 ^ c3 ^ k1;
+        c3 = lo0;
+    }
+    const uint32_t w[4] = {c0, c1, c2, c3};
+    return w[slot & 3];
+}
+
+int smore_pairs_rows(smore_ctx* c, const int32_t* v, const int32_t* cc, int64_t n, int K, uint64_t seed,
+                     uint64_t unit, int32_t* w_ids, int64_t* nw, int32_t* c_ids, int64_t* nc) {
+    if (!c || !nw || !nc || (n > 0 && (!v || !cc || !w_ids || !c_ids)) || n < 0 || K < 0 || K > 10)
+        return SMORE_EINVAL;
+    if (!c->has_graph) return fail(c, SMORE_ESTATE, "no graph");
+    const HostGraph& g = *c->g;
+    const int64_t V = g.V;
+    std::vector<int32_t> ws, cs;
+    ws.reserve((size_t)n);
+    cs.reserve((size_t)n * (K + 1));
+    for (int64_t i = 0; i < n; ++i) {
+        if (v[i] < 0 || v[i] >= V || cc[i] < 0 || cc[i] >= V) return fail(c, SMORE_EINVAL, "pair id out of range");
+        ws.push_back(v[i]);
+        cs.push_back(cc[i]);
+        // caller_pair_kernel's draws: stream 3, unit + i / PAIR_BLOCK, slots
+        // 2K (i % PAIR_BLOCK) + 2q (index), + 1 (p)
+        const uint64_t u = unit + (uint64_t)i / PAIR_BLOCK;
+        const uint32_t base = 2u * (uint32_t)K * (uint32_t)((uint64_t)i % PAIR_BLOCK);
+        for (int q = 0; q < K; ++q) {
+            const uint32_t ki = philox_word(seed, 3, u, base + 2u * (uint32_t)q);
+            const uint32_t kp = philox_word(seed, 3, u, base + 2u * (uint32_t)q + 1u);
+            const uint32_t ni = (uint32_t)(((uint64_t)ki * (uint64_t)V) >> 32);
+            const AliasEntry e = g.ntab[ni];
+            cs.push_back(kp < e.thresh ? (int32_t)ni : (e.alias & ID_MASK));
+        }
+    }
+    std::sort(ws.begin(), ws.end());
+    ws.erase(std::unique(ws.begin(), ws.end()), ws.end());
+    std::sort(cs.begin(), cs.end());
+    cs.erase(std::unique(cs.begin(), cs.end()), cs.end());
+    std::copy(ws.begin(), ws.end(), w_ids);
+    std::copy(cs.begin(), cs.end(), c_ids);
+    *nw = (int64_t)ws.size();
+    *nc = (int64_t)cs.size();
+    return SMORE_OK;
+}
+
+// rows `ids` of table `which` from (to_table) / to a host buffer, through the
+// device buffers of slot `which`, queued on the context stream (the host
+// buffer is read / written when the stream gets there: synchronize first)
+static int rows_io_async(smore_ctx* c, int which, const int32_t* ids, int64_t n, float* rows, bool to_table) {
+    if (!c || n < 0 || (n > 0 && (!ids || !rows))) return SMORE_EINVAL;
+    int rc;
+    if ((rc = check_table(c, which))) return rc;
+    if (n == 0) return SMORE_OK;
+    for (int64_t i = 0; i < n; ++i)
+        if (ids[i] < 0 || ids[i] >= c->g->V) return fail(c, SMORE_EINVAL, "row id out of range");
+    if ((rc = set_device(c))) return rc;
+    if (c->io_cap[which] < (size_t)n) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        dfree(c->d_io_ids[which]);
+        dfree(c->d_io_rows[which]);
+        c->io_cap[which] = 0;
+        const size_t cap = std::max<size_t>((size_t)n, 4096);
+        HIPCHK(c, hipMalloc((void**)&c->d_io_ids[which], cap * sizeof(int32_t)));
+        HIPCHK(c, hipMalloc((void**)&c->d_io_rows[which], cap * c->dim * sizeof(float)));
+        c->io_cap[which] = cap;
+    }
+    const size_t bytes = (size_t)n * c->dim * sizeof(float);
+    HIPCHK(c, hipMemcpyAsync(c->d_io_ids[which], ids, (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    if (to_table) HIPCHK(c, hipMemcpyAsync(c->d_io_rows[which], rows, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, launch_rows_io(c->d_table[which], c->d_io_ids[which], (uint64_t)n, c->dpad, c->dim, c->d_io_rows[which],
+                             to_table ? 1 : 0, c->stream));
+    if (!to_table) HIPCHK(c, hipMemcpyAsync(rows, c->d_io_rows[which], bytes, hipMemcpyDeviceToHost, c->stream));
+    return SMORE_OK;
+}
+
+int smore_set_rows(smore_ctx* c, int which, const int32_t* ids, int64_t n, const float* rows) {
+    int rc = rows_io_async(c, which, ids, n, const_cast<float*>(rows), true);
+    if (rc == SMORE_OK && c && n > 0) HIPCHK(c, hipStreamSynchronize(c->stream));
+    return rc;
+}
+
+int smore_get_rows(smore_ctx* c, int which, const int32_t* ids, int64_t n, float* rows) {
+    int rc = rows_io_async(c, which, ids, n, rows, false);
+    if (rc == SMORE_OK && c && n > 0) HIPCHK(c, hipStreamSynchronize(c->stream));
+    return rc;
+}
+
+int smore_train_pairs_rows(smore_ctx* c, const int32_t* v, const int32_t* cc, int64_t n, int K, double alpha,
+                           uint64_t seed, uint64_t unit, int mode, const int32_t* w_ids, int64_t nw, float* w_rows,
+                           const int32_t* c_ids, int64_t nc, float* c_rows) {
+    int rc;
+    if (!c) return SMORE_EINVAL;
+    if ((rc = rows_io_async(c, 0, w_ids, nw, w_rows, true))) return rc;
+    if ((rc = rows_io_async(c, 1, c_ids, nc, c_rows, true))) return rc;
+    if ((rc = train_pairs_core(c, v, cc, n, K, alpha, seed, unit, mode))) return rc;
+    if ((rc = rows_io_async(c, 0, w_ids, nw, w_rows, false))) return rc;
+    if ((rc = rows_io_async(c, 1, c_ids, nc, c_rows, false))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipGetLastError());
     return SMORE_OK;

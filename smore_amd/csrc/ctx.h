@@ -93,6 +93,7 @@ struct smore_ctx {
     int sh_lvl_eff[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // its per-slot drain levels (EdgeArgs::sh_lvl)
     // pre-drawn edge-sample records (train_draw.hip) and per-phase timing
     int32_t* d_rec = nullptr;
+    unsigned long long* d_split = nullptr;   // hot / cold record counts of the split draw (2 per chunk buffer)
     // DeepWalk pair records: per-walk pair counts, their exclusive scan, scan scratch
     uint32_t* d_pcount = nullptr;
     uint64_t* d_poff = nullptr;
@@ -152,6 +153,10 @@ struct smore_ctx {
     // caller-supplied pairs (smore_train_pairs): a chunk of (v, c) on the device
     int32_t* d_pairs = nullptr;
     size_t pairs_cap = 0;               // pairs
+    // row transfers (smore_set_rows / smore_get_rows): ids and dense rows
+    int32_t* d_io_ids[2] = {nullptr, nullptr};   // [W, C] of smore_train_pairs_rows
+    float* d_io_rows[2] = {nullptr, nullptr};
+    size_t io_cap[2] = {0, 0};          // rows
     // the last hybrid hot maps' host side (capi build_hot_maps): row flags and
     // the C-row touch law they were made from, for the block tables' own tags
     std::vector<uint8_t> hot_c, hot_w;

@@ -840,7 +840,8 @@ pair_train_kernel(EdgeArgs a) {
     row_valid<G, M>(ev, lane, a.dpad);
     uint32_t round = 0;
     __shared__ uint64_t s_next;
-    const uint64_t span = CH_ROUNDS * gpb;
+    const uint64_t sl = a.pair_slice ? (uint64_t)a.pair_slice : CH_ROUNDS;   // records per group slice
+    const uint64_t span = sl * gpb;
     for (;;) {
         __syncthreads();   // every wave has read the previous s_next
         if (threadIdx.x == 0) s_next = atomicAdd(a.work, 1ull) * span;
@@ -848,8 +849,8 @@ pair_train_kernel(EdgeArgs a) {
         const uint64_t c0 = s_next;
         if (c0 >= count) break;
         const uint64_t lim = c0 + span < count ? c0 + span : count;
-        const uint64_t s0 = c0 + gib * CH_ROUNDS;
-        const uint64_t s1 = s0 + CH_ROUNDS < lim ? s0 + CH_ROUNDS : lim;
+        const uint64_t s0 = c0 + gib * sl;
+        const uint64_t s1 = s0 + sl < lim ? s0 + sl : lim;
         int32_t cv = -1;
         float wv[M], wv0[M], rows[KMAX + 1][M];
 #pragma unroll

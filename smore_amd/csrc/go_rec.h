@@ -474,7 +474,8 @@ go_pair_kernel(EdgeArgs a) {
         return;
     }
     __shared__ uint64_t s_next;
-    const uint64_t span = CH_ROUNDS * gpb;
+    const uint64_t sl = a.pair_slice ? (uint64_t)a.pair_slice : CH_ROUNDS;   // records per group slice
+    const uint64_t span = sl * gpb;
     for (;;) {
         __syncthreads();
         if (threadIdx.x == 0) s_next = atomicAdd(a.work, 1ull) * span;
@@ -482,8 +483,8 @@ go_pair_kernel(EdgeArgs a) {
         const uint64_t c0 = s_next;
         if (c0 >= count) break;
         const uint64_t lim = c0 + span < count ? c0 + span : count;
-        const uint64_t s0 = c0 + gib * CH_ROUNDS;
-        slice(s0 < lim ? s0 : lim, s0 + CH_ROUNDS < lim ? s0 + CH_ROUNDS : lim);
+        const uint64_t s0 = c0 + gib * sl;
+        slice(s0 < lim ? s0 : lim, s0 + sl < lim ? s0 + sl : lim);
     }
     if constexpr (MODE == MODE_HYBRID) {
         if (sh.n > 0) {

@@ -48,4 +48,26 @@ hipError_t launch_copy(const void* src, void* dst, uint64_t n16, int blocks, int
     return hipGetLastError();
 }
 
+// rows `ids` of a table [*][dpad] to / from a dense host-order buffer [n][dim]
+// (smore_set_rows / smore_get_rows: the Go UpdatePairs hook moves only the
+// rows a batch touches); one float per thread
+__global__ void __launch_bounds__(256) rows_io_kernel(float* T, const int32_t* ids, uint64_t n, int dpad, int dim,
+                                                      float* buf, int to_table) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n * (uint64_t)dim) return;
+    const uint64_t r = i / (uint64_t)dim, e = i - r * (uint64_t)dim;
+    float* t = T + (uint64_t)ids[r] * (uint64_t)dpad + e;
+    if (to_table) *t = buf[i];
+    else buf[i] = *t;
+}
+
+hipError_t launch_rows_io(float* T, const int32_t* ids, uint64_t n, int dpad, int dim, float* buf, int to_table,
+                          hipStream_t st) {
+    const uint64_t m = n * (uint64_t)dim;
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(rows_io_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, T, ids, n, dpad, dim, buf,
+                       to_table);
+    return hipGetLastError();
+}
+
 }  // namespace smore

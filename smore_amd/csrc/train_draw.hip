@@ -121,6 +121,108 @@ __global__ void __launch_bounds__(256) draw_kernel(DevGraph g, uint64_t seed, ui
     if (c < 0) atomicAdd(skipped, 1ull);
 }
 
+// Hot/cold record split (hybrid scatter): the same draws as
+// draw_kernel<KMAX, 0>, each record written with its learning rate in word
+// 2 + KMAX (the rate of its global sample index, as the update kernel would
+// compute it: base 1 for LINE, 0 for MF / BPR) and placed by whether any of
+// its ids carries a hot tag: hot records fill rec[0 ..) in arrival order,
+// the others rec[.. count) from the back (one counter add per wave each), so
+// counts[0] hot records then count - counts[0] cold ones.  The cold ones touch
+// no hot row and run through the plain-store update kernel (more resident
+// blocks, less code), the hot ones through the hybrid kernel.
+template <int KMAX>
+__global__ void __launch_bounds__(256) draw_split_kernel(DevGraph g, uint64_t seed, uint64_t begin, uint64_t count,
+                                                         int K, double alpha0, uint64_t total, int base, int32_t* rec,
+                                                         unsigned long long* skipped, unsigned long long* counts) {
+    constexpr int RW = rec_width(KMAX);
+    static_assert(RW > 2 + KMAX, "a record needs a free word for the rate");
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= count) return;
+    const uint64_t s = begin + t;
+    const uint4 b0 = philox_block(seed, 0, s, 0);
+    const uint32_t vi = draw_index(b0.y, g.V);
+    const uint4 p0 = ldr(g.vt32 + 2 * (uint64_t)vi), p1 = ldr(g.vt32 + 2 * (uint64_t)vi + 1);
+    uint32_t nidx[KMAX], np[KMAX];
+#pragma unroll
+    for (int j = 0; j < KMAX; j += 2) {
+        if (j < K) {
+            const uint4 b = philox_block(seed, 0, s, 1 + j / 2);
+            nidx[j] = draw_index(b.x, g.V);
+            np[j] = b.y;
+            if (j + 1 < KMAX) {
+                nidx[j + 1] = draw_index(b.z, g.V);
+                np[j + 1] = b.w;
+            }
+        }
+    }
+    uint2 ne[KMAX];
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j)
+        if (j < K) ne[j] = ldr(g.ntab + nidx[j]);
+    const bool acc = b0.x < p0.x;
+    const int32_t tv = alias_pick(vi, make_uint2(p0.x, p0.y), b0.x);
+    const uint32_t off = acc ? p0.z : p1.x, br = acc ? p0.w : p1.y;
+    int32_t c = -1;
+    if (br != 0) {
+        const uint4 ce = ldr(g.ct16 + (uint64_t)off + draw_index(b0.w, br));
+        c = b0.z < ce.x ? (int32_t)ce.z : (int32_t)ce.y;
+    }
+    int32_t w[RW];
+    w[0] = tv;
+    w[1] = c;
+    bool hot = tag_hot(tv) || (c >= 0 && tag_hot(c));
+#pragma unroll
+    for (int j = 0; j < RW - 2; ++j) {
+        w[2 + j] = (j < KMAX && j < K) ? alias_pick(nidx[j], ne[j], np[j]) : -1;
+        if (j < KMAX && j < K) hot = hot || tag_hot(w[2 + j]);
+    }
+    w[2 + KMAX] = __float_as_int(alpha_at(s + (uint64_t)base, alpha0, total));
+    // wave-aggregated slots: one counter add per wave and class
+    const uint64_t act = __ballot(1), hm = __ballot(hot);
+    const int lane = (int)__lane_id();
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int leader = __ffsll((unsigned long long)act) - 1;
+    unsigned long long hb = 0, cb = 0;
+    if (lane == leader) {
+        const int nh = __popcll(hm), nc = __popcll(act & ~hm);
+        if (nh) hb = atomicAdd(counts, (unsigned long long)nh);
+        if (nc) cb = atomicAdd(counts + 1, (unsigned long long)nc);
+    }
+    hb = __shfl(hb, leader);
+    cb = __shfl(cb, leader);
+    const uint64_t idx = hot ? hb + (uint64_t)__popcll(hm & below)
+                             : count - 1 - (cb + (uint64_t)__popcll(act & ~hm & below));
+    i32x4* o = reinterpret_cast<i32x4*>(rec + idx * RW);
+#pragma unroll
+    for (int q = 0; q < RW / 4; ++q) {
+        const i32x4 x = {w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
+        __builtin_nontemporal_store(x, o + q);
+    }
+    if (c < 0) atomicAdd(skipped, 1ull);
+}
+
+hipError_t launch_draw_split(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K, double alpha0,
+                             uint64_t total, int base, int32_t* rec, unsigned long long* skipped,
+                             unsigned long long* counts, hipStream_t st) {
+    const int block = 256;
+    const dim3 grid((unsigned)((count + block - 1) / block));
+    switch (kmax_of(K)) {
+        case 5:
+            hipLaunchKernelGGL(draw_split_kernel<5>, grid, dim3(block), 0, st, g, seed, begin, count, K, alpha0, total,
+                               base, rec, skipped, counts);
+            break;
+        case 10:
+            hipLaunchKernelGGL(draw_split_kernel<10>, grid, dim3(block), 0, st, g, seed, begin, count, K, alpha0,
+                               total, base, rec, skipped, counts);
+            break;
+        default:
+            hipLaunchKernelGGL(draw_split_kernel<20>, grid, dim3(block), 0, st, g, seed, begin, count, K, alpha0,
+                               total, base, rec, skipped, counts);
+            break;
+    }
+    return hipGetLastError();
+}
+
 // packed draw tables from the device graph (after any re-tagging)
 __global__ void pack_vertex_kernel(DevGraph g, uint4* vt32) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -33,7 +33,9 @@ struct EdgeArgs {
     const uint64_t* count_dev;     // non-null: the record count is read here (device-side pair totals)
     const uint64_t* rec_base;      // non-null: the launch's records are [*rec_base, *count_dev) (block buckets)
     unsigned long long* work;      // Hogwild edge kernels: chunk counter, zeroed per launch
-    int alpha_rec;                 // 1: learning rate in record word 2 + KMAX (DeepWalk pairs)
+    int alpha_rec;                 // learning rate in record word 2 + KMAX: 1 walk pairs (pair kernels),
+                                   // 2 independent samples (the edge kernel: the hot/cold split)
+    uint32_t pair_slice;           // pair kernels: records per group slice (0: CH_ROUNDS)
     uint64_t begin, count, total, seed;
     double alpha0;
     float reg;
@@ -116,6 +118,12 @@ hipError_t scan_pair_counts(const uint32_t* count, uint64_t* off, uint64_t n, vo
 hipError_t launch_pair_emit(const DevGraph& g, const WalkArgs& w, uint64_t seed, int K, double alpha0,
                             const uint64_t* off, int32_t* rec, hipStream_t st);
 hipError_t launch_pack(const DevGraph& g, uint64_t E, uint4* vt32, uint4* ct16, hipStream_t st);
+// draw_split_kernel (train_draw.hip): the draws with the rate in the record,
+// hot records from the front, the others from the back; counts[0] / [1] the
+// hot / cold records (zeroed by the caller)
+hipError_t launch_draw_split(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K, double alpha0,
+                             uint64_t total, int base, int32_t* rec, unsigned long long* skipped,
+                             unsigned long long* counts, hipStream_t st);
 hipError_t launch_draw(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K, int32_t* rec,
                        unsigned long long* skipped, hipStream_t st);
 constexpr int SH_HASH = 256;   // entries of the super-hot row hash (power of two)
@@ -196,6 +204,9 @@ hipError_t launch_block_pair_count(const WalkArgs& w, const BlockArgs& b, uint64
                                    hipStream_t st);
 hipError_t launch_block_pair_emit(const WalkArgs& w, const BlockArgs& b, uint64_t seed, int K, double alpha0,
                                   const uint64_t* off, int32_t* rec, hipStream_t st);
+// rows `ids` of T [*][dpad] from (to_table 1) / to (0) buf [n][dim] (membw.hip)
+hipError_t launch_rows_io(float* T, const int32_t* ids, uint64_t n, int dpad, int dim, float* buf, int to_table,
+                          hipStream_t st);
 // streaming copy of n16 16-B words (membw.hip); variant 1 = non-temporal
 hipError_t launch_copy(const void* src, void* dst, uint64_t n16, int blocks, int variant, hipStream_t st);
 hipError_t launch_init_uniform(float* T, int64_t rows, int dim, int dpad, uint64_t seed,

@@ -204,13 +204,22 @@ class ProNet:
             raise ValueError("v and c must have the same length")
         for a in (v, c):
             if a.size and (a.min() < 0 or a.max() >= self.MAX_vid):
-                raise IndexError("train_pairs: vertex id out of range [0, %d)" % self.MAX_vid)
+                raise _lib.SmoreError("train_pairs: vertex id out of range [0, %d)" % self.MAX_vid)
         v = np.ascontiguousarray(v, np.int32)
         c = np.ascontiguousarray(c, np.int32)
         self._chk(lib.smore_train_pairs(self.ctx, ptr(v), ptr(c), len(v), int(K), float(alpha), int(seed), int(unit),
                                         _lib.MODE[mode]), "train_pairs")
 
     # ---- 2-D block schedule, one replica's side (smore_block_*)
+    def save_graph(self, path):
+        """The built graph to a binary file (smore_save_graph)."""
+        self._chk(lib.smore_save_graph(self.ctx, path.encode()), "save_graph")
+
+    def load_graph(self, path, vertex_method="out_degrees", negative_method="degrees"):
+        """A graph written by save_graph (smore_load_graph), uploaded."""
+        self._chk(lib.smore_load_graph(self.ctx, path.encode(), _lib.VM[vertex_method], _lib.NM[negative_method]),
+                  "load_graph")
+
     def block_setup(self, model, nparts, part, K, mode="hybrid"):
         """This context as part `part` of `nparts`: W part bounds, 2 nparts C
         blocks and the cells' draw tables (smore_block_setup; model "line2" or
@@ -274,6 +283,42 @@ class ProNet:
         n = C.c_uint64()
         self._chk(lib.smore_block_walk_records(self.ctx, int(block), C.byref(n)), "block_walk_records")
         return n.value
+
+    def pairs_rows(self, v, c, K, seed, unit=0):
+        """(W row ids, C row ids) a train_pairs batch touches: its vertices, and
+        its contexts plus the K negatives it will draw (smore_pairs_rows)."""
+        v = np.ascontiguousarray(v, np.int32)
+        c = np.ascontiguousarray(c, np.int32)
+        w_ids = np.zeros(max(1, len(v)), np.int32)
+        c_ids = np.zeros(max(1, len(v) * (int(K) + 1)), np.int32)
+        nw, nc = C.c_int64(), C.c_int64()
+        self._chk(lib.smore_pairs_rows(self.ctx, ptr(v), ptr(c), len(v), int(K), int(seed), int(unit), ptr(w_ids),
+                                       C.byref(nw), ptr(c_ids), C.byref(nc)), "pairs_rows")
+        return w_ids[:nw.value].copy(), c_ids[:nc.value].copy()
+
+    def set_rows(self, which, ids, rows):
+        ids = np.ascontiguousarray(ids, np.int32)
+        rows = np.ascontiguousarray(rows, np.float32)
+        self._chk(lib.smore_set_rows(self.ctx, int(which), ptr(ids), len(ids), ptr(rows)), "set_rows")
+
+    def get_rows(self, which, ids):
+        ids = np.ascontiguousarray(ids, np.int32)
+        out = np.zeros((len(ids), self.dim), np.float32)
+        self._chk(lib.smore_get_rows(self.ctx, int(which), ptr(ids), len(ids), ptr(out)), "get_rows")
+        return out
+
+    def train_pairs_rows(self, v, c, K, alpha, seed, unit, mode, w_ids, w_rows, c_ids, c_rows):
+        """smore_train_pairs_rows: the touched rows up, the pairs, the rows back
+        (w_rows / c_rows float32 [n][dim], updated in place)."""
+        v = np.ascontiguousarray(v, np.int32)
+        c = np.ascontiguousarray(c, np.int32)
+        w_ids = np.ascontiguousarray(w_ids, np.int32)
+        c_ids = np.ascontiguousarray(c_ids, np.int32)
+        assert w_rows.dtype == np.float32 and w_rows.flags.c_contiguous and c_rows.dtype == np.float32
+        assert c_rows.flags.c_contiguous
+        self._chk(lib.smore_train_pairs_rows(self.ctx, ptr(v), ptr(c), len(v), int(K), float(alpha), int(seed),
+                                             int(unit), _lib.MODE[mode], ptr(w_ids), len(w_ids), ptr(w_rows),
+                                             ptr(c_ids), len(c_ids), ptr(c_rows)), "train_pairs_rows")
 
     def census_begin(self):
         """Row census: the following walk-model calls count the rows their

@@ -259,3 +259,34 @@ def test_c2_line_blocks_quality(smore):
         print("C2 LINE-2 blocks", n, res[n], "one", l1, res[n] / l1, flush=True)
     for n in (2, 4, 8):
         assert res[n] <= 1.05 * l1, res
+
+
+@pytest.mark.parametrize("mode", ["atomic", "hybrid"])
+def test_block_walks_parallel_modes_train(smore, graph, mode):
+    """DeepWalk in the block schedule on 2 and 4 replicas (cuda:0) in the
+    Hogwild modes: every replica holds the gathered tables, they stay finite,
+    and the held-out LINE objective is within 10 % of one context's."""
+    K, dim, wt = 5, 32, 6
+    order = orc.deepwalk_order(graph.V, wt, 0)
+    held = orc.sample_line(graph, SEED + 7, 0, 50_000, 5)
+    one = _ctx(smore, dim)
+    one.train_deepwalk(0, wt * graph.V, wt, 20, 4, K, 0.025, SEED, order, mode)
+    l1 = _heldout_loss(one.get_table(0), one.get_table(1), held)
+    one.close()
+    for n in (2, 4):
+        g = smore.Group([0] * n)
+        g.LoadEdgeList(PL1K, 1)
+        g.alloc_tables(dim, 2)
+        g.primary.init_table_glibc(0, 0)
+        g.primary.zero_table(1)
+        g.broadcast_tables()
+        g.set_schedule("blocks")
+        g.train_deepwalk(0, wt * graph.V, wt, 20, 4, K, 0.025, SEED, order, mode, per=1000)
+        W, C = g.primary.get_table(0), g.primary.get_table(1)
+        for r in g.replicas[1:]:
+            np.testing.assert_array_equal(r.get_table(0), W)
+            np.testing.assert_array_equal(r.get_table(1), C)
+        g.close()
+        ln = _heldout_loss(W, C, held)
+        print("pl1k DeepWalk blocks", mode, n, ln, "one", l1, flush=True)
+        assert np.isfinite(W).all() and np.isfinite(C).all() and ln <= 1.10 * l1, (n, ln, l1)

@@ -198,3 +198,101 @@ def test_census_deepwalk_rates(smore):
     off, _ = pn.csr()
     deg = np.diff(off).astype(np.float64)
     assert np.corrcoef(rw, deg)[0, 1] > 0.9
+
+
+def test_pairs_rows_flow_matches_oracle_and_scales_with_pairs(smore):
+    """The Go UpdatePairs hook's flow (go/pkg/pronet/hip.go updatePairsHIP):
+    per call only the rows the batch touches move -- smore_pairs_rows (the
+    vertices, contexts and the negatives the call will draw, on the host),
+    smore_set_rows from the caller's tables, smore_train_pairs,
+    smore_get_rows back -- one walk's pairs per call, as the reference's
+    callers pass them (internal/models/deepwalk/deepwalk.go:120).  Serial Go
+    rules: the caller's tables end bit-exact with the oracle's Go UpdatePairs
+    applied call by call.  (Per-call time against the CPU path at config 5's
+    size: tools/pairs_rows_bench.py)"""
+    import time
+    g = orc.Graph.from_file(PL100W, 1)
+    dim, K, seed = 16, 5, 99
+    pn = smore.ProNet(0)
+    pn.LoadEdgeList(PL100W, 1)
+    pn.set_semantics("go")
+    pn.alloc_tables(dim, 2)
+    rng = np.random.default_rng(5)
+    W = ((rng.random((g.V, dim)) - 0.5) / dim).astype(np.float32)
+    Cc = np.zeros((g.V, dim), np.float32)
+    Wo, Co = W.copy(), Cc.copy()
+    gg = orc.GoGraph.from_file(PL100W, 1)
+    for call in range(40):
+        n = int(rng.integers(20, 120))
+        v = rng.integers(0, g.V, n).astype(np.int32)
+        c = rng.integers(0, g.V, n).astype(np.int32)
+        unit = 1000 + call
+        wi, ci = pn.pairs_rows(v, c, K, seed, unit)
+        assert set(v) <= set(wi) and set(c) <= set(ci) and len(wi) <= n and len(ci) <= n * (K + 1)
+        if call % 2:     # the three calls, or the combined one
+            pn.set_rows(0, wi, W[wi])
+            pn.set_rows(1, ci, Cc[ci])
+            pn.train_pairs(v, c, K, 0.025, seed, unit, "serial")
+            W[wi] = pn.get_rows(0, wi)
+            Cc[ci] = pn.get_rows(1, ci)
+        else:
+            wr, cr = W[wi], Cc[ci]
+            pn.train_pairs_rows(v, c, K, 0.025, seed, unit, "serial", wi, wr, ci, cr)
+            W[wi] = wr
+            Cc[ci] = cr
+        orc.update_pairs_f32(gg, Wo, Co, dim, v, c, K, 0.025, seed, unit, go=True)
+    np.testing.assert_array_equal(W, Wo)
+    np.testing.assert_array_equal(Cc, Co)
+    pn.close()
+
+
+def test_pairs_rows_per_call_cost(smore):
+    """The hook's per-call cost at config 5's size (1.13M vertices, d=128,
+    one walk's 380 pairs per call, Hogwild atomic): moving only the touched
+    rows costs far less than moving both whole tables (round 4's hook), and
+    less than the CPU path on the same calls (the oracle's fp64 Go
+    UpdatePairs, 1 thread; the Go reference is not runnable here)."""
+    import time
+    from smore_amd import graphgen
+    V, (src, dst, w) = graphgen.config_edges("c5")
+    K, seed, dim, P, calls = 5, 7, 128, 380, 300
+    pn = smore.ProNet(0)
+    pn.set_graph_edges(V, src, dst, w)
+    pn.set_semantics("go")
+    pn.alloc_tables(dim, 2)
+    rng = np.random.default_rng(1)
+    W = ((rng.random((V, dim)) - 0.5) / dim).astype(np.float32)
+    Cc = np.zeros((V, dim), np.float32)
+    batches = [(rng.integers(0, V, P).astype(np.int32), rng.integers(0, V, P).astype(np.int32)) for _ in range(calls)]
+
+    def rows_call(i, v, c):
+        wi, ci = pn.pairs_rows(v, c, K, seed, i)
+        wr, cr = W[wi], Cc[ci]
+        pn.train_pairs_rows(v, c, K, 0.025, seed, i, "atomic", wi, wr, ci, cr)
+        W[wi] = wr
+        Cc[ci] = cr
+
+    rows_call(0, *batches[0])   # warm-up
+    t0 = time.perf_counter()
+    for i, (v, c) in enumerate(batches):
+        rows_call(i, v, c)
+    rows_ms = (time.perf_counter() - t0) * 1e3 / calls
+    t0 = time.perf_counter()
+    for i, (v, c) in enumerate(batches[:3]):
+        pn.set_table(0, W)
+        pn.set_table(1, Cc)
+        pn.train_pairs(v, c, K, 0.025, seed, i, "atomic")
+        W[:] = pn.get_table(0)
+        Cc[:] = pn.get_table(1)
+    tab_ms = (time.perf_counter() - t0) * 1e3 / 3
+    gg = orc.GoGraph(V, src, dst, w)
+    W64, C64 = W.astype(np.float64), Cc.astype(np.float64)
+    t0 = time.perf_counter()
+    for i, (v, c) in enumerate(batches):
+        orc.update_pairs_f64(gg, W64, C64, v, c, K, 0.025, seed, i, go=True)
+    cpu_ms = (time.perf_counter() - t0) * 1e3 / calls
+    print("pairs per call %d: rows %.3f ms, whole tables %.1f ms, CPU %.3f ms per call" % (P, rows_ms, tab_ms, cpu_ms),
+          flush=True)
+    pn.close()
+    assert rows_ms * 20 < tab_ms, (rows_ms, tab_ms)
+    assert rows_ms < cpu_ms, (rows_ms, cpu_ms)

@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--mode", default="hybrid")
     ap.add_argument("--seed", type=int, default=20251015)
     ap.add_argument("--hot-tau", type=float, default=None, help="hybrid: hot-row threshold")
+    ap.add_argument("--combine-rows", type=int, default=None, help="hybrid: LDS write-combined rows (0: off)")
     args = ap.parse_args()
 
     import torch  # noqa: F401  (one HIP runtime with torch, as bench.py)
@@ -50,6 +51,8 @@ def main():
     pn.alloc_tables(dim, 2)
     if args.hot_tau is not None:
         pn.set_hot_threshold(args.hot_tau)
+    if args.combine_rows is not None:
+        pn.set_write_combine(args.combine_rows, 0)
     pn.init_table_glibc(0, 0)
     pn.zero_table(1)
     S = args.samples

@@ -168,8 +168,10 @@ def main():
             # rank in the census's touch rates (0 = the hottest row)
             for t, T in (("W", W), ("C", C)):
                 nrm = np.sqrt((T.astype(np.float64) ** 2).sum(1))
-                rate = p.row_rates("census", K, 0 if t == "W" else 1) if not line else p.row_rates("line2", K,
-                                                                                                   0 if t == "W" else 1)
+                try:
+                    rate = p.row_rates("census" if not line else "line2", K, 0 if t == "W" else 1)
+                except smore_amd._lib.SmoreError:   # no census (the block schedule): the LINE-2 law
+                    rate = p.row_rates("line2", K, 0 if t == "W" else 1)
                 rank = np.empty(len(rate), np.int64)
                 rank[np.argsort(-rate)] = np.arange(len(rate))
                 top = np.argsort(-nrm)[:8]
