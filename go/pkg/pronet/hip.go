@@ -490,14 +490,19 @@ func (pn *ProNet) pairSession() *pairSession {
 	return s
 }
 
-// updatePairsHIP is (*ProNet).UpdatePairs under -tags smore_hip: the tables go
-// up (fp64 -> fp32), the library runs Go UpdatePair for each pair in order
-// (negatives drawn on the device from the rng's next word as the Philox unit,
-// duplicates of the context skipped, the context's gradient deferred), and
-// the tables come back.  The copies cost O(MaxVid x dim) per call, so batch the
-// pairs (a chunk of walks per call), or keep the tables on the GPU across
-// batches with (*HIP).BeginPairs / Pairs / EndPairs.  UpdatePairs has no error
-// path (the reference panics on a bad index): failures panic.
+// updatePairsHIP is (*ProNet).UpdatePairs under -tags smore_hip.  Only the
+// rows the batch touches move (round 4 moved both whole tables per call, O(MaxVid
+// x dim), ~180 ms per call at config 5's size): the library lists them
+// (smore_pairs_rows: the vertices, the contexts and the negatives this call
+// will draw, on the host), they go up fp64 -> fp32, the library runs Go
+// UpdatePair for each pair in order (negatives from the rng's next word as the
+// Philox unit, duplicates of the context skipped, the context's gradient
+// deferred), and the same rows come back (smore_train_pairs_rows, one
+// synchronisation) -- O(pairs x dim) per call.  The session's device tables
+// are allocated once; rows a call does not touch are never read.  Batches from
+// concurrent goroutines run one after another (each sees the rows the previous
+// one wrote back).  UpdatePairs has no error path (the reference panics on a
+// bad index): failures panic.
 func updatePairsHIP(pn *ProNet, wVertex, wContext [][]float64, vertices, contexts []int64, dim,
 	negativeSamples int, alpha float64, rng *rand.Rand) {
 	if len(vertices) == 0 {
@@ -509,15 +514,78 @@ func updatePairsHIP(pn *ProNet, wVertex, wContext [][]float64, vertices, context
 	if s.err != nil {
 		panic(s.err)
 	}
-	if err := s.h.BeginPairs(wVertex, wContext, dim); err != nil {
+	if err := s.h.alloc(dim, 2); err != nil {
 		panic(err)
 	}
-	if err := s.h.Pairs(vertices, contexts, negativeSamples, alpha, rng.Uint64()); err != nil {
+	if err := s.h.PairsRows(wVertex, wContext, vertices, contexts, negativeSamples, alpha, rng.Uint64()); err != nil {
 		panic(err)
 	}
-	if err := s.h.EndPairs(wVertex, wContext); err != nil {
-		panic(err)
+}
+
+// PairsRows runs UpdatePair over (vertices[i], contexts[i]) in order against
+// the caller's tables w (vertex) and c (context), moving only the rows the
+// batch touches (smore_pairs_rows + smore_train_pairs_rows).
+func (h *HIP) PairsRows(w, c [][]float64, vertices, contexts []int64, negativeSamples int, alpha float64,
+	unit uint64) error {
+	n := len(vertices)
+	if n != len(contexts) {
+		return fmt.Errorf("PairsRows: %d vertices, %d contexts", n, len(contexts))
 	}
+	if n == 0 {
+		return nil
+	}
+	K := negativeSamples
+	v := (*[1 << 40]C.int32_t)(C.malloc(C.size_t(4 * n)))[:n:n]
+	cc := (*[1 << 40]C.int32_t)(C.malloc(C.size_t(4 * n)))[:n:n]
+	wi := (*[1 << 40]C.int32_t)(C.malloc(C.size_t(4 * n)))[:n:n]
+	ci := (*[1 << 40]C.int32_t)(C.malloc(C.size_t(4 * n * (K + 1))))[: n*(K+1) : n*(K+1)]
+	defer C.free(unsafe.Pointer(&v[0]))
+	defer C.free(unsafe.Pointer(&cc[0]))
+	defer C.free(unsafe.Pointer(&wi[0]))
+	defer C.free(unsafe.Pointer(&ci[0]))
+	for i := 0; i < n; i++ {
+		// range-check before narrowing: an id >= 2^31 must not wrap to a small valid one
+		if vertices[i] < 0 || vertices[i] >= h.maxVid || contexts[i] < 0 || contexts[i] >= h.maxVid {
+			return fmt.Errorf("PairsRows: pair %d (%d, %d) out of range [0, %d)", i, vertices[i], contexts[i], h.maxVid)
+		}
+		v[i], cc[i] = C.int32_t(vertices[i]), C.int32_t(contexts[i])
+	}
+	var nw, nc C.int64_t
+	if rc := C.smore_pairs_rows(h.ctx, &v[0], &cc[0], C.int64_t(n), C.int(K), C.uint64_t(h.cfg.Seed), C.uint64_t(unit),
+		&wi[0], &nw, &ci[0], &nc); rc != C.SMORE_OK {
+		return h.err("smore_pairs_rows")
+	}
+	d := h.dim
+	wr := (*[1 << 40]C.float)(C.malloc(C.size_t(4 * int(nw) * d)))[: int(nw)*d : int(nw)*d]
+	cr := (*[1 << 40]C.float)(C.malloc(C.size_t(4 * int(nc) * d)))[: int(nc)*d : int(nc)*d]
+	defer C.free(unsafe.Pointer(&wr[0]))
+	defer C.free(unsafe.Pointer(&cr[0]))
+	gather := func(t [][]float64, ids []C.int32_t, buf []C.float) {
+		for i, id := range ids {
+			row := t[id]
+			for k := 0; k < d; k++ {
+				buf[i*d+k] = C.float(row[k])
+			}
+		}
+	}
+	scatter := func(t [][]float64, ids []C.int32_t, buf []C.float) {
+		for i, id := range ids {
+			row := t[id]
+			for k := 0; k < d; k++ {
+				row[k] = float64(buf[i*d+k])
+			}
+		}
+	}
+	gather(w, wi[:nw], wr)
+	gather(c, ci[:nc], cr)
+	if rc := C.smore_train_pairs_rows(h.ctx, &v[0], &cc[0], C.int64_t(n), C.int(K), C.double(alpha),
+		C.uint64_t(h.cfg.Seed), C.uint64_t(unit), C.int(h.cfg.Mode), &wi[0], nw, &wr[0], &ci[0], nc,
+		&cr[0]); rc != C.SMORE_OK {
+		return h.err("smore_train_pairs_rows")
+	}
+	scatter(w, wi[:nw], wr)
+	scatter(c, ci[:nc], cr)
+	return nil
 }
 
 // BeginPairs puts w (vertex) and c (context) on the GPU for Pairs calls.

@@ -118,15 +118,38 @@ int main(int argc, char** argv) {
     const int ntab = model == SMORE_LINE1 ? 1 : 2;
     CHECK("alloc_tables", smore_group_alloc_tables(G, (int)dim, ntab));
     smore_ctx* c0 = smore_group_ctx(G, 0);
+    if (model == -5) {   /* (*HIP).PairsRows: list the touched rows, gather, train, scatter back */
+        int32_t* wi = malloc(4 * npairs + 4);
+        int32_t* ci = malloc(4 * npairs * (K + 1) + 4);
+        int64_t nw = 0, nc = 0;
+        CHECK("pairs_rows", smore_pairs_rows(c0, pv, pc, npairs, (int)K, seed, unit, wi, &nw, ci, &nc));
+        float* wr = malloc(4 * nw * dim + 4);
+        float* cr = malloc(4 * nc * dim + 4);
+        for (int64_t i = 0; i < nw; ++i)
+            for (int64_t k = 0; k < dim; ++k) wr[i * dim + k] = (float)T[0][wi[i] * dim + k];
+        for (int64_t i = 0; i < nc; ++i)
+            for (int64_t k = 0; k < dim; ++k) cr[i * dim + k] = (float)T[1][ci[i] * dim + k];
+        CHECK("train_pairs_rows", smore_train_pairs_rows(c0, pv, pc, npairs, (int)K, ad[0], seed, unit, (int)mode,
+                                                         wi, nw, wr, ci, nc, cr));
+        for (int64_t i = 0; i < nw; ++i)
+            for (int64_t k = 0; k < dim; ++k) T[0][wi[i] * dim + k] = (double)wr[i * dim + k];
+        for (int64_t i = 0; i < nc; ++i)
+            for (int64_t k = 0; k < dim; ++k) T[1][ci[i] * dim + k] = (double)cr[i * dim + k];
+        smore_group_destroy(G);
+        FILE* o = fopen(argv[2], "wb");
+        if (!o) return 3;
+        fwrite(T[0], 8, V * dim, o);
+        fwrite(T[1], 8, V * dim, o);
+        fclose(o);
+        return 0;
+    }
     float* buf = malloc(4 * V * dim + 4);
     for (int t = 0; t < ntab; ++t) {
         for (int64_t i = 0; i < V * dim; ++i) buf[i] = (float)T[t][i];
         CHECK("set_table", smore_set_table(c0, t, buf, V, (int)dim));
     }
     CHECK("broadcast", smore_group_broadcast_tables(G));
-    if (model == -5) {   /* Pairs: smore_train_pairs on replica 0 with the session's seed and mode */
-        CHECK("train_pairs", smore_train_pairs(c0, pv, pc, npairs, (int)K, ad[0], seed, unit, (int)mode));
-    } else if (model >= 0) {
+    if (model >= 0) {
         const uint64_t step = ((uint64_t)1 << 27) * (uint64_t)gpus;
         for (uint64_t done = 0; done < (uint64_t)total;) {
             uint64_t n = (uint64_t)total - done;

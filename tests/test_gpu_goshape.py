@@ -186,7 +186,8 @@ def test_go_shim_ctdne_serial_bit_exact(tmp_path):
 @pytest.mark.parametrize("mode", [SERIAL, ATOMIC])
 def test_go_shim_update_pairs(tmp_path, mode):
     """(*ProNet).UpdatePairs under -tags smore_hip (hip.go updatePairsHIP ->
-    BeginPairs, Pairs = smore_train_pairs, EndPairs): in serial mode bit-exact
+    PairsRows = smore_pairs_rows, gather the touched rows, smore_train_pairs_rows,
+    scatter them back; rows no pair touches never move): in serial mode bit-exact
     with the oracle's Go UpdatePair over the caller's pairs (negatives skipped
     when equal to the context, deferred context); atomic mode (Hogwild order,
     ~240 updates per row of a 98-vertex graph, so the tables themselves differ
