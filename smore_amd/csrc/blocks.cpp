@@ -76,7 +76,7 @@ void block_sh_sets(smore_ctx* c, bool walk, bool on, int64_t Mg, const std::vect
     const int flush_cap = c->sh_flush > 0 ? c->sh_flush : sh_flush_max(walk);
     B.sh_flush = flush_cap;
     if (cap == 0) return;
-    const double M = (double)Mg, stale = sh_stale_max();
+    const double M = (double)Mg, stale = sh_stale_max(walk);
     const bool two_tier = c->sh_flush <= 0;
     for (int k = 0; k < B.nb; ++k) {
         // A cell concentrates its samples on 1/nb of the C rows, so a hub row
@@ -90,7 +90,7 @@ void block_sh_sets(smore_ctx* c, bool walk, bool on, int64_t Mg, const std::vect
         for (size_t i = 0; i < pcb[k].size(); ++i) {
             if (!hcb[k][i]) continue;
             const double p = pcb[k][i];
-            const double f = two_tier ? (double)sh_slot_interval(M * p, flush_cap) : (double)flush_cap;
+            const double f = two_tier ? (double)sh_slot_interval(M * p, flush_cap, walk) : (double)flush_cap;
             if (M * p * f <= stale) r.push_back({p, (int32_t)(B.cb[k] + (int64_t)i)});
         }
         const int64_t n = std::min<int64_t>(cap, (int64_t)r.size());
@@ -107,8 +107,15 @@ void block_sh_sets(smore_ctx* c, bool walk, bool on, int64_t Mg, const std::vect
         B.sh_n[k] = (int)n;
         if (two_tier && n > 0) {
             int lv[8];
-            sh_slot_levels(Mg, flush_cap, r.data(), n, lv);
+            sh_slot_levels(Mg, flush_cap, walk, r.data(), n, lv);
             std::copy(lv, lv + 8, B.sh_lvl[k].begin());
+        }
+        if (getenv("SMORE_SH_DEBUG")) {
+            const auto& l = B.sh_lvl[k];
+            fprintf(stderr, "[sh] block %d/%d M %lld rows %lld of %zu flush %d lvl %d %d %d %d %d %d %d %d top", k, B.nb,
+                    (long long)Mg, (long long)n, r.size(), flush_cap, l[0], l[1], l[2], l[3], l[4], l[5], l[6], l[7]);
+            for (int64_t i = 0; i < std::min<int64_t>(n, 4); ++i) fprintf(stderr, " %d:%.3g", r[i].second, M * r[i].first);
+            fprintf(stderr, "\n");
         }
     }
 }
@@ -136,6 +143,30 @@ EdgeArgs cell_args(smore_ctx* c, int k, bool walk) {
     a.sh_flush_w = 0;
     std::copy(B.sh_lvl[k].begin(), B.sh_lvl[k].end(), a.sh_lvl);
     return a;
+}
+
+// A cell's launch: the context's grid, capped so that its hottest row takes
+// at most SMORE_CELL_RATE concurrent updates per round (M p_max).  A cell
+// concentrates its samples on 1/N of the W rows and 1/2N of the C rows, so
+// its hub rows are up to 2N times as contended as at one GPU, where M p_max
+// is ~130-260 (C5 DeepWalk, C2 LINE-2); Hogwild on a row with ~2000 updates in
+// flight (C5 DeepWalk, 8 GPUs) diverges whether the row is atomic or
+// write-combined.
+int cell_grid(smore_ctx* c, const EdgeArgs& a, int k) {
+    const int grid = launch_grid(c, a);
+    const auto& B = c->blk;
+    if (a.mode == SMORE_SERIAL || (size_t)k >= B.pmax_c.size()) return grid;
+    double cap = cell_rate_default(a.alpha_rec == 1);
+    if (const char* e = getenv("SMORE_CELL_RATE")) cap = atof(e);
+    // which side's hub sets the cap: both (default), SMORE_CELL_SIDE=c or w
+    const char* side = getenv("SMORE_CELL_SIDE");
+    const double pmax = side && side[0] == 'c' ? B.pmax_c[k]
+                        : side && side[0] == 'w' ? B.pmax_w[k] : std::max(B.pmax_w[k], B.pmax_c[k]);
+    if (cap <= 0 || pmax <= 0) return grid;
+    const int gpb = 256 / lanes_of(c->dpad);
+    const double groups = cap / pmax;
+    const int g = std::max(8, (int)(groups / gpb) / 8 * 8);   // whole rounds of the 8 XCDs
+    return std::min(grid, g);
 }
 
 int grow_events(smore_ctx* c, std::vector<hipEvent_t>& v, size_t n) {
@@ -285,17 +316,27 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
     // flags of its C rows and (LINE-2) of this part's W rows
     std::vector<std::vector<double>> pcb((size_t)nb);
     std::vector<std::vector<uint8_t>> hcb((size_t)nb), hwb((size_t)nb);
-    if (hyb) {
+    // the hottest row of each cell (its launch's concurrency cap, cell_grid):
+    // walks the scaled global law, LINE-2 the cell's exact one
+    B.pmax_w.assign((size_t)nb, 0.0);
+    B.pmax_c.assign((size_t)nb, 0.0);
+    double wmax = 0.0;
+    for (int64_t v = wlo; v < whi; ++v) wmax = std::max(wmax, ps[v] * nparts);
+    {
         par_blocks([&](int k) {
             const int64_t lo = B.cb[k], n = B.cb[k + 1] - lo;
             auto& pcx = pcb[k];
             pcx.assign((size_t)n, 0.0);
             hcb[k].assign((size_t)n, 0);
-            if (walk) {
+            if (walk) {   // capi build_hot_maps' scaled law (hot_pc)
+                double mx = 0.0;
                 for (int64_t i = 0; i < n; ++i) {
-                    pcx[i] = c->hot_pc[lo + i];
-                    hcb[k][i] = c->hot_c[lo + i];
+                    pcx[i] = (pc[lo + i] + K * pn[lo + i]) * nb;
+                    hcb[k][i] = hyb ? c->hot_c[lo + i] : 0;
+                    mx = std::max(mx, pcx[i]);
                 }
+                B.pmax_w[k] = wmax;
+                B.pmax_c[k] = mx;
                 return;
             }
             std::vector<double> pw((size_t)(whi - wlo), 0.0);
@@ -307,11 +348,18 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
             }
             for (int64_t i = 0; i < n; ++i) pnb += pn[lo + i];
             hwb[k].assign(pw.size(), 0);
-            for (size_t i = 0; i < pw.size(); ++i) hwb[k][i] = m > 0 && (double)M * pw[i] / m > tau;
+            double mw = 0.0, mc = 0.0;
+            for (size_t i = 0; i < pw.size(); ++i) {
+                hwb[k][i] = m > 0 && (double)M * pw[i] / m > tau;
+                if (m > 0) mw = std::max(mw, pw[i] / m);
+            }
             for (int64_t i = 0; i < n; ++i) {
                 pcx[i] = (m > 0 ? pcx[i] / m : 0.0) + (pnb > 0 ? K * pn[lo + i] / pnb : 0.0);
                 hcb[k][i] = (double)M * pcx[i] > tau;
+                mc = std::max(mc, pcx[i]);
             }
+            B.pmax_w[k] = mw;
+            B.pmax_c[k] = mc;
         });
     }
     auto hc = [&](int k, int64_t x) -> uint32_t { return hyb ? hcb[k][x - B.cb[k]] : 0u; };
@@ -363,6 +411,10 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
     std::vector<int2> hash;
     std::vector<int32_t> ids;
     block_sh_sets(c, walk, hyb && !small, M, pcb, hcb, hash, ids);
+    if (getenv("SMORE_SH_DEBUG"))
+        for (int k = 0; k < nb; ++k)
+            fprintf(stderr, "[cell] part %d/%d block %d M %lld M*pmax_w %.4g M*pmax_c %.4g\n", part, nparts, k,
+                    (long long)M, M * B.pmax_w[k], M * B.pmax_c[k]);
     if ((rc = upload(c, B.d_sh_hash, hash.data(), hash.size()))) return rc;
     if ((rc = upload(c, B.d_sh_ids, ids.data(), ids.size()))) return rc;
     B.key = key;
@@ -430,7 +482,7 @@ int smore_block_train_edges_async(smore_ctx* c, int block, uint64_t begin, uint6
     a.seed = seed;
     a.alpha0 = alpha0;
     a.count = count;
-    const int grid = launch_grid(c, a);
+    const int grid = cell_grid(c, a, block);
     BlockArgs ba = block_args(c);
     ba.atom_off = B.atom_off[block];
     ba.natoms = (uint32_t)na;
@@ -612,7 +664,7 @@ int smore_block_train_walks_async(smore_ctx* c, int block) {
     a.count = B.rec_bound;   // the grid's bound; the launch reads its range on the device
     a.rec_base = B.d_off + (size_t)block * B.walks;
     a.count_dev = B.d_off + (size_t)(block + 1) * B.walks;
-    const int grid = B.mode == SMORE_SERIAL ? 1 : launch_grid(c, a);
+    const int grid = B.mode == SMORE_SERIAL ? 1 : cell_grid(c, a, block);
     HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
     HIPCHK(c, launch_edge_train(a, grid, c->stream));
     return SMORE_OK;

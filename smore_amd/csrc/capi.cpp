@@ -457,6 +457,27 @@ constexpr double SH_STALE_MAX = 65536.0;
 // that other workgroups cannot see yet; flush = budget / (M * p_top) within
 // [8, 32] rounds keeps that at the config-4 level (flush 32) on hotter graphs
 constexpr double SH_AUTO_BUDGET = 6144.0;
+// the pair-record kernels' budget (and staleness bound): 1024 hidden updates,
+// the one-GPU C5 DeepWalk top row's at its 8-round drain.  A walk group runs
+// a walk's records in order, so a hub context row's hidden updates come in
+// correlated bursts; 4096 (drain 32 at one GPU) cost C5 held-out loss +6 %,
+// and under the 2-D block schedule (a cell's rows nb times hotter: the top
+// row M p = 512 per round at 2 GPUs) it diverged (loss 2.6e8; budget 1024:
+// 0.5308, one GPU 0.5309; profiles/r05/walk_blocks.txt)
+constexpr double SH_PAIR_BUDGET = 1024.0;
+// the 2-D block schedule's per-cell concurrency cap (blocks.cpp cell_grid):
+// at most this many updates per round on a cell's hottest row (0: no cap)
+constexpr double CELL_RATE_PAIRS = 512.0, CELL_RATE_EDGES = 512.0;
+static double sh_budget(bool pairs) {
+    if (const char* e = getenv("SMORE_SH_BUDGET")) return atof(e);
+    return pairs ? SH_PAIR_BUDGET : SH_AUTO_BUDGET;
+}
+// rows whose hidden updates would pass this even at a 1-round drain (edge
+// rule) / the budget (pair rule) stay on atomics; SMORE_SH_STALE overrides
+static double sh_stale(bool pairs) {
+    if (const char* e = getenv("SMORE_SH_STALE")) return atof(e);
+    return pairs ? SH_PAIR_BUDGET : SH_STALE_MAX;
+}
 
 // hot-row threshold defaults (smore_set_hot_threshold(ctx, -1)): the C++
 // rules' edge-record kernel takes 1.0 (C4 / C2 update 4 % / 12 % faster than
@@ -485,18 +506,19 @@ constexpr int EDGE_FLUSH_MAX = 32, PAIR_FLUSH_MAX = 8;
 // drain interval of one write-combined row with M * p expected updates per
 // round: the budget of hidden updates over that rate, a power of two in
 // [1, cap] (cap a power of two) -- the two-tier drain's unit
-static int slot_interval(double Mp, int cap) {
+static int slot_interval(double Mp, int cap, double budget) {
     int f = 1;
-    while (2 * f <= cap && (double)(2 * f) * Mp <= SH_AUTO_BUDGET) f *= 2;
+    while (2 * f <= cap && (double)(2 * f) * Mp <= budget) f *= 2;
     return f;
 }
 
 // EdgeArgs::sh_lvl of n slots sorted by rate: lvl[j] = the slots whose own
 // interval is at most 2^j (and below cap, which every slot drains at)
-static void sh_levels(int64_t M, int cap, const std::pair<double, int32_t>* r, int64_t n, int (&lvl)[8]) {
+static void sh_levels(int64_t M, int cap, double budget, const std::pair<double, int32_t>* r, int64_t n,
+                      int (&lvl)[8]) {
     for (int j = 0; j < 8; ++j) {
         int64_t k = 0;
-        while (k < n && slot_interval((double)M * r[k].first, cap) <= (1 << j) && (1 << j) < cap) ++k;
+        while (k < n && slot_interval((double)M * r[k].first, cap, budget) <= (1 << j) && (1 << j) < cap) ++k;
         lvl[j] = (int)k;
     }
 }
@@ -558,8 +580,9 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_
     }
     // super-hot rows: the hottest hot context rows, write-combined per block
     {
-        double stale_max = SH_STALE_MAX;   // SMORE_SH_STALE overrides (tuning)
-        if (const char* e = getenv("SMORE_SH_STALE")) stale_max = atof(e);
+        // the pair-record kernels (walks) pass PAIR_FLUSH_MAX: their budget
+        const bool pairs = flush_max == PAIR_FLUSH_MAX;
+        const double stale_max = sh_stale(pairs), budget = sh_budget(pairs);
         std::vector<std::pair<double, int32_t>> r;
         const int flush_cap = c->sh_flush > 0 ? c->sh_flush : flush_max;
         for (int64_t v = 0; v < V; ++v) {
@@ -569,7 +592,7 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_
             // M * p * sh_flush updates; rows above SH_STALE_MAX stay on atomics
             // (on small graphs that is every hot row)
             // (two tiers: each row at its own interval, slot_interval)
-            const double f = two_tier ? (double)slot_interval((double)M * p, flush_cap) : (double)flush_cap;
+            const double f = two_tier ? (double)slot_interval((double)M * p, flush_cap, budget) : (double)flush_cap;
             if (hc[v] && (double)M * p * f <= stale_max) r.push_back({p, (int32_t)v});
             // two tables (SMORE_SH_WROWS=1 only): the hub W rows compete for
             // the same slots (key v | SH_WKEY)
@@ -603,13 +626,21 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_
         // (slot_interval) is shorter also at its own (a prefix per level: r is
         // sorted by rate)
         for (int& x : c->sh_lvl_eff) x = 0;
-        if (two_tier) sh_levels(M, flush_cap, r.data(), n, c->sh_lvl_eff);
+        if (two_tier) sh_levels(M, flush_cap, budget, r.data(), n, c->sh_lvl_eff);
+        if (getenv("SMORE_SH_DEBUG")) {
+            const int* l = c->sh_lvl_eff;
+            fprintf(stderr, "[sh] global M %lld rows %lld of %zu flush %d lvl %d %d %d %d %d %d %d %d top", (long long)M,
+                    (long long)n, r.size(), flush_cap, l[0], l[1], l[2], l[3], l[4], l[5], l[6], l[7]);
+            for (int64_t i = 0; i < std::min<int64_t>(n, 4); ++i)
+                fprintf(stderr, " %d:%.3g", r[i].second, (double)M * r[i].first);
+            fprintf(stderr, "\n");
+        }
         // the automatic interval follows the hottest row drained on it (with
         // their own interval, W rows do not count)
         int64_t top = 0;
         while (top < n && wflush && (r[top].second & SH_WKEY)) ++top;
         if (c->sh_flush <= 0 && top < n && !two_tier) {
-            const double f = SH_AUTO_BUDGET / ((double)M * r[top].first);
+            const double f = budget / ((double)M * r[top].first);
             c->sh_flush_eff = (int)std::max(8.0, std::min((double)flush_cap, std::floor(f)));
         }
     }
@@ -2067,14 +2098,11 @@ int hot_maps(smore_ctx* c, int model, int K, int64_t M, bool walk, double w_scal
 }
 int launch_grid(smore_ctx* c, const EdgeArgs& a) { return edge_grid(c, a, false, 0); }
 int sh_flush_max(bool walk) { return walk ? PAIR_FLUSH_MAX : EDGE_FLUSH_MAX; }
-int sh_slot_interval(double Mp, int cap) { return slot_interval(Mp, cap); }
-void sh_slot_levels(int64_t M, int cap, const std::pair<double, int32_t>* r, int64_t n, int (&lvl)[8]) {
-    sh_levels(M, cap, r, n, lvl);
+int sh_slot_interval(double Mp, int cap, bool walk) { return slot_interval(Mp, cap, sh_budget(walk)); }
+void sh_slot_levels(int64_t M, int cap, bool walk, const std::pair<double, int32_t>* r, int64_t n, int (&lvl)[8]) {
+    sh_levels(M, cap, sh_budget(walk), r, n, lvl);
 }
 double hot_tau_default(bool walk) { return walk ? HOT_TAU_WALK : HOT_TAU_EDGE; }
-double sh_stale_max() {
-    const char* e = getenv("SMORE_SH_STALE");
-    return e ? atof(e) : SH_STALE_MAX;
-}
-double sh_auto_budget() { return SH_AUTO_BUDGET; }
+double cell_rate_default(bool walk) { return walk ? CELL_RATE_PAIRS : CELL_RATE_EDGES; }
+double sh_stale_max(bool walk) { return sh_stale(walk); }
 }  // namespace smore_host

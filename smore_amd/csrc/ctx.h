@@ -180,6 +180,7 @@ struct smore_ctx {
         std::vector<int> sh_n;
         std::vector<std::array<int, 8>> sh_lvl;   // per block: EdgeArgs::sh_lvl
         int sh_flush = 32;              // every slot's drain interval
+        std::vector<double> pmax_w, pmax_c;   // per block: the cell's largest per-sample W / C row probability
         std::string key;
         // walk records of the current round, bucketed by C block: per (block,
         // walk) counts and their exclusive scan (nb * walks + 1)
@@ -323,11 +324,11 @@ void part_bounds(const std::vector<double>& ps, int n, std::vector<int64_t>& bou
 int hot_maps(smore_ctx* c, int model, int K, int64_t M, bool walk, double w_scale, double c_scale);
 int launch_grid(smore_ctx* c, const EdgeArgs& a);
 int sh_flush_max(bool walk);
-int sh_slot_interval(double Mp, int cap);
-void sh_slot_levels(int64_t M, int cap, const std::pair<double, int32_t>* r, int64_t n, int (&lvl)[8]);
+int sh_slot_interval(double Mp, int cap, bool walk);
+void sh_slot_levels(int64_t M, int cap, bool walk, const std::pair<double, int32_t>* r, int64_t n, int (&lvl)[8]);
 double hot_tau_default(bool walk);
-double sh_stale_max();
-double sh_auto_budget();
+double cell_rate_default(bool walk);
+double sh_stale_max(bool walk);
 inline float* table_ptr(smore_ctx* c, int which) {
     if (which < 0 || which > 1) return nullptr;
     return c->d_table[which];

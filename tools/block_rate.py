@@ -121,7 +121,11 @@ def main():
                         pn.block_train_walks((2 * r + s) % nb, sync=False)
                 ep = timed(epoch)
                 units_r = sum(recs)
-                cells = recs
+                for s in range(nb):      # per-cell launch times (one pass, synchronised per cell)
+                    b = (2 * r + s) % nb
+                    t1 = time.perf_counter()
+                    pn.block_train_walks(b)
+                    cells.append([b, int(recs[b]), round((time.perf_counter() - t1) * 1e3, 3)])
             row = {"config": args.config, "model": args.model, "nparts": n, "part": r, "setup_s": round(setup_s, 2),
                    "epoch_ms": round(ep * 1e3, 3), "units": units_r,
                    "rate_M_per_s": round(units_r / ep / 1e6, 2),
