@@ -250,7 +250,7 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
     if (hyb) {
         M = resident_groups(c, walk, K, mode);
         small = c->hot_tau < 0 && 16.0 * (double)M >= (double)V;
-        tau = c->hot_tau >= 0 ? c->hot_tau : small ? 0.0 : hot_tau_default(walk);
+        tau = c->hot_tau >= 0 ? c->hot_tau : small ? 0.0 : hot_tau_cell_default(walk);
         if (walk && (rc = hot_maps(c, SMORE_LINE2, K, M, true, (double)nparts, (double)nb))) return rc;
     }
     const int T = (int)std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), (unsigned)nb);

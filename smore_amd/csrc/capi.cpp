@@ -466,8 +466,14 @@ constexpr double SH_AUTO_BUDGET = 6144.0;
 // 0.5308, one GPU 0.5309; profiles/r05/walk_blocks.txt)
 constexpr double SH_PAIR_BUDGET = 1024.0;
 // the 2-D block schedule's per-cell concurrency cap (blocks.cpp cell_grid):
-// at most this many updates per round on a cell's hottest row (0: no cap)
-constexpr double CELL_RATE_PAIRS = 512.0, CELL_RATE_EDGES = 512.0;
+// at most this many updates per round on a cell's hottest row (0: no cap).
+// Walk cells need it: C5 DeepWalk on 8 GPUs (top row M p = 2048 per round)
+// diverged without it and reached 1.027 x the one-GPU held-out loss with 512
+// (1024: 1.027, 256: 1.024).  LINE-2 cells do not: C2 on 8 GPUs with the
+// atomic scatter is at 0.99 x one GPU uncapped; what the hybrid loses there is
+// the cold rows' plain stores (HOT_TAU_CELL), and the cap costs the hub cells
+// 1.5-3 x (C4, 8 GPUs: predicted speed-up 3.4 x capped vs 4.9 x)
+constexpr double CELL_RATE_PAIRS = 512.0, CELL_RATE_EDGES = 0.0;
 static double sh_budget(bool pairs) {
     if (const char* e = getenv("SMORE_SH_BUDGET")) return atof(e);
     return pairs ? SH_PAIR_BUDGET : SH_AUTO_BUDGET;
@@ -487,6 +493,12 @@ static double sh_stale(bool pairs) {
 // the context rows' atomics: Go DeepWalk AUC on the 920-vertex graph 0.881 at
 // 1.0 vs 0.900 at 0.3, serial 0.906); DESIGN.md 8, profiles/r03/tau
 constexpr double HOT_TAU_EDGE = 1.0, HOT_TAU_WALK = 0.3;
+// LINE-2 cells of the 2-D block schedule: a cell's law is its C block's
+// (1/2N of the rows) renormalised, so more of its updates land on rows just
+// under the threshold, where plain stores collide.  C2 LINE-2 held-out loss
+// on 8 GPUs / one GPU: tau 1.0 1.065, 0.5 1.026, 0.3 1.020 (atomic 0.99);
+// C4 8-GPU predicted speed-up 4.9 x at 0.3 and 0.5 (profiles/r05/blocks.md)
+constexpr double HOT_TAU_CELL = 0.3;
 
 // PAIR_FLUSH_MAX: the pair-record kernels' automatic drain interval (8 rounds,
 // the floor, instead of up to 32): a group runs a walk's consecutive records,
@@ -2103,6 +2115,7 @@ void sh_slot_levels(int64_t M, int cap, bool walk, const std::pair<double, int32
     sh_levels(M, cap, sh_budget(walk), r, n, lvl);
 }
 double hot_tau_default(bool walk) { return walk ? HOT_TAU_WALK : HOT_TAU_EDGE; }
+double hot_tau_cell_default(bool walk) { return walk ? HOT_TAU_WALK : HOT_TAU_CELL; }
 double cell_rate_default(bool walk) { return walk ? CELL_RATE_PAIRS : CELL_RATE_EDGES; }
 double sh_stale_max(bool walk) { return sh_stale(walk); }
 }  // namespace smore_host

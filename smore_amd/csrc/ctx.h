@@ -327,6 +327,7 @@ int sh_flush_max(bool walk);
 int sh_slot_interval(double Mp, int cap, bool walk);
 void sh_slot_levels(int64_t M, int cap, bool walk, const std::pair<double, int32_t>* r, int64_t n, int (&lvl)[8]);
 double hot_tau_default(bool walk);
+double hot_tau_cell_default(bool walk);
 double cell_rate_default(bool walk);
 double sh_stale_max(bool walk);
 inline float* table_ptr(smore_ctx* c, int which) {

@@ -284,7 +284,7 @@ struct smore_group {
     // the 2-D block schedule (smore_group_set_schedule): per replica the
     // compute-done event of a sub-round and the receive-done events of the
     // last two rotations (by sub-round parity)
-    int schedule = SMORE_SCHED_REPLICAS;
+    int schedule = SMORE_SCHED_BLOCKS;   // include/smore_hip.h: the default
     std::vector<hipEvent_t> bdone, brecv;
 };
 
@@ -858,10 +858,10 @@ static int group_rounds(smore_group* g, uint64_t begin, uint64_t end, uint64_t p
     return SMORE_OK;
 }
 
-// the block schedule applies: asked for, and the C++ rules (the Go rules keep
-// the replicas)
+// the block schedule applies: asked for (the default), more than one replica,
+// and the C++ rules (the Go rules keep the replicas)
 static bool blocks_for(const smore_group* g) {
-    return g->schedule == SMORE_SCHED_BLOCKS && g->ctx[0]->semantics == SMORE_SEM_CPP;
+    return g->schedule == SMORE_SCHED_BLOCKS && g->ctx.size() > 1 && g->ctx[0]->semantics == SMORE_SEM_CPP;
 }
 
 // the census key of a walk-model call: the model and every argument that

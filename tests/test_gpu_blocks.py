@@ -228,39 +228,6 @@ def _heldout_loss(W, C, draws):
     return float(loss.mean())
 
 
-def test_c2_line_blocks_quality(smore):
-    """Config 2's LINE-2 (1M vertices / 40M slots, d=64, K 5, hybrid), 2^31
-    samples in total, on 2 / 4 / 8 replicas in the block schedule (the
-    group's default epoch) against one context: held-out loss within 5 %."""
-    from smore_amd import graphgen
-    V, (src, dst, w) = graphgen.config_edges("c2")
-    dim, K, T = 64, 5, 1 << 31
-    one = smore.ProNet(0)
-    one.set_graph_edges(V, src, dst, w)
-    held = one.sample_edges("line2", (1 << 40) + 17, 100_000, K, SEED + 1)
-    one.alloc_tables(dim, 2)
-    one.init_table_glibc(0, 0)
-    one.zero_table(1)
-    one.train_edges("line2", 0, T, T, K, 0.025, 0.0, SEED, "hybrid")
-    l1 = _heldout_loss(one.get_table(0), one.get_table(1), held)
-    one.close()
-    res = {1: l1}
-    for n in (2, 4, 8):
-        g = smore.Group([0] * n)
-        g.set_graph_edges(V, src, dst, w)
-        g.alloc_tables(dim, 2)
-        g.primary.init_table_glibc(0, 0)
-        g.primary.zero_table(1)
-        g.broadcast_tables()
-        g.set_schedule("blocks")
-        g.train_edges("line2", 0, T, T, K, 0.025, 0.0, SEED, "hybrid")
-        res[n] = _heldout_loss(g.primary.get_table(0), g.primary.get_table(1), held)
-        g.close()
-        print("C2 LINE-2 blocks", n, res[n], "one", l1, res[n] / l1, flush=True)
-    for n in (2, 4, 8):
-        assert res[n] <= 1.05 * l1, res
-
-
 @pytest.mark.parametrize("mode", ["atomic", "hybrid"])
 def test_block_walks_parallel_modes_train(smore, graph, mode):
     """DeepWalk in the block schedule on 2 and 4 replicas (cuda:0) in the

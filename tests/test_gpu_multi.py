@@ -275,6 +275,7 @@ def test_source_partition_draws(smore):
 
 def _local_group(smore, n, dim=32, path=PL1K):
     g = smore.Group([0] * n)
+    g.set_schedule("replicas")   # these tests check the replica schedule's machinery
     g.LoadEdgeList(path, 1)
     g.alloc_tables(dim, 2)
     g.primary.init_table_glibc(0, 0)
@@ -411,6 +412,7 @@ def test_local_group_deepwalk_matches_emulation(smore, rule):
     g = orc.Graph.from_file(PL1K, 1)
     n, dim, wt, steps, window, K, alpha0 = 3, 16, 2, 10, 2, 3, 0.025
     grp = smore.Group([0] * n)
+    grp.set_schedule("replicas")
     grp.LoadEdgeList(PL1K, 1)
     grp.alloc_tables(dim, 2)
     grp.primary.init_table_glibc(0, 0)
@@ -490,6 +492,7 @@ def test_local_group_walk_partition(smore):
     one.train_deepwalk(0, wt * g.V, wt, 40, 5, K, 0.025, SEED, order, "atomic")
     l1 = _heldout_loss(one.get_table(0), one.get_table(1), held)
     grp = smore.Group([0] * 4)
+    grp.set_schedule("replicas")
     grp.LoadEdgeList(PL1K, 1)
     grp.alloc_tables(dim, 2)
     grp.primary.init_table_glibc(0, 0)
@@ -520,12 +523,12 @@ def _edge_auc(W, C, off, tgt, seed=3):
 def test_c5_deepwalk_group_defaults(smore):
     """Config 5's DeepWalk (the Youtube-sized stand-in, d=128, 10 walks per
     vertex, 40 steps, window 5, K 5, hybrid) on 2, 4 and 8 replicas with the
-    group's defaults (replicated tables, the adaptive rule at c0 64 from a row
-    census of the walks, 4 pair updates per row per replica per exchange)
-    against one context that walked everything: held-out LINE objective
-    within 10 % / 12 % / 45 % and edge AUC within 0.012 / 0.01 / 0.02
-    (measured 1.035-1.06 / 1.066 / 1.345x and -0.009 / -0.0003 / -0.004,
-    DESIGN.md 10)."""
+    group's defaults -- the 2-D block schedule: W parts owned,
+    C blocks rotating, every replica walking every walk and keeping its own
+    centres' pairs -- against one context that walked everything: held-out
+    LINE objective within 5 % and edge AUC within 0.005 (measured 1.007 /
+    1.012 / 1.024x and +0.0001 / +0.0004 / -0.0006; the replica schedule
+    measured 1.035-1.06 / 1.066 / 1.345x, profiles/r05/blocks.md)."""
     from smore_amd import graphgen
     V, (src, dst, w) = graphgen.config_edges("c5")
     dim, wt, K = 128, 10, 5
@@ -542,8 +545,7 @@ def test_c5_deepwalk_group_defaults(smore):
                                                                                off, tgt)
     one.close()
     res = {1: (l1, a1)}
-    bounds = ((2, 1.10, 0.012), (4, 1.12, 0.01), (8, 1.45, 0.02))
-    for n, _, _ in bounds:
+    for n in (2, 4, 8):
         g = smore.Group([0] * n)
         g.set_graph_edges(V, src, dst, w)
         g.alloc_tables(dim, 2)
@@ -554,19 +556,19 @@ def test_c5_deepwalk_group_defaults(smore):
         W, C = g.primary.get_table(0), g.primary.get_table(1)
         g.close()
         res[n] = (_heldout_loss(W, C, held), _edge_auc(W, C, off, tgt))
-        print("C5 DeepWalk group", n, res[n], "one", res[1], flush=True)
-    for n, lb, ab in bounds:
-        assert np.isfinite(res[n][0]) and res[n][0] <= lb * l1, res
-        assert res[n][1] >= a1 - ab, res
+        print("C5 DeepWalk group", n, res[n], "one", res[1], res[n][0] / l1, flush=True)
+    for n in (2, 4, 8):
+        assert np.isfinite(res[n][0]) and res[n][0] <= 1.05 * l1, res
+        assert res[n][1] >= a1 - 0.005, res
 
 
 def test_c2_line_group_defaults(smore):
     """Config 2's LINE-2 (1M vertices / 40M slots, d=64, K 5, hybrid) at
-    2^31 samples in total on 4 and 8 replicas with the group's defaults (W
-    partitioned by source, adaptive c0 2048, 6.7 samples per row per replica
-    per exchange) against one context that ran every sample: held-out loss
-    within 12 % / 25 % (measured 1.08 / 1.19x; the sample efficiency and the
-    effective speed-up, 2.9-3.1x / 4.4-5.4x, are in DESIGN.md 10)."""
+    2^31 samples in total on 2, 4 and 8 replicas with the group's defaults
+    (the 2-D block schedule, its cells' hot threshold 0.3) against one context
+    that ran every sample: held-out loss within 5 % (measured 1.019 / 1.013 /
+    1.019x; the replica schedule measured 1.08 / 1.19x at 4 / 8; the
+    predicted 8-GPU speed-up is in DESIGN.md 10)."""
     from smore_amd import graphgen
     V, (src, dst, w) = graphgen.config_edges("c2")
     dim, K, T = 64, 5, 1 << 31
@@ -580,7 +582,7 @@ def test_c2_line_group_defaults(smore):
     l1 = _heldout_loss(one.get_table(0), one.get_table(1), held)
     one.close()
     res = {1: l1}
-    for n in (4, 8):
+    for n in (2, 4, 8):
         g = smore.Group([0] * n)
         g.set_graph_edges(V, src, dst, w)
         g.alloc_tables(dim, 2)
@@ -590,5 +592,6 @@ def test_c2_line_group_defaults(smore):
         g.train_edges("line2", 0, T, T, K, 0.025, 0.0, SEED, "hybrid")
         res[n] = _heldout_loss(g.primary.get_table(0), g.primary.get_table(1), held)
         g.close()
-        print("C2 LINE-2 group", n, res[n], "one", l1, flush=True)
-    assert res[4] <= 1.12 * l1 and res[8] <= 1.25 * l1, res
+        print("C2 LINE-2 group", n, res[n], "one", l1, res[n] / l1, flush=True)
+    for n in (2, 4, 8):
+        assert res[n] <= 1.05 * l1, res
