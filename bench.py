@@ -327,6 +327,7 @@ def main():
               file=sys.stderr, flush=True)
     import torch
     dist = None
+    node_rank = local                       # this process's index on the node (the graph builder is 0)
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
@@ -352,19 +353,19 @@ def main():
         # (smore_save_graph); the others read it (smore_load_graph) instead of
         # generating and building 400M slots each under a shared CPU quota
         path = graph_file(args.config)
-        if local == 0:
+        if node_rank == 0:
             V, (src, dst, w) = graphgen.config_edges(args.config)
             t_build = time.perf_counter()
             pn.set_graph_edges(V, src, dst, w)
             pn.save_graph(path)
             src = dst = w = None
         dist.barrier()
-        t_build = time.perf_counter() if local != 0 else t_build
-        if local != 0:
+        t_build = time.perf_counter() if node_rank != 0 else t_build
+        if node_rank != 0:
             pn.load_graph(path)
         V = pn.MAX_vid
         dist.barrier()
-        if local == 0:
+        if node_rank == 0:
             os.remove(path)
     t_ready = time.perf_counter()
     setup = {"rank": rank, "setup_s": round(t_ready - t_gen, 2), "graph_s": round(t_ready - t_build, 2),

@@ -828,6 +828,23 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
             a.K = K;
         }
     }
+    // C++ BPR's hybrid runs the plain-store kernel on graphs above the
+    // small-graph cap (16 M < V; below it every row is hot and the hybrid is
+    // the atomic scatter): C3 at 2^28 samples, held-out BPR objective +0.11 %
+    // of the atomic scatter's and the same ranking accuracy (0.82548 vs
+    // 0.82549), update 80.3 ms per 2^26 against the tagged kernel's 97.6 -- its
+    // ~170 hot rows are hub items drawn as positives, whose collisions cost
+    // less than the hybrid kernel's code shape (2 blocks per CU against 3;
+    // DESIGN.md 8, profiles/r05/bpr).  SMORE_BPR_SCATTER=tagged keeps the
+    // tagged hybrid kernel.
+    if (model == SMORE_BPR && !go && mode == SMORE_HYBRID) {
+        const char* e = getenv("SMORE_BPR_SCATTER");
+        EdgeArgs t = a;
+        t.sh_rows = 0;
+        const int64_t Mb = (int64_t)edge_grid(c, t, false, 0) * (256 / lanes_of(c->dpad));
+        const bool small = c->hot_tau < 0 && 16.0 * (double)Mb >= (double)c->g->V;
+        if (!small && !(e && !strcmp(e, "tagged"))) a.mode = mode = SMORE_HOGWILD;
+    }
     // C++ BPR combines its hub rows only with SMORE_BPR_COMBINE=1 (measured in
     // the hub items are positives, the negatives are uniform)
     const char* bpr_comb = getenv("SMORE_BPR_COMBINE");

@@ -264,6 +264,13 @@ bool build_graph(int64_t V, int64_t E, const int32_t* src, const int32_t* dst, c
     g.vtab.resize((size_t)V); g.ntab.resize((size_t)V);
     build_cpp_vn_tables(g);
     phase("v/n tables");
+    build_ctx_tables(g);
+    phase("ctx tables");
+    return true;
+}
+
+void build_ctx_tables(HostGraph& g) {
+    const int64_t V = g.V, E = g.E;
     // per-vertex context tables, alias remapped to the target vid
     // (src/proNet.cpp:517-537); vertices are independent -> threads
     g.cprob.resize((size_t)E); g.calias.resize((size_t)E);
@@ -279,8 +286,6 @@ bool build_graph(int64_t V, int64_t E, const int32_t* src, const int32_t* dst, c
                          g.ctab.data() + off);
         }
     });
-    phase("ctx tables");
-    return true;
 }
 
 void build_cpp_vn_tables(HostGraph& g) {

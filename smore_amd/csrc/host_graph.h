@@ -83,6 +83,11 @@ bool build_graph(int64_t V, int64_t E, const int32_t* src, const int32_t* dst, c
 // stored methods (src/proNet.cpp:457-510).
 void build_cpp_vn_tables(HostGraph& g);
 
+// (Re)build the per-vertex context tables (cprob, calias remapped to target
+// ids, ctab) from the CSR and the weights (src/proNet.cpp:517-537), threaded
+// over vertices; deterministic, so a graph file need not store them.
+void build_ctx_tables(HostGraph& g);
+
 // Text edge list(s) -> names + directed slots (src/proNet.cpp:115-236), parsed
 // in parallel (loader.cpp); with a cache directory, a binary copy keyed by the
 // input's content hash is written on the first load and read on later ones.

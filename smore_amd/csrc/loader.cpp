@@ -301,14 +301,17 @@ uint64_t content_key(const std::vector<std::unique_ptr<Mapped>>& maps, bool undi
 }
 
 // ---------------------------------------------------------------- built-graph cache
-// The whole HostGraph of one (input, undirected, vertex method, negative
-// method): names, CSR, degrees, the three alias tables in both
-// representations.  Arrays are read back with parallel pread()s.
+// The HostGraph of one (input, undirected, vertex method, negative method):
+// names, CSR, degrees, weights, the vertex and negative alias tables.  The
+// per-edge context tables (cprob, calias, ctab: 20 of the 24 bytes per slot)
+// are rebuilt on load (build_ctx_tables, deterministic): C4's file is 2.3 GB
+// instead of 11.9, which a tmpfs write takes ~12 s for (bench.py N > 1: one
+// rank builds, the others read).  Arrays are read back with parallel pread()s.
 constexpr char GRAPH_MAGIC[8] = {'S', 'M', 'O', 'R', 'E', 'G', 'C', '2'};
 // Version of the rules that produce a HostGraph (build_graph's CSR order, the
 // degree methods, alias_cpp, alias_encode).  Bump it whenever one of them
 // changes: a cache written under other rules is then rebuilt, never reused.
-constexpr uint64_t GRAPH_BUILDER_VERSION = 3;
+constexpr uint64_t GRAPH_BUILDER_VERSION = 4;
 
 // cheap consistency checks of a graph read back from a cache file (a truncated
 // or corrupted file must not drive out-of-bounds device reads)
@@ -325,7 +328,7 @@ bool graph_sane(const HostGraph& g) {
             if (g.valias[v] < -1 || g.valias[v] >= V || g.nalias[v] < -1 || g.nalias[v] >= V) ok = false;
         const int64_t eb = E * t / nt, ee = E * (t + 1) / nt;
         for (int64_t e = eb; e < ee && ok; ++e)
-            if (g.targets[e] < 0 || g.targets[e] >= V || g.calias[e] < -1 || g.calias[e] >= V) ok = false;
+            if (g.targets[e] < 0 || g.targets[e] >= V || !(g.weights[e] >= 0.0)) ok = false;
     });
     return ok;
 }
@@ -342,8 +345,7 @@ std::vector<Blk> graph_blocks(HostGraph& g, std::string& names_blob, bool weight
                           {g.out_deg.data(), V * 8}, {g.in_deg.data(), V * 8},
                           {g.vprob.data(), V * 8}, {g.valias.data(), V * 8},
                           {g.nprob.data(), V * 8}, {g.nalias.data(), V * 8},
-                          {g.cprob.data(), E * 8}, {g.calias.data(), E * 8},
-                          {g.vtab.data(), V * 8}, {g.ntab.data(), V * 8}, {g.ctab.data(), E * 8}};
+                          {g.vtab.data(), V * 8}, {g.ntab.data(), V * 8}};
     if (!weights_one) b.push_back({g.weights.data(), E * 8});
     return b;
 }
@@ -430,8 +432,7 @@ bool load_graph_cache(const std::string& fn, uint64_t key, int vm, int nm, HostG
     g.offsets.resize(V + 1); g.targets.resize(E); g.weights.resize(E);
     g.out_deg.resize(V); g.in_deg.resize(V);
     g.vprob.resize(V); g.valias.resize(V); g.nprob.resize(V); g.nalias.resize(V);
-    g.cprob.resize(E); g.calias.resize(E);
-    g.vtab.resize(V); g.ntab.resize(V); g.ctab.resize(E);
+    g.vtab.resize(V); g.ntab.resize(V);
     std::string blob(std::max<uint64_t>(hdr[5], 1), '\0');
     phase("allocate");
     std::vector<Blk> blks = graph_blocks(g, blob, hdr[6] != 0);
@@ -459,7 +460,7 @@ bool load_graph_cache(const std::string& fn, uint64_t key, int vm, int nm, HostG
     });
     close(fd);
     phase("read");
-    if (!good || !graph_sane(g)) return false;
+    if (!good) { if (verbose) fprintf(stderr, "[graph cache] short read\n"); return false; }
     if (hdr[6]) {   // all-one weights are not stored: fill them on every thread
         const unsigned nf = std::max(1u, std::min<unsigned>(threads_for(E * 8), 32u));
         run_threads(nf, [&](unsigned t) {
@@ -467,6 +468,9 @@ bool load_graph_cache(const std::string& fn, uint64_t key, int vm, int nm, HostG
                       1.0);
         });
     }
+    if (!graph_sane(g)) { if (verbose) fprintf(stderr, "[graph cache] inconsistent arrays\n"); return false; }
+    build_ctx_tables(g);
+    phase("ctx tables");
     // names: newline-separated; threads take byte ranges, count their lines,
     // then fill their slice of the pre-sized vector
     const size_t nb = (size_t)hdr[5];

@@ -80,7 +80,10 @@ class ProNet:
         """Graph from ids: directed edge slots src->dst (weight w) in push order."""
         src = np.ascontiguousarray(src, np.int32)
         dst = np.ascontiguousarray(dst, np.int32)
-        w = np.ascontiguousarray(w, np.float64)
+        # w None: unit weights (np.ascontiguousarray(None) would be one NaN)
+        w = np.ones(len(src)) if w is None else np.ascontiguousarray(w, np.float64)
+        if len(dst) != len(src) or len(w) != len(src):
+            raise ValueError("set_graph_edges: src, dst and w need one entry per edge slot")
         self._chk(lib.smore_set_graph_edges(self.ctx, int(V), len(src), ptr(src), ptr(dst), ptr(w),
                                             _lib.VM[self.vertex_method], _lib.NM[self.negative_method]),
                   "set_graph_edges")
@@ -589,7 +592,10 @@ class Group:
     def set_graph_edges(self, V, src, dst, w, vertex_method="out_degrees", negative_method="degrees"):
         src = np.ascontiguousarray(src, np.int32)
         dst = np.ascontiguousarray(dst, np.int32)
-        w = np.ascontiguousarray(w, np.float64)
+        # w None: unit weights (np.ascontiguousarray(None) would be one NaN)
+        w = np.ones(len(src)) if w is None else np.ascontiguousarray(w, np.float64)
+        if len(dst) != len(src) or len(w) != len(src):
+            raise ValueError("set_graph_edges: src, dst and w need one entry per edge slot")
         self._chk(lib.smore_group_set_graph_edges(self.g, int(V), len(src), ptr(src), ptr(dst), ptr(w),
                                                   _lib.VM[vertex_method], _lib.NM[negative_method]),
                   "set_graph_edges")

@@ -211,3 +211,34 @@ def test_corrupt_graph_cache_is_rebuilt(tmp_path):
     assert h2 != 2, "corrupt graph cache was used"
     np.testing.assert_array_equal(c1[0], c2[0])
     np.testing.assert_array_equal(c1[1], c2[1])
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+def test_graph_file_round_trip(tmp_path, weighted):
+    """smore_save_graph / smore_load_graph (bench.py's build-once start-up and
+    the loader cache): the file holds the CSR, weights and the vertex / negative
+    tables; the per-edge context tables are rebuilt on load
+    (build_ctx_tables) and equal the built graph's bit for bit, in both the
+    (prob, alias) and the encoded device form."""
+    import smore_amd
+    rng = np.random.default_rng(3)
+    V, E = 5000, 60_000
+    src = (rng.zipf(1.5, E) % V).astype(np.int32)
+    dst = rng.integers(0, V, E).astype(np.int32)
+    w = rng.integers(1, 7, E).astype(np.float64) if weighted else None
+    a = smore_amd.ProNet(-1)
+    a.set_graph_edges(V, src, dst, w)
+    path = str(tmp_path / "g.graph")
+    a.save_graph(path)
+    b = smore_amd.ProNet(-1)
+    b.load_graph(path)
+    for x, y in zip(a.csr(), b.csr()):
+        np.testing.assert_array_equal(x, y)
+    assert a.names == b.names
+    for which in (0, 1, 2):
+        for x, y in zip(a.alias(which), b.alias(which)):
+            np.testing.assert_array_equal(x, y)
+        for x, y in zip(a.alias_encoded(which), b.alias_encoded(which)):
+            np.testing.assert_array_equal(x, y)
+    # the context tables are not stored: 24 -> 4 (+8 weighted) bytes per slot
+    assert os.path.getsize(path) < (4 + (8 if weighted else 0)) * 2 * E + 200 * V

@@ -3,6 +3,7 @@
 headline LINE-2 C4 number is bench.py's).  One JSON line per config:
 
   c2   LINE order 2, 1M vertices / 20M lines, d=64, K=5   (M edge-updates/s)
+  c4   LINE order 2, 10M vertices / 200M lines (bench.py's headline config)
   c3   BPR (C++ rule: 5 rounds per sample), 2M users x 1M items / 100M edges,
        d=128, negatives uniform over items (BPR's "no_degrees")   (M BPR samples/s)
   c5   DeepWalk, Youtube-links-sized stand-in (1.13M vertices / 3M lines),
@@ -39,13 +40,15 @@ def pairs_per_walk(L, window):
 
 
 def run_edges(pn, model, S, steps, K, mode, seed=7):
+    """mean ms per call, and the mean (draw, update) phase ms"""
     total = (steps + 1) * S
-    ms = []
+    ms, ph = [], []
     for k in range(steps + 1):
         pn.train_edges(model, k * S, S, total, K, 0.025, 0.0, seed, mode)
         if k:
             ms.append(pn.last_kernel_ms())
-    return float(np.mean(ms))
+            ph.append(pn.last_phase_ms()[:2])
+    return float(np.mean(ms)), [round(float(x), 3) for x in np.mean(ph, axis=0)]
 
 
 def main():
@@ -66,20 +69,21 @@ def main():
         build = time.perf_counter() - t0
         out = {"config": cfg, "vertices": V, "edge_slots": pn.MAX_line, "mode": args.mode,
                "build_s": round(build, 1)}
-        if cfg == "c2":
+        if cfg in ("c2", "c4"):
             S = 1 << 27
             pn.alloc_tables(64, 2)
             pn.init_table_uniform(0, 1)
             pn.zero_table(1)
-            ms = run_edges(pn, "line2", S, args.steps, 5, args.mode)
+            ms, ph = run_edges(pn, "line2", S, args.steps, 5, args.mode)
             out.update(model="line2", dim=64, K=5, samples_per_call=S, ms_per_call=round(ms, 3),
-                       value=round(S / ms / 1e3, 1), unit="M edge-updates/s")
+                       draw_update_ms=ph, value=round(S / ms / 1e3, 1), unit="M edge-updates/s")
         elif cfg == "c3":
             S = 1 << 26
             pn.alloc_tables(128, 1)
             pn.init_table_uniform(0, 1)
-            ms = run_edges(pn, "bpr", S, args.steps, 5, args.mode)
+            ms, ph = run_edges(pn, "bpr", S, args.steps, 5, args.mode)
             out.update(model="bpr", dim=128, rounds=5, samples_per_call=S, ms_per_call=round(ms, 3),
+                       draw_update_ms=ph,
                        value=round(S / ms / 1e3, 1), unit="M BPR samples/s (5 rounds each)")
         elif cfg == "c5":
             steps_, window, K, walk_times = 40, 5, 5, 1

@@ -73,12 +73,14 @@ def main():
                     dt[r][b] = sum(v) / len(v)
         any_row = next(iter(meas.values()))
         xfer = any_row["block_bytes_max"] / (args.link_gbs * 1e9) * 1e3
-        ep = simulate(n, dt, xfer)
-        bound = max(sum(dt[r]) for r in range(n))
+        # walks: every replica generates the round's walks before its cells
+        prep = sum(d.get("prepare_ms", 0.0) for d in meas.values()) / len(meas)
+        ep = simulate(n, dt, xfer) + prep
+        bound = max(sum(dt[r]) for r in range(n)) + prep
         units = sum(d["units"] for d in meas.values()) / len(meas)
         one_rate = one["units"] / one["epoch_ms"]
         print(json.dumps({"config": any_row["config"], "model": any_row["model"], "nparts": n,
-                          "parts_measured": sorted(meas), "xfer_ms": round(xfer, 3),
+                          "parts_measured": sorted(meas), "xfer_ms": round(xfer, 3), "prepare_ms": round(prep, 3),
                           "epoch_ms_sim": round(ep, 3), "epoch_ms_no_stall": round(bound, 3),
                           "stall_frac": round(1 - bound / ep, 4),
                           "speedup_pred": round(n * units / ep / one_rate, 3),
