@@ -23,12 +23,14 @@ def _json_line(out):
     return json.loads(lines[0])
 
 
-def _check_contract(d, n):
+def _check_contract(d, n, schedule="blocks"):
     assert d["metric"] == "M edge-updates/sec (d=64, neg=5)" and d["unit"] == "M edge-updates/s"
     assert d["n_gpus"] == n and d["steps"] == 2 and d["warmup"] == 1
     assert d["value"] > 0 and d["ms_per_step"] > 0 and d["higher_is_better"] is True
     assert d["scaling"] == "weak" and d["dtype"] == "f32" and d["vs_baseline"] is None
-    assert d["config"]["parallelism"] == "replicas%d" % n and "workload" in d["config"]
+    par = "replicas%d" % n if n == 1 else "%s%d" % (schedule, n)
+    assert d["config"]["parallelism"] == par and "workload" in d["config"]
+    assert d["setup"]["max_setup_s"] > 0 and len(d["setup"]["ranks"]) == n
     r = d["roofline"]
     for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
         assert k in r
@@ -46,16 +48,20 @@ def test_bench_json_line_n1():
     assert d["cpu_baseline"] is None and d["config"]["sync"] == "none"
 
 
-def test_bench_json_line_n2_gloo_ranks():
+@pytest.mark.parametrize("schedule", ["blocks", "replicas"])
+def test_bench_json_line_n2_gloo_ranks(schedule):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
-                        "--dist-backend", "gloo"] + SMALL, cwd=ROOT, capture_output=True, text=True, timeout=300,
+                        "--dist-backend", "gloo", "--schedule", schedule] + SMALL, cwd=ROOT, capture_output=True, text=True, timeout=300,
                        env=env)
     assert p.returncode == 0, p.stderr[-2000:]
     d = _json_line(p.stdout)
-    _check_contract(d, 2)
-    assert d["config"]["sync"].startswith("adaptive") and "1/2 step" in d["config"]["sync"]
+    _check_contract(d, 2, schedule)
+    if schedule == "blocks":
+        assert d["config"]["sync"].startswith("blocks")
+    else:
+        assert d["config"]["sync"].startswith("adaptive") and "1/2 step" in d["config"]["sync"]
