@@ -478,6 +478,17 @@ static double sh_budget(bool pairs) {
     if (const char* e = getenv("SMORE_SH_BUDGET")) return atof(e);
     return pairs ? SH_PAIR_BUDGET : SH_AUTO_BUDGET;
 }
+// LINE-2 cells of the 2-D block schedule (blocks.cpp block_sh_sets): twice the
+// edge budget.  A cell's hub rows are 2N times hotter, so at the edge budget
+// they drain every 1-2 rounds and the hub cells are bound by those drains'
+// memory-side atomics; C4 on 8 GPUs predicted 4.9 x at 6144, 5.5 x at 9216,
+// 5.8 x at 12288, 6.3 x at 24576, for C2 held-out loss 1.019 / 1.031 / 1.037 /
+// 1.077 x one GPU (profiles/r05/blocks)
+constexpr double SH_CELL_BUDGET = 12288.0;
+static double cell_budget(bool walk) {
+    if (const char* e = getenv("SMORE_SH_BUDGET")) return atof(e);
+    return walk ? SH_PAIR_BUDGET : SH_CELL_BUDGET;
+}
 // rows whose hidden updates would pass this even at a 1-round drain (edge
 // rule) / the budget (pair rule) stay on atomics; SMORE_SH_STALE overrides
 static double sh_stale(bool pairs) {
@@ -2127,9 +2138,9 @@ int hot_maps(smore_ctx* c, int model, int K, int64_t M, bool walk, double w_scal
 }
 int launch_grid(smore_ctx* c, const EdgeArgs& a) { return edge_grid(c, a, false, 0); }
 int sh_flush_max(bool walk) { return walk ? PAIR_FLUSH_MAX : EDGE_FLUSH_MAX; }
-int sh_slot_interval(double Mp, int cap, bool walk) { return slot_interval(Mp, cap, sh_budget(walk)); }
+int sh_slot_interval(double Mp, int cap, bool walk) { return slot_interval(Mp, cap, cell_budget(walk)); }
 void sh_slot_levels(int64_t M, int cap, bool walk, const std::pair<double, int32_t>* r, int64_t n, int (&lvl)[8]) {
-    sh_levels(M, cap, sh_budget(walk), r, n, lvl);
+    sh_levels(M, cap, cell_budget(walk), r, n, lvl);
 }
 double hot_tau_default(bool walk) { return walk ? HOT_TAU_WALK : HOT_TAU_EDGE; }
 double hot_tau_cell_default(bool walk) { return walk ? HOT_TAU_WALK : HOT_TAU_CELL; }

@@ -71,9 +71,11 @@ def main():
         return best
 
     # the one-GPU path over the same work
+    one_phase = None
     if line:
         one = timed(lambda: pn.train_edges("line2", 0, S, total, K, 0.025, 0.0, args.seed, args.mode, sync=False))
         units = S
+        one_phase = [round(x, 3) for x in pn.last_phase_ms()[:2]]
     else:
         one = timed(lambda: pn.train_deepwalk(0, args.walks, wt, steps, window, K, 0.025, args.seed, order,
                                               args.mode))
@@ -82,7 +84,8 @@ def main():
         pn.census_end(1.0)
         units = float(pn.row_rates("census", K, 0).sum())   # pairs of the walks
     print(json.dumps({"config": args.config, "model": args.model, "nparts": 1, "epoch_ms": round(one * 1e3, 3),
-                      "units": units, "rate_M_per_s": round(units / one / 1e6, 2)}), flush=True)
+                      "units": units, "rate_M_per_s": round(units / one / 1e6, 2), "draw_update_ms": one_phase}),
+          flush=True)
     for n in args.nparts:
         nb = 2 * n
         for r in args.parts:
@@ -109,7 +112,9 @@ def main():
                     if cnt[b]:
                         t1 = time.perf_counter()
                         pn.block_train_edges(b, 0, int(cnt[b]), total, K, 0.025, args.seed, args.mode)
-                        cells.append([b, int(cnt[b]), round((time.perf_counter() - t1) * 1e3, 3)])
+                        ph = pn.last_phase_ms()
+                        cells.append([b, int(cnt[b]), round((time.perf_counter() - t1) * 1e3, 3)] +
+                                     ([round(ph[0], 3), round(ph[1], 3)] if ph else []))
                 units_r = mine
             else:
                 prep = timed(lambda: pn.block_prepare_walks(0, args.walks, wt, steps, window, K, 0.025, args.seed,

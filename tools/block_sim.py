@@ -61,7 +61,7 @@ def main():
         meas = rows[n]
         by_block = defaultdict(list)
         for r, d in meas.items():
-            for b, _, ms in d["cells"]:
+            for b, _, ms, *_ in d["cells"]:
                 by_block[b].append(ms)
         dt = [[0.0] * nb for _ in range(n)]
         for r in range(n):
