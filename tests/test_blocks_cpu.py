@@ -79,7 +79,7 @@ def _worker(rank, world, port, subrounds, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,subrounds", [(2, 4), (2, 11), (3, 6), (3, 17)])
+@pytest.mark.parametrize("world,subrounds", [(2, 4), (2, 11), (3, 6), (3, 17), (4, 8), (8, 21)])
 def test_block_rotation_gloo(world, subrounds):
     """Whole epochs and a partial one: the holder of every block after the
     drain is ((b - s) mod 2N) // 2 and no rank ever trains a stale block."""
