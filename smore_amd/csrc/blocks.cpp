@@ -28,7 +28,7 @@ using namespace smore_host;
 
 namespace {
 
-constexpr uint64_t WALK_ROUND_MAX = (uint64_t)1 << 18;   // walks per prepared block round
+constexpr uint64_t WALK_ROUND_MAX = (uint64_t)1 << 20;   // walks per prepared block round
 
 int check_ctx(smore_ctx* c) {
     if (!c) return SMORE_EINVAL;
@@ -57,7 +57,7 @@ int64_t resident_groups(smore_ctx* c, bool walk, int K, int mode) {
     a.mode = mode;
     a.count = (uint64_t)1 << 30;
     a.alpha_rec = walk ? 1 : 0;
-    a.sh_rows = mode == SMORE_HYBRID ? std::min(c->sh_max, 8192 / std::max(1, c->dpad)) : 0;
+    a.sh_rows = mode == SMORE_HYBRID ? std::min(c->sh_max, sh_rows_max(c->dpad)) : 0;
     return (int64_t)launch_grid(c, a) * (256 / lanes_of(c->dpad));
 }
 
@@ -67,7 +67,7 @@ int64_t resident_groups(smore_ctx* c, bool walk, int K, int mode) {
 void block_sh_sets(smore_ctx* c, bool walk, bool on, int64_t Mg, const std::vector<std::vector<double>>& pcb,
                    const std::vector<std::vector<uint8_t>>& hcb, std::vector<int2>& hash, std::vector<int32_t>& ids) {
     auto& B = c->blk;
-    const int cap = on ? std::max(0, std::min(c->sh_max, 8192 / std::max(1, c->dpad))) : 0;
+    const int cap = on ? std::max(0, std::min(c->sh_max, sh_rows_max(c->dpad))) : 0;
     B.sh_cap = std::max(cap, 1);
     B.sh_n.assign((size_t)B.nb, 0);
     B.sh_lvl.assign((size_t)B.nb, std::array<int, 8>{});
@@ -563,7 +563,7 @@ int smore_block_prepare_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint6
     B.walks = 0;
     if (walk_begin >= walk_end) return SMORE_OK;
     const uint64_t nw = walk_end - walk_begin;
-    if (nw > WALK_ROUND_MAX) return fail(c, SMORE_EINVAL, "a block round holds at most 2^18 walks");
+    if (nw > WALK_ROUND_MAX) return fail(c, SMORE_EINVAL, "a block round holds at most 2^20 walks");
     if (order) {
         if (walk_begin < order_base) return fail(c, SMORE_EINVAL, "walk order slice does not cover the range");
         order -= order_base;

@@ -624,7 +624,7 @@ static int build_hot_maps(smore_ctx* c, int model, int K, int64_t M, double tau_
                 r.push_back({ps[v] * w_scale, (int32_t)(v | SH_WKEY)});
         }
         const int64_t cap =
-            small ? 0 : std::max<int64_t>(0, std::min<int64_t>(c->sh_max, 8192 / std::max(1, c->dpad)));
+            small ? 0 : std::max<int64_t>(0, std::min<int64_t>(c->sh_max, sh_rows_max(c->dpad)));
         const int64_t n = std::min<int64_t>(cap, (int64_t)r.size());
         std::partial_sort(r.begin(), r.begin() + n, r.end(), [](const auto& x, const auto& y) {
             return x.first > y.first || (x.first == y.first && x.second < y.second);
@@ -860,7 +860,7 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
     // the hub items are positives, the negatives are uniform)
     const char* bpr_comb = getenv("SMORE_BPR_COMBINE");
     const bool combine = mode == SMORE_HYBRID && (go || model != SMORE_BPR || (bpr_comb && atoi(bpr_comb) != 0));
-    a.sh_rows = combine ? std::min(c->sh_max, 8192 / std::max(1, c->dpad)) : 0;   // LDS bound for the grid
+    a.sh_rows = combine ? std::min(c->sh_max, sh_rows_max(c->dpad)) : 0;   // LDS bound for the grid
     const int grid = edge_grid(c, a, false, go ? 1 : 0);
     if (mode == SMORE_HYBRID) {
         const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
@@ -1419,7 +1419,7 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
         c->rec_cap = chunk * pb * RW;
     }
     const bool combine = mode == SMORE_HYBRID;
-    ar.sh_rows = combine ? std::min(c->sh_max, 8192 / std::max(1, c->dpad)) : 0;
+    ar.sh_rows = combine ? std::min(c->sh_max, sh_rows_max(c->dpad)) : 0;
     ar.alpha_rec = 1;
     ar.work = c->d_work;
     ar.count = chunk * pb;   // grid for the most pairs a chunk can have
@@ -1651,7 +1651,7 @@ int smore_train_app_async(smore_ctx* c, uint64_t unit_begin, uint64_t unit_end, 
     a.work = c->d_work;
     a.count = chunk;
     const int combine = mode == SMORE_HYBRID;
-    a.sh_rows = combine ? std::min(c->sh_max, 8192 / std::max(1, c->dpad)) : 0;
+    a.sh_rows = combine ? std::min(c->sh_max, sh_rows_max(c->dpad)) : 0;
     const int grid = edge_grid(c, a);
     if (mode == SMORE_HYBRID) {
         const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
@@ -1732,7 +1732,7 @@ int smore_train_hpe_async(smore_ctx* c, uint64_t begin, uint64_t count, uint64_t
     a.work = c->d_work;
     a.count = chunk * nrec;
     const int combine = mode == SMORE_HYBRID;
-    a.sh_rows = combine ? std::min(c->sh_max, 8192 / std::max(1, c->dpad)) : 0;
+    a.sh_rows = combine ? std::min(c->sh_max, sh_rows_max(c->dpad)) : 0;
     const int grid = edge_grid(c, a);
     if (mode == SMORE_HYBRID) {
         const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));
@@ -1847,7 +1847,7 @@ static int train_pairs_core(smore_ctx* c, const int32_t* v, const int32_t* cc, i
     a.work = c->d_work;
     a.count = chunk;
     const bool combine = mode == SMORE_HYBRID;
-    a.sh_rows = combine ? std::min(c->sh_max, 8192 / std::max(1, c->dpad)) : 0;
+    a.sh_rows = combine ? std::min(c->sh_max, sh_rows_max(c->dpad)) : 0;
     const int grid = edge_grid(c, a, false, go ? 2 : 0);
     if (mode == SMORE_HYBRID) {
         const int64_t M = (int64_t)grid * (256 / lanes_of(c->dpad));

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "device_common.h"
 
@@ -126,9 +127,24 @@ hipError_t launch_draw_split(const DevGraph& g, uint64_t seed, uint64_t begin, u
                              unsigned long long* counts, hipStream_t st);
 hipError_t launch_draw(const DevGraph& g, uint64_t seed, uint64_t begin, uint64_t count, int K, int32_t* rec,
                        unsigned long long* skipped, hipStream_t st);
-constexpr int SH_HASH = 256;   // entries of the super-hot row hash (power of two)
+constexpr int SH_HASH = 256;   // entries of the super-hot row hash (power of two, > the rows)
 constexpr int32_t SH_WKEY = 1 << 30;   // write-combine key bit: a W row of a two-table model
 // dynamic LDS of the hybrid edge kernel: hash, slot ids, pending deltas
+// write-combined rows that fit the LDS budget: SMORE_SH_LDS floats of pending
+// deltas (default 8192: 32 KB, three 256-thread blocks per CU with the hash,
+// ids and sigmoid table), below the hash's size.  160 rows at d=64 (40 KB,
+// hash 512) measured slower at one GPU (84.1 vs 83.6 ms per 2^27, C4) and in
+// the block schedule's cells (C4, 8 GPUs: 5.44 vs 5.76 x predicted)
+inline int sh_rows_max(int dpad) {
+    static const int lds = [] {
+        const char* e = getenv("SMORE_SH_LDS");
+        const int v = e ? atoi(e) : 8192;
+        return v > 0 ? v : 8192;
+    }();
+    const int r = lds / (dpad > 0 ? dpad : 1);
+    return r < SH_HASH - 1 ? r : SH_HASH - 1;
+}
+
 inline size_t sh_lds_bytes(int sh_rows, int dpad) {
     return sh_rows > 0 ? SH_HASH * 8 + (size_t)sh_rows * 4 + (size_t)sh_rows * dpad * 4 : 0;
 }
