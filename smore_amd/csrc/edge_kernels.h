@@ -840,7 +840,15 @@ pair_train_kernel(EdgeArgs a) {
     row_valid<G, M>(ev, lane, a.dpad);
     uint32_t round = 0;
     __shared__ uint64_t s_next;
-    const uint64_t sl = a.pair_slice ? (uint64_t)a.pair_slice : CH_ROUNDS;   // records per group slice
+    // records per group slice: CH_ROUNDS, or for a launch with fewer than
+    // CH_ROUNDS records per resident group (a cell of the 2-D block schedule:
+    // ~360k records at 8 GPUs) an even share, so every group works -- at
+    // CH_ROUNDS a 360k-record cell ran on 352 of 768 blocks, 128 records deep
+    uint64_t sl = a.pair_slice ? (uint64_t)a.pair_slice : CH_ROUNDS;
+    if (!a.pair_slice) {
+        const uint64_t groups = (uint64_t)gridDim.x * gpb;
+        if (count < groups * CH_ROUNDS) sl = count > groups ? (count + groups - 1) / groups : 1;
+    }
     const uint64_t span = sl * gpb;
     for (;;) {
         __syncthreads();   // every wave has read the previous s_next
