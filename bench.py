@@ -18,6 +18,7 @@ all-reduced over RCCL every `--sync-every` steps, overlapping the next step
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
+import atexit
 import csv
 import json
 import os
@@ -358,6 +359,9 @@ def main():
             t_build = time.perf_counter()
             pn.set_graph_edges(V, src, dst, w)
             pn.save_graph(path)
+            # a run that fails before the removal below must not leave a
+            # multi-GB file in host memory (/dev/shm)
+            atexit.register(lambda p=path: os.path.exists(p) and os.remove(p))
             src = dst = w = None
         dist.barrier()
         t_build = time.perf_counter() if node_rank != 0 else t_build
