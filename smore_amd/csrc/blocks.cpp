@@ -273,8 +273,9 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
         auto blk_of = [&](int64_t x) {
             return (int)(std::upper_bound(B.cb.begin(), B.cb.end(), x) - B.cb.begin()) - 1;
         };
-        auto each_atom = [&](auto&& f) {
-            for (int64_t v = wlo; v < whi; ++v) {
+        // vertices [vb, ve) of the part, in order
+        auto each_atom = [&](int64_t vb, int64_t ve, auto&& f) {
+            for (int64_t v = vb; v < ve; ++v) {
                 const int64_t off = g.offsets[v], br = g.offsets[v + 1] - off;
                 if (br == 0 || ps[v] <= 0) continue;
                 const double s = ps[v] / (double)br;
@@ -285,23 +286,55 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
                 }
             }
         };
-        std::vector<uint64_t> cnt((size_t)nb, 0);
-        each_atom([&](int64_t, int64_t x, double w) {
-            if (w > 0) cnt[blk_of(x)]++;
+        // two passes over vertex slices on every host thread (count per
+        // (slice, block), then fill); the slices' order keeps each block's
+        // atoms in vertex order, as one pass would
+        const int TS = (int)std::max(1u, std::min(std::thread::hardware_concurrency(), 64u));
+        std::vector<int64_t> vs((size_t)TS + 1);
+        {   // slices of equal edge count
+            const int64_t e0 = g.offsets[wlo], e1 = g.offsets[whi];
+            for (int t = 0; t <= TS; ++t) {
+                const int64_t e = e0 + (e1 - e0) * t / TS;
+                vs[t] = t == 0 ? wlo : t == TS ? whi
+                                 : std::lower_bound(g.offsets.begin() + wlo, g.offsets.begin() + whi, e) -
+                                       g.offsets.begin();
+            }
+        }
+        auto par_slices = [&](auto&& f) {
+            std::vector<std::thread> th;
+            for (int t = 0; t < TS; ++t) th.emplace_back([&, t] { f(t); });
+            for (auto& x : th) x.join();
+        };
+        std::vector<uint64_t> cnt((size_t)TS * nb, 0);
+        par_slices([&](int t) {
+            uint64_t* ct = cnt.data() + (size_t)t * nb;
+            each_atom(vs[t], vs[t + 1], [&](int64_t, int64_t x, double w) {
+                if (w > 0) ct[blk_of(x)]++;
+            });
         });
-        for (int k = 0; k < nb; ++k) B.atom_off[k + 1] = B.atom_off[k] + cnt[k];
+        std::vector<uint64_t> start((size_t)TS * nb);
+        for (int k = 0; k < nb; ++k) {
+            uint64_t acc = B.atom_off[k];
+            for (int t = 0; t < TS; ++t) {
+                start[(size_t)t * nb + k] = acc;
+                acc += cnt[(size_t)t * nb + k];
+            }
+            B.atom_off[k + 1] = acc;
+        }
         const uint64_t A = B.atom_off[nb];
         if (A == 0) return fail(c, SMORE_EINVAL, "block schedule: a part without edges");
         av.resize(A);
         ac.resize(A);
         aw.resize(A);
-        std::vector<uint64_t> pos(B.atom_off.begin(), B.atom_off.end() - 1);
-        each_atom([&](int64_t v, int64_t x, double w) {
-            if (w <= 0) return;
-            const uint64_t p = pos[blk_of(x)]++;
-            av[p] = (int32_t)v;
-            ac[p] = (int32_t)x;
-            aw[p] = w;
+        par_slices([&](int t) {
+            uint64_t* pos = start.data() + (size_t)t * nb;
+            each_atom(vs[t], vs[t + 1], [&](int64_t v, int64_t x, double w) {
+                if (w <= 0) return;
+                const uint64_t p = pos[blk_of(x)]++;
+                av[p] = (int32_t)v;
+                ac[p] = (int32_t)x;
+                aw[p] = w;
+            });
         });
         double tot = 0.0;
         for (int k = 0; k < nb; ++k) {
