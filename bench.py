@@ -276,17 +276,27 @@ def block_schedule(count, per, world, rank, counts):
             cur += int(cnt[b])
 
 
-def run_block_step(pn, bsync, k, world, rank, S, total, K, seed, mode):
+def run_block_step(pn, bsync, k, world, rank, S, total, K, seed, mode, cell_events=None):
     """One bench step in the block schedule: one epoch (2N sub-rounds) of the
     rank's samples [(k*world + rank)*S, +S), each sub-round one cell launch
-    followed by its C block's rotation (dist.BlockSync)."""
+    followed by its C block's rotation (dist.BlockSync).  cell_events: a list
+    that gets a (start, end) CUDA event pair around each cell (read after the
+    timed region, so no host wait inside it)."""
+    import torch
     base = k * world * S
     for s, b, lo, n in block_schedule(world * S, S, world, rank, pn.block_counts):
         assert bsync.block() == b
 
         def train(blk, lo=lo, n=n):
             if n:
+                ev = None
+                if cell_events is not None:
+                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    ev[0].record()
                 pn.block_train_edges(blk, base + lo, n, total, K, 0.025, seed, mode, sync=False)
+                if ev is not None:
+                    ev[1].record()
+                    cell_events.append(ev)
         bsync.sub_round(train)
 
 
@@ -413,13 +423,15 @@ def main():
                   flush=True)
     n_launch = max(1, args.launches) if (sync is not None and sync.hot_idx) else n_ex
     phase = [0.0, 0.0, 0]     # exposed draw ms, update ms, update launches (timed steps)
+    cell_events = []          # block schedule: (start, end) events of the timed steps' cells
 
     S, K = args.samples, args.negative
     total = (args.warmup + args.steps) * S * world     # alpha schedule over the whole job
 
     def step(k, timed=False):
         if bsync is not None:
-            run_block_step(pn, bsync, k, world, rank, S, total, K, args.seed, args.mode)
+            run_block_step(pn, bsync, k, world, rank, S, total, K, args.seed, args.mode,
+                           cell_events if timed else None)
             return
 
         def on_launch():
@@ -464,6 +476,9 @@ def main():
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
+    if cell_events:           # block schedule: the cells (draw + update kernels) as the "update" time
+        upd_ms = sum(a.elapsed_time(b) for a, b in cell_events)
+        launches = len(cell_events)
     if dist:
         t = torch.tensor([el], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -552,7 +567,8 @@ def main():
                                            "note": "the path's algorithmic read+write bytes per second over the "
                                                    "library's float4 device copy (membw.hip, 4 GiB, best of "
                                                    "default / non-temporal policy and 4 / 8 blocks per CU)"},
-                         "kernel": {"name": "edge_train_kernel (gather/update/scatter)",
+                         "kernel": {"name": ("block cells: block_draw_kernel + edge_train_kernel per cell"
+                                             if blocks else "edge_train_kernel (gather/update/scatter)"),
                                     "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
                                     "bytes_per_update_read": R_upd, "bytes_per_update_write": Wb,
                                     "achieved_rw": round((R_upd + Wb) * S / upd_s / 1e9, 1),
