@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--seed", type=int, default=20251015)
     ap.add_argument("--hot-tau", type=float, default=None, help="hybrid: hot-row threshold")
     ap.add_argument("--combine-rows", type=int, default=None, help="hybrid: LDS write-combined rows (0: off)")
+    ap.add_argument("--skip-one", action="store_true", help="no one-GPU reference (profiling the cells alone)")
     args = ap.parse_args()
 
     import torch  # noqa: F401  (one HIP runtime with torch, as bench.py)
@@ -72,7 +73,9 @@ def main():
 
     # the one-GPU path over the same work
     one_phase = None
-    if line:
+    if args.skip_one:
+        one, units = None, None
+    elif line:
         one = timed(lambda: pn.train_edges("line2", 0, S, total, K, 0.025, 0.0, args.seed, args.mode, sync=False))
         units = S
         one_phase = [round(x, 3) for x in pn.last_phase_ms()[:2]]
@@ -83,9 +86,10 @@ def main():
         pn.train_deepwalk(0, args.walks, wt, steps, window, K, 0.025, args.seed, order, args.mode)
         pn.census_end(1.0)
         units = float(pn.row_rates("census", K, 0).sum())   # pairs of the walks
-    print(json.dumps({"config": args.config, "model": args.model, "nparts": 1, "epoch_ms": round(one * 1e3, 3),
-                      "units": units, "rate_M_per_s": round(units / one / 1e6, 2), "draw_update_ms": one_phase}),
-          flush=True)
+    if one is not None:
+        print(json.dumps({"config": args.config, "model": args.model, "nparts": 1, "epoch_ms": round(one * 1e3, 3),
+                          "units": units, "rate_M_per_s": round(units / one / 1e6, 2), "draw_update_ms": one_phase}),
+              flush=True)
     for n in args.nparts:
         nb = 2 * n
         for r in args.parts:
@@ -134,11 +138,11 @@ def main():
             row = {"config": args.config, "model": args.model, "nparts": n, "part": r, "setup_s": round(setup_s, 2),
                    "epoch_ms": round(ep * 1e3, 3), "units": units_r,
                    "rate_M_per_s": round(units_r / ep / 1e6, 2),
-                   "per_gpu_factor": round((units_r / ep) / (units / one), 4),
+                   "per_gpu_factor": round((units_r / ep) / (units / one), 4) if one else None,
                    "cells": cells}
             if not line:
                 row["prepare_ms"] = round(prep * 1e3, 3)
-                row["per_gpu_factor_with_prepare"] = round((units_r / (ep + prep)) / (units / one), 4)
+                row["per_gpu_factor_with_prepare"] = round((units_r / (ep + prep)) / (units / one), 4) if one else None
             # the C block a rotation moves: its bytes (xGMI time is estimated in DESIGN.md 10)
             _, cb = pn.block_bounds()
             row["block_bytes_max"] = int(np.diff(cb).max()) * dim * 4
