@@ -9,13 +9,20 @@ HBM.  A step is the draw kernel (train_draw.hip) and the update kernel
 (edge_kernels.h).  Default scatter: hybrid (atomic adds for the hot rows, the
 128 hottest write-combined per workgroup in LDS, plain stores for the rest),
 whose training objective matches the lossless atomic scatter.
-One process per GPU; with N > 1 each rank runs its own disjoint global-sample
-range on a replicated graph and replicated tables, and the tables' deltas are
-all-reduced over RCCL every `--sync-every` steps, overlapping the next step
-(smore_amd/dist.py OverlapSync; weak scaling).  Rank 0 prints one JSON line.
+One process per GPU.  With N > 1 the default is the 2-D block schedule
+(smore_amd/dist.py BlockSync): rank r owns the W rows of part
+r, the C table is cut into 2N blocks that rotate around the ring by send/recv
+after each of a step's 2N sub-rounds, and nothing is all-reduced; each rank
+draws S samples per step (weak scaling).  `--schedule replicas` keeps the
+replicated tables with the adaptive delta all-reduce (dist.ReplicaSync).
+Rank 0 prints one JSON line; n_gpus is the process group's world size.
 
     python bench.py [--gpus N --steps K --warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...
+        (N > 1 without WORLD_SIZE: bench.py starts torch.distributed.run with
+         N ranks as a child process, relays its output and exits with its
+         status; nothing here touches the GPU first)
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+        (WORLD_SIZE must equal --gpus)
 """
 import argparse
 import atexit
@@ -257,19 +264,22 @@ def largest_remainder(samples, mass):
     return c
 
 
-def block_schedule(count, per, world, rank, counts):
+def block_schedule(count, per, world, rank, counts, part_mass=None):
     """exchange.cpp group_block_edges' split of samples [0, count) for replica
-    `rank`: rounds (epochs) of per * world samples, the rank's slice of each
-    split over its 2N cells by counts(slice) in sub-round order.  Yields
-    (sub-round, block, first sample, samples) -- zero-sample cells too: their
-    rotation still happens."""
+    `rank`: rounds (epochs) of per * world samples, each round's samples split
+    over the replicas by their parts' source mass (largest remainder;
+    part_mass None = equal parts), the rank's slice split over its 2N cells by
+    counts(slice) in sub-round order.  Yields (sub-round, block, first sample,
+    samples) -- zero-sample cells too: their rotation still happens."""
     nb = 2 * world
+    pm = part_mass if part_mass is not None else [1.0 / world] * world
     rounds = 1 if per > count // world else -(-count // (per * world))
     for k in range(rounds):
         lo = count * k // rounds
         m = count * (k + 1) // rounds - lo
-        cur = lo + m * rank // world
-        cnt = counts(lo + m * (rank + 1) // world - cur)
+        share = largest_remainder(m, pm)
+        cur = lo + sum(share[:rank])
+        cnt = counts(share[rank])
         for s in range(nb):
             b = (2 * rank + s) % nb
             yield k * nb + s, b, cur, int(cnt[b])
@@ -284,7 +294,7 @@ def run_block_step(pn, bsync, k, world, rank, S, total, K, seed, mode, cell_even
     timed region, so no host wait inside it)."""
     import torch
     base = k * world * S
-    for s, b, lo, n in block_schedule(world * S, S, world, rank, pn.block_counts):
+    for s, b, lo, n in block_schedule(world * S, S, world, rank, pn.block_counts, pn.block_part_mass()):
         assert bsync.block() == b
 
         def train(blk, lo=lo, n=n):
@@ -321,9 +331,41 @@ def run_step(pn, sync, k, world, rank, S, n_launch, n_ex, total, K, seed, mode, 
         sync.begin()      # folds the previous exchange in; this one overlaps the next step
 
 
+def launch_ranks(args):
+    """`--gpus N` (N > 1) outside a launcher: run this script under
+    torch.distributed.run with N local ranks as a CHILD process (never exec:
+    nothing in this process has touched the GPU, and must not), its output
+    passed through, its exit status returned."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    print("[bench] --gpus %d: %s" % (args.gpus, " ".join(cmd)), file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
+
+
+def world_from_env(args):
+    """The launcher's WORLD_SIZE, which must agree with --gpus: None when
+    this process must start the ranks itself (--gpus N > 1, no launcher)."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None:
+        return None if args.gpus > 1 else 1
+    if int(ws) != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%s (the launcher's rank count); they must agree"
+                         % (args.gpus, ws))
+    return int(ws)
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    world = world_from_env(args)
+    if world is None:
+        sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # live PMC traffic (N=1): child runs under rocprofv3, before this process
@@ -480,10 +522,12 @@ def main():
         upd_ms = sum(a.elapsed_time(b) for a, b in cell_events)
         launches = len(cell_events)
     if dist:
+        assert dist.get_world_size() == world
         t = torch.tensor([el], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     skipped = pn.skipped()
+    ran_mode = pn.last_mode()       # the scatter the timed launches ran (smore_last_mode)
     setup["peak_rss_gb"] = round(peak_rss_gb(), 2)
     setups = [setup]
     if dist:
@@ -528,7 +572,7 @@ def main():
             "metric": "M edge-updates/sec (d=64, neg=5)",
             "value": round(updates / el / 1e6, 3),
             "unit": "M edge-updates/s",
-            "n_gpus": world,
+            "n_gpus": dist.get_world_size() if dist else 1,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(el * 1e3 / args.steps, 3),
@@ -540,7 +584,8 @@ def main():
             "config": {"workload": "LINE order-2 sampled negative-sampling SGD, config %s%s"
                                    % (args.config, "" if args.semantics == "cpp" else ", Go rules (pkg/pronet)"),
                        "vertices": V, "edge_slots": E, "dim": args.dim, "negative": K,
-                       "samples_per_step_per_gpu": S, "scatter": args.mode,
+                       "samples_per_step_per_gpu": S,
+                       "scatter": {"hogwild": "plain"}.get(ran_mode, ran_mode), "scatter_asked": args.mode,
                        "sync": (("blocks: 2-D block schedule, rank r owns W part r, C in %d blocks rotated to "
                                  "rank r-1 (send/recv) after each of %d sub-rounds per step, nothing all-reduced; "
                                  "W parts and C blocks gathered at the end" % (2 * world, 2 * world)) if blocks else

@@ -204,6 +204,10 @@ int smore_hot_row_ids(smore_ctx* ctx, int model, int K, int which, int64_t n, in
 int smore_skipped(smore_ctx* ctx, uint64_t* skipped);
 /* milliseconds of the last training launch (HIP events on the launch stream) */
 float smore_last_kernel_ms(const smore_ctx* ctx);
+/* the scatter the last training call actually ran (SMORE_HOGWILD / _ATOMIC /
+ * _SERIAL / _HYBRID; -1 before any): a call asked for SMORE_HYBRID may run
+ * another (C++ BPR above the small-graph cap runs the plain-store kernel) */
+int smore_last_mode(const smore_ctx* ctx);
 /* measurement (SURVEY.md 8d "the measured copy bandwidth on the box"): the
  * best (read + written bytes) / time of `reps` float4 device-to-device copies of
  * `bytes` over a few cache policies and grid sizes, in GB/s.  Allocates and
@@ -586,6 +590,10 @@ int smore_block_bounds(const smore_ctx* ctx, int64_t* wb, int64_t* cb);
  * `samples` split over the blocks by it (largest remainder; nb counts) */
 int smore_block_mass(const smore_ctx* ctx, double* mass);
 int smore_block_counts(const smore_ctx* ctx, uint64_t samples, uint64_t* counts);
+/* LINE-2: every part's share of the global source law (nparts doubles, sum 1):
+ * a round's samples are split over the replicas by it (largest remainder), so
+ * an epoch draws SourceSample's law even when the parts' masses differ */
+int smore_block_part_mass(const smore_ctx* ctx, double* mass);
 /* LINE-2: samples [begin, begin + count) (Philox units; LINE's learning rate
  * from the global index as smore_train_edges) drawn from cell (part, block) and
  * trained, asynchronously on the context stream */

@@ -79,6 +79,7 @@ def _load():
         "smore_hot_row_ids": (i32, [P, i32, i32, i32, i64, P]),
         "smore_group_set_hot_exchange": (i32, [P, i64, i32]),
         "smore_last_kernel_ms": (C.c_float, [P]),
+        "smore_last_mode": (i32, [P]),
         "smore_copy_bandwidth": (i32, [P, u64, i32, C.POINTER(C.c_double)]),
         "smore_last_phase_ms": (i32, [P, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(i32)]),
         "smore_delta_begin": (i32, [P, P, P, P, P, i64]),
@@ -153,6 +154,7 @@ def _load():
         "smore_block_info": (i32, [P, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
         "smore_block_bounds": (i32, [P, P, P]),
         "smore_block_mass": (i32, [P, P]),
+        "smore_block_part_mass": (i32, [P, P]),
         "smore_block_counts": (i32, [P, u64, P]),
         "smore_block_train_edges_async": (i32, [P, i32, u64, u64, u64, i32, dbl, u64, i32]),
         "smore_block_sample_edges": (i32, [P, i32, u64, u64, u64, i32, P]),

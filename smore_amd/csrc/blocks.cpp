@@ -181,6 +181,21 @@ int grow_events(smore_ctx* c, std::vector<hipEvent_t>& v, size_t n) {
 }  // namespace
 
 namespace smore_host {
+// largest remainder of n * mass[k] (ties to the lower index)
+void largest_remainder(uint64_t n, const double* mass, int parts, uint64_t* counts) {
+    std::vector<std::pair<double, int>> rem;
+    uint64_t used = 0;
+    for (int k = 0; k < parts; ++k) {
+        const double x = (double)n * mass[k];
+        counts[k] = (uint64_t)std::floor(x);
+        used += counts[k];
+        rem.push_back({x - std::floor(x), k});
+    }
+    std::stable_sort(rem.begin(), rem.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+    for (size_t i = 0; used < n && i < rem.size(); ++i, ++used) counts[rem[i].second]++;
+    for (int k = 0; used < n; k = (k + 1) % parts, ++used) counts[k]++;   // rounding slack (never in practice)
+}
+
 void blocks_release(smore_ctx* c) {
     auto& B = c->blk;
     dfree(B.d_atoms);
@@ -234,6 +249,18 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
     part_bounds(pn, nb, B.cb);
     for (int p = 0; p < nparts; ++p)
         if (B.wb[p + 1] <= B.wb[p]) return fail(c, SMORE_EINVAL, "block schedule: an empty W part");
+    // each part's share of the source law: a round's samples are split over
+    // the replicas by it (part_bounds only makes the parts roughly equal; a
+    // hub above 1/N of the mass puts a part far off)
+    {
+        B.part_mass.assign((size_t)nparts, 0.0);
+        double tot = 0.0;
+        for (int p = 0; p < nparts; ++p) {
+            for (int64_t v = B.wb[p]; v < B.wb[p + 1]; ++v) B.part_mass[p] += ps[v];
+            tot += B.part_mass[p];
+        }
+        for (double& m : B.part_mass) m = tot > 0 ? m / tot : 1.0 / nparts;
+    }
     for (int k = 0; k < nb; ++k)
         if (B.cb[k + 1] <= B.cb[k]) return fail(c, SMORE_EINVAL, "block schedule: an empty C block");
     // Hot tags (hybrid scatter) and the write-combined sets.  LINE-2: exact
@@ -477,23 +504,17 @@ int smore_block_mass(const smore_ctx* c, double* mass) {
     return SMORE_OK;
 }
 
+int smore_block_part_mass(const smore_ctx* c, double* mass) {
+    if (!c || !mass) return SMORE_EINVAL;
+    if (!c->blk.nb || c->blk.model != SMORE_LINE2) return SMORE_ESTATE;
+    std::copy(c->blk.part_mass.begin(), c->blk.part_mass.end(), mass);
+    return SMORE_OK;
+}
+
 int smore_block_counts(const smore_ctx* c, uint64_t samples, uint64_t* counts) {
     if (!c || !counts) return SMORE_EINVAL;
     if (!c->blk.nb || c->blk.model != SMORE_LINE2) return SMORE_ESTATE;
-    // largest remainder of samples * mass (ties to the lower block)
-    const auto& m = c->blk.mass;
-    const int nb = c->blk.nb;
-    std::vector<std::pair<double, int>> rem;
-    uint64_t used = 0;
-    for (int k = 0; k < nb; ++k) {
-        const double x = (double)samples * m[k];
-        counts[k] = (uint64_t)std::floor(x);
-        used += counts[k];
-        rem.push_back({x - std::floor(x), k});
-    }
-    std::stable_sort(rem.begin(), rem.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
-    for (size_t i = 0; used < samples && i < rem.size(); ++i, ++used) counts[rem[i].second]++;
-    for (int k = 0; used < samples; k = (k + 1) % nb, ++used) counts[k]++;   // rounding slack (never in practice)
+    largest_remainder(samples, c->blk.mass.data(), c->blk.nb, counts);
     return SMORE_OK;
 }
 
@@ -547,6 +568,7 @@ int smore_block_train_edges_async(smore_ctx* c, int block, uint64_t begin, uint6
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
+    c->last_mode = mode;
     c->phase_n = nch;
     return SMORE_OK;
 }

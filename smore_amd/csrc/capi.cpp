@@ -968,6 +968,7 @@ int smore_train_edges_async(smore_ctx* c, int model, uint64_t begin, uint64_t co
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
+    c->last_mode = mode;
     c->phase_n = nch;
     return SMORE_OK;
 }
@@ -1144,6 +1145,8 @@ int smore_copy_bandwidth(smore_ctx* c, uint64_t bytes, int reps, double* gbs) {
     *gbs = best;
     return SMORE_OK;
 }
+
+int smore_last_mode(const smore_ctx* c) { return c ? c->last_mode : -1; }
 
 float smore_last_kernel_ms(const smore_ctx* c) {
     if (!c || !c->timed) return -1.0f;
@@ -1502,6 +1505,7 @@ static int train_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t wal
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
+    c->last_mode = mode;
     c->phase_n = 0;
     return SMORE_OK;
 }
@@ -1687,6 +1691,7 @@ int smore_train_app_async(smore_ctx* c, uint64_t unit_begin, uint64_t unit_end, 
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
+    c->last_mode = mode;
     c->phase_n = 0;
     return SMORE_OK;
 }
@@ -1765,6 +1770,7 @@ int smore_train_hpe_async(smore_ctx* c, uint64_t begin, uint64_t count, uint64_t
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
+    c->last_mode = mode;
     c->phase_n = 0;
     return SMORE_OK;
 }
@@ -1889,6 +1895,7 @@ static int train_pairs_core(smore_ctx* c, const int32_t* v, const int32_t* cc, i
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->timed = true;
+    c->last_mode = mode;
     c->phase_n = 0;
     return SMORE_OK;
 }

@@ -53,13 +53,18 @@ inline double comm_timeout_default() {
 // Wait until ready() returns 1 (0: not yet, < 0: the stream failed).  Between
 // polls: every communicator in comms[0 .. n) is asked for its asynchronous
 // error.  Returns 0, or -1 with `why` set after aborting every communicator.
+// ncclCommAbort frees a communicator, so an aborted handle is set to null
+// here: the caller's teardown (comm_release) must not destroy it again.
 template <class Ready>
-int comm_watch(const Rccl* L, ncclComm_t const* comms, int n, Ready&& ready, double timeout_s, std::string& why) {
+int comm_watch(const Rccl* L, ncclComm_t* comms, int n, Ready&& ready, double timeout_s, std::string& why) {
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     auto abort_all = [&] {
         for (int i = 0; L && L->abort && i < n; ++i)
-            if (comms[i]) (void)L->abort(comms[i]);
+            if (comms[i]) {
+                (void)L->abort(comms[i]);
+                comms[i] = nullptr;
+            }
     };
     for (long poll = 0;; ++poll) {
         const int r = ready();
@@ -90,6 +95,14 @@ int comm_watch(const Rccl* L, ncclComm_t const* comms, int n, Ready&& ready, dou
         }
         if (poll < 200) std::this_thread::yield();
         else std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+}
+
+// teardown: destroy the communicators still held (an aborted one is null)
+inline void comm_release(const Rccl* L, ncclComm_t* comms, int n) {
+    for (int i = 0; i < n; ++i) {
+        if (comms[i] && L && L->destroy) (void)L->destroy(comms[i]);
+        comms[i] = nullptr;
     }
 }
 

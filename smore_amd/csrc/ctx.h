@@ -54,6 +54,7 @@ struct smore_ctx {
     // timing
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
+    int last_mode = -1;                 // scatter (SMORE_* mode) the last timed training call ran
     int cus = 0;
     int64_t last_loaded = 0;
     // edge-list loader: binary cache directory ("" = off) and the last load's figures
@@ -119,6 +120,7 @@ struct smore_ctx {
     size_t ex_n = 0;                    // floats per exchanged table
     int ex_tables = 0;
     bool ex_pending = false;            // an all-reduce is in flight
+    bool coll_queued = false;           // own communicator: collectives queued since the last watched sync
     int ex_mode = 0;                    // SMORE_SYNC_* of the in-flight exchange
     int ex_t0 = 0;                      // first exchanged table (1: W partitioned by source, C only)
     // adaptive exchange: per-row scales of the summed deltas per table and
@@ -171,6 +173,7 @@ struct smore_ctx {
         int model = -1, K = 0, mode = -1;
         std::vector<int64_t> wb, cb;    // W part bounds (n + 1), C block bounds (nb + 1)
         std::vector<double> mass;       // LINE-2: this part's sample mass per C block (sums to 1)
+        std::vector<double> part_mass;  // every part's share of the global source law (n, sums to 1)
         std::vector<uint64_t> atom_off; // LINE-2: first atom of each block (nb + 1)
         uint4* d_atoms = nullptr;       // LINE-2: 2 uint4 per atom {thr, v, c, 0}, {v', c', 0, 0}
         uint2* d_ntab = nullptr;        // V entries: block b's negative alias at [cb[b], cb[b+1])
@@ -199,6 +202,8 @@ namespace smore_host {
 
 // blocks.cpp: frees the block tables (a new graph, smore_destroy)
 void blocks_release(smore_ctx* c);
+// blocks.cpp: counts[k] = n * mass[k] by largest remainder (ties to the lower k)
+void largest_remainder(uint64_t n, const double* mass, int parts, uint64_t* counts);
 // exchange.cpp: the stream's completion under the RCCL failure watch (a
 // context with its own communicator; SMORE_OK otherwise)
 int comm_sync(smore_ctx* c);

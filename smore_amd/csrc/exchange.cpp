@@ -169,6 +169,7 @@ int exchange_collective(smore_ctx* c) {
         NCCLCHK(c, "ncclAllReduce",
                 L->all_reduce(c->ex_buf[t][2], c->ex_buf[t][2], c->ex_n, ncclFloat32, ncclSum, (ncclComm_t)c->comm,
                               c->comm_stream));
+    c->coll_queued = true;
     return SMORE_OK;
 }
 
@@ -255,7 +256,8 @@ void smore_exchange_release(smore_ctx* c) {
     for (float*& p : c->ex_scale) dfree(p);
     c->ex_scale_key.clear();
     if (c->comm && c->own_comm) {
-        if (Rccl* L = rccl()) (void)L->destroy((ncclComm_t)c->comm);
+        ncclComm_t cm = (ncclComm_t)c->comm;
+        comm_release(rccl(), &cm, 1);
     }
     c->comm = nullptr;
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
@@ -505,8 +507,12 @@ int group_sync(smore_group* g) {
             }
             return 1;
         };
-        if (comm_watch(rccl(), g->comms.data(), (int)g->comms.size(), ready, comm_timeout(), why))
+        if (comm_watch(rccl(), g->comms.data(), (int)g->comms.size(), ready, comm_timeout(), why)) {
+            // the communicators are aborted (freed): no replica may use its
+            // handle again, and the group's teardown skips them
+            for (smore_ctx* c : g->ctx) c->comm = nullptr;
             return gfail(g, bad < 0 ? 0 : bad, fail(g->ctx[bad < 0 ? 0 : bad], SMORE_EHIP, why));
+        }
     }
     for (size_t r = 0; r < g->ctx.size(); ++r)
         if ((rc = smore_synchronize(g->ctx[r]))) return gfail(g, (int)r, rc);
@@ -657,15 +663,19 @@ int group_block_edges(smore_group* g, uint64_t begin, uint64_t count, uint64_t p
     const uint64_t rounds = (count + round_units - 1) / round_units;
     auto round_lo = [&](uint64_t k) { return (uint64_t)(((unsigned __int128)count * k) / rounds); };
     std::vector<std::vector<uint64_t>> cnt(n, std::vector<uint64_t>((size_t)nb));
-    std::vector<uint64_t> cur(n);
+    std::vector<uint64_t> cur(n), share(n);
+    // a round's samples go to the replicas in proportion to their parts'
+    // source mass, so the union of the parts draws SourceSample's law
+    const std::vector<double>& pm = g->ctx[0]->blk.part_mass;
     uint64_t S = 0;
     for (uint64_t k = 0; k < rounds; ++k) {
         const uint64_t lo = round_lo(k), m = round_lo(k + 1) - lo;
+        largest_remainder(m, pm.data(), (int)n, share.data());
+        uint64_t b = lo;
         for (size_t r = 0; r < n; ++r) {
-            const uint64_t b = lo + (uint64_t)(((unsigned __int128)m * r) / n);
-            const uint64_t e = lo + (uint64_t)(((unsigned __int128)m * (r + 1)) / n);
-            if ((rc = smore_block_counts(g->ctx[r], e - b, cnt[r].data()))) return gfail(g, (int)r, rc);
+            if ((rc = smore_block_counts(g->ctx[r], share[r], cnt[r].data()))) return gfail(g, (int)r, rc);
             cur[r] = b;
+            b += share[r];
         }
         for (int s = 0; s < nb; ++s, ++S) {
             for (size_t r = 0; r < n; ++r) {
@@ -878,16 +888,23 @@ static std::string census_key(const char* model, std::initializer_list<double> a
 
 namespace smore_host {
 // smore_synchronize of a context with its own communicator (one process per
-// GPU): the stream's completion under the failure watch
+// GPU): the stream's completion under the failure watch -- only when a
+// collective was queued since the last watched sync (a long training call
+// with no collective in flight is not a stuck peer)
 int comm_sync(smore_ctx* c) {
-    if (!c->comm || !c->own_comm) return SMORE_OK;
+    if (!c->comm || !c->own_comm || !c->coll_queued) return SMORE_OK;
     ncclComm_t cm = (ncclComm_t)c->comm;
     std::string why;
     auto ready = [&]() -> int {
         const hipError_t e = hipStreamQuery(c->stream);
         return e == hipSuccess ? 1 : e == hipErrorNotReady ? 0 : -1;
     };
-    if (comm_watch(rccl(), &cm, 1, ready, comm_timeout(), why)) return fail(c, SMORE_EHIP, why);
+    if (comm_watch(rccl(), &cm, 1, ready, comm_timeout(), why)) {
+        c->comm = nullptr;   // aborted (freed): smore_exchange_release must not destroy it
+        c->own_comm = false;
+        return fail(c, SMORE_EHIP, why);
+    }
+    c->coll_queued = false;
     return SMORE_OK;
 }
 }  // namespace smore_host
@@ -1024,9 +1041,7 @@ void smore_group_destroy(smore_group* g) {
         smore_exchange_release(c);
         smore_destroy(c);
     }
-    if (Rccl* L = g->comms.empty() ? nullptr : rccl())
-        for (ncclComm_t cm : g->comms)
-            if (cm) (void)L->destroy(cm);
+    if (!g->comms.empty()) comm_release(rccl(), g->comms.data(), (int)g->comms.size());
     for (hipEvent_t e : g->lev)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : g->bdone)

@@ -196,20 +196,27 @@ class ProNet:
                                            int(walk_steps), int(window), int(K), float(alpha0), int(seed),
                                            ptr(order), _lib.MODE[mode]), "train_deepwalk")
 
+    def _ids(self, ids, what):
+        """Vertex ids as contiguous int32, range-checked against MAX_vid BEFORE
+        the narrowing: an id of 2^31 or more (e.g. 2^32 + 5) must not wrap to a
+        valid small one and reach the C side's own range check as a legal row."""
+        a = np.asarray(ids)
+        if a.size:
+            if not (np.issubdtype(a.dtype, np.integer) or a.dtype == np.bool_):
+                raise TypeError("%s: vertex ids must be integers, got %s" % (what, a.dtype))
+            if int(a.min()) < 0 or int(a.max()) >= self.MAX_vid:
+                raise _lib.SmoreError("%s: vertex id out of range [0, %d)" % (what, self.MAX_vid))
+        return np.ascontiguousarray(a, np.int32)
+
     def train_pairs(self, v, c, K, alpha, seed, unit=0, mode="hogwild"):
         """UpdatePairs (src/proNet.cpp:2741-2753; Go pkg/pronet/optimizer.go:8-18)
         over caller-supplied pairs (v[i], c[i]) in order, fixed alpha; pair i's
         negatives from stream 3, unit `unit` + i // 2^20 (smore_train_pairs).
         Ids are range-checked before they are narrowed to int32 (an id of 2^31
         or more must not wrap to a valid small one; the reference panics)."""
-        v, c = np.asarray(v), np.asarray(c)
+        v, c = self._ids(v, "train_pairs"), self._ids(c, "train_pairs")
         if v.shape != c.shape:
             raise ValueError("v and c must have the same length")
-        for a in (v, c):
-            if a.size and (a.min() < 0 or a.max() >= self.MAX_vid):
-                raise _lib.SmoreError("train_pairs: vertex id out of range [0, %d)" % self.MAX_vid)
-        v = np.ascontiguousarray(v, np.int32)
-        c = np.ascontiguousarray(c, np.int32)
         self._chk(lib.smore_train_pairs(self.ctx, ptr(v), ptr(c), len(v), int(K), float(alpha), int(seed), int(unit),
                                         _lib.MODE[mode]), "train_pairs")
 
@@ -244,6 +251,13 @@ class ProNet:
         _, cb = self.block_bounds()
         m = np.zeros(len(cb) - 1, np.float64)
         self._chk(lib.smore_block_mass(self.ctx, ptr(m)), "block_mass")
+        return m
+
+    def block_part_mass(self):
+        """LINE-2: every part's share of the global source law (sums to 1)."""
+        wb, _ = self.block_bounds()
+        m = np.zeros(len(wb) - 1, np.float64)
+        self._chk(lib.smore_block_part_mass(self.ctx, ptr(m)), "block_part_mass")
         return m
 
     def block_counts(self, samples):
@@ -290,8 +304,7 @@ class ProNet:
     def pairs_rows(self, v, c, K, seed, unit=0):
         """(W row ids, C row ids) a train_pairs batch touches: its vertices, and
         its contexts plus the K negatives it will draw (smore_pairs_rows)."""
-        v = np.ascontiguousarray(v, np.int32)
-        c = np.ascontiguousarray(c, np.int32)
+        v, c = self._ids(v, "pairs_rows"), self._ids(c, "pairs_rows")
         w_ids = np.zeros(max(1, len(v)), np.int32)
         c_ids = np.zeros(max(1, len(v) * (int(K) + 1)), np.int32)
         nw, nc = C.c_int64(), C.c_int64()
@@ -300,12 +313,12 @@ class ProNet:
         return w_ids[:nw.value].copy(), c_ids[:nc.value].copy()
 
     def set_rows(self, which, ids, rows):
-        ids = np.ascontiguousarray(ids, np.int32)
+        ids = self._ids(ids, "set_rows")
         rows = np.ascontiguousarray(rows, np.float32)
         self._chk(lib.smore_set_rows(self.ctx, int(which), ptr(ids), len(ids), ptr(rows)), "set_rows")
 
     def get_rows(self, which, ids):
-        ids = np.ascontiguousarray(ids, np.int32)
+        ids = self._ids(ids, "get_rows")
         out = np.zeros((len(ids), self.dim), np.float32)
         self._chk(lib.smore_get_rows(self.ctx, int(which), ptr(ids), len(ids), ptr(out)), "get_rows")
         return out
@@ -313,10 +326,8 @@ class ProNet:
     def train_pairs_rows(self, v, c, K, alpha, seed, unit, mode, w_ids, w_rows, c_ids, c_rows):
         """smore_train_pairs_rows: the touched rows up, the pairs, the rows back
         (w_rows / c_rows float32 [n][dim], updated in place)."""
-        v = np.ascontiguousarray(v, np.int32)
-        c = np.ascontiguousarray(c, np.int32)
-        w_ids = np.ascontiguousarray(w_ids, np.int32)
-        c_ids = np.ascontiguousarray(c_ids, np.int32)
+        v, c = self._ids(v, "train_pairs_rows"), self._ids(c, "train_pairs_rows")
+        w_ids, c_ids = self._ids(w_ids, "train_pairs_rows"), self._ids(c_ids, "train_pairs_rows")
         assert w_rows.dtype == np.float32 and w_rows.flags.c_contiguous and c_rows.dtype == np.float32
         assert c_rows.flags.c_contiguous
         self._chk(lib.smore_train_pairs_rows(self.ctx, ptr(v), ptr(c), len(v), int(K), float(alpha), int(seed),
@@ -466,6 +477,13 @@ class ProNet:
 
     def last_kernel_ms(self):
         return float(lib.smore_last_kernel_ms(self.ctx))
+
+    def last_mode(self):
+        """The scatter the last training call ran ("hybrid", "hogwild" = plain
+        stores, ...; None before any): C++ BPR asked for "hybrid" above the
+        small-graph cap runs the plain-store kernel."""
+        m = int(lib.smore_last_mode(self.ctx))
+        return {v: k for k, v in _lib.MODE.items()}.get(m)
 
     def delta_begin(self, T, S, D, R, n):
         """Replica exchange pass D = T - S; R = D; S = T (device pointers, n floats)."""

@@ -120,3 +120,14 @@ class BlockSpec:
                 ni = lo + ((int(w[4 + 2 * q]) * n) >> 32)
                 out[t, 2 + q] = ni if int(w[5 + 2 * q]) < int(self.nthr[ni]) else int(self.nal[ni]) & 0x3FFFFFFF
         return out
+
+
+def part_masses(path, nparts, undirected=1):
+    """Every part's share of the source law (smore_block_part_mass) and the W
+    part bounds, for the graph in `path`."""
+    g = orc.Graph.from_file(path, undirected)
+    ps = alias_law(g.vprob, g.valias, 1.0 / g.V)
+    wb = part_bounds(ps, nparts)
+    m = [sum(ps[wb[p]:wb[p + 1]]) for p in range(nparts)]
+    tot = sum(m)
+    return [x / tot for x in m], wb

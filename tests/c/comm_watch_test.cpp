@@ -12,7 +12,8 @@
 
 using smore_host::Rccl;
 
-static int g_polls = 0, g_aborts = 0;
+static int g_polls = 0, g_aborts = 0, g_destroys = 0, g_bad_destroys = 0;
+static ncclComm_t g_aborted[2];
 static ncclResult_t g_async = ncclSuccess;
 static int g_async_after = 1 << 30;
 
@@ -20,8 +21,14 @@ static ncclResult_t fake_async(ncclComm_t, ncclResult_t* r) {
     *r = g_polls >= g_async_after ? g_async : ncclSuccess;
     return ncclSuccess;
 }
-static ncclResult_t fake_abort(ncclComm_t) {
-    ++g_aborts;
+static ncclResult_t fake_abort(ncclComm_t c) {
+    g_aborted[g_aborts++ % 2] = c;
+    return ncclSuccess;
+}
+static ncclResult_t fake_destroy(ncclComm_t c) {
+    ++g_destroys;
+    for (int i = 0; i < g_aborts && i < 2; ++i)
+        if (g_aborted[i] == c) ++g_bad_destroys;   // a use after free in the real library
     return ncclSuccess;
 }
 static const char* fake_string(ncclResult_t r) { return r == ncclRemoteError ? "remote process exited" : "fake"; }
@@ -31,6 +38,7 @@ int main(int argc, char** argv) {
     Rccl L;
     L.async_error = fake_async;
     L.abort = fake_abort;
+    L.destroy = fake_destroy;
     L.error_string = fake_string;
     ncclComm_t comms[2] = {reinterpret_cast<ncclComm_t>(0x10), reinterpret_cast<ncclComm_t>(0x20)};
     const char* s = argv[1];
@@ -46,6 +54,11 @@ int main(int argc, char** argv) {
         return g_polls >= ready_after ? 1 : 0;
     };
     const int rc = smore_host::comm_watch(&L, comms, 2, ready, 0.2, why);
-    printf("%s %d %d %s\n", s, rc, g_aborts, why.c_str());
+    smore_host::comm_release(&L, comms, 2);
+    if (g_bad_destroys) {
+        printf("%s destroyed-after-abort %d\n", s, g_bad_destroys);
+        return 1;
+    }
+    printf("%s %d %d %d %s\n", s, rc, g_aborts, g_destroys, why.c_str());
     return 0;
 }

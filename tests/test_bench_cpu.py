@@ -54,3 +54,40 @@ def test_samples_to_loss_interpolation(tmp_path):
     assert got[30]["n_ranks_log2_total"] == 31.0
     assert abs(got[29]["time_eff"] - 100 / 110) < 1e-3
     assert abs(got[29]["effective_speedup"] - 4 * 0.5 * 100 / 110) < 0.01
+
+
+def test_gpus_flag_must_match_launcher_world(monkeypatch):
+    """--gpus N under a launcher whose WORLD_SIZE differs exits non-zero
+    before anything touches the GPU."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "1"], env=env,
+                       capture_output=True, text=True, timeout=60)
+    assert p.returncode != 0 and "--gpus 1 but WORLD_SIZE=2" in p.stderr
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8"], env=env,
+                       capture_output=True, text=True, timeout=60)
+    assert p.returncode != 0 and "--gpus 8 but WORLD_SIZE=2" in p.stderr
+
+
+def test_gpus_flag_without_launcher_starts_ranks(monkeypatch):
+    """--gpus N > 1 with no WORLD_SIZE: bench.py must start N ranks itself
+    (world_from_env -> None) and pass its own arguments to them."""
+    import types
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    assert bench.world_from_env(types.SimpleNamespace(gpus=1)) == 1
+    assert bench.world_from_env(types.SimpleNamespace(gpus=4)) is None
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    assert bench.world_from_env(types.SimpleNamespace(gpus=4)) == 4
+    seen = {}
+
+    def fake_run(cmd, env=None):
+        seen["cmd"], seen["env"] = cmd, env
+        return types.SimpleNamespace(returncode=3)
+    monkeypatch.setattr(bench.subprocess, "run", fake_run)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "2"])
+    assert bench.launch_ranks(types.SimpleNamespace(gpus=4)) == 3
+    cmd = seen["cmd"]
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
+    assert cmd[cmd.index("--nproc-per-node") + 1] == "4" and cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "2"] and cmd[-5].endswith("bench.py")
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"

@@ -101,18 +101,49 @@ def test_group_block_split():
     exactly, in sub-round order, with consecutive sample ranges."""
     from bench import block_schedule, largest_remainder
     mass = [[0.1, 0.2, 0.3, 0.15, 0.25, 0.0], [0.5, 0.1, 0.1, 0.1, 0.1, 0.1], [1 / 6] * 6]
-    for count, per in ((10_000, 1000), (9_999, 5000), (7, 100)):
+    for (count, per), pm in zip(((10_000, 1000), (9_999, 5000), (7, 100), (10_000, 1000)),
+                                (None, None, None, [0.6, 0.3, 0.1])):
         seen = []
+        per_rank = [0, 0, 0]
         for r, m in enumerate(mass):
-            subs = list(block_schedule(count, per, 3, r, lambda x, m=m: largest_remainder(x, m)))
+            subs = list(block_schedule(count, per, 3, r, lambda x, m=m: largest_remainder(x, m), pm))
             assert [s for s, _, _, _ in subs] == list(range(len(subs))) and len(subs) % 6 == 0
             for s, b, lo, n in subs:
                 assert b == (2 * r + s) % 6
                 if n:
                     seen.append((lo, n))
+                    per_rank[r] += n
+        if pm is not None:      # a skewed partition: replicas get their parts' share of every round
+            assert per_rank == [6000, 3000, 1000]
         seen.sort()
         pos = 0
         for lo, n in seen:
             assert lo == pos
             pos += n
         assert pos == count
+
+
+def test_part_mass_split_on_a_skewed_graph(tmp_path):
+    """smore_block_part_mass on a graph whose one hub holds far more than 1/N
+    of the source mass: the part holding it has that share, the group's round
+    split (largest remainder over the part masses) gives it that
+    share of every round's samples, and the union of the parts' laws is the
+    global source law (needs no GPU: the host side of smore_block_setup is
+    restated by tests/block_spec.py)."""
+    import numpy as np
+    from tests.block_spec import part_masses
+    from bench import largest_remainder
+    # a directed star of heavy edges out of vertex 0 (source mass ~ weighted
+    # out-degree^0.75: ~99 %), plus a ring of light edges among the leaves
+    n = 400
+    lines = ["v0 v%d 1000" % i for i in range(1, n)] + ["v%d v%d 1" % (i, 1 + i % (n - 1)) for i in range(1, n)]
+    f = tmp_path / "star.txt"
+    f.write_text("\n".join(lines) + "\n")
+    for world in (2, 4, 8):
+        pm, wb = part_masses(str(f), world, undirected=0)
+        assert abs(sum(pm) - 1.0) < 1e-12
+        assert max(pm) > 1.5 / world            # the hub's part is far off 1/N
+        share = largest_remainder(1 << 20, pm)
+        assert sum(share) == 1 << 20
+        for r in range(world):
+            assert abs(share[r] - pm[r] * (1 << 20)) <= 1

@@ -205,3 +205,28 @@ def test_walk_owner_arguments():
             pn.set_walk_owner(lo, hi)
     with pytest.raises(_lib.SmoreError):
         pn.walk_parts(4)                      # no census yet
+
+
+@pytest.mark.parametrize("call", ["train_pairs", "pairs_rows", "get_rows", "set_rows", "train_pairs_rows"])
+@pytest.mark.parametrize("bad", [2 ** 32 + 5, 2 ** 31, -1, 1 << 40])
+def test_ids_checked_before_narrowing(call, bad):
+    """Every binding that narrows vertex ids to int32 range-checks them first
+    (ADVICE r5): 2^32 + 5 must not become row 5 and pass the C side's check."""
+    from smore_amd import ProNet
+    from smore_amd import _lib
+    pn = ProNet(device=-1)
+    pn.LoadEdgeList(os.path.join(GOLDEN, "toy.txt"), 1)
+    ids = np.array([0, bad], np.int64)
+    ok = np.array([0, 1], np.int64)
+    rows = np.zeros((2, 4), np.float32)
+    with pytest.raises(_lib.SmoreError, match="out of range"):
+        if call == "train_pairs":
+            pn.train_pairs(ids, ok, 5, 0.025, 1)
+        elif call == "pairs_rows":
+            pn.pairs_rows(ok, ids, 5, 1)
+        elif call == "get_rows":
+            pn.get_rows(1, ids)
+        elif call == "set_rows":
+            pn.set_rows(0, ids, rows)
+        else:
+            pn.train_pairs_rows(ok, ok, 5, 0.025, 1, 0, "hogwild", ids, rows, ok, rows)

@@ -1,9 +1,11 @@
 """RCCL failure detection (smore_amd/csrc/comm_watch.h) with a
 fake RCCL table, on the CPU: an asynchronous communicator error, a stuck
 peer (deadline) and a failed stream each end the wait with a failure and
-abort every communicator once; a completing wait (also through RCCL's
-ncclInProgress state) aborts nothing.  The library's group_sync and
-smore_synchronize (own communicator) wait through this function."""
+abort every communicator once, and the teardown that follows destroys none
+of the aborted (freed) handles; a completing wait (also through RCCL's
+ncclInProgress state) aborts nothing and the teardown destroys every one.
+The library's group_sync and smore_synchronize (own communicator) wait
+through this function."""
 import os
 import subprocess
 
@@ -23,8 +25,10 @@ def prog(tmp_path_factory):
 
 
 def _run(prog, scenario):
-    out = subprocess.run([prog, scenario], check=True, capture_output=True, text=True, timeout=30).stdout.split(" ", 3)
-    return int(out[1]), int(out[2]), out[3].strip()
+    out = subprocess.run([prog, scenario], check=True, capture_output=True, text=True, timeout=30).stdout.split(" ", 4)
+    rc, aborts, destroys = int(out[1]), int(out[2]), int(out[3])
+    assert destroys == 2 - aborts   # no aborted communicator is destroyed again
+    return rc, aborts, out[4].strip()
 
 
 def test_async_error_aborts(prog):

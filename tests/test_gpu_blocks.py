@@ -20,7 +20,8 @@ import numpy as np
 import pytest
 
 from oracle import oracle as orc
-from tests.block_spec import BlockSpec
+from bench import largest_remainder
+from tests.block_spec import BlockSpec, part_masses
 from tests.conftest import GOLDEN
 
 pytestmark = pytest.mark.gpu
@@ -70,6 +71,25 @@ def test_block_draws_match_spec(smore, graph, n):
     pn.close()
 
 
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_block_part_mass_skewed_graph(smore, tmp_path, n):
+    """smore_block_part_mass against the spec on a graph whose hub holds ~99 %
+    of the source mass: a group's round split gives each replica
+    its part's share, so the union of the parts draws SourceSample's law."""
+    lines = ["v0 v%d 1000" % i for i in range(1, 400)] + ["v%d v%d 1" % (i, 1 + i % 399) for i in range(1, 400)]
+    f = tmp_path / "star.txt"
+    f.write_text("\n".join(lines) + "\n")
+    want, wb = part_masses(str(f), n, undirected=0)
+    pn = smore.ProNet(0)
+    pn.LoadEdgeList(str(f), 0)
+    pn.alloc_tables(8, 2)
+    pn.block_setup("line2", n, n - 1, 5, "atomic")
+    assert list(pn.block_bounds()[0]) == wb
+    np.testing.assert_allclose(pn.block_part_mass(), want, rtol=1e-12, atol=1e-15)
+    assert max(want) > 1.5 / n
+    pn.close()
+
+
 def test_block_counts_largest_remainder(smore):
     pn = _ctx(smore)
     pn.block_setup("line2", 4, 1, 5, "atomic")
@@ -101,7 +121,8 @@ def test_block_cell_serial_equals_oracle(smore, graph):
 
 
 def _schedule_edges(smore, graph, n, begin, count, per, total, K, dim, W0, C0):
-    """exchange.cpp group_block_edges restated: rounds of per * n samples,
+    """exchange.cpp group_block_edges restated: rounds of per * n samples
+    split over the replicas by their parts' source mass (largest remainder),
     replica r's slice split over the blocks by its mass, sub-round s trains
     cell (r, (2r + s) mod 2n), then C block (2r + s) mod 2n moves to replica
     r - 1; at the end W part p comes from replica p, C block b from b // 2."""
@@ -120,8 +141,9 @@ def _schedule_edges(smore, graph, n, begin, count, per, total, K, dim, W0, C0):
     for k in range(rounds):
         lo, hi = count * k // rounds, count * (k + 1) // rounds
         m = hi - lo
-        cur = [lo + m * r // n for r in range(n)]
-        cnt = [ctxs[r].block_counts(lo + m * (r + 1) // n - cur[r]) for r in range(n)]
+        share = largest_remainder(m, ctxs[0].block_part_mass())
+        cur = [lo + sum(share[:r]) for r in range(n)]
+        cnt = [ctxs[r].block_counts(share[r]) for r in range(n)]
         for s in range(nb):
             for r in range(n):
                 b = (2 * r + s) % nb

@@ -255,10 +255,13 @@ def _bpr_objective(W, draws, dim):
 
 
 def test_c3_full_grid_hybrid_matches_atomic(c3):
-    """C3 BPR's benched scatter (hybrid, the edge-record default tau 1.0) on the
-    full grid, d=128, 2^28 samples, vs the lossless atomic scatter: held-out
-    BPR objective within 1 % and the held-out ranking accuracy within 0.5
-    points (measured in DESIGN.md 8)."""
+    """C3 BPR asked for the hybrid scatter on the full grid (d=128, 2^28
+    samples) vs the lossless atomic scatter.  Above the small-graph cap, C++
+    BPR's "hybrid" runs the PLAIN-STORE kernel (capi.cpp: its ~170 hot rows are
+    hub items drawn as positives; smore_last_mode says "hogwild"), so this
+    pins the plain stores' loss: held-out BPR objective within 1 % and the
+    held-out ranking accuracy within 0.5 points (VERDICT r3 weak 5, r5 weak 6;
+    measured in DESIGN.md 8)."""
     g, pn = c3
     dim, total = 128, 1 << 28
     held = orc.sample_bpr(g, SEED + 1, 0, 100_000)
@@ -267,6 +270,7 @@ def test_c3_full_grid_hybrid_matches_atomic(c3):
         pn.alloc_tables(dim, 1)
         pn.init_table_uniform(0, 7)
         pn.train_edges("bpr", 0, total, total, 5, 0.025, 0.0, SEED, mode)
+        assert pn.last_mode() == {"atomic": "atomic", "hybrid": "hogwild"}[mode]
         W = pn.get_table(0)
         assert np.isfinite(W).all()
         res[mode] = _bpr_objective(W, held, dim)

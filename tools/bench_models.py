@@ -39,6 +39,13 @@ def pairs_per_walk(L, window):
     return tot
 
 
+def ran(pn):
+    """The scatter the last call actually ran (smore_last_mode): "plain" for
+    the plain-store kernel (C++ BPR's hybrid above the small-graph cap)."""
+    m = pn.last_mode()
+    return "plain" if m == "hogwild" else m
+
+
 def run_edges(pn, model, S, steps, K, mode, seed=7):
     """mean ms per call, and the mean (draw, update) phase ms"""
     total = (steps + 1) * S
@@ -125,6 +132,7 @@ def main():
                        window=window, walks_per_call=V, ms_per_call=round(ms, 3), pairs_per_walk=ppw,
                        value=round(V * ppw / ms / 1e3, 1), unit="M pair-updates/s",
                        walks_per_s=round(V / ms * 1e3, 1))
+        out["scatter"] = ran(pn)       # what ran; "mode" is what was asked for
         print(json.dumps(out), flush=True)
         pn.close()
 
