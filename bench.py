@@ -392,7 +392,7 @@ def main():
 
     import smore_amd
     from smore_amd import graphgen
-    from smore_amd.dist import BlockSync, ReplicaSync, table_tensor
+    from smore_amd.dist import BlockSync, ReplicaSync, block_hubs, table_tensor
 
     t_gen = time.perf_counter()
     pn = smore_amd.ProNet(local)
@@ -459,7 +459,11 @@ def main():
         pn.block_setup("line2", world, rank, args.negative, args.mode)
         setup["block_setup_s"] = round(time.perf_counter() - t_bs, 2)
         wb, cb = pn.block_bounds()
-        bsync = BlockSync(table_tensor(pn, 0), table_tensor(pn, 1), wb, cb)
+        # the hub C rows' slots: every cell trains them, exchanged after every
+        # sub-round (S / 2N samples per rank)
+        hubs = block_hubs(pn, args.samples / (2 * world))
+        setup["hubs"] = int(pn.block_hubs()[0])
+        bsync = BlockSync(table_tensor(pn, 0), table_tensor(pn, 1), wb, cb, hubs=hubs)
         if rank == 0:
             print("[bench] block schedule set up in %.1f s" % (time.perf_counter() - t_bs), file=sys.stderr,
                   flush=True)
@@ -587,8 +591,10 @@ def main():
                        "samples_per_step_per_gpu": S,
                        "scatter": {"hogwild": "plain"}.get(ran_mode, ran_mode), "scatter_asked": args.mode,
                        "sync": (("blocks: 2-D block schedule, rank r owns W part r, C in %d blocks rotated to "
-                                 "rank r-1 (send/recv) after each of %d sub-rounds per step, nothing all-reduced; "
-                                 "W parts and C blocks gathered at the end" % (2 * world, 2 * world)) if blocks else
+                                 "rank r-1 (send/recv) after each of %d sub-rounds per step; the %d hub C rows "
+                                 "trained in every cell on per-rank slots, their deltas all-reduced after each "
+                                 "sub-round (adaptive scales); W parts and C blocks gathered at the end"
+                                 % (2 * world, 2 * world, setup.get("hubs", 0))) if blocks else
                                 "%s%s every %s%s%s" % (
                            args.sync, " c0=%g" % c0 if args.sync == "adaptive" else "",
                            "%d steps" % args.sync_every if n_ex == 1 else "1/%d step" % n_ex,

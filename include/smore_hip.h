@@ -594,6 +594,28 @@ int smore_block_counts(const smore_ctx* ctx, uint64_t samples, uint64_t* counts)
  * a round's samples are split over the replicas by it (largest remainder), so
  * an epoch draws SourceSample's law even when the parts' masses differ */
 int smore_block_part_mass(const smore_ctx* ctx, double* mass);
+/* LINE-2: the weight cell (part, block) gives its negative steps (an fp32
+ * value; 1 with SMORE_NEG_LAW=0): NegativeSample's share of the block over the
+ * cell's share of the part's samples -- the epoch's negatives then follow
+ * NegativeSample's law */
+int smore_block_neg_scale(const smore_ctx* ctx, int block, double* weight);
+/* LINE-2 hub C rows: the `hubs` C rows with the most expected
+ * touches per sample are taken out of the rotating blocks; every cell draws
+ * them (contexts and negatives, with 1/nb of their mass) on its part's own
+ * copy in the C table's slot rows V .. V + H - 1, kept equal over the parts by
+ * an exchange after every sub-round.  -1: automatic (4096, at most V / 8nb),
+ * 0: none.  Takes effect at the next smore_block_setup. */
+int smore_block_set_hubs(smore_ctx* ctx, int64_t hubs);
+/* the setup's hubs: count, the first slot row (V), their C rows and expected
+ * touches per sample (each array H entries, or null) */
+int smore_block_hubs(const smore_ctx* ctx, int64_t* hubs, int64_t* first_slot, int32_t* rows, double* rates);
+/* slots <- hub rows (before a run's first cell) / hub rows <- slots (after its
+ * last exchange), on the context stream */
+int smore_block_hubs_load(smore_ctx* ctx);
+int smore_block_hubs_store(smore_ctx* ctx);
+/* the slots' exchange scales for `samples` per part per exchange and c0 (the
+ * adaptive rule of SMORE_SYNC_ADAPTIVE over the nparts parts; H floats) */
+int smore_block_hub_scales(const smore_ctx* ctx, double samples, double c0, float* scales);
 /* LINE-2: samples [begin, begin + count) (Philox units; LINE's learning rate
  * from the global index as smore_train_edges) drawn from cell (part, block) and
  * trained, asynchronously on the context stream */

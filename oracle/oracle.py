@@ -70,7 +70,7 @@ def _declare(L):
     L.orc_train_deepwalk_f64.restype = C.c_int
     L.orc_train_deepwalk_f64.argtypes = [P, P, P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, dbl, u64, P]
     L.orc_train_records_f32.restype = C.c_int
-    L.orc_train_records_f32.argtypes = [C.c_int, P, P, C.c_int, P, i64, C.c_int, dbl, dbl, u64, u64]
+    L.orc_train_records_f32.argtypes = [C.c_int, P, P, C.c_int, P, i64, C.c_int, dbl, dbl, u64, u64, C.c_float]
     L.orc_train_edge_f32.restype = C.c_int
     L.orc_train_edge_f32.argtypes = [P, C.c_int, P, P, C.c_int, C.c_int, C.c_int, dbl, dbl, u64, u64, u64, u64, C.c_int]
     L.orc_train_bpr_f32.restype = C.c_int
@@ -266,12 +266,13 @@ def train_edge_f32(g, model, W, C_, dim, K, alpha0, reg, total, begin, end, seed
                                     begin, end, seed, threads)
 
 
-def train_records_f32(model, W, C_, rec, K, alpha0, reg, total, begin):
+def train_records_f32(model, W, C_, rec, K, alpha0, reg, total, begin, neg_scale=1.0):
     """The fp32 update over explicit records {v, c, n_1..n_K} in order
-    (orc_train_records_f32); record i has the rate of sample begin + i."""
+    (orc_train_records_f32); record i has the rate of sample begin + i; the
+    negatives step with alpha * neg_scale (a block cell's weight, fp32)."""
     rec = np.ascontiguousarray(rec, np.int32)
     return lib().orc_train_records_f32(MODEL[model], ptr(W), ptr(C_), W.shape[1], ptr(rec), len(rec), K, alpha0, reg,
-                                       total, begin)
+                                       total, begin, float(neg_scale))
 
 
 def train_bpr_f64(g, W, alpha0, total, begin, end, seed):

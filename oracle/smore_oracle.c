@@ -653,8 +653,17 @@ static float dot_spec(const float* a, const float* b, int dpad) {
  * Rows are updated in place, so a repeated id (negative == positive, or
  * v == c in a shared table) sees the earlier update exactly as the
  * reference's in-place vector<double> update does. */
+static void update_edge_f32_w(int model, float* W, float* C, int dpad, int32_t v, int32_t c,
+                              const int32_t* negs, int K, float alpha, float reg, float* e, float nsc);
 static void update_edge_f32(int model, float* W, float* C, int dpad, int32_t v, int32_t c,
                             const int32_t* negs, int K, float alpha, float reg, float* e) {
+    update_edge_f32_w(model, W, C, dpad, v, c, negs, K, alpha, reg, e, 1.0f);
+}
+
+/* nsc: the negatives' step weight of a block-schedule cell (blocks.cpp
+ * cell_args): negative j steps with alpha * nsc (== alpha when nsc == 1) */
+static void update_edge_f32_w(int model, float* W, float* C, int dpad, int32_t v, int32_t c,
+                              const int32_t* negs, int K, float alpha, float reg, float* e, float nsc) {
     float* wv = W + (int64_t)v * dpad;
     float* T = (model == 0) ? C : W;
     for (int d = 0; d < dpad; ++d) e[d] = 0.0f;
@@ -674,7 +683,7 @@ static void update_edge_f32(int model, float* W, float* C, int dpad, int32_t v, 
             }
         } else {
             float label = j < 0 ? 1.0f : 0.0f;
-            float gg = (label - fast_sigmoid_f32(f)) * alpha;
+            float gg = (label - fast_sigmoid_f32(f)) * (j < 0 ? alpha : alpha * nsc);
             for (int d = 0; d < dpad; ++d) {
                 float ce = cr[d], we = wv[d];
                 e[d] = fmaf(gg, ce, e[d]);
@@ -739,7 +748,7 @@ int orc_train_edge_f32(const orc_graph* g, int model, float* W, float* C, int di
  * begin + i.  The records of the block schedule's cells (smore_block_sample_edges)
  * are checked through it. */
 int orc_train_records_f32(int model, float* W, float* C, int dpad, const int32_t* rec, int64_t count, int K,
-                          double alpha0, double reg, uint64_t total, uint64_t begin) {
+                          double alpha0, double reg, uint64_t total, uint64_t begin, float neg_scale) {
     sig_init();
     uint64_t base = (model == 2) ? 0 : 1;
     float* e = (float*)malloc(sizeof(float) * dpad);
@@ -751,7 +760,7 @@ int orc_train_records_f32(int model, float* W, float* C, int dpad, const int32_t
         c &= 0x3FFFFFFF;
         for (int j = 0; j < K; ++j) negs[j] = r[2 + j] & 0x3FFFFFFF;
         float alpha = (float)orc_alpha_line(begin + (uint64_t)i + base, alpha0, total);
-        update_edge_f32(model, W, C, dpad, v, c, negs, K, alpha, (float)reg, e);
+        update_edge_f32_w(model, W, C, dpad, v, c, negs, K, alpha, (float)reg, e, neg_scale);
     }
     free(e);
     return 0;

@@ -15,9 +15,12 @@
 // BlockSync).  The samples of a cell follow the one-GPU law restricted to the
 // cell (train_blocks.hip); a call's samples are spread over the cells in
 // proportion to their mass, so an epoch (nb sub-rounds) draws the one-GPU
-// law.  What changes is the order (cell by cell) and the negatives (drawn in
-// the context's block: the law restricted to the block; blocks have equal
-// negative mass).
+// law of (source, context).  What changes is the order (cell by cell) and the
+// negatives: drawn in the context's block (the law restricted to the block;
+// blocks have equal negative mass), while a cell's sample count follows the
+// block's CONTEXT mass -- so each cell weights its negative steps by the
+// block's negative share over its sample share (cell_args, neg_law_on), and
+// an epoch's expected negative updates per row are NegativeSample's.
 #include <cmath>
 #include <numeric>
 #include <thread>
@@ -43,7 +46,18 @@ BlockArgs block_args(const smore_ctx* c) {
     b.ntab = c->blk.d_ntab;
     b.nb = c->blk.nb;
     for (int k = 0; k <= c->blk.nb; ++k) b.cb[k] = (int32_t)c->blk.cb[k];
+    b.hub_ntab = c->blk.d_hub_ntab;
+    b.hub_off = c->blk.hub_off;
+    b.nhub = (uint32_t)c->blk.nhub;
+    b.H = (int32_t)c->blk.H;
+    b.V = (int32_t)c->g->V;
     return b;
+}
+
+// a probability as a Philox-word threshold (word < thr with probability p)
+uint32_t prob_thr(double p) {
+    const double t = std::ceil(std::ldexp(p, 32));
+    return !(t > 0) ? 0u : t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
 }
 
 // the resident sample groups of this context's update launches (the hot
@@ -62,10 +76,12 @@ int64_t resident_groups(smore_ctx* c, bool walk, int K, int mode) {
 }
 
 // per-block write-combined rows: the hottest hot C rows of each block under
-// its cell's C-row law (pcb, flags hcb), with the edge rule's staleness bound
-// and a two-tier drain (capi build_hot_maps)
+// its cell's C-row law (pcb, flags hcb; entry i of block k is row cb[k] + i,
+// or hub slot V + i - rows past the block's rows), with the edge rule's
+// staleness bound and a two-tier drain (capi build_hot_maps)
 void block_sh_sets(smore_ctx* c, bool walk, bool on, int64_t Mg, const std::vector<std::vector<double>>& pcb,
                    const std::vector<std::vector<uint8_t>>& hcb, std::vector<int2>& hash, std::vector<int32_t>& ids) {
+    const int64_t V = c->g->V;
     auto& B = c->blk;
     const int cap = on ? std::max(0, std::min(c->sh_max, sh_rows_max(c->dpad))) : 0;
     B.sh_cap = std::max(cap, 1);
@@ -87,11 +103,13 @@ void block_sh_sets(smore_ctx* c, bool walk, bool on, int64_t Mg, const std::vect
         // its own interval), so the hubs stay within the staleness bound
         // without draining every other row as often.
         std::vector<std::pair<double, int32_t>> r;
+        const int64_t rows = B.cb[k + 1] - B.cb[k];
         for (size_t i = 0; i < pcb[k].size(); ++i) {
             if (!hcb[k][i]) continue;
             const double p = pcb[k][i];
             const double f = two_tier ? (double)sh_slot_interval(M * p, flush_cap, walk) : (double)flush_cap;
-            if (M * p * f <= stale) r.push_back({p, (int32_t)(B.cb[k] + (int64_t)i)});
+            const int64_t id = (int64_t)i < rows ? B.cb[k] + (int64_t)i : V + ((int64_t)i - rows);
+            if (M * p * f <= stale) r.push_back({p, (int32_t)id});
         }
         const int64_t n = std::min<int64_t>(cap, (int64_t)r.size());
         std::partial_sort(r.begin(), r.begin() + n, r.end(), [](const auto& x, const auto& y) {
@@ -120,6 +138,30 @@ void block_sh_sets(smore_ctx* c, bool walk, bool on, int64_t Mg, const std::vect
     }
 }
 
+// NegativeSample's law over an epoch (SMORE_NEG_LAW=0: off).  A cell (r, b)
+// draws its K negatives from block b's restricted law, but the cells of part r
+// get its samples in proportion to their CONTEXT mass m(r, b), while
+// NegativeSample (src/proNet.cpp:623-633) would put a share pn(b) (~1/nb:
+// blocks are cut to equal negative mass) of them in block b.  Scaling the
+// cell's negative steps by pn(b) / m(r, b) makes part r's expected negative
+// updates per row exactly the one-GPU ones (tests/test_blocks_cpu.py computes
+// the epoch marginal).  LINE-2 cells take m(r, b) from the atoms' mass; walk
+// cells from the round's record counts, on the device (neg_scale_of).
+bool neg_law_on() {
+    const char* e = getenv("SMORE_NEG_LAW");
+    return !e || atoi(e) != 0;
+}
+
+// hub C rows of a block setup (smore_block_set_hubs / $SMORE_HUBS; -1:
+// automatic), at most the C table's slot rows and half the vertices
+constexpr int64_t HUB_AUTO = 4096;
+int64_t hub_count(const smore_ctx* c, int64_t V, int nb) {
+    int64_t h = c->blk_hubs;
+    if (const char* e = getenv("SMORE_HUBS")) h = atoll(e);
+    if (h < 0) h = std::min<int64_t>(HUB_AUTO, V / (8 * (int64_t)nb));
+    return std::max<int64_t>(0, std::min(std::min(h, c->c_slots), V / 2));
+}
+
 // the update-kernel arguments shared by a context's cell launches
 EdgeArgs cell_args(smore_ctx* c, int k, bool walk) {
     const auto& B = c->blk;
@@ -142,6 +184,15 @@ EdgeArgs cell_args(smore_ctx* c, int k, bool walk) {
     a.sh_flush = std::max(1, B.sh_flush);
     a.sh_flush_w = 0;
     std::copy(B.sh_lvl[k].begin(), B.sh_lvl[k].end(), a.sh_lvl);
+    if (neg_law_on() && (size_t)k < B.nmass.size()) {
+        if (walk) {
+            a.neg_scale = (float)B.nmass[k];
+            a.neg_lo = B.d_off;
+            a.neg_hi = B.d_off + (size_t)B.nb * B.walks;
+        } else if ((size_t)k < B.mass.size() && B.mass[k] > 0) {
+            a.neg_scale = (float)(B.nmass[k] / B.mass[k]);
+        }
+    }
     return a;
 }
 
@@ -181,6 +232,22 @@ int grow_events(smore_ctx* c, std::vector<hipEvent_t>& v, size_t n) {
 }  // namespace
 
 namespace smore_host {
+// the exchange of the hub slots after every sub-round, one late (the rule of
+// replica_sync.hip): slot j's summed delta is scaled by
+// s + (1 - s) / N with s = min(1, c0 / k_j), k_j = its expected updates per
+// exchange over all parts -- the sum for slots updated a few times per
+// sub-round, towards the mean for the hubs that take hundreds of thousands
+// (each part's copy reaches the same local equilibrium; summing N of them
+// would overshoot)
+void hub_scales(const smore_ctx::Blocks& B, double samples, double c0, float* out) {
+    const double N = (double)B.n;
+    for (int64_t j = 0; j < B.H; ++j) {
+        const double k = B.hub_rate[j] * samples * N;
+        const double s = k > 0 ? std::min(1.0, c0 / k) : 1.0;
+        out[j] = (float)(s + (1.0 - s) / N);
+    }
+}
+
 // largest remainder of n * mass[k] (ties to the lower index)
 void largest_remainder(uint64_t n, const double* mass, int parts, uint64_t* counts) {
     std::vector<std::pair<double, int>> rem;
@@ -204,6 +271,10 @@ void blocks_release(smore_ctx* c) {
     dfree(B.d_sh_ids);
     dfree(B.d_count);
     dfree(B.d_off);
+    dfree(B.d_hub_ntab);
+    dfree(B.d_hub_ids);
+    for (float*& p : B.d_hub_ex) dfree(p);
+    dfree(B.d_hub_scale);
     B = smore_ctx::Blocks{};
 }
 }  // namespace smore_host
@@ -231,9 +302,11 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
     const int64_t V = g.V;
     const int nb = 2 * nparts;
     if (V < nb) return fail(c, SMORE_EINVAL, "block schedule: fewer vertices than blocks");
-    char key[256];
-    snprintf(key, sizeof key, "%d/%d/%d/%d/%d/%lld/%lld/%d/%d/%d/%.9g/%s", model, nparts, part, K, mode, (long long)V,
-             (long long)g.E, c->dpad, c->sh_max, c->sh_flush, c->hot_tau, getenv("SMORE_SH_STALE") ? getenv("SMORE_SH_STALE") : "");
+    const int64_t H = walk ? 0 : hub_count(c, V, nb);
+    char key[288];
+    snprintf(key, sizeof key, "%d/%d/%d/%d/%d/%lld/%lld/%d/%d/%d/%.9g/%lld/%s", model, nparts, part, K, mode,
+             (long long)V, (long long)g.E, c->dpad, c->sh_max, c->sh_flush, c->hot_tau, (long long)H,
+             getenv("SMORE_SH_STALE") ? getenv("SMORE_SH_STALE") : "");
     if (c->blk.key == key) return SMORE_OK;
     blocks_release(c);
     auto& B = c->blk;
@@ -245,10 +318,52 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
     B.mode = mode;
     std::vector<double> ps, pn, pc;
     draw_probabilities(g, ps, pn, pc);
+    // hub C rows: the H rows with the most expected touches per sample (as
+    // a positive context plus K times as a negative); slot j is row V + j
+    std::vector<int32_t> hub_of;
+    double pnH = 0.0;
+    if (H > 0) {
+        std::vector<int32_t> idx((size_t)V);
+        std::iota(idx.begin(), idx.end(), 0);
+        auto q = [&](int32_t x) { return pc[x] + (double)K * pn[x]; };
+        std::partial_sort(idx.begin(), idx.begin() + H, idx.end(), [&](int32_t a, int32_t b) {
+            return q(a) > q(b) || (q(a) == q(b) && a < b);
+        });
+        hub_of.assign((size_t)V, -1);
+        B.hubs.assign(idx.begin(), idx.begin() + H);
+        B.hub_rate.resize((size_t)H);
+        for (int64_t j = 0; j < H; ++j) {
+            hub_of[B.hubs[j]] = (int32_t)j;
+            B.hub_rate[j] = q(B.hubs[j]);
+            pnH += pn[B.hubs[j]];
+        }
+        B.H = H;
+    }
     part_bounds(ps, nparts, B.wb);
-    part_bounds(pn, nb, B.cb);
+    {   // C blocks of equal NON-hub negative mass (the hubs are in every block)
+        std::vector<double> pcut = pn;
+        for (int32_t x : B.hubs) pcut[x] = 0.0;
+        part_bounds(pcut, nb, B.cb);
+    }
     for (int p = 0; p < nparts; ++p)
         if (B.wb[p + 1] <= B.wb[p]) return fail(c, SMORE_EINVAL, "block schedule: an empty W part");
+    for (int k = 0; k < nb; ++k)
+        if (B.cb[k + 1] <= B.cb[k]) return fail(c, SMORE_EINVAL, "block schedule: an empty C block");
+    auto is_hub = [&](int64_t x) { return H > 0 && hub_of[x] >= 0; };
+    // NegativeSample's share of each block: its non-hub rows, plus 1/nb of
+    // every hub's (cell_args' negative weight)
+    std::vector<double> nraw((size_t)nb, 0.0);
+    {
+        B.nmass.assign((size_t)nb, 0.0);
+        double tot = 0.0;
+        for (int k = 0; k < nb; ++k) {
+            for (int64_t x = B.cb[k]; x < B.cb[k + 1]; ++x)
+                if (!is_hub(x)) nraw[k] += pn[x];
+            nraw[k] += pnH / nb;
+            tot += nraw[k];
+        }
+        for (int k = 0; k < nb; ++k) B.nmass[k] = tot > 0 ? nraw[k] / tot : 1.0 / nb;
+    }
     // each part's share of the source law: a round's samples are split over
     // the replicas by it (part_bounds only makes the parts roughly equal; a
     // hub above 1/N of the mass puts a part far off)
@@ -261,8 +376,6 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
         }
         for (double& m : B.part_mass) m = tot > 0 ? m / tot : 1.0 / nparts;
     }
-    for (int k = 0; k < nb; ++k)
-        if (B.cb[k + 1] <= B.cb[k]) return fail(c, SMORE_EINVAL, "block schedule: an empty C block");
     // Hot tags (hybrid scatter) and the write-combined sets.  LINE-2: exact
     // per cell from its atoms -- W row v: its atoms' share of the cell's mass;
     // C row x: its atoms' share plus K times its share of the block's negative
@@ -290,16 +403,23 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
         for (auto& x : th) x.join();
     };
     // LINE-2 atoms of this part: the TargetSample outcomes of its sources,
-    // bucketed by the context's block
+    // bucketed by the context's block -- bucket nb: the hub contexts (as
+    // slot ids), shared by every block's cell
+    const int NBK = nb + (H > 0 ? 1 : 0);
     B.mass.assign((size_t)nb, 0.0);
-    B.atom_off.assign((size_t)nb + 1, 0);
+    B.hub_p.assign((size_t)nb, 0.0);
+    B.atom_off.assign((size_t)NBK + 1, 0);
     std::vector<int32_t> av, ac;
     std::vector<double> aw;
+    std::vector<double> hubw;   // LINE-2: per hub slot, the part's atom mass of that context
+    double mH = 0.0;
     const int64_t wlo = B.wb[part], whi = B.wb[part + 1];
     if (!walk) {
-        auto blk_of = [&](int64_t x) {
+        auto bucket_of = [&](int64_t x) {
+            if (is_hub(x)) return nb;
             return (int)(std::upper_bound(B.cb.begin(), B.cb.end(), x) - B.cb.begin()) - 1;
         };
+        auto id_of = [&](int64_t x) { return is_hub(x) ? (int32_t)(V + hub_of[x]) : (int32_t)x; };
         // vertices [vb, ve) of the part, in order
         auto each_atom = [&](int64_t vb, int64_t ve, auto&& f) {
             for (int64_t v = vb; v < ve; ++v) {
@@ -314,7 +434,7 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
             }
         };
         // two passes over vertex slices on every host thread (count per
-        // (slice, block), then fill); the slices' order keeps each block's
+        // (slice, bucket), then fill); the slices' order keeps each bucket's
         // atoms in vertex order, as one pass would
         const int TS = (int)std::max(1u, std::min(std::thread::hardware_concurrency(), 64u));
         std::vector<int64_t> vs((size_t)TS + 1);
@@ -332,48 +452,58 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
             for (int t = 0; t < TS; ++t) th.emplace_back([&, t] { f(t); });
             for (auto& x : th) x.join();
         };
-        std::vector<uint64_t> cnt((size_t)TS * nb, 0);
+        std::vector<uint64_t> cnt((size_t)TS * NBK, 0);
         par_slices([&](int t) {
-            uint64_t* ct = cnt.data() + (size_t)t * nb;
+            uint64_t* ct = cnt.data() + (size_t)t * NBK;
             each_atom(vs[t], vs[t + 1], [&](int64_t, int64_t x, double w) {
-                if (w > 0) ct[blk_of(x)]++;
+                if (w > 0) ct[bucket_of(x)]++;
             });
         });
-        std::vector<uint64_t> start((size_t)TS * nb);
-        for (int k = 0; k < nb; ++k) {
+        std::vector<uint64_t> start((size_t)TS * NBK);
+        for (int k = 0; k < NBK; ++k) {
             uint64_t acc = B.atom_off[k];
             for (int t = 0; t < TS; ++t) {
-                start[(size_t)t * nb + k] = acc;
-                acc += cnt[(size_t)t * nb + k];
+                start[(size_t)t * NBK + k] = acc;
+                acc += cnt[(size_t)t * NBK + k];
             }
             B.atom_off[k + 1] = acc;
         }
-        const uint64_t A = B.atom_off[nb];
+        const uint64_t A = B.atom_off[NBK];
         if (A == 0) return fail(c, SMORE_EINVAL, "block schedule: a part without edges");
         av.resize(A);
         ac.resize(A);
         aw.resize(A);
         par_slices([&](int t) {
-            uint64_t* pos = start.data() + (size_t)t * nb;
+            uint64_t* pos = start.data() + (size_t)t * NBK;
             each_atom(vs[t], vs[t + 1], [&](int64_t v, int64_t x, double w) {
                 if (w <= 0) return;
-                const uint64_t p = pos[blk_of(x)]++;
+                const uint64_t p = pos[bucket_of(x)]++;
                 av[p] = (int32_t)v;
-                ac[p] = (int32_t)x;
+                ac[p] = id_of(x);
                 aw[p] = w;
             });
         });
+        std::vector<double> m((size_t)NBK, 0.0);
+        for (int k = 0; k < NBK; ++k)
+            for (uint64_t p = B.atom_off[k]; p < B.atom_off[k + 1]; ++p) m[k] += aw[p];
+        if (H > 0) {
+            mH = m[nb];
+            B.hub_off = B.atom_off[nb];
+            B.nhub = B.atom_off[nb + 1] - B.atom_off[nb];
+            hubw.assign((size_t)H, 0.0);
+            for (uint64_t p = B.hub_off; p < B.hub_off + B.nhub; ++p) hubw[ac[p] - V] += aw[p];
+        }
+        // a cell's mass: its block's atoms plus 1/nb of the part's hub atoms
         double tot = 0.0;
         for (int k = 0; k < nb; ++k) {
-            double m = 0.0;
-            for (uint64_t p = B.atom_off[k]; p < B.atom_off[k + 1]; ++p) m += aw[p];
-            B.mass[k] = m;
-            tot += m;
+            B.mass[k] = m[k] + mH / nb;
+            B.hub_p[k] = B.mass[k] > 0 ? (mH / nb) / B.mass[k] : 0.0;
+            tot += B.mass[k];
         }
-        for (double& m : B.mass) m /= tot;
+        for (double& x : B.mass) x /= tot;
     }
-    // per block: the C-row law of its cell (over [cb[k], cb[k+1])) and the
-    // flags of its C rows and (LINE-2) of this part's W rows
+    // per block: the C-row law of its cell (over [cb[k], cb[k+1]) then the H
+    // hub slots) and the flags of its C rows and (LINE-2) of this part's W rows
     std::vector<std::vector<double>> pcb((size_t)nb);
     std::vector<std::vector<uint8_t>> hcb((size_t)nb), hwb((size_t)nb);
     // the hottest row of each cell (its launch's concurrency cap, cell_grid):
@@ -386,8 +516,8 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
         par_blocks([&](int k) {
             const int64_t lo = B.cb[k], n = B.cb[k + 1] - lo;
             auto& pcx = pcb[k];
-            pcx.assign((size_t)n, 0.0);
-            hcb[k].assign((size_t)n, 0);
+            pcx.assign((size_t)(n + H), 0.0);
+            hcb[k].assign((size_t)(n + H), 0);
             if (walk) {   // capi build_hot_maps' scaled law (hot_pc)
                 double mx = 0.0;
                 for (int64_t i = 0; i < n; ++i) {
@@ -400,21 +530,25 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
                 return;
             }
             std::vector<double> pw((size_t)(whi - wlo), 0.0);
-            double m = 0.0, pnb = 0.0;
+            double mraw = 0.0;   // the cell's raw atom mass (its block's, plus 1/nb of the hub atoms')
             for (uint64_t p = B.atom_off[k]; p < B.atom_off[k + 1]; ++p) {
                 pw[av[p] - wlo] += aw[p];
                 pcx[ac[p] - lo] += aw[p];
-                m += aw[p];
+                mraw += aw[p];
             }
-            for (int64_t i = 0; i < n; ++i) pnb += pn[lo + i];
+            for (uint64_t p = B.hub_off; p < B.hub_off + B.nhub; ++p) pw[av[p] - wlo] += aw[p] / nb;
+            for (int64_t j = 0; j < H; ++j) pcx[n + j] = hubw[j] / nb;
+            mraw += mH / nb;
             hwb[k].assign(pw.size(), 0);
             double mw = 0.0, mc = 0.0;
             for (size_t i = 0; i < pw.size(); ++i) {
-                hwb[k][i] = m > 0 && (double)M * pw[i] / m > tau;
-                if (m > 0) mw = std::max(mw, pw[i] / m);
+                hwb[k][i] = mraw > 0 && (double)M * pw[i] / mraw > tau;
+                if (mraw > 0) mw = std::max(mw, pw[i] / mraw);
             }
-            for (int64_t i = 0; i < n; ++i) {
-                pcx[i] = (m > 0 ? pcx[i] / m : 0.0) + (pnb > 0 ? K * pn[lo + i] / pnb : 0.0);
+            const double pnb = nraw[k];
+            for (int64_t i = 0; i < n + H; ++i) {
+                const double pneg = i < n ? (is_hub(lo + i) ? 0.0 : pn[lo + i]) : pn[B.hubs[i - n]] / nb;
+                pcx[i] = (mraw > 0 ? pcx[i] / mraw : 0.0) + (pnb > 0 ? K * pneg / pnb : 0.0);
                 hcb[k][i] = (double)M * pcx[i] > tau;
                 mc = std::max(mc, pcx[i]);
             }
@@ -422,49 +556,83 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
             B.pmax_c[k] = mc;
         });
     }
-    auto hc = [&](int k, int64_t x) -> uint32_t { return hyb ? hcb[k][x - B.cb[k]] : 0u; };
+    // one tag per hub slot and per W row of the shared hub atoms (a row's
+    // tag must not depend on the cell that draws it): hot in any cell
+    std::vector<uint8_t> hubhot((size_t)H, 0), hwh;
+    if (H > 0 && hyb) {
+        hwh.assign((size_t)(whi - wlo), 0);
+        for (int k = 0; k < nb; ++k) {
+            const int64_t n = B.cb[k + 1] - B.cb[k];
+            for (int64_t j = 0; j < H; ++j) hubhot[j] |= hcb[k][n + j];
+            for (size_t i = 0; i < hwh.size(); ++i) hwh[i] |= hwb[k][i];
+        }
+        for (int k = 0; k < nb; ++k) {
+            const int64_t n = B.cb[k + 1] - B.cb[k];
+            for (int64_t j = 0; j < H; ++j) hcb[k][n + j] = hubhot[j];
+        }
+    }
+    auto hc = [&](int k, int64_t x) -> uint32_t {
+        if (!hyb) return 0u;
+        if (x >= V) return hubhot[x - V];
+        return hcb[k][x - B.cb[k]];
+    };
     auto hw = [&](int k, int64_t v) -> uint32_t { return hyb && !walk ? hwb[k][v - wlo] : 0u; };
-    // negative tables: block k's law restricted to [cb[k], cb[k+1]) (Go alias
-    // rule, power 1: any exact encoding of the law), ids absolute
+    // negative tables: block k's law over its non-hub rows and 1/nb of every
+    // hub's (Go alias rule, power 1: any exact encoding of the law), ids
+    // absolute (hub slots V + j); entries of the rows in place, of the slots
+    // at [k * H, (k + 1) * H)
     {
         hvec<AliasEntry> nt((size_t)V);
+        std::vector<AliasEntry> hnt((size_t)nb * (size_t)H);
         par_blocks([&](int k) {
-            const int64_t lo = B.cb[k], n = B.cb[k + 1] - lo;
-            std::vector<double> prob((size_t)n);
-            std::vector<int64_t> alias((size_t)n);
-            std::vector<int32_t> self((size_t)n);
-            alias_go(pn.data() + lo, n, 1.0, prob.data(), alias.data());
-            for (int64_t i = 0; i < n; ++i) {
-                alias[i] += lo;
-                self[i] = (int32_t)(lo + i);
+            const int64_t lo = B.cb[k], n = B.cb[k + 1] - lo, nn = n + H;
+            std::vector<double> wt((size_t)nn), prob((size_t)nn);
+            std::vector<int64_t> alias((size_t)nn);
+            std::vector<int32_t> self((size_t)nn);
+            auto id = [&](int64_t i) { return (int32_t)(i < n ? lo + i : V + (i - n)); };
+            for (int64_t i = 0; i < nn; ++i) {
+                wt[i] = i < n ? (is_hub(lo + i) ? 0.0 : pn[lo + i]) : pn[B.hubs[i - n]] / nb;
+                self[i] = id(i);
             }
-            alias_encode(prob.data(), alias.data(), n, self.data(), nt.data() + lo);
-            for (int64_t i = 0; i < n; ++i) {
-                const uint32_t al = (uint32_t)nt[lo + i].alias;
-                nt[lo + i].alias = (int32_t)(al | (hc(k, al) << 30) | (hc(k, lo + i) << 31));
+            alias_go(wt.data(), nn, 1.0, prob.data(), alias.data());
+            for (int64_t i = 0; i < nn; ++i) alias[i] = id(alias[i]);
+            std::vector<AliasEntry> e((size_t)nn);
+            alias_encode(prob.data(), alias.data(), nn, self.data(), e.data());
+            for (int64_t i = 0; i < nn; ++i) {
+                const uint32_t al = (uint32_t)e[i].alias;
+                e[i].alias = (int32_t)(al | (hc(k, al) << 30) | (hc(k, self[i]) << 31));
+                if (i < n) nt[lo + i] = e[i];
+                else hnt[(size_t)k * H + (i - n)] = e[i];
             }
         });
         if ((rc = upload(c, B.d_ntab, reinterpret_cast<const uint2*>(nt.data()), (size_t)V, true))) return rc;
+        if (H > 0) {
+            if ((rc = upload(c, B.d_hub_ntab, reinterpret_cast<const uint2*>(hnt.data()), hnt.size()))) return rc;
+            if ((rc = upload(c, B.d_hub_ids, B.hubs.data(), B.hubs.size()))) return rc;
+        }
     }
-    // LINE-2: one alias table per block over its atoms, tagged per cell
+    // LINE-2: one alias table per block over its atoms and one over the part's
+    // hub atoms, tagged per cell (the hub atoms with their any-cell tags)
     if (!walk) {
-        hvec<uint4> at((size_t)B.atom_off[nb] * 2);
-        par_blocks([&](int k) {
-            const uint64_t a0 = B.atom_off[k], n = B.atom_off[k + 1] - a0;
+        hvec<uint4> at((size_t)B.atom_off[NBK] * 2);
+        auto table = [&](int k, uint64_t a0, uint64_t n, bool hubs) {
             if (n == 0) return;
             std::vector<double> prob(n);
             std::vector<int64_t> alias(n);
             std::vector<AliasEntry> e(n);
             alias_go(aw.data() + a0, (int64_t)n, 1.0, prob.data(), alias.data());
             alias_encode(prob.data(), alias.data(), (int64_t)n, nullptr, e.data());
+            auto tw = [&](int32_t v) -> uint32_t { return hubs ? (hyb ? hwh[v - wlo] : 0u) : hw(k, v); };
             for (uint64_t i = 0; i < n; ++i) {
                 const uint64_t s = a0 + i, a = a0 + (uint64_t)e[i].alias;
-                at[2 * s] = make_uint4(e[i].thresh, (uint32_t)av[s] | (hw(k, av[s]) << 30),
+                at[2 * s] = make_uint4(e[i].thresh, (uint32_t)av[s] | (tw(av[s]) << 30),
                                        (uint32_t)ac[s] | (hc(k, ac[s]) << 30), 0u);
-                at[2 * s + 1] = make_uint4((uint32_t)av[a] | (hw(k, av[a]) << 30),
+                at[2 * s + 1] = make_uint4((uint32_t)av[a] | (tw(av[a]) << 30),
                                            (uint32_t)ac[a] | (hc(k, ac[a]) << 30), 0u, 0u);
             }
-        });
+        };
+        par_blocks([&](int k) { table(k, B.atom_off[k], B.atom_off[k + 1] - B.atom_off[k], false); });
+        if (H > 0) table(0, B.hub_off, B.nhub, true);
         if ((rc = upload(c, B.d_atoms, at.data(), at.size(), true))) return rc;
     }
     c->hot_M = M;
@@ -473,11 +641,59 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
     block_sh_sets(c, walk, hyb && !small, M, pcb, hcb, hash, ids);
     if (getenv("SMORE_SH_DEBUG"))
         for (int k = 0; k < nb; ++k)
-            fprintf(stderr, "[cell] part %d/%d block %d M %lld M*pmax_w %.4g M*pmax_c %.4g\n", part, nparts, k,
-                    (long long)M, M * B.pmax_w[k], M * B.pmax_c[k]);
+            fprintf(stderr, "[cell] part %d/%d block %d M %lld M*pmax_w %.4g M*pmax_c %.4g hubs %lld hub_p %.4g\n", part,
+                    nparts, k, (long long)M, M * B.pmax_w[k], M * B.pmax_c[k], (long long)H, B.hub_p[k]);
     if ((rc = upload(c, B.d_sh_hash, hash.data(), hash.size()))) return rc;
     if ((rc = upload(c, B.d_sh_ids, ids.data(), ids.size()))) return rc;
     B.key = key;
+    return SMORE_OK;
+}
+
+int smore_block_set_hubs(smore_ctx* c, int64_t hubs) {
+    if (!c || hubs < -1) return SMORE_EINVAL;
+    c->blk_hubs = hubs;
+    return SMORE_OK;
+}
+
+int smore_block_hubs(const smore_ctx* c, int64_t* H, int64_t* first_slot, int32_t* rows, double* rates) {
+    if (!c) return SMORE_EINVAL;
+    if (!c->blk.nb) return SMORE_ESTATE;
+    const auto& B = c->blk;
+    if (H) *H = B.H;
+    if (first_slot) *first_slot = c->g->V;
+    if (rows) std::copy(B.hubs.begin(), B.hubs.end(), rows);
+    if (rates) std::copy(B.hub_rate.begin(), B.hub_rate.end(), rates);
+    return SMORE_OK;
+}
+
+int smore_block_hubs_load(smore_ctx* c) {
+    int rc;
+    if ((rc = check_ctx(c))) return rc;
+    if (!c->blk.nb) return fail(c, SMORE_ESTATE, "no block setup");
+    if (!c->blk.H) return SMORE_OK;
+    if ((rc = set_device(c))) return rc;
+    float* C = c->d_table[1];
+    HIPCHK(c, launch_rows_gather(C, c->blk.d_hub_ids, (uint64_t)c->blk.H, c->dpad, C + (size_t)c->g->V * c->dpad,
+                                 c->stream));
+    return SMORE_OK;
+}
+
+int smore_block_hubs_store(smore_ctx* c) {
+    int rc;
+    if ((rc = check_ctx(c))) return rc;
+    if (!c->blk.nb) return fail(c, SMORE_ESTATE, "no block setup");
+    if (!c->blk.H) return SMORE_OK;
+    if ((rc = set_device(c))) return rc;
+    float* C = c->d_table[1];
+    HIPCHK(c, launch_rows_scatter(C, c->blk.d_hub_ids, (uint64_t)c->blk.H, c->dpad, C + (size_t)c->g->V * c->dpad,
+                                  c->stream));
+    return SMORE_OK;
+}
+
+int smore_block_hub_scales(const smore_ctx* c, double samples, double c0, float* scales) {
+    if (!c || !scales || !(samples > 0.0) || !(c0 > 0.0)) return SMORE_EINVAL;
+    if (!c->blk.nb) return SMORE_ESTATE;
+    hub_scales(c->blk, samples, c0, scales);
     return SMORE_OK;
 }
 
@@ -511,6 +727,15 @@ int smore_block_part_mass(const smore_ctx* c, double* mass) {
     return SMORE_OK;
 }
 
+int smore_block_neg_scale(const smore_ctx* c, int block, double* w) {
+    if (!c || !w) return SMORE_EINVAL;
+    if (!c->blk.nb || c->blk.model != SMORE_LINE2) return SMORE_ESTATE;
+    if (block < 0 || block >= c->blk.nb) return SMORE_EINVAL;
+    const EdgeArgs a = cell_args(const_cast<smore_ctx*>(c), block, false);
+    *w = a.neg_scale > 0.0f ? (double)a.neg_scale : 1.0;
+    return SMORE_OK;
+}
+
 int smore_block_counts(const smore_ctx* c, uint64_t samples, uint64_t* counts) {
     if (!c || !counts) return SMORE_EINVAL;
     if (!c->blk.nb || c->blk.model != SMORE_LINE2) return SMORE_ESTATE;
@@ -530,7 +755,7 @@ int smore_block_train_edges_async(smore_ctx* c, int block, uint64_t begin, uint6
     if (count == 0) return SMORE_OK;
     if ((rc = set_device(c))) return rc;
     const uint64_t na = B.atom_off[block + 1] - B.atom_off[block];
-    if (na == 0) return fail(c, SMORE_EINVAL, "block without atoms (mass 0) asked for samples");
+    if (na == 0 && B.nhub == 0) return fail(c, SMORE_EINVAL, "block without atoms (mass 0) asked for samples");
     EdgeArgs a = cell_args(c, block, false);
     a.total = total;
     a.seed = seed;
@@ -540,6 +765,7 @@ int smore_block_train_edges_async(smore_ctx* c, int block, uint64_t begin, uint6
     BlockArgs ba = block_args(c);
     ba.atom_off = B.atom_off[block];
     ba.natoms = (uint32_t)na;
+    ba.hub_thr = B.nhub ? prob_thr(B.hub_p[block]) : 0u;
     const int RW = rec_width(kmax_of(K));
     const uint64_t chunk_max = mode == SMORE_SERIAL ? ((uint64_t)1 << 30) / (uint64_t)RW : (uint64_t)1 << 27;
     const uint64_t chunk = std::min<uint64_t>(count, chunk_max);
@@ -586,7 +812,8 @@ int smore_block_sample_edges(smore_ctx* c, int block, uint64_t seed, uint64_t be
     BlockArgs ba = block_args(c);
     ba.atom_off = B.atom_off[block];
     ba.natoms = (uint32_t)(B.atom_off[block + 1] - B.atom_off[block]);
-    if (ba.natoms == 0) return fail(c, SMORE_EINVAL, "block without atoms");
+    ba.hub_thr = B.nhub ? prob_thr(B.hub_p[block]) : 0u;
+    if (ba.natoms == 0 && B.nhub == 0) return fail(c, SMORE_EINVAL, "block without atoms");
     const int RW = rec_width(kmax_of(K));
     int32_t* d = nullptr;
     HIPCHK(c, hipMalloc((void**)&d, count * RW * sizeof(int32_t)));

@@ -265,6 +265,10 @@ int smore_alloc_tables(smore_ctx* c, int dim, int ntables) {
     c->dpad = (dim + 3) / 4 * 4;
     c->ntables = ntables;
     size_t bytes = (size_t)c->g->V * c->dpad * sizeof(float);
+    // the C table of a two-table model carries HUB_SLOTS_MAX rows after V: the
+    // block schedule's hub slots (blocks.cpp), never part of a rotating block
+    c->c_slots = ntables == 2 ? std::min<int64_t>(HUB_SLOTS_MAX, c->g->V) : 0;
+    const size_t cbytes = bytes + (size_t)c->c_slots * c->dpad * sizeof(float);
     // The embedding tables live in UNCACHED device memory: every row access is
     // served memory-side (Infinity Cache / HBM), which is coherent across the
     // 8 XCDs.  In the default coarse-grained memory each XCD's L2 keeps its own
@@ -281,8 +285,10 @@ int smore_alloc_tables(smore_ctx* c, int dim, int ntables) {
         else if (!strcmp(e, "finegrained")) flags = hipDeviceMallocFinegrained;
         else if (!strcmp(e, "contiguous")) flags = hipDeviceMallocContiguous;
     }
-    for (int t = 0; t < ntables; ++t) HIPCHK(c, hipExtMallocWithFlags((void**)&c->d_table[t], bytes, flags));
-    for (int t = 0; t < ntables; ++t) HIPCHK(c, hipMemset(c->d_table[t], 0, bytes));
+    for (int t = 0; t < ntables; ++t)
+        HIPCHK(c, hipExtMallocWithFlags((void**)&c->d_table[t], t == 1 ? cbytes : bytes, flags));
+    for (int t = 0; t < ntables; ++t) HIPCHK(c, hipMemset(c->d_table[t], 0, t == 1 ? cbytes : bytes));
+    c->blk.key.clear();   // the block tables' hub slots live in the new C table
     return SMORE_OK;
 }
 

@@ -55,6 +55,8 @@ struct smore_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     int last_mode = -1;                 // scatter (SMORE_* mode) the last timed training call ran
+    int64_t blk_hubs = -1;              // hub C rows of the block schedule (smore_block_set_hubs; -1 automatic)
+    int64_t c_slots = 0;                // rows after V in the C table (the block schedule's hub slots)
     int cus = 0;
     int64_t last_loaded = 0;
     // edge-list loader: binary cache directory ("" = off) and the last load's figures
@@ -174,7 +176,24 @@ struct smore_ctx {
         std::vector<int64_t> wb, cb;    // W part bounds (n + 1), C block bounds (nb + 1)
         std::vector<double> mass;       // LINE-2: this part's sample mass per C block (sums to 1)
         std::vector<double> part_mass;  // every part's share of the global source law (n, sums to 1)
-        std::vector<uint64_t> atom_off; // LINE-2: first atom of each block (nb + 1)
+        std::vector<double> nmass;      // NegativeSample's share of each C block (nb, sums to 1)
+        std::vector<uint64_t> atom_off; // LINE-2: first atom of each block (nb + 1; + 1: the hub atoms' end)
+        // hub C rows (smore_block_set_hubs): the H hottest C
+        // rows are taken out of the blocks and trained in every cell on every
+        // part, each part on its own copy in the C table's slot rows V .. V + H
+        // (never inside a rotating block), the copies kept equal by a small
+        // exchange after every sub-round
+        int64_t H = 0;
+        std::vector<int32_t> hubs;      // hub j's C row
+        std::vector<double> hub_rate;   // hub j's expected C-row touches per sample (context + K negative law)
+        uint64_t hub_off = 0, nhub = 0; // LINE-2: this part's hub atoms, atoms [hub_off, hub_off + nhub)
+        std::vector<double> hub_p;      // LINE-2: per block, a cell sample's probability of being a hub atom
+        uint2* d_hub_ntab = nullptr;    // nb x H: block k's negative alias entries of the hub slots
+        int32_t* d_hub_ids = nullptr;   // H: the hubs' C rows (slot gather / scatter)
+        float* d_hub_ex[3] = {nullptr, nullptr, nullptr};   // group exchange over the slots: S, D, R
+        float* d_hub_scale = nullptr;   // group exchange: per-slot scales (adaptive rule)
+        std::string hub_scale_key;
+        bool hub_pending = false;       // group exchange: an all-reduce of R is in flight
         uint4* d_atoms = nullptr;       // LINE-2: 2 uint4 per atom {thr, v, c, 0}, {v', c', 0, 0}
         uint2* d_ntab = nullptr;        // V entries: block b's negative alias at [cb[b], cb[b+1])
         int2* d_sh_hash = nullptr;      // nb x SH_HASH: per-block write-combined rows
@@ -200,8 +219,13 @@ void smore_exchange_release(smore_ctx* c);
 
 namespace smore_host {
 
+// rows after V in a two-table model's C table: the block schedule's hub slots
+constexpr int64_t HUB_SLOTS_MAX = 65536;
+
 // blocks.cpp: frees the block tables (a new graph, smore_destroy)
 void blocks_release(smore_ctx* c);
+// blocks.cpp: the hub slots' exchange scales for `samples` per part per exchange
+void hub_scales(const smore_ctx::Blocks& B, double samples, double c0, float* out);
 // blocks.cpp: counts[k] = n * mass[k] by largest remainder (ties to the lower k)
 void largest_remainder(uint64_t n, const double* mass, int parts, uint64_t* counts);
 // exchange.cpp: the stream's completion under the RCCL failure watch (a

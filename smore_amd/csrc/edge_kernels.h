@@ -173,12 +173,15 @@ __device__ __forceinline__ void gather_ctx_rows(const EdgeArgs& a, int lane, con
 // REG (two tables only): reg_rt selects Opt_SigmoidRegSGD (src/proNet.cpp:
 // 1332-1351, HPE's UpdateCommunity) instead of Opt_SigmoidSGD at run time:
 // g = label - sig(f); e = fmaf(alpha, g*c - reg*w, e); c = fmaf(alpha, g*w - reg*c, c).
+// nsc: the negatives' step weight (EdgeArgs::neg_scale; 1 everywhere but the
+// block schedule's cells): negative k uses alpha * nsc, which is alpha bit for
+// bit when nsc == 1.
 template <int G, int M, int KMAX, int MODE, int SHARED = -1, bool WOUT = true, bool REG = false>
 __device__ __forceinline__ void sgd_update_rows(const EdgeArgs& a, const float* s_sig, int lane,
                                                 const bool (&ev)[M], int32_t v, const int32_t (&id)[KMAX + 1],
                                                 bool hotw, const bool (&hot)[KMAX + 1], float alpha, bool shared_rt,
                                                 bool mf_rt, const ShState& sh, float (&wv)[M],
-                                                float (&rows)[KMAX + 1][M], bool reg_rt = false) {
+                                                float (&rows)[KMAX + 1][M], bool reg_rt = false, float nsc = 1.0f) {
     constexpr bool DELTA = MODE == MODE_ATOMIC || MODE == MODE_HYBRID;
     const bool shared = SHARED < 0 ? shared_rt : SHARED == 1;
     const bool mf = SHARED == 0 ? false : mf_rt;
@@ -271,7 +274,7 @@ __device__ __forceinline__ void sgd_update_rows(const EdgeArgs& a, const float* 
                     nk[m] = __builtin_fmaf(alpha, t2, ce);
                 }
             } else {
-                const float gg = ((k == 0 ? 1.0f : 0.0f) - fast_sigmoid(f, s_sig)) * alpha;
+                const float gg = ((k == 0 ? 1.0f : 0.0f) - fast_sigmoid(f, s_sig)) * (k == 0 ? alpha : alpha * nsc);
 #pragma unroll
                 for (int m = 0; m < M; ++m) {
                     const float ce = rows[k][m];
@@ -576,6 +579,16 @@ __device__ __forceinline__ void sh_drain_w(const ShState& sh, const int32_t* sh_
     }
 }
 
+// the launch's negative-gradient weight (EdgeArgs::neg_scale / neg_lo / neg_hi)
+__device__ __forceinline__ float neg_scale_of(const EdgeArgs& a, uint64_t count) {
+    if (a.neg_lo && a.neg_hi) {
+        const uint64_t tot = *a.neg_hi - *a.neg_lo;
+        return count > 0 && tot > 0 && a.neg_scale > 0.0f
+                   ? (float)((double)a.neg_scale * (double)tot / (double)count) : 1.0f;
+    }
+    return a.neg_scale > 0.0f ? a.neg_scale : 1.0f;
+}
+
 // ------------------------------------------------------------------ edge kernel
 // LINE-2 (W,C; SHARED 0), LINE-1 / MF (W,W; SHARED 1, Opt_SGD for MF at run
 // time) and BPR (W,W; SHARED 2, UpdateBPRPair); the scatter MODE is
@@ -592,6 +605,7 @@ edge_train_kernel(EdgeArgs a) {
     // records of this launch: [0, count) of a.rec, or a block bucket [*rec_base, *count_dev)
     const uint64_t rb = a.rec_base ? *a.rec_base : 0;
     const uint64_t count = (a.count_dev ? *a.count_dev : a.count) - rb;
+    const float nsc = neg_scale_of(a, count);
     const int32_t* const recs = a.rec + rb * (uint64_t)rec_width(KMAX);
     const uint64_t gpb = blockDim.x / G;                 // groups per block
     uint64_t r0 = (uint64_t)blockIdx.x * gpb;            // block-uniform round base
@@ -621,7 +635,7 @@ edge_train_kernel(EdgeArgs a) {
             if constexpr (KMAX == 5) bpr_update_rows<G, M, KMAX, MODE>(a, s_sig, lane, ev, v, id, hotw, hot, alpha, wv, rows, sh);
         } else {
             sgd_update_rows<G, M, KMAX, MODE, SHARED, true, true>(a, s_sig, lane, ev, v, id, hotw, hot, alpha, shared,
-                                                                  mf, sh, wv, rows, reg);
+                                                                  mf, sh, wv, rows, reg, nsc);
         }
     };
     // the update of one sample, ids tagged as drawn (c < 0: source without out-edges)
@@ -792,7 +806,7 @@ edge_train_kernel(EdgeArgs a) {
                         xa.hots(hot);
                         sgd_update_rows<G, M, KMAX, MODE, SHARED>(a, s_sig, lane, ev, xa.v(), id,
                                                                  scatter_atomic<MODE>(xa.w[0]), hot, xa.alpha, shared,
-                                                                 mf, sh, wva, rowsa);
+                                                                 mf, sh, wva, rowsa, false, nsc);
                     }
                 }
                 xa = xb;
@@ -834,6 +848,7 @@ pair_train_kernel(EdgeArgs a) {
     constexpr int RW = rec_width(KMAX);
     const uint64_t rb = a.rec_base ? *a.rec_base : 0;   // a block bucket: [*rec_base, *count_dev)
     const uint64_t count = (a.count_dev ? *a.count_dev : a.count) - rb;
+    const float nsc = neg_scale_of(a, count);
     const int32_t* const recs = a.rec + rb * (uint64_t)RW;
     const uint64_t gpb = blockDim.x / G, gib = threadIdx.x / G;
     bool ev[M];
@@ -906,7 +921,7 @@ pair_train_kernel(EdgeArgs a) {
             gather_ctx_rows<G, M, KMAX>(a, lane, ev, id, rows);
             // word 0 bit 31: HPE community record (Opt_SigmoidRegSGD)
             sgd_update_rows<G, M, KMAX, MODE, 0, false, true>(a, s_sig, lane, ev, v, id, false, hot, alpha, false,
-                                                              false, sh, wv, rows, tv < 0);
+                                                              false, sh, wv, rows, tv < 0, nsc);
             if constexpr (MODE == MODE_HYBRID) sh_tick(a, sh, sh_ids, a.W, a.C, round);
         }
         flush_w();

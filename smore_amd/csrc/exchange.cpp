@@ -288,6 +288,9 @@ struct smore_group {
     // last two rotations (by sub-round parity)
     int schedule = SMORE_SCHED_BLOCKS;   // include/smore_hip.h: the default
     std::vector<hipEvent_t> bdone, brecv;
+    // the block schedule's hub slots (blocks.cpp): per replica the event
+    // after its exchange pass (compute stream) and after the all-reduce
+    std::vector<hipEvent_t> hready, hdone;
 };
 
 namespace {
@@ -642,6 +645,119 @@ int block_finish(smore_group* g, uint64_t S) {
     return group_sync(g);
 }
 
+// ---- the hub slots of the LINE-2 block schedule (blocks.cpp): every part
+// trains its own copy of the H hub C rows in every cell; after each
+// sub-round the copies' deltas are all-reduced one late (begin / cycle / end
+// of replica_sync.hip on the slot rows, per-slot adaptive scales), on the
+// comm streams ahead of the rotation
+double hub_c0() {
+    const char* e = getenv("SMORE_HUB_C0");
+    const double v = e ? atof(e) : 0.0;
+    return v > 0 ? v : 2048.0;
+}
+
+float* hub_slots(smore_ctx* c) { return c->d_table[1] + (size_t)c->g->V * c->dpad; }
+
+int hub_ex_start(smore_group* g, double samples_per_exchange) {
+    const size_t n = g->ctx.size();
+    if (!g->ctx[0]->blk.H) return SMORE_OK;
+    if (g->hready.size() != n) {
+        g->hready.assign(n, nullptr);
+        g->hdone.assign(n, nullptr);
+        for (size_t r = 0; r < n; ++r) {
+            (void)hipSetDevice(g->ctx[r]->device);
+            if (hipEventCreateWithFlags(&g->hready[r], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&g->hdone[r], hipEventDisableTiming) != hipSuccess)
+                return gfail(g, (int)r, fail(g->ctx[r], SMORE_EHIP, "hub exchange: events"));
+        }
+    }
+    const double c0 = hub_c0();
+    char key[96];
+    snprintf(key, sizeof key, "%.17g/%.17g", samples_per_exchange, c0);
+    for (size_t r = 0; r < n; ++r) {
+        smore_ctx* c = g->ctx[r];
+        auto& B = c->blk;
+        int rc;
+        if ((rc = set_device(c))) return gfail(g, (int)r, rc);
+        const size_t nf = (size_t)B.H * c->dpad;
+        for (float*& p : B.d_hub_ex)
+            if (!p && hipMalloc((void**)&p, nf * sizeof(float)) != hipSuccess)
+                return gfail(g, (int)r, fail(c, SMORE_EHIP, "hub exchange buffers"));
+        if (B.hub_scale_key != key) {
+            std::vector<float> sc((size_t)B.H);
+            hub_scales(B, samples_per_exchange, c0, sc.data());
+            if ((rc = upload(c, B.d_hub_scale, sc.data(), sc.size()))) return gfail(g, (int)r, rc);
+            B.hub_scale_key = key;
+        }
+        if ((rc = smore_block_hubs_load(c))) return gfail(g, (int)r, rc);
+        if (hipMemcpyAsync(B.d_hub_ex[0], hub_slots(c), nf * sizeof(float), hipMemcpyDeviceToDevice, c->stream) !=
+            hipSuccess)
+            return gfail(g, (int)r, fail(c, SMORE_EHIP, "hub exchange: snapshot"));
+        B.hub_pending = false;
+    }
+    return SMORE_OK;
+}
+
+// after every replica's cell of a sub-round: the exchange pass on the compute
+// stream, then the all-reduce of the slots' deltas on the comm streams
+int hub_ex_post(smore_group* g) {
+    const size_t n = g->ctx.size();
+    if (!g->ctx[0]->blk.H) return SMORE_OK;
+    std::vector<float*> bufs;
+    std::vector<hipStream_t> st;
+    for (size_t r = 0; r < n; ++r) {
+        smore_ctx* c = g->ctx[r];
+        auto& B = c->blk;
+        (void)hipSetDevice(c->device);
+        float* const* x = B.d_hub_ex;
+        hipError_t e = hipSuccess;
+        if (B.hub_pending) {
+            e = hipStreamWaitEvent(c->stream, g->hdone[r], 0);
+            if (e == hipSuccess)
+                e = launch_delta_cycle_rows(hub_slots(c), x[0], x[1], x[2], B.d_hub_scale, (uint64_t)B.H, c->dpad,
+                                            c->cus, c->stream);
+        } else {
+            e = launch_delta_begin(hub_slots(c), x[0], x[1], x[2], (uint64_t)B.H * c->dpad, c->cus, c->stream);
+        }
+        if (e == hipSuccess) e = hipEventRecord(g->hready[r], c->stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(c->comm_stream, g->hready[r], 0);
+        if (e != hipSuccess) return gfail(g, (int)r, fail(c, SMORE_EHIP, "hub exchange pass"));
+        bufs.push_back(x[2]);
+        st.push_back(c->comm_stream);
+    }
+    int rc;
+    if ((rc = coll_allreduce(g, bufs, (size_t)g->ctx[0]->blk.H * g->ctx[0]->dpad, st, "hub ncclAllReduce"))) return rc;
+    for (size_t r = 0; r < n; ++r) {
+        (void)hipSetDevice(g->ctx[r]->device);
+        if (hipEventRecord(g->hdone[r], g->ctx[r]->comm_stream) != hipSuccess)
+            return gfail(g, (int)r, fail(g->ctx[r], SMORE_EHIP, "hub exchange: event"));
+        g->ctx[r]->blk.hub_pending = true;
+    }
+    return SMORE_OK;
+}
+
+// the last exchange's end (every copy of the slots equal again), then the
+// slots back into the hub rows, before block_finish gathers the blocks
+int hub_ex_finish(smore_group* g) {
+    if (!g->ctx[0]->blk.H) return SMORE_OK;
+    for (size_t r = 0; r < g->ctx.size(); ++r) {
+        smore_ctx* c = g->ctx[r];
+        auto& B = c->blk;
+        (void)hipSetDevice(c->device);
+        if (B.hub_pending) {
+            float* const* x = B.d_hub_ex;
+            if (hipStreamWaitEvent(c->stream, g->hdone[r], 0) != hipSuccess ||
+                launch_delta_end_rows(hub_slots(c), x[0], x[1], x[2], B.d_hub_scale, (uint64_t)B.H, c->dpad, c->cus,
+                                      c->stream) != hipSuccess)
+                return gfail(g, (int)r, fail(c, SMORE_EHIP, "hub exchange end"));
+            B.hub_pending = false;
+        }
+        int rc;
+        if ((rc = smore_block_hubs_store(c))) return gfail(g, (int)r, rc);
+    }
+    return SMORE_OK;
+}
+
 // samples per row per replica per epoch of the LINE-2 block schedule (the C4
 // bench's one epoch per 2^27-sample step: 13.4 per row)
 constexpr double EDGE_BLOCK_PER_ROW = 13.42;
@@ -667,6 +783,7 @@ int group_block_edges(smore_group* g, uint64_t begin, uint64_t count, uint64_t p
     // a round's samples go to the replicas in proportion to their parts'
     // source mass, so the union of the parts draws SourceSample's law
     const std::vector<double>& pm = g->ctx[0]->blk.part_mass;
+    if ((rc = hub_ex_start(g, (double)std::min<uint64_t>(per, count / n) / nb))) return rc;
     uint64_t S = 0;
     for (uint64_t k = 0; k < rounds; ++k) {
         const uint64_t lo = round_lo(k), m = round_lo(k + 1) - lo;
@@ -687,9 +804,11 @@ int group_block_edges(smore_group* g, uint64_t begin, uint64_t count, uint64_t p
                     return gfail(g, (int)r, rc);
                 cur[r] += x;
             }
+            if ((rc = hub_ex_post(g))) return rc;
             if ((rc = group_rotate(g, S))) return rc;
         }
     }
+    if ((rc = hub_ex_finish(g))) return rc;
     return block_finish(g, S);
 }
 
@@ -1047,6 +1166,10 @@ void smore_group_destroy(smore_group* g) {
     for (hipEvent_t e : g->bdone)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : g->brecv)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : g->hready)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : g->hdone)
         if (e) (void)hipEventDestroy(e);
     if (g->ldone) (void)hipEventDestroy(g->ldone);
     delete g;

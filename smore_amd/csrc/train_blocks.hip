@@ -38,11 +38,15 @@ __device__ __forceinline__ int block_of(const BlockArgs& b, int32_t x) {
     return lo;
 }
 
-// a negative of block k: index over the block, alias entry of vertex cb[k] + i
+// a negative of block k: index over the block's rows and the H hub slots,
+// alias entry of vertex cb[k] + i, or of hub slot j = i - rows (id V + j)
 __device__ __forceinline__ int32_t block_negative(const BlockArgs& b, int k, uint32_t ki, uint32_t kp) {
     const int32_t lo = b.cb[k];
-    const uint32_t i = (uint32_t)lo + draw_index(ki, (uint32_t)(b.cb[k + 1] - lo));
-    return alias_pick(i, b.ntab[i], kp);
+    const uint32_t nk = (uint32_t)(b.cb[k + 1] - lo);
+    const uint32_t i = draw_index(ki, nk + (uint32_t)b.H);
+    if (i < nk) return alias_pick((uint32_t)lo + i, b.ntab[(uint32_t)lo + i], kp);
+    const uint32_t j = i - nk;
+    return alias_pick((uint32_t)b.V + j, b.hub_ntab[(uint64_t)k * (uint32_t)b.H + j], kp);
 }
 
 template <int KMAX>
@@ -53,7 +57,10 @@ __global__ void __launch_bounds__(256) block_draw_kernel(BlockArgs b, int blk, u
     if (t >= count) return;
     const uint64_t s = begin + t;
     const uint4 b0 = philox_block(seed, 0, s, 0);
-    const uint64_t ai = b.atom_off + draw_index(b0.y, b.natoms);
+    // a hub atom of the part (word 2 against the cell's hub share), else one
+    // of the block's own atoms
+    const bool hub = b.nhub > 0 && (b.natoms == 0 || b0.z < b.hub_thr);
+    const uint64_t ai = hub ? b.hub_off + draw_index(b0.y, b.nhub) : b.atom_off + draw_index(b0.y, b.natoms);
     const uint4 e0 = b.atoms[2 * ai], e1 = b.atoms[2 * ai + 1];
     const bool acc = b0.x < e0.x;
     int32_t w[RW];
@@ -75,6 +82,39 @@ __global__ void __launch_bounds__(256) block_draw_kernel(BlockArgs b, int blk, u
         const i32x4 x = {w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
         __builtin_nontemporal_store(x, o + q);
     }
+}
+
+__global__ void __launch_bounds__(256) rows_gather_kernel(const float4* __restrict__ T, const int32_t* __restrict__ idx,
+                                                          uint64_t n4, int dp4, float4* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = T[(uint64_t)idx[i / dp4] * dp4 + i % dp4];
+}
+
+__global__ void __launch_bounds__(256) rows_scatter_kernel(float4* __restrict__ T, const int32_t* __restrict__ idx,
+                                                           uint64_t n4, int dp4, const float4* __restrict__ in) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * blockDim.x)
+        T[(uint64_t)idx[i / dp4] * dp4 + i % dp4] = in[i];
+}
+
+static unsigned rows_grid(uint64_t n4) {
+    const uint64_t g = (n4 + 255) / 256;
+    return (unsigned)(g < 4096 ? (g ? g : 1) : 4096);
+}
+
+hipError_t launch_rows_gather(const float* T, const int32_t* idx, uint64_t n, int dpad, float* out, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const uint64_t n4 = n * (uint64_t)(dpad / 4);
+    hipLaunchKernelGGL(rows_gather_kernel, dim3(rows_grid(n4)), dim3(256), 0, st, reinterpret_cast<const float4*>(T),
+                       idx, n4, dpad / 4, reinterpret_cast<float4*>(out));
+    return hipGetLastError();
+}
+
+hipError_t launch_rows_scatter(float* T, const int32_t* idx, uint64_t n, int dpad, const float* in, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const uint64_t n4 = n * (uint64_t)(dpad / 4);
+    hipLaunchKernelGGL(rows_scatter_kernel, dim3(rows_grid(n4)), dim3(256), 0, st, reinterpret_cast<float4*>(T), idx,
+                       n4, dpad / 4, reinterpret_cast<const float4*>(in));
+    return hipGetLastError();
 }
 
 hipError_t launch_block_draw(const BlockArgs& b, int blk, uint64_t seed, uint64_t begin, uint64_t count, int K,

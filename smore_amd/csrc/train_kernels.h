@@ -37,6 +37,17 @@ struct EdgeArgs {
     int alpha_rec;                 // learning rate in record word 2 + KMAX: 1 walk pairs (pair kernels),
                                    // 2 independent samples (the edge kernel: the hot/cold split)
     uint32_t pair_slice;           // pair kernels: records per group slice (0: CH_ROUNDS)
+    // negative-gradient weight (2-D block schedule): a cell
+    // draws its negatives from its C block's restricted law, but gets samples
+    // in proportion to the block's CONTEXT mass; weighting the negatives'
+    // step by NegativeSample's block mass over the cell's share restores the
+    // epoch's negative law.  neg_scale <= 0: 1 (off).  neg_lo / neg_hi
+    // non-null (walk cells): neg_scale is the block's negative share and the
+    // weight is computed on the device from the round's record counts,
+    // neg_scale * (*neg_hi - *neg_lo) / records.
+    float neg_scale;
+    const uint64_t* neg_lo;
+    const uint64_t* neg_hi;
     uint64_t begin, count, total, seed;
     double alpha0;
     float reg;
@@ -213,9 +224,20 @@ struct BlockArgs {
     const uint2* ntab;        // V entries: block k's negative alias over its vertices [cb[k], cb[k+1])
     int nb;                   // C blocks
     int32_t cb[BLOCK_MAX + 1];
+    // hub C rows (blocks.cpp): slots V .. V + H - 1, drawn in every block.  A
+    // block's negative alias runs over its rows then the H slots (entries
+    // hub_ntab[k * H + j]); a LINE-2 sample takes a hub atom of the part
+    // (atoms [hub_off, hub_off + nhub)) iff Philox word 2 < hub_thr.
+    const uint2* hub_ntab;
+    uint64_t hub_off;
+    uint32_t nhub, hub_thr;
+    int32_t H, V;
 };
 hipError_t launch_block_draw(const BlockArgs& b, int blk, uint64_t seed, uint64_t begin, uint64_t count, int K,
                              int32_t* rec, hipStream_t st);
+// rows idx[0 .. n) of T to out (gather) / from in (scatter), dpad floats each
+hipError_t launch_rows_gather(const float* T, const int32_t* idx, uint64_t n, int dpad, float* out, hipStream_t st);
+hipError_t launch_rows_scatter(float* T, const int32_t* idx, uint64_t n, int dpad, const float* in, hipStream_t st);
 hipError_t launch_block_pair_count(const WalkArgs& w, const BlockArgs& b, uint64_t seed, uint32_t* count,
                                    hipStream_t st);
 hipError_t launch_block_pair_emit(const WalkArgs& w, const BlockArgs& b, uint64_t seed, int K, double alpha0,

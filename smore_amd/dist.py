@@ -51,6 +51,33 @@ def table_tensor(pn, which):
     return t
 
 
+def hub_slots_tensor(pn):
+    """Zero-copy view of the C table's hub slot rows V .. V + H of the block
+    setup (blocks.cpp), or None without hubs."""
+    H, first, _, _ = pn.block_hubs()
+    if not H:
+        return None
+    ptr, stride = pn.table_device(1)
+    p = ptr + first * stride * 4
+    t = torch.as_tensor(_DeviceArray(p, (H, stride)), device="cuda")
+    if t.data_ptr() != p:
+        raise RuntimeError("slot view is not zero-copy")
+    return t
+
+
+def block_hubs(pn, samples_per_exchange, c0=2048.0):
+    """BlockSync's `hubs` argument for a ProNet context after block_setup
+    (None without hubs): its slot view, the adaptive scales for
+    `samples_per_exchange` samples per rank per sub-round, the fused HIP
+    passes, and the context's slot load / store."""
+    slots = hub_slots_tensor(pn)
+    if slots is None:
+        return None
+    scale = torch.from_numpy(pn.block_hub_scales(samples_per_exchange, c0)).to(slots.device)
+    return {"slots": slots, "scale": scale, "passes": HipPasses(pn), "load": pn.block_hubs_load,
+            "store": pn.block_hubs_store}
+
+
 class DeltaAllReduce:
     """Synchronous snapshot-delta exchange over same-shaped tensors on every rank."""
 
@@ -214,9 +241,18 @@ class BlockSync:
 
     W, C: the table tensors (rows x stride; CPU tensors in the gloo tests).
     Over gloo, CUDA blocks are staged through host memory (gloo's send/recv
-    take CPU tensors)."""
+    take CPU tensors).
 
-    def __init__(self, W, C, w_bounds, c_bounds, group=None):
+    hubs (LINE-2 hub C rows, blocks.cpp): a dict with `slots` (this rank's
+    copy of the H hub rows, a view of C's slot rows), `scale` (per-slot
+    exchange scales), optional `passes` (HipPasses / TorchPasses), `load` and
+    `store` (slots <- hub rows / hub rows <- slots).  Every cell trains the
+    slots; after each sub-round their deltas are all-reduced one late
+    (OverlapSync, adaptive per-slot scales) ahead of the rotation; finish()
+    folds the last exchange in (every rank's slots equal) and, with
+    gather=True, stores the slots into the hub rows before the gather."""
+
+    def __init__(self, W, C, w_bounds, c_bounds, group=None, hubs=None):
         self.W, self.C = W, C
         self.wb = [int(x) for x in w_bounds]
         self.cb = [int(x) for x in c_bounds]
@@ -230,6 +266,13 @@ class BlockSync:
         self.staged = dist.get_backend(group) == "gloo" and C.is_cuda
         self.s = 0                 # sub-rounds done
         self.pending = [None, None]   # (works, post) of the last two rotations, by sub-round parity
+        self.hubs = hubs
+        self.hub_sync = None
+        if hubs is not None:
+            if hubs.get("load") is not None:
+                hubs["load"]()        # slots <- hub rows, on the current stream
+            self.hub_sync = OverlapSync([hubs["slots"]], group=group, passes=hubs.get("passes"),
+                                        row_scale=[hubs["scale"]])
 
     def block(self, s=None):
         """The C block this rank trains at sub-round s (default: the next)."""
@@ -255,6 +298,8 @@ class BlockSync:
         self._wait(s & 1)               # the block received at sub-round s - 2
         b = self.block(s)
         train(b)
+        if self.hub_sync is not None:
+            self.hub_sync.begin()       # the hub slots' deltas, one late, ahead of the rotation
         send, recv = self.rows(b), self.rows((b + 2) % self.nb)
         dst = self.ranks[(self.rank - 1) % self.world]
         src = self.ranks[(self.rank + 1) % self.world]
@@ -283,6 +328,10 @@ class BlockSync:
     def finish(self, gather=True):
         self._wait(0)
         self._wait(1)
+        if self.hub_sync is not None:
+            self.hub_sync.end()         # every rank's slots equal
+            if gather and self.hubs.get("store") is not None:
+                self.hubs["store"]()    # hub rows <- slots, before the blocks are gathered
         if not gather:
             return
         for p in range(self.world):

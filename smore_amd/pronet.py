@@ -260,6 +260,37 @@ class ProNet:
         self._chk(lib.smore_block_part_mass(self.ctx, ptr(m)), "block_part_mass")
         return m
 
+    def block_neg_scale(self, block):
+        """LINE-2: the negative-step weight of cell (part, block) (fp32 value)."""
+        w = C.c_double()
+        self._chk(lib.smore_block_neg_scale(self.ctx, int(block), C.byref(w)), "block_neg_scale")
+        return w.value
+
+    def block_set_hubs(self, hubs):
+        """LINE-2 hub C rows of the next block_setup (-1 automatic, 0 none)."""
+        self._chk(lib.smore_block_set_hubs(self.ctx, int(hubs)), "block_set_hubs")
+
+    def block_hubs(self):
+        """(H, first slot row V, hub C rows [H] int32, expected touches per sample [H])."""
+        h, first = C.c_int64(), C.c_int64()
+        self._chk(lib.smore_block_hubs(self.ctx, C.byref(h), C.byref(first), None, None), "block_hubs")
+        rows = np.zeros(max(1, h.value), np.int32)
+        rates = np.zeros(max(1, h.value), np.float64)
+        self._chk(lib.smore_block_hubs(self.ctx, None, None, ptr(rows), ptr(rates)), "block_hubs")
+        return h.value, first.value, rows[:h.value].copy(), rates[:h.value].copy()
+
+    def block_hubs_load(self):
+        self._chk(lib.smore_block_hubs_load(self.ctx), "block_hubs_load")
+
+    def block_hubs_store(self):
+        self._chk(lib.smore_block_hubs_store(self.ctx), "block_hubs_store")
+
+    def block_hub_scales(self, samples, c0):
+        h = self.block_hubs()[0]
+        out = np.zeros(max(1, h), np.float32)
+        self._chk(lib.smore_block_hub_scales(self.ctx, float(samples), float(c0), ptr(out)), "block_hub_scales")
+        return out[:h].copy()
+
     def block_counts(self, samples):
         """LINE-2: `samples` split over the C blocks by mass (largest remainder)."""
         _, cb = self.block_bounds()

@@ -21,7 +21,7 @@ import pytest
 
 from oracle import oracle as orc
 from bench import largest_remainder
-from tests.block_spec import BlockSpec, part_masses
+from tests.block_spec import BlockSpec, part_masses, skewed_graph_lines
 from tests.conftest import GOLDEN
 
 pytestmark = pytest.mark.gpu
@@ -49,16 +49,22 @@ def _ctx(smore, dim=32):
     return pn
 
 
-@pytest.mark.parametrize("n", [2, 3, 4])
-def test_block_draws_match_spec(smore, graph, n):
+@pytest.mark.parametrize("n,hubs", [(2, -1), (3, -1), (4, -1), (2, 0), (4, 0), (3, 100)])
+def test_block_draws_match_spec(smore, graph, n, hubs):
+    """Bit-exact cell draws against tests/block_spec.py, with the automatic
+    hub rows (pl1k: 1000 / 8nb), none, and many."""
     K = 5
     pn = _ctx(smore)
+    pn.block_set_hubs(hubs)
     for r in range(n):
-        spec = BlockSpec(graph, n, r)
+        spec = BlockSpec(graph, n, r, K, hubs)
         pn.block_setup("line2", n, r, K, "atomic")
         wb, cb = pn.block_bounds()
         assert list(wb) == spec.wb and list(cb) == spec.cb
+        H, first, rows, _ = pn.block_hubs()
+        assert H == spec.H and first == graph.V and list(rows) == spec.hubs
         np.testing.assert_allclose(pn.block_mass(), spec.mass, rtol=1e-12, atol=0)
+        np.testing.assert_allclose([pn.block_neg_scale(k) for k in range(2 * n)], spec.neg_w, rtol=1e-6)
         assert abs(pn.block_mass().sum() - 1.0) < 1e-12
         for k in range(2 * n):
             if spec.mass[k] == 0:
@@ -67,18 +73,22 @@ def test_block_draws_match_spec(smore, graph, n):
             want = spec.draw(k, SEED, (1 << 33) + 977 * k, 600, K)
             np.testing.assert_array_equal(got, want)
             assert ((got[:, 0] >= wb[r]) & (got[:, 0] < wb[r + 1])).all()
-            assert ((got[:, 1:] >= cb[k]) & (got[:, 1:] < cb[k + 1])).all()
+            ctx = got[:, 1:]
+            slot = ctx >= graph.V
+            assert ((ctx >= cb[k]) & (ctx < cb[k + 1]) | slot & (ctx < graph.V + H)).all()
+            assert not np.isin(ctx[~slot], rows).any()     # a hub row is only ever drawn as its slot
+            if H:
+                assert slot.any()
     pn.close()
 
 
 @pytest.mark.parametrize("n", [2, 4, 8])
 def test_block_part_mass_skewed_graph(smore, tmp_path, n):
-    """smore_block_part_mass against the spec on a graph whose hub holds ~99 %
-    of the source mass: a group's round split gives each replica
+    """smore_block_part_mass against the spec on a graph whose parts differ by
+    ~13 % of source mass: a group's round split gives each replica
     its part's share, so the union of the parts draws SourceSample's law."""
-    lines = ["v0 v%d 1000" % i for i in range(1, 400)] + ["v%d v%d 1" % (i, 1 + i % 399) for i in range(1, 400)]
-    f = tmp_path / "star.txt"
-    f.write_text("\n".join(lines) + "\n")
+    f = tmp_path / "skewed.txt"
+    f.write_text(skewed_graph_lines())
     want, wb = part_masses(str(f), n, undirected=0)
     pn = smore.ProNet(0)
     pn.LoadEdgeList(str(f), 0)
@@ -86,7 +96,7 @@ def test_block_part_mass_skewed_graph(smore, tmp_path, n):
     pn.block_setup("line2", n, n - 1, 5, "atomic")
     assert list(pn.block_bounds()[0]) == wb
     np.testing.assert_allclose(pn.block_part_mass(), want, rtol=1e-12, atol=1e-15)
-    assert max(want) > 1.5 / n
+    assert max(want) > 1.1 / n
     pn.close()
 
 
@@ -108,34 +118,55 @@ def test_block_cell_serial_equals_oracle(smore, graph):
     pn = _ctx(smore, dim)
     W, C = pn.get_table(0), pn.get_table(1)
     pn.block_setup("line2", 3, 2, K, "serial")
+    H, V, rows, _ = pn.block_hubs()
+    assert H > 0
+    pn.block_hubs_load()                 # slots V .. V + H <- the hub rows
+    C = np.concatenate([C, C[rows]])     # the oracle's table with the slot rows
     begin = 5000
     for k in (0, 3, 5, 1):
         n = 700
         rec = pn.block_sample_edges(k, SEED, begin, n, K)
         pn.block_train_edges(k, begin, n, total, K, 0.025, SEED, "serial")
-        orc.train_records_f32("line2", W, C, rec, K, 0.025, 0.0, total, begin)
+        w = pn.block_neg_scale(k)
+        assert w != 1.0          # the epoch negative-law weight is on (SMORE_NEG_LAW default)
+        orc.train_records_f32("line2", W, C, rec, K, 0.025, 0.0, total, begin, w)
         begin += n
+    assert (C[V:] != C[rows]).any()      # the slots trained, the hub rows did not
     np.testing.assert_array_equal(pn.get_table(0), W)
-    np.testing.assert_array_equal(pn.get_table(1), C)
+    np.testing.assert_array_equal(pn.get_table(1), C[:V])
+    pn.block_hubs_store()                # hub rows <- slots
+    C[rows] = C[V:]
+    np.testing.assert_array_equal(pn.get_table(1), C[:V])
     pn.close()
 
 
-def _schedule_edges(smore, graph, n, begin, count, per, total, K, dim, W0, C0):
+def _schedule_edges(smore, graph, n, begin, count, per, total, K, dim, W0, C0, hubs=-1):
     """exchange.cpp group_block_edges restated: rounds of per * n samples
     split over the replicas by their parts' source mass (largest remainder),
     replica r's slice split over the blocks by its mass, sub-round s trains
-    cell (r, (2r + s) mod 2n), then C block (2r + s) mod 2n moves to replica
-    r - 1; at the end W part p comes from replica p, C block b from b // 2."""
+    cell (r, (2r + s) mod 2n) on replica r's tables and its own copy of the
+    hub slots (rows V .. V + H), then the slots' one-late exchange (begin /
+    cycle with the per-slot scales, the all-reduce summing the replicas in
+    order) and C block (2r + s) mod 2n moves to replica r - 1; at the end the
+    last exchange's end, the slots back into the hub rows, W part p from
+    replica p, C block b from b // 2."""
     nb = 2 * n
     ctxs, specs = [], []
     for r in range(n):
         p = smore.ProNet(0)
         p.LoadEdgeList(PL1K, 1)
         p.alloc_tables(dim, 2)
+        p.block_set_hubs(hubs)
         p.block_setup("line2", n, r, K, "serial")
         ctxs.append(p)
+    H, V, hub_rows, _ = ctxs[0].block_hubs()
+    sc = ctxs[0].block_hub_scales(min(per, count // n) / nb, 2048.0)[:, None] if H else None
     Ws = [W0.copy() for _ in range(n)]
-    Cs = [C0.copy() for _ in range(n)]
+    Cs = [np.concatenate([C0, C0[hub_rows]]) for _ in range(n)]
+    Ss = [c[V:].copy() for c in Cs]
+    Ds = [np.zeros_like(x) for x in Ss]
+    Rs = [np.zeros_like(x) for x in Ss]
+    pending = False
     wb, cb = ctxs[0].block_bounds()
     rounds = -(-count // (per * n)) if per * n < count else 1
     for k in range(rounds):
@@ -150,12 +181,37 @@ def _schedule_edges(smore, graph, n, begin, count, per, total, K, dim, W0, C0):
                 x = int(cnt[r][b])
                 if x:
                     rec = ctxs[r].block_sample_edges(b, SEED, begin + cur[r], x, K)
-                    orc.train_records_f32("line2", Ws[r], Cs[r], rec, K, 0.025, 0.0, total, begin + cur[r])
+                    orc.train_records_f32("line2", Ws[r], Cs[r], rec, K, 0.025, 0.0, total, begin + cur[r],
+                                          ctxs[r].block_neg_scale(b))
                 cur[r] += x
+            if H:          # the hub slots' exchange (replica_sync.hip passes, fp32)
+                for r in range(n):
+                    T = Cs[r][V:]
+                    if pending:
+                        X = sc * Rs[r] - Ds[r]
+                        tn, sn = T + X, Ss[r] + X
+                        Ds[r] = tn - sn
+                        T[:] = tn
+                        Ss[r] = tn.copy()
+                    else:
+                        Ds[r] = T - Ss[r]
+                        Ss[r] = T.copy()
+                    Rs[r] = Ds[r].copy()
+                tot = Rs[0].copy()
+                for r in range(1, n):
+                    tot = tot + Rs[r]
+                Rs = [tot.copy() for _ in range(n)]
+                pending = True
             moved = [Cs[r][cb[(2 * r + s) % nb]:cb[(2 * r + s) % nb + 1]].copy() for r in range(n)]
             for r in range(n):
                 b = (2 * r + s) % nb
                 Cs[(r - 1) % n][cb[b]:cb[b + 1]] = moved[r]
+    if H:
+        for r in range(n):
+            if pending:
+                X = sc * Rs[r] - Ds[r]
+                Cs[r][V:] += X
+            Cs[r][hub_rows] = Cs[r][V:]
     W, C = W0.copy(), C0.copy()
     for p in range(n):
         W[wb[p]:wb[p + 1]] = Ws[p][wb[p]:wb[p + 1]]
@@ -166,10 +222,12 @@ def _schedule_edges(smore, graph, n, begin, count, per, total, K, dim, W0, C0):
     return W, C
 
 
-@pytest.mark.parametrize("n", [2, 3])
-def test_block_group_serial_equals_schedule(smore, graph, n):
+@pytest.mark.parametrize("n,hubs", [(2, -1), (3, -1), (2, 0), (3, 0)])
+def test_block_group_serial_equals_schedule(smore, graph, n, hubs):
     K, dim, total = 5, 32, 10 ** 6
     g = smore.Group([0] * n)
+    for r in g.replicas:
+        r.block_set_hubs(hubs)
     g.LoadEdgeList(PL1K, 1)
     g.alloc_tables(dim, 2)
     g.primary.init_table_glibc(0, 0)
@@ -179,7 +237,7 @@ def test_block_group_serial_equals_schedule(smore, graph, n):
     g.set_schedule("blocks")
     begin, count, per = 1000, 9000, 1500
     g.train_edges("line2", begin, count, total, K, 0.025, 0.0, SEED, "serial", per=per)
-    W, C = _schedule_edges(smore, graph, n, begin, count, per, total, K, dim, W0, C0)
+    W, C = _schedule_edges(smore, graph, n, begin, count, per, total, K, dim, W0, C0, hubs)
     for r in g.replicas:
         np.testing.assert_array_equal(r.get_table(0), W)
         np.testing.assert_array_equal(r.get_table(1), C)
