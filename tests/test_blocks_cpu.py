@@ -190,3 +190,123 @@ def test_block_negative_law_c2():
     g = orc.Graph(V, src, dst, w)
     for world in (2, 4, 8):
         _neg_law_check(g, world, "c2")
+
+
+# ---- the hub slots in BlockSync (dist.py): every cell also trains this
+# rank's copy of H hub rows (slots V .. V + H of C), exchanged one late after
+# every sub-round with per-slot scales (OverlapSync over the slots, TorchPasses)
+HUBS = 3
+
+
+def _hub_scale():
+    return torch.tensor([1.0, 0.75, 0.5])
+
+
+def _cell_hubs(W, C, wb, cb, r, b, s):
+    """A cell that touches W part r, C block b and the hub slots (the shape of
+    a LINE-2 cell with hub atoms and hub negatives)."""
+    _cell(W, C, wb, cb, r, b, s)
+    h = C[V:V + HUBS]
+    w = W[wb[r]:wb[r + 1]]
+    h.mul_(0.995).add_(torch.tanh(w.mean(0) + h) * (0.01 * (r + 1)) + 0.0005 * (b + s))
+    w.add_(h.mean(0) * 0.01)
+
+
+def _reference_hubs(world, subrounds, hub_rows):
+    """BlockSync with hubs restated in one process: per-rank tables, cells in
+    sub-round order, after each sub-round the slots' begin / cycle passes and
+    the summed deltas, then the rotation; at the end the last exchange's end,
+    the slots into the hub rows and the gather."""
+    torch.manual_seed(0)
+    W0, C0 = torch.randn(V, D), torch.randn(V, D)
+    wb, cb = _bounds(world)
+    nb = 2 * world
+    Ws = [W0.clone() for _ in range(world)]
+    Cs = [torch.cat([C0, C0[hub_rows]]) for _ in range(world)]
+    S = [c[V:].clone() for c in Cs]
+    Dd = [torch.zeros(HUBS, D) for _ in range(world)]
+    R = [torch.zeros(HUBS, D) for _ in range(world)]
+    sc = _hub_scale().view(-1, 1)
+    pending = False
+    for s in range(subrounds):
+        for r in range(world):
+            _cell_hubs(Ws[r], Cs[r], wb, cb, r, (2 * r + s) % nb, s)
+        for r in range(world):
+            T = Cs[r][V:]
+            if pending:                       # TorchPasses.cycle: end, then begin
+                R[r].mul_(sc).sub_(Dd[r])
+                T.add_(R[r])
+                S[r].add_(R[r])
+            torch.sub(T, S[r], out=Dd[r])
+            R[r].copy_(Dd[r])
+            S[r].copy_(T)
+        tot = R[0].clone()
+        for r in range(1, world):
+            tot += R[r]
+        R = [tot.clone() for _ in range(world)]
+        pending = True
+        moved = [Cs[r][cb[(2 * r + s) % nb]:cb[(2 * r + s) % nb + 1]].clone() for r in range(world)]
+        for r in range(world):
+            b = (2 * r + s) % nb
+            Cs[(r - 1) % world][cb[b]:cb[b + 1]] = moved[r]
+    for r in range(world):
+        R[r].mul_(sc).sub_(Dd[r])
+        Cs[r][V:].add_(R[r])
+        Cs[r][hub_rows] = Cs[r][V:].clone()
+    W, C = W0.clone(), C0.clone()
+    for p in range(world):
+        W[wb[p]:wb[p + 1]] = Ws[p][wb[p]:wb[p + 1]]
+    for b in range(nb):
+        holder = ((b - subrounds) % nb) // 2
+        C[cb[b]:cb[b + 1]] = Cs[holder][cb[b]:cb[b + 1]]
+    return W, C
+
+
+def _worker_hubs(rank, world, port, subrounds, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from smore_amd.dist import BlockSync, TorchPasses
+    hub_rows = torch.tensor([5, 17, 40])
+    torch.manual_seed(0)
+    W, C0 = torch.randn(V, D), torch.randn(V, D)
+    C = torch.cat([C0, torch.zeros(HUBS, D)])
+    wb, cb = _bounds(world)
+
+    def load():
+        C[V:] = C[hub_rows].clone()
+
+    def store():
+        C[hub_rows] = C[V:].clone()
+    hubs = {"slots": C[V:], "scale": _hub_scale(), "passes": TorchPasses(), "load": load, "store": store}
+    bs = BlockSync(W, C[:V], wb, cb, hubs=hubs)
+    for _ in range(subrounds):
+        s = bs.s
+        bs.sub_round(lambda b: _cell_hubs(W, C, wb, cb, rank, b, s))
+    bs.finish(gather=True)
+    RW, RC = _reference_hubs(world, subrounds, hub_rows)
+    exact = world == 2            # sums of 2 are order-free; gloo's ring may add 3+ in another order
+    if exact:
+        ok = torch.equal(W, RW) and torch.equal(C[:V], RC)
+    else:
+        ok = torch.allclose(W, RW, atol=1e-5, rtol=1e-5) and torch.allclose(C[:V], RC, atol=1e-5, rtol=1e-5)
+    ok = ok and torch.equal(C[hub_rows], C[V:])
+    out[rank] = int(ok)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,subrounds", [(2, 4), (2, 9), (3, 7), (4, 8)])
+def test_block_rotation_with_hubs_gloo(world, subrounds):
+    """BlockSync with hub slots over gloo equals its one-process restatement
+    (bit for bit at 2 ranks), and every rank ends with the hub rows equal to
+    the exchanged slots."""
+    ctx = mp.get_context("spawn")
+    out = ctx.Array("i", [0] * world)
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_hubs, args=(r, world, port, subrounds, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert list(out) == [1] * world

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--hot-tau", type=float, default=None, help="hybrid: hot-row threshold")
     ap.add_argument("--combine-rows", type=int, default=None, help="hybrid: LDS write-combined rows (0: off)")
     ap.add_argument("--skip-one", action="store_true", help="no one-GPU reference (profiling the cells alone)")
+    ap.add_argument("--hubs", type=int, default=-1, help="line2: hub C rows (-1 the library's default, 0 none)")
     args = ap.parse_args()
 
     import torch  # noqa: F401  (one HIP runtime with torch, as bench.py)
@@ -56,6 +57,7 @@ def main():
         pn.set_write_combine(args.combine_rows, 0)
     pn.init_table_glibc(0, 0)
     pn.zero_table(1)
+    pn.block_set_hubs(args.hubs)
     S = args.samples
     total = S * 100
     wt, steps, window = 10, 40, 5
@@ -136,6 +138,7 @@ def main():
                     pn.block_train_walks(b)
                     cells.append([b, int(recs[b]), round((time.perf_counter() - t1) * 1e3, 3)])
             row = {"config": args.config, "model": args.model, "nparts": n, "part": r, "setup_s": round(setup_s, 2),
+                   "hubs": int(pn.block_hubs()[0]),
                    "epoch_ms": round(ep * 1e3, 3), "units": units_r,
                    "rate_M_per_s": round(units_r / ep / 1e6, 2),
                    "per_gpu_factor": round((units_r / ep) / (units / one), 4) if one else None,

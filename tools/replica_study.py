@@ -85,6 +85,8 @@ def main():
                     help="group schedule (blocks: --per-row = samples per row per replica per epoch for line2; "
                          "deepwalk: --walks-per-epoch)")
     ap.add_argument("--walks-per-epoch", type=int, default=0, help="blocks, deepwalk: walks per epoch (0: default)")
+    ap.add_argument("--hubs", type=int, nargs="+", default=[-1],
+                    help="blocks: hub C rows per setting (-1 the library's default, 0 none)")
     args = ap.parse_args()
 
     import smore_amd
@@ -125,14 +127,18 @@ def main():
     held = g1.primary.sample_edges("line2", (1 << 40) + 17, 100_000, K, args.seed + 1)
     off, tgt = g1.primary.csr()
     pairs_per_walk = None
-    for n, tot, period, c0, rule in itertools.product(args.ranks, args.totals, args.periods, args.c0, args.rules):
-        if n == 1 and (period != args.periods[0] or c0 != args.c0[0] or rule != args.rules[0]):
+    for n, tot, period, c0, rule, hubs in itertools.product(args.ranks, args.totals, args.periods, args.c0,
+                                                            args.rules, args.hubs):
+        if n == 1 and (period != args.periods[0] or c0 != args.c0[0] or rule != args.rules[0] or
+                       hubs != args.hubs[0]):
             continue
         # one replica at a time on the GPU: free the others' memory
         for m in [m for m in groups if m not in (1, n)]:
             groups.pop(m).close()
         g = group(n)
         g.set_adaptive(c0)
+        for r in g.replicas:
+            r.block_set_hubs(hubs)
         p = g.primary
         p.init_table_glibc(0, 0)
         p.zero_table(1)
@@ -184,6 +190,8 @@ def main():
                     "c0": c0, "period": period, "per_row": args.per_row, "mode": args.mode,
                     "combine_rows": args.combine_rows, "hot_tau": args.hot_tau, "hot_exchange": args.hot_exchange,
                     "walk_partition": args.walk_partition,
+                    "hubs": int(p.block_hubs()[0]) if n > 1 and args.schedule == "blocks" else 0,
+                    "neg_law": os.environ.get("SMORE_NEG_LAW", "1"), "hub_c0": os.environ.get("SMORE_HUB_C0", ""),
                     "finite": bool(np.isfinite(W).all() and np.isfinite(C).all()),
                     "loss": round(heldout_loss(W, C, held), 5), "auc": round(edge_auc(W, C, off, tgt), 5),
                     "replica_spread_rel": spread, "wall_s": round(el, 2)})
