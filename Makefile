@@ -60,7 +60,10 @@ ref:
 clean:
 	rm -rf build smore_amd/lib smore_amd/bin
 
-# the Go shim's call sequence as a C program (tests/test_gpu_goshape.py)
-goshape: tests/c/go_shape
+# the Go shim's call sequence as a C program (tests/test_gpu_goshape.py), and
+# the Go UpdatePairs hook under concurrent callers (tests/test_gpu_pairs.py)
+goshape: tests/c/go_shape tests/c/pairs_mt
 tests/c/go_shape: tests/c/go_shape.c include/smore_hip.h $(LIB)
 	gcc -std=c11 -O2 -Wall -Iinclude -o $@ $< -L$(dir $(LIB)) -lsmore_hip -Wl,-rpath,'$$ORIGIN/../../smore_amd/lib'
+tests/c/pairs_mt: tests/c/pairs_mt.c include/smore_hip.h $(LIB)
+	gcc -std=gnu11 -O2 -Wall -Iinclude -o $@ $< -L$(dir $(LIB)) -lsmore_hip -lpthread -Wl,-rpath,'$$ORIGIN/../../smore_amd/lib'

@@ -469,7 +469,7 @@ func init() { hipUpdatePairs = updatePairsHIP }
 // run one after another (each sees the tables the previous one wrote back)
 type pairSession struct {
 	once sync.Once // the context is made exactly once, before any caller uses it
-	mu   sync.Mutex
+	mu   sync.Mutex // guards the tables' (re)allocation only; training calls combine in the library
 	h    *HIP
 	err  error
 }
@@ -499,25 +499,31 @@ func (pn *ProNet) pairSession() *pairSession {
 // Philox unit, duplicates of the context skipped, the context's gradient
 // deferred), and the same rows come back (smore_train_pairs_rows, one
 // synchronisation) -- O(pairs x dim) per call.  The session's device tables
-// are allocated once; rows a call does not touch are never read.  Batches from
-// concurrent goroutines run one after another (each sees the rows the previous
-// one wrote back).  UpdatePairs has no error path (the reference panics on a
-// bad index): failures panic.
+// are allocated once; rows a call does not touch are never read.  Concurrent
+// goroutines do NOT take turns on a lock: each calls
+// smore_train_pairs_rows_mt, which combines every batch queued while the
+// device is busy into one call (the union of their rows up once, the batches
+// in queue order, the union back; capi.cpp PairCombiner), so the reference's
+// `workers` goroutines share one synchronisation instead of paying one each.
+// UpdatePairs has no error path (the reference panics on a bad index):
+// failures panic.
 func updatePairsHIP(pn *ProNet, wVertex, wContext [][]float64, vertices, contexts []int64, dim,
 	negativeSamples int, alpha float64, rng *rand.Rand) {
 	if len(vertices) == 0 {
 		return
 	}
 	s := pn.pairSession()
-	s.mu.Lock()
-	defer s.mu.Unlock()
 	if s.err != nil {
 		panic(s.err)
 	}
-	if err := s.h.alloc(dim, 2); err != nil {
+	s.mu.Lock()
+	err := s.h.alloc(dim, 2)
+	s.mu.Unlock()
+	if err != nil {
 		panic(err)
 	}
-	if err := s.h.PairsRows(wVertex, wContext, vertices, contexts, negativeSamples, alpha, rng.Uint64()); err != nil {
+	if err := s.h.pairsRows(wVertex, wContext, vertices, contexts, negativeSamples, alpha, rng.Uint64(),
+		true); err != nil {
 		panic(err)
 	}
 }
@@ -527,6 +533,13 @@ func updatePairsHIP(pn *ProNet, wVertex, wContext [][]float64, vertices, context
 // batch touches (smore_pairs_rows + smore_train_pairs_rows).
 func (h *HIP) PairsRows(w, c [][]float64, vertices, contexts []int64, negativeSamples int, alpha float64,
 	unit uint64) error {
+	return h.pairsRows(w, c, vertices, contexts, negativeSamples, alpha, unit, false)
+}
+
+// pairsRows: PairsRows; concurrent = true goes through the combining entry
+// point (smore_train_pairs_rows_mt), safe from several goroutines at once.
+func (h *HIP) pairsRows(w, c [][]float64, vertices, contexts []int64, negativeSamples int, alpha float64,
+	unit uint64, concurrent bool) error {
 	n := len(vertices)
 	if n != len(contexts) {
 		return fmt.Errorf("PairsRows: %d vertices, %d contexts", n, len(contexts))
@@ -578,9 +591,15 @@ func (h *HIP) PairsRows(w, c [][]float64, vertices, contexts []int64, negativeSa
 	}
 	gather(w, wi[:nw], wr)
 	gather(c, ci[:nc], cr)
-	if rc := C.smore_train_pairs_rows(h.ctx, &v[0], &cc[0], C.int64_t(n), C.int(K), C.double(alpha),
-		C.uint64_t(h.cfg.Seed), C.uint64_t(unit), C.int(h.cfg.Mode), &wi[0], nw, &wr[0], &ci[0], nc,
-		&cr[0]); rc != C.SMORE_OK {
+	var rc C.int
+	if concurrent { // cgo calls a C function only by name: two call sites
+		rc = C.smore_train_pairs_rows_mt(h.ctx, &v[0], &cc[0], C.int64_t(n), C.int(K), C.double(alpha),
+			C.uint64_t(h.cfg.Seed), C.uint64_t(unit), C.int(h.cfg.Mode), &wi[0], nw, &wr[0], &ci[0], nc, &cr[0])
+	} else {
+		rc = C.smore_train_pairs_rows(h.ctx, &v[0], &cc[0], C.int64_t(n), C.int(K), C.double(alpha),
+			C.uint64_t(h.cfg.Seed), C.uint64_t(unit), C.int(h.cfg.Mode), &wi[0], nw, &wr[0], &ci[0], nc, &cr[0])
+	}
+	if rc != C.SMORE_OK {
 		return h.err("smore_train_pairs_rows")
 	}
 	scatter(w, wi[:nw], wr)

@@ -537,6 +537,19 @@ int smore_get_rows(smore_ctx* ctx, int which, const int32_t* ids, int64_t n, flo
 int smore_train_pairs_rows(smore_ctx* ctx, const int32_t* v, const int32_t* c, int64_t n, int K, double alpha,
                            uint64_t seed, uint64_t unit, int mode, const int32_t* w_ids, int64_t nw, float* w_rows,
                            const int32_t* c_ids, int64_t nc, float* c_rows);
+/* smore_train_pairs_rows for CONCURRENT callers (the one thread-safe entry
+ * point; the reference's UpdatePairs runs from `workers` goroutines,
+ * internal/models/deepwalk/deepwalk.go:96-120): requests queued while the
+ * context is busy are combined into one device call -- the union of their
+ * rows up once (each from the earliest request holding it), the batches in
+ * queue order, the union back -- and each caller gets its rows and status.
+ * One caller alone: the same result as smore_train_pairs_rows.  No other call
+ * may use the context meanwhile. */
+int smore_train_pairs_rows_mt(smore_ctx* ctx, const int32_t* v, const int32_t* c, int64_t n, int K, double alpha,
+                              uint64_t seed, uint64_t unit, int mode, const int32_t* w_ids, int64_t nw, float* w_rows,
+                              const int32_t* c_ids, int64_t nc, float* c_rows);
+/* device calls made by smore_train_pairs_rows_mt and the requests they served */
+int smore_pairs_combine_stats(const smore_ctx* ctx, uint64_t* calls, uint64_t* requests);
 
 /* ---- row census (the walk models' multi-GPU exchange rates) ---------------
  * Between smore_census_begin and smore_census_end the walk-model calls of this

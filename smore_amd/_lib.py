@@ -144,6 +144,8 @@ def _load():
         "smore_set_rows": (i32, [P, i32, P, i64, P]),
         "smore_get_rows": (i32, [P, i32, P, i64, P]),
         "smore_train_pairs_rows": (i32, [P, P, P, i64, i32, dbl, u64, u64, i32, P, i64, P, P, i64, P]),
+        "smore_train_pairs_rows_mt": (i32, [P, P, P, i64, i32, dbl, u64, u64, i32, P, i64, P, P, i64, P]),
+        "smore_pairs_combine_stats": (i32, [P, P, P]),
         "smore_census_begin": (i32, [P]),
         "smore_census_end": (i32, [P, dbl]),
         "smore_set_walk_owner": (i32, [P, i64, i64]),

@@ -51,6 +51,7 @@ BlockArgs block_args(const smore_ctx* c) {
     b.nhub = (uint32_t)c->blk.nhub;
     b.H = (int32_t)c->blk.H;
     b.V = (int32_t)c->g->V;
+    b.hub_of = c->blk.d_hub_of;
     return b;
 }
 
@@ -204,9 +205,20 @@ EdgeArgs cell_args(smore_ctx* c, int k, bool walk) {
 // flight (C5 DeepWalk, 8 GPUs) diverges whether the row is atomic or
 // write-combined.
 int cell_grid(smore_ctx* c, const EdgeArgs& a, int k) {
-    const int grid = launch_grid(c, a);
+    int grid = launch_grid(c, a);
     const auto& B = c->blk;
     if (a.mode == SMORE_SERIAL || (size_t)k >= B.pmax_c.size()) return grid;
+    // LINE-2 cells: the one-GPU launch's Hogwild concurrency cap (capi
+    // edge_grid: at most V / 16 resident sample groups) applied to the rows a
+    // cell updates -- its block's C rows and the hub slots -- so a small
+    // graph's cells (C2 at 8 GPUs: 62k rows per block) keep the one-GPU ratio
+    // of in-flight updates per row instead of 16 times it
+    if (a.alpha_rec == 0 && !getenv("SMORE_CELL_NOCAP")) {
+        const int64_t rows = B.cb[k + 1] - B.cb[k] + B.H;
+        const int gpb = 256 / lanes_of(c->dpad);
+        const int64_t cap = std::max<int64_t>(8, (rows / 16 + gpb - 1) / gpb);
+        if (cap < grid) grid = (int)cap;
+    }
     double cap = cell_rate_default(a.alpha_rec == 1);
     if (const char* e = getenv("SMORE_CELL_RATE")) cap = atof(e);
     // which side's hub sets the cap: both (default), SMORE_CELL_SIDE=c or w
@@ -273,6 +285,7 @@ void blocks_release(smore_ctx* c) {
     dfree(B.d_off);
     dfree(B.d_hub_ntab);
     dfree(B.d_hub_ids);
+    dfree(B.d_hub_of);
     for (float*& p : B.d_hub_ex) dfree(p);
     dfree(B.d_hub_scale);
     B = smore_ctx::Blocks{};
@@ -302,7 +315,7 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
     const int64_t V = g.V;
     const int nb = 2 * nparts;
     if (V < nb) return fail(c, SMORE_EINVAL, "block schedule: fewer vertices than blocks");
-    const int64_t H = walk ? 0 : hub_count(c, V, nb);
+    const int64_t H = hub_count(c, V, nb);
     char key[288];
     snprintf(key, sizeof key, "%d/%d/%d/%d/%d/%lld/%lld/%d/%d/%d/%.9g/%lld/%s", model, nparts, part, K, mode,
              (long long)V, (long long)g.E, c->dpad, c->sh_max, c->sh_flush, c->hot_tau, (long long)H,
@@ -518,12 +531,17 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
             auto& pcx = pcb[k];
             pcx.assign((size_t)(n + H), 0.0);
             hcb[k].assign((size_t)(n + H), 0);
-            if (walk) {   // capi build_hot_maps' scaled law (hot_pc)
+            if (walk) {   // capi build_hot_maps' scaled law (hot_pc); the hub slots at their global rate
                 double mx = 0.0;
                 for (int64_t i = 0; i < n; ++i) {
-                    pcx[i] = (pc[lo + i] + K * pn[lo + i]) * nb;
-                    hcb[k][i] = hyb ? c->hot_c[lo + i] : 0;
+                    pcx[i] = is_hub(lo + i) ? 0.0 : (pc[lo + i] + K * pn[lo + i]) * nb;
+                    hcb[k][i] = hyb && !is_hub(lo + i) ? c->hot_c[lo + i] : 0;
                     mx = std::max(mx, pcx[i]);
+                }
+                for (int64_t j = 0; j < H; ++j) {
+                    pcx[n + j] = B.hub_rate[j];
+                    hcb[k][n + j] = hyb && (double)M * B.hub_rate[j] > tau;
+                    mx = std::max(mx, pcx[n + j]);
                 }
                 B.pmax_w[k] = wmax;
                 B.pmax_c[k] = mx;
@@ -559,7 +577,10 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
     // one tag per hub slot and per W row of the shared hub atoms (a row's
     // tag must not depend on the cell that draws it): hot in any cell
     std::vector<uint8_t> hubhot((size_t)H, 0), hwh;
-    if (H > 0 && hyb) {
+    if (H > 0 && hyb && walk) {
+        const int64_t n0 = B.cb[1] - B.cb[0];
+        for (int64_t j = 0; j < H; ++j) hubhot[j] = hcb[0][n0 + j];
+    } else if (H > 0 && hyb) {
         hwh.assign((size_t)(whi - wlo), 0);
         for (int k = 0; k < nb; ++k) {
             const int64_t n = B.cb[k + 1] - B.cb[k];
@@ -609,6 +630,11 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
         if (H > 0) {
             if ((rc = upload(c, B.d_hub_ntab, reinterpret_cast<const uint2*>(hnt.data()), hnt.size()))) return rc;
             if ((rc = upload(c, B.d_hub_ids, B.hubs.data(), B.hubs.size()))) return rc;
+            if (walk) {   // the pair kernels' hub lookup: slot j | hot tag << 30
+                std::vector<int32_t> ho((size_t)V, -1);
+                for (int64_t j = 0; j < H; ++j) ho[B.hubs[j]] = (int32_t)(j | ((int64_t)hubhot[j] << 30));
+                if ((rc = upload(c, B.d_hub_of, ho.data(), ho.size()))) return rc;
+            }
         }
     }
     // LINE-2: one alias table per block over its atoms and one over the part's
@@ -757,6 +783,7 @@ int smore_block_train_edges_async(smore_ctx* c, int block, uint64_t begin, uint6
     const uint64_t na = B.atom_off[block + 1] - B.atom_off[block];
     if (na == 0 && B.nhub == 0) return fail(c, SMORE_EINVAL, "block without atoms (mass 0) asked for samples");
     EdgeArgs a = cell_args(c, block, false);
+    if (const char* e = getenv("SMORE_EDGE_CHUNK")) a.pair_slice = (uint32_t)std::max(0, atoi(e));
     a.total = total;
     a.seed = seed;
     a.alpha0 = alpha0;

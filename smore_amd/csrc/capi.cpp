@@ -12,8 +12,10 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
 #include <limits>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -2019,6 +2021,155 @@ int smore_train_pairs_rows(smore_ctx* c, const int32_t* v, const int32_t* cc, in
     if ((rc = rows_io_async(c, 1, c_ids, nc, c_rows, false))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipGetLastError());
+    return SMORE_OK;
+}
+
+// ---------------------------------------------------------------- combining
+// The reference's callers run UpdatePairs from `workers` goroutines at once,
+// each on its own walk's ~380 pairs (internal/models/deepwalk/deepwalk.go:
+// 96-120; pkg/pronet/optimizer.go:8-18).  A GPU call per batch costs a
+// synchronisation and two small transfers whatever the batch, so a serialised
+// hook loses to the CPU path once two goroutines run.  Flat combining: every
+// caller queues its request; whichever finds the context idle becomes the
+// leader, takes every request queued so far and runs them as ONE call -- the
+// union of their rows up once (each row from the earliest request that holds
+// it), the batches' pair kernels in queue order on the stream (each batch sees
+// the rows the earlier ones wrote: the serial order of the queue), the union
+// back once, every request's rows copied out of it -- then wakes the others.
+// A caller whose request ran in another's call returns its status.
+struct PairReq {
+    const int32_t *v, *cc;
+    int64_t n;
+    int K;
+    double alpha;
+    uint64_t seed, unit;
+    int mode;
+    const int32_t* w_ids;
+    int64_t nw;
+    float* w_rows;
+    const int32_t* c_ids;
+    int64_t nc;
+    float* c_rows;
+    int rc = SMORE_OK;
+    bool done = false;
+};
+
+struct PairCombiner {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<PairReq*> q;
+    bool busy = false;
+    uint64_t calls = 0, requests = 0;   // combined device calls, requests served
+};
+
+namespace {
+// the union of the requests' rows of one table: sorted unique ids, and per id
+// its first (request, row) in queue order
+struct RowUnion {
+    std::vector<int32_t> ids;
+    std::vector<float> rows;
+};
+
+void row_union(const std::vector<PairReq*>& reqs, int which, int dim, RowUnion& u) {
+    struct Src {
+        int32_t id;
+        uint32_t req;
+        int64_t pos;
+    };
+    std::vector<Src> all;
+    for (uint32_t r = 0; r < reqs.size(); ++r) {
+        const PairReq* q = reqs[r];
+        const int32_t* ids = which ? q->c_ids : q->w_ids;
+        const int64_t n = which ? q->nc : q->nw;
+        for (int64_t i = 0; i < n; ++i) all.push_back({ids[i], r, i});
+    }
+    std::stable_sort(all.begin(), all.end(), [](const Src& a, const Src& b) { return a.id < b.id; });
+    u.ids.clear();
+    u.rows.clear();
+    for (size_t i = 0; i < all.size(); ++i) {
+        if (i && all[i].id == all[i - 1].id) continue;   // the earliest request's copy
+        u.ids.push_back(all[i].id);
+        const PairReq* q = reqs[all[i].req];
+        const float* src = (which ? q->c_rows : q->w_rows) + all[i].pos * dim;
+        u.rows.insert(u.rows.end(), src, src + dim);
+    }
+}
+
+void row_scatter(const std::vector<PairReq*>& reqs, int which, int dim, const RowUnion& u) {
+    for (PairReq* q : reqs) {
+        const int32_t* ids = which ? q->c_ids : q->w_ids;
+        const int64_t n = which ? q->nc : q->nw;
+        float* dst = which ? q->c_rows : q->w_rows;
+        for (int64_t i = 0; i < n; ++i) {
+            const size_t k = (size_t)(std::lower_bound(u.ids.begin(), u.ids.end(), ids[i]) - u.ids.begin());
+            std::copy(u.rows.begin() + k * dim, u.rows.begin() + (k + 1) * dim, dst + i * dim);
+        }
+    }
+}
+}  // namespace
+
+int smore_train_pairs_rows_mt(smore_ctx* c, const int32_t* v, const int32_t* cc, int64_t n, int K, double alpha,
+                              uint64_t seed, uint64_t unit, int mode, const int32_t* w_ids, int64_t nw, float* w_rows,
+                              const int32_t* c_ids, int64_t nc, float* c_rows) {
+    if (!c) return SMORE_EINVAL;
+    if (n < 0 || nw < 0 || nc < 0 || (n > 0 && (!v || !cc)) || (nw > 0 && (!w_ids || !w_rows)) ||
+        (nc > 0 && (!c_ids || !c_rows)))
+        return SMORE_EINVAL;
+    std::shared_ptr<PairCombiner> pc;
+    {
+        static std::mutex create_mu;   // the context's combiner, made once
+        std::lock_guard<std::mutex> g(create_mu);
+        if (!c->pair_comb) c->pair_comb = std::make_shared<PairCombiner>();
+        pc = c->pair_comb;
+    }
+    PairReq me{v, cc, n, K, alpha, seed, unit, mode, w_ids, nw, w_rows, c_ids, nc, c_rows};
+    std::unique_lock<std::mutex> lk(pc->mu);
+    pc->q.push_back(&me);
+    pc->cv.wait(lk, [&] { return me.done || !pc->busy; });
+    if (me.done) return me.rc;
+    // leader: every queued request (its own among them) in one device call
+    pc->busy = true;
+    std::vector<PairReq*> reqs;
+    reqs.swap(pc->q);
+    lk.unlock();
+    int rc = SMORE_OK;
+    const int dim = c->dim;
+    RowUnion uw, uc;
+    if (dim <= 0) rc = fail(c, SMORE_ESTATE, "tables not allocated");
+    if (!rc) {
+        row_union(reqs, 0, dim, uw);
+        row_union(reqs, 1, dim, uc);
+        rc = rows_io_async(c, 0, uw.ids.data(), (int64_t)uw.ids.size(), uw.rows.data(), true);
+        if (!rc) rc = rows_io_async(c, 1, uc.ids.data(), (int64_t)uc.ids.size(), uc.rows.data(), true);
+    }
+    for (PairReq* q : reqs) {
+        q->rc = rc ? rc : train_pairs_core(c, q->v, q->cc, q->n, q->K, q->alpha, q->seed, q->unit, q->mode);
+    }
+    if (!rc) rc = rows_io_async(c, 0, uw.ids.data(), (int64_t)uw.ids.size(), uw.rows.data(), false);
+    if (!rc) rc = rows_io_async(c, 1, uc.ids.data(), (int64_t)uc.ids.size(), uc.rows.data(), false);
+    if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = fail(c, SMORE_EHIP, "pairs combine: sync");
+    if (!rc) {
+        row_scatter(reqs, 0, dim, uw);
+        row_scatter(reqs, 1, dim, uc);
+    }
+    lk.lock();
+    for (PairReq* q : reqs) {
+        if (rc) q->rc = rc;
+        q->done = true;
+    }
+    pc->calls++;
+    pc->requests += reqs.size();
+    pc->busy = false;
+    lk.unlock();
+    pc->cv.notify_all();
+    return me.rc;
+}
+
+int smore_pairs_combine_stats(const smore_ctx* c, uint64_t* calls, uint64_t* requests) {
+    if (!c) return SMORE_EINVAL;
+    std::shared_ptr<PairCombiner> pc = c->pair_comb;
+    if (calls) *calls = pc ? pc->calls : 0;
+    if (requests) *requests = pc ? pc->requests : 0;
     return SMORE_OK;
 }
 

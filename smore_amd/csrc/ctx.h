@@ -55,6 +55,9 @@ struct smore_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     int last_mode = -1;                 // scatter (SMORE_* mode) the last timed training call ran
+    // smore_train_pairs_rows_mt: the combining queue of concurrent callers
+    // (capi.cpp PairCombiner; created on first use)
+    std::shared_ptr<struct PairCombiner> pair_comb;
     int64_t blk_hubs = -1;              // hub C rows of the block schedule (smore_block_set_hubs; -1 automatic)
     int64_t c_slots = 0;                // rows after V in the C table (the block schedule's hub slots)
     int cus = 0;
@@ -190,6 +193,7 @@ struct smore_ctx {
         std::vector<double> hub_p;      // LINE-2: per block, a cell sample's probability of being a hub atom
         uint2* d_hub_ntab = nullptr;    // nb x H: block k's negative alias entries of the hub slots
         int32_t* d_hub_ids = nullptr;   // H: the hubs' C rows (slot gather / scatter)
+        int32_t* d_hub_of = nullptr;    // walks: V entries, -1 or the vertex's slot | hot tag << 30
         float* d_hub_ex[3] = {nullptr, nullptr, nullptr};   // group exchange over the slots: S, D, R
         float* d_hub_scale = nullptr;   // group exchange: per-slot scales (adaptive rule)
         std::string hub_scale_key;

@@ -744,8 +744,16 @@ edge_train_kernel(EdgeArgs a) {
         // XCD clocks) takes fewer chunks instead of stretching the launch by
         // a whole fixed share.  Within a chunk the block's groups take samples
         // c0 + gib, c0 + gib + gpb, ... with the row prefetch above.
+        // Chunks shrink for a short launch (a cell of the 2-D block schedule:
+        // ~8M samples over ~768 blocks is ~5 chunks of CH_ROUNDS per block,
+        // so the last chunks leave most blocks idle): about 16 chunks per
+        // block, at least 8 rounds each, at most CH_ROUNDS (a one-GPU launch
+        // of 2^27 samples keeps CH_ROUNDS).
         __shared__ uint64_t s_next;
-        const uint64_t span = CH_ROUNDS * gpb;
+        uint64_t ch_rounds = count / ((uint64_t)gridDim.x * gpb * 16u);
+        ch_rounds = ch_rounds < 8 ? 8 : ch_rounds > CH_ROUNDS ? CH_ROUNDS : ch_rounds;
+        if (a.pair_slice && !a.alpha_rec) ch_rounds = a.pair_slice;   // fixed (SMORE_EDGE_CHUNK, experiments)
+        const uint64_t span = ch_rounds * gpb;
         auto grab = [&]() -> uint64_t {
             __syncthreads();   // every wave has read the previous s_next
             if (threadIdx.x == 0) s_next = atomicAdd(a.work, 1ull) * span;

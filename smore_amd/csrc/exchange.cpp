@@ -291,6 +291,9 @@ struct smore_group {
     // the block schedule's hub slots (blocks.cpp): per replica the event
     // after its exchange pass (compute stream) and after the all-reduce
     std::vector<hipEvent_t> hready, hdone;
+    // same-device studies (SMORE_LOCAL_SERIAL=1): the replicas' cells run one
+    // after another, each with the whole GPU as on its own device
+    std::vector<hipEvent_t> lser;
 };
 
 namespace {
@@ -758,6 +761,38 @@ int hub_ex_finish(smore_group* g) {
     return SMORE_OK;
 }
 
+// SMORE_LOCAL_SERIAL=1 on a same-device group: replica r's next launch
+// waits for the previous launch of replica r - 1 (of replica n - 1 for r = 0),
+// so cells never share the GPU -- each runs with the whole device's
+// concurrency, as on N GPUs (the quality studies' fidelity knob)
+bool local_serial(const smore_group* g) {
+    const char* e = getenv("SMORE_LOCAL_SERIAL");
+    return g->local && e && atoi(e) != 0;
+}
+
+int serial_before(smore_group* g, size_t r) {
+    if (!local_serial(g)) return SMORE_OK;
+    const size_t n = g->ctx.size();
+    if (g->lser.size() != n) {
+        g->lser.assign(n, nullptr);
+        for (size_t q = 0; q < n; ++q)
+            if (hipEventCreateWithFlags(&g->lser[q], hipEventDisableTiming) != hipSuccess)
+                return gfail(g, (int)q, fail(g->ctx[q], SMORE_EHIP, "serial events"));
+        for (size_t q = 0; q < n; ++q) (void)hipEventRecord(g->lser[q], g->ctx[q]->stream);
+    }
+    const size_t p = (r + n - 1) % n;
+    if (hipStreamWaitEvent(g->ctx[r]->stream, g->lser[p], 0) != hipSuccess)
+        return gfail(g, (int)r, fail(g->ctx[r], SMORE_EHIP, "serial wait"));
+    return SMORE_OK;
+}
+
+int serial_after(smore_group* g, size_t r) {
+    if (!local_serial(g)) return SMORE_OK;
+    if (hipEventRecord(g->lser[r], g->ctx[r]->stream) != hipSuccess)
+        return gfail(g, (int)r, fail(g->ctx[r], SMORE_EHIP, "serial record"));
+    return SMORE_OK;
+}
+
 // samples per row per replica per epoch of the LINE-2 block schedule (the C4
 // bench's one epoch per 2^27-sample step: 13.4 per row)
 constexpr double EDGE_BLOCK_PER_ROW = 13.42;
@@ -783,7 +818,9 @@ int group_block_edges(smore_group* g, uint64_t begin, uint64_t count, uint64_t p
     // a round's samples go to the replicas in proportion to their parts'
     // source mass, so the union of the parts draws SourceSample's law
     const std::vector<double>& pm = g->ctx[0]->blk.part_mass;
-    if ((rc = hub_ex_start(g, (double)std::min<uint64_t>(per, count / n) / nb))) return rc;
+    const char* se = getenv("SMORE_HUB_SPLIT");
+    const int split = se && atoi(se) > 1 ? std::min(64, atoi(se)) : 1;
+    if ((rc = hub_ex_start(g, (double)std::min<uint64_t>(per, count / n) / nb / split))) return rc;
     uint64_t S = 0;
     for (uint64_t k = 0; k < rounds; ++k) {
         const uint64_t lo = round_lo(k), m = round_lo(k + 1) - lo;
@@ -795,16 +832,22 @@ int group_block_edges(smore_group* g, uint64_t begin, uint64_t count, uint64_t p
             b += share[r];
         }
         for (int s = 0; s < nb; ++s, ++S) {
-            for (size_t r = 0; r < n; ++r) {
-                const int bk = (int)((2 * r + (size_t)s) % (size_t)nb);
-                if ((rc = block_wait(g, r, S))) return rc;
-                const uint64_t x = cnt[r][bk];
-                if (x && (rc = smore_block_train_edges_async(g->ctx[r], bk, begin + cur[r], x, total, K, alpha0,
-                                                             seed, mode)))
-                    return gfail(g, (int)r, rc);
-                cur[r] += x;
+            // a cell in `split` launches, the hub slots exchanged after each
+            // (SMORE_HUB_SPLIT; one by default)
+            for (int q = 0; q < split; ++q) {
+                for (size_t r = 0; r < n; ++r) {
+                    const int bk = (int)((2 * r + (size_t)s) % (size_t)nb);
+                    if (q == 0 && (rc = block_wait(g, r, S))) return rc;
+                    const uint64_t x0 = cnt[r][bk] * q / split, x = cnt[r][bk] * (q + 1) / split - x0;
+                    if ((rc = serial_before(g, r))) return rc;
+                    if (x && (rc = smore_block_train_edges_async(g->ctx[r], bk, begin + cur[r] + x0, x, total, K,
+                                                                 alpha0, seed, mode)))
+                        return gfail(g, (int)r, rc);
+                    if ((rc = serial_after(g, r))) return rc;
+                }
+                if ((rc = hub_ex_post(g))) return rc;
             }
-            if ((rc = hub_ex_post(g))) return rc;
+            for (size_t r = 0; r < n; ++r) cur[r] += cnt[r][(2 * r + (size_t)s) % (size_t)nb];
             if ((rc = group_rotate(g, S))) return rc;
         }
     }
@@ -825,6 +868,21 @@ int group_block_walks(smore_group* g, int rule, uint64_t walk_begin, uint64_t wa
         if ((rc = smore_block_setup(g->ctx[r], SMORE_CENSUS, (int)n, (int)r, K, mode))) return gfail(g, (int)r, rc);
     if ((rc = ensure_block_events(g))) return rc;
     if (per == 0 || per > WALK_BLOCK_ROUND) per = WALK_BLOCK_ROUND;
+    {   // the hub slots' exchange: pair records per replica per sub-round
+        const int L = walk_steps + 1;
+        double ppw = 0.0;   // expected pairs per walk (SkipGrams' random shrink / Walklets' two ranges)
+        for (int i = 0; i < L; ++i) {
+            if (rule == 1) {
+                ppw += (double)(std::min(L - 1, i + window) - std::min(L - 1, i + window_min - 1)) +
+                       (double)(std::max(0, i - window_min + 1) - std::max(0, i - window));
+            } else {
+                for (int r = 1; r <= window; ++r)
+                    ppw += (double)(std::min(L - 1, i + r) - std::max(0, i - r)) / window;
+            }
+        }
+        const double walks = (double)std::min<uint64_t>(per, walk_end - walk_begin);
+        if ((rc = hub_ex_start(g, std::max(1.0, walks * ppw / (double)(n * nb))))) return rc;
+    }
     uint64_t S = 0;
     for (uint64_t lo = walk_begin; lo < walk_end; lo += per) {
         const uint64_t hi = std::min(walk_end, lo + per);
@@ -835,12 +893,16 @@ int group_block_walks(smore_group* g, int rule, uint64_t walk_begin, uint64_t wa
         for (int s = 0; s < nb; ++s, ++S) {
             for (size_t r = 0; r < n; ++r) {
                 if ((rc = block_wait(g, r, S))) return rc;
+                if ((rc = serial_before(g, r))) return rc;
                 if ((rc = smore_block_train_walks_async(g->ctx[r], (int)((2 * r + (size_t)s) % (size_t)nb))))
                     return gfail(g, (int)r, rc);
+                if ((rc = serial_after(g, r))) return rc;
             }
+            if ((rc = hub_ex_post(g))) return rc;
             if ((rc = group_rotate(g, S))) return rc;
         }
     }
+    if ((rc = hub_ex_finish(g))) return rc;
     return block_finish(g, S);
 }
 
@@ -1170,6 +1232,8 @@ void smore_group_destroy(smore_group* g) {
     for (hipEvent_t e : g->hready)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : g->hdone)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : g->lser)
         if (e) (void)hipEventDestroy(e);
     if (g->ldone) (void)hipEventDestroy(g->ldone);
     delete g;

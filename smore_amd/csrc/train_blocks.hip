@@ -151,6 +151,21 @@ __device__ __forceinline__ void scale_ranges(int i, int L, int wmin, int wmax, i
     rg[1][1] = i + wmax >= L ? L - 1 : i + wmax;
 }
 
+// a walk pair's block and C word: the context's block and tagged id, or for
+// a hub context (b.hub_of) block (walk + i) mod nb and its slot id
+__device__ __forceinline__ int pair_block(const BlockArgs& b, int32_t cj, uint64_t walk, int i, int32_t& cw) {
+    const int32_t x = cj & ID_MASK;
+    if (b.hub_of) {
+        const int32_t h = b.hub_of[x];
+        if (h >= 0) {
+            cw = (b.V + (h & ID_MASK)) | (h & (1 << 30));
+            return (int)((walk + (uint64_t)i) % (uint64_t)b.nb);
+        }
+    }
+    cw = cj & (ID_MASK | (1 << 30));
+    return block_of(b, x);
+}
+
 // per (block, walk) pair counts of the owned centers: count[k * nwalks + t]
 __global__ void __launch_bounds__(256) block_pair_count_kernel(WalkArgs w, BlockArgs b, uint64_t seed,
                                                                uint32_t* count) {
@@ -177,7 +192,10 @@ __global__ void __launch_bounds__(256) block_pair_count_kernel(WalkArgs w, Block
         if (v < w.own_lo || v >= w.own_hi) continue;
         for (int q = 0; q < nr; ++q)
             for (int j = rg[q][0]; j <= rg[q][1]; ++j)
-                if (j != i) cnt[block_of(b, walk[j] & ID_MASK)]++;
+                if (j != i) {
+                    int32_t cw;
+                    cnt[pair_block(b, walk[j], w.walk_begin + t, i, cw)]++;
+                }
     }
     for (int k = 0; k < b.nb; ++k) count[(uint64_t)k * w.nwalks + t] = cnt[k];
 }
@@ -219,12 +237,12 @@ __global__ void __launch_bounds__(256) block_pair_emit_kernel(WalkArgs w, BlockA
                     slot += 2u * (uint32_t)K;
                     continue;
                 }
-                const int32_t cj = walk[j];
-                const int k = block_of(b, cj & ID_MASK);
+                int32_t cw;
+                const int k = pair_block(b, walk[j], unit, i, cw);
                 int32_t x[RW];
-                // W row walk[i] with its W tag, C row walk[j] with its C tag
+                // W row walk[i] with its W tag, C row walk[j] (or its hub slot) with its C tag
                 x[0] = v | (int32_t)((((uint32_t)vi >> 31) & 1u) << 30);
-                x[1] = cj & (ID_MASK | (1 << 30));
+                x[1] = cw;
 #pragma unroll
                 for (int n = 0; n < RW - 2; ++n) x[2 + n] = -1;
 #pragma unroll

@@ -232,6 +232,10 @@ struct BlockArgs {
     uint64_t hub_off;
     uint32_t nhub, hub_thr;
     int32_t H, V;
+    // walk cells: per vertex -1, or its hub slot j | hot tag << 30; a pair
+    // whose context is a hub goes to block (walk + center position) mod nb
+    // (a center's hub pairs stay together) as slot id V + j
+    const int32_t* hub_of;
 };
 hipError_t launch_block_draw(const BlockArgs& b, int blk, uint64_t seed, uint64_t begin, uint64_t count, int K,
                              int32_t* rec, hipStream_t st);

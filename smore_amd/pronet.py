@@ -365,6 +365,17 @@ class ProNet:
                                              int(unit), _lib.MODE[mode], ptr(w_ids), len(w_ids), ptr(w_rows),
                                              ptr(c_ids), len(c_ids), ptr(c_rows)), "train_pairs_rows")
 
+    def train_pairs_rows_mt(self, v, c, K, alpha, seed, unit, mode, w_ids, w_rows, c_ids, c_rows):
+        """smore_train_pairs_rows_mt: as train_pairs_rows, safe from concurrent
+        threads (their calls are combined into one device call)."""
+        v, c = self._ids(v, "train_pairs_rows_mt"), self._ids(c, "train_pairs_rows_mt")
+        w_ids, c_ids = self._ids(w_ids, "train_pairs_rows_mt"), self._ids(c_ids, "train_pairs_rows_mt")
+        assert w_rows.dtype == np.float32 and w_rows.flags.c_contiguous and c_rows.dtype == np.float32
+        assert c_rows.flags.c_contiguous
+        self._chk(lib.smore_train_pairs_rows_mt(self.ctx, ptr(v), ptr(c), len(v), int(K), float(alpha), int(seed),
+                                                int(unit), _lib.MODE[mode], ptr(w_ids), len(w_ids), ptr(w_rows),
+                                                ptr(c_ids), len(c_ids), ptr(c_rows)), "train_pairs_rows_mt")
+
     def census_begin(self):
         """Row census: the following walk-model calls count the rows their
         records would update instead of training (smore_census_begin)."""

@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--combine-rows", type=int, default=None, help="hybrid: LDS write-combined rows (0: off)")
     ap.add_argument("--skip-one", action="store_true", help="no one-GPU reference (profiling the cells alone)")
     ap.add_argument("--hubs", type=int, default=-1, help="line2: hub C rows (-1 the library's default, 0 none)")
+    ap.add_argument("--split", type=int, default=1, help="line2: launches per cell (the hub slots' exchanges)")
     args = ap.parse_args()
 
     import torch  # noqa: F401  (one HIP runtime with torch, as bench.py)
@@ -105,19 +106,26 @@ def main():
                 cnt = pn.block_counts(S)      # weak scaling: S samples per GPU per epoch, as bench.py
                 mine = S
 
+                def cell(b, b0, x, sync):
+                    for q in range(args.split):      # the cell in --split launches
+                        lo, hi = x * q // args.split, x * (q + 1) // args.split
+                        if hi > lo:
+                            pn.block_train_edges(b, b0 + lo, hi - lo, total, K, 0.025, args.seed, args.mode,
+                                                 sync=sync and q + 1 == args.split)
+
                 def epoch():
                     b0 = 0
                     for s in range(nb):
                         b = (2 * r + s) % nb
                         if cnt[b]:
-                            pn.block_train_edges(b, b0, int(cnt[b]), total, K, 0.025, args.seed, args.mode, sync=False)
+                            cell(b, b0, int(cnt[b]), False)
                         b0 += int(cnt[b])
                 ep = timed(epoch)
                 for s in range(nb):      # per-cell launch times (one pass, synchronised per cell)
                     b = (2 * r + s) % nb
                     if cnt[b]:
                         t1 = time.perf_counter()
-                        pn.block_train_edges(b, 0, int(cnt[b]), total, K, 0.025, args.seed, args.mode)
+                        cell(b, 0, int(cnt[b]), True)
                         ph = pn.last_phase_ms()
                         cells.append([b, int(cnt[b]), round((time.perf_counter() - t1) * 1e3, 3)] +
                                      ([round(ph[0], 3), round(ph[1], 3)] if ph else []))
@@ -138,7 +146,7 @@ def main():
                     pn.block_train_walks(b)
                     cells.append([b, int(recs[b]), round((time.perf_counter() - t1) * 1e3, 3)])
             row = {"config": args.config, "model": args.model, "nparts": n, "part": r, "setup_s": round(setup_s, 2),
-                   "hubs": int(pn.block_hubs()[0]),
+                   "hubs": int(pn.block_hubs()[0]), "split": args.split,
                    "epoch_ms": round(ep * 1e3, 3), "units": units_r,
                    "rate_M_per_s": round(units_r / ep / 1e6, 2),
                    "per_gpu_factor": round((units_r / ep) / (units / one), 4) if one else None,

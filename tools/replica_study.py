@@ -192,6 +192,8 @@ def main():
                     "walk_partition": args.walk_partition,
                     "hubs": int(p.block_hubs()[0]) if n > 1 and args.schedule == "blocks" else 0,
                     "neg_law": os.environ.get("SMORE_NEG_LAW", "1"), "hub_c0": os.environ.get("SMORE_HUB_C0", ""),
+                    "hub_split": os.environ.get("SMORE_HUB_SPLIT", ""),
+                    "local_serial": os.environ.get("SMORE_LOCAL_SERIAL", ""),
                     "finite": bool(np.isfinite(W).all() and np.isfinite(C).all()),
                     "loss": round(heldout_loss(W, C, held), 5), "auc": round(edge_auc(W, C, off, tgt), 5),
                     "replica_spread_rel": spread, "wall_s": round(el, 2)})
