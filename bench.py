@@ -294,20 +294,22 @@ def run_block_step(pn, bsync, k, world, rank, S, total, K, seed, mode, cell_even
     timed region, so no host wait inside it)."""
     import torch
     base = k * world * S
+    L = pn.block_cell_launches()      # a cell in L launches, the hub slots exchanged after each
     for s, b, lo, n in block_schedule(world * S, S, world, rank, pn.block_counts, pn.block_part_mass()):
         assert bsync.block() == b
 
-        def train(blk, lo=lo, n=n):
-            if n:
+        def train(blk, q=0, lo=lo, n=n):
+            x0, x1 = n * q // L, n * (q + 1) // L
+            if x1 > x0:
                 ev = None
                 if cell_events is not None:
                     ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                     ev[0].record()
-                pn.block_train_edges(blk, base + lo, n, total, K, 0.025, seed, mode, sync=False)
+                pn.block_train_edges(blk, base + lo + x0, x1 - x0, total, K, 0.025, seed, mode, sync=False)
                 if ev is not None:
                     ev[1].record()
                     cell_events.append(ev)
-        bsync.sub_round(train)
+        bsync.sub_round(train, L)
 
 
 def run_step(pn, sync, k, world, rank, S, n_launch, n_ex, total, K, seed, mode, sync_every, on_launch=None):
@@ -461,7 +463,7 @@ def main():
         wb, cb = pn.block_bounds()
         # the hub C rows' slots: every cell trains them, exchanged after every
         # sub-round (S / 2N samples per rank)
-        hubs = block_hubs(pn, args.samples / (2 * world))
+        hubs = block_hubs(pn, args.samples / (2 * world) / pn.block_cell_launches())
         setup["hubs"] = int(pn.block_hubs()[0])
         bsync = BlockSync(table_tensor(pn, 0), table_tensor(pn, 1), wb, cb, hubs=hubs)
         if rank == 0:

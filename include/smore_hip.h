@@ -616,8 +616,9 @@ int smore_block_neg_scale(const smore_ctx* ctx, int block, double* weight);
  * touches per sample are taken out of the rotating blocks; every cell draws
  * them (contexts and negatives, with 1/nb of their mass) on its part's own
  * copy in the C table's slot rows V .. V + H - 1, kept equal over the parts by
- * an exchange after every sub-round.  -1: automatic (4096, at most V / 8nb),
- * 0: none.  Takes effect at the next smore_block_setup. */
+ * an exchange after every launch.  -1: automatic (LINE-2: none at 2 parts,
+ * else 4096, at most V / 8nb; walk models: none), 0: none.  Takes effect at
+ * the next smore_block_setup. */
 int smore_block_set_hubs(smore_ctx* ctx, int64_t hubs);
 /* the setup's hubs: count, the first slot row (V), their C rows and expected
  * touches per sample (each array H entries, or null) */
@@ -629,6 +630,10 @@ int smore_block_hubs_store(smore_ctx* ctx);
 /* the slots' exchange scales for `samples` per part per exchange and c0 (the
  * adaptive rule of SMORE_SYNC_ADAPTIVE over the nparts parts; H floats) */
 int smore_block_hub_scales(const smore_ctx* ctx, double samples, double c0, float* scales);
+/* LINE-2: launches per cell of the setup (4 with hub slots, else 1;
+ * $SMORE_CELL_LAUNCHES overrides): a cell's samples are trained in this many
+ * consecutive launches with the hub slots exchanged after each */
+int smore_block_cell_launches(const smore_ctx* ctx);
 /* LINE-2: samples [begin, begin + count) (Philox units; LINE's learning rate
  * from the global index as smore_train_edges) drawn from cell (part, block) and
  * trained, asynchronously on the context stream */

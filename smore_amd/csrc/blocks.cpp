@@ -155,11 +155,17 @@ bool neg_law_on() {
 
 // hub C rows of a block setup (smore_block_set_hubs / $SMORE_HUBS; -1:
 // automatic), at most the C table's slot rows and half the vertices
+// Automatic: none at 2 parts (a cell's rows are only 4 times hotter than
+// one GPU's, and the hub copies' exchange costs more than it saves: C4 at
+// 2^34 samples 1.057 vs 1.008 times one GPU's held-out loss), else 4096 --
+// C4 at 8 parts: the five hub cells (10-14 ms against 7.7) disappear.
 constexpr int64_t HUB_AUTO = 4096;
-int64_t hub_count(const smore_ctx* c, int64_t V, int nb) {
+// Walk cells: none unless asked for (C5 DeepWalk at 8 parts with 4096:
+// 1.14 times one GPU's held-out loss against 1.02 without).
+int64_t hub_count(const smore_ctx* c, int64_t V, int nb, bool walk) {
     int64_t h = c->blk_hubs;
     if (const char* e = getenv("SMORE_HUBS")) h = atoll(e);
-    if (h < 0) h = std::min<int64_t>(HUB_AUTO, V / (8 * (int64_t)nb));
+    if (h < 0) h = nb <= 4 || walk ? 0 : std::min<int64_t>(HUB_AUTO, V / (8 * (int64_t)nb));
     return std::max<int64_t>(0, std::min(std::min(h, c->c_slots), V / 2));
 }
 
@@ -260,6 +266,17 @@ void hub_scales(const smore_ctx::Blocks& B, double samples, double c0, float* ou
     }
 }
 
+// launches per LINE-2 cell: with hub slots, 4 -- the slots are exchanged
+// after each, so their copies are at most a quarter cell apart (C4, 8 parts:
+// 1.042 times one GPU's held-out loss against 1.079 with one launch per
+// cell, at 6.27 against 6.55 predicted); without, 1.  SMORE_CELL_LAUNCHES
+// overrides (1..64).
+int cell_launches(const smore_ctx::Blocks& B) {
+    int k = B.H > 0 && B.model == SMORE_LINE2 ? 4 : 1;
+    if (const char* e = getenv("SMORE_CELL_LAUNCHES")) k = atoi(e);
+    return std::max(1, std::min(64, k));
+}
+
 // largest remainder of n * mass[k] (ties to the lower index)
 void largest_remainder(uint64_t n, const double* mass, int parts, uint64_t* counts) {
     std::vector<std::pair<double, int>> rem;
@@ -315,7 +332,7 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
     const int64_t V = g.V;
     const int nb = 2 * nparts;
     if (V < nb) return fail(c, SMORE_EINVAL, "block schedule: fewer vertices than blocks");
-    const int64_t H = hub_count(c, V, nb);
+    const int64_t H = hub_count(c, V, nb, walk);
     char key[288];
     snprintf(key, sizeof key, "%d/%d/%d/%d/%d/%lld/%lld/%d/%d/%d/%.9g/%lld/%s", model, nparts, part, K, mode,
              (long long)V, (long long)g.E, c->dpad, c->sh_max, c->sh_flush, c->hot_tau, (long long)H,
@@ -714,6 +731,11 @@ int smore_block_hubs_store(smore_ctx* c) {
     HIPCHK(c, launch_rows_scatter(C, c->blk.d_hub_ids, (uint64_t)c->blk.H, c->dpad, C + (size_t)c->g->V * c->dpad,
                                   c->stream));
     return SMORE_OK;
+}
+
+int smore_block_cell_launches(const smore_ctx* c) {
+    if (!c || !c->blk.nb) return 1;
+    return cell_launches(c->blk);
 }
 
 int smore_block_hub_scales(const smore_ctx* c, double samples, double c0, float* scales) {

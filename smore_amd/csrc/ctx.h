@@ -228,6 +228,8 @@ constexpr int64_t HUB_SLOTS_MAX = 65536;
 
 // blocks.cpp: frees the block tables (a new graph, smore_destroy)
 void blocks_release(smore_ctx* c);
+// blocks.cpp: launches per LINE-2 cell (the hub slots are exchanged after each)
+int cell_launches(const smore_ctx::Blocks& B);
 // blocks.cpp: the hub slots' exchange scales for `samples` per part per exchange
 void hub_scales(const smore_ctx::Blocks& B, double samples, double c0, float* out);
 // blocks.cpp: counts[k] = n * mass[k] by largest remainder (ties to the lower k)

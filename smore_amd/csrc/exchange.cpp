@@ -818,8 +818,7 @@ int group_block_edges(smore_group* g, uint64_t begin, uint64_t count, uint64_t p
     // a round's samples go to the replicas in proportion to their parts'
     // source mass, so the union of the parts draws SourceSample's law
     const std::vector<double>& pm = g->ctx[0]->blk.part_mass;
-    const char* se = getenv("SMORE_HUB_SPLIT");
-    const int split = se && atoi(se) > 1 ? std::min(64, atoi(se)) : 1;
+    const int split = cell_launches(g->ctx[0]->blk);
     if ((rc = hub_ex_start(g, (double)std::min<uint64_t>(per, count / n) / nb / split))) return rc;
     uint64_t S = 0;
     for (uint64_t k = 0; k < rounds; ++k) {
@@ -833,7 +832,7 @@ int group_block_edges(smore_group* g, uint64_t begin, uint64_t count, uint64_t p
         }
         for (int s = 0; s < nb; ++s, ++S) {
             // a cell in `split` launches, the hub slots exchanged after each
-            // (SMORE_HUB_SPLIT; one by default)
+            // (blocks.cpp cell_launches)
             for (int q = 0; q < split; ++q) {
                 for (size_t r = 0; r < n; ++r) {
                     const int bk = (int)((2 * r + (size_t)s) % (size_t)nb);

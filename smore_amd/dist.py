@@ -292,14 +292,21 @@ class BlockSync:
                 post()
             self.pending[slot] = None
 
-    def sub_round(self, train):
-        """Train this rank's cell of the next sub-round and start its rotation."""
+    def sub_round(self, train, parts=1):
+        """Train this rank's cell of the next sub-round and start its rotation.
+        parts > 1: the cell in `parts` launches, train(block, q) for q in
+        range(parts), the hub slots exchanged after each (blocks.cpp
+        cell_launches)."""
         s = self.s
         self._wait(s & 1)               # the block received at sub-round s - 2
         b = self.block(s)
-        train(b)
-        if self.hub_sync is not None:
-            self.hub_sync.begin()       # the hub slots' deltas, one late, ahead of the rotation
+        for q in range(parts):
+            if parts == 1:
+                train(b)
+            else:
+                train(b, q)
+            if self.hub_sync is not None:
+                self.hub_sync.begin()   # the hub slots' deltas, one late, ahead of the rotation
         send, recv = self.rows(b), self.rows((b + 2) % self.nb)
         dst = self.ranks[(self.rank - 1) % self.world]
         src = self.ranks[(self.rank + 1) % self.world]
@@ -316,10 +323,10 @@ class BlockSync:
         self.pending[s & 1] = (dist.batch_isend_irecv(ops), post)
         self.s += 1
 
-    def epoch(self, train):
+    def epoch(self, train, parts=1):
         """nb sub-rounds: every cell of this rank's W part once."""
         for _ in range(self.nb):
-            self.sub_round(train)
+            self.sub_round(train, parts)
 
     def holder(self, b):
         """The rank holding C block b's latest rows once the transfers drained."""

@@ -285,6 +285,10 @@ class ProNet:
     def block_hubs_store(self):
         self._chk(lib.smore_block_hubs_store(self.ctx), "block_hubs_store")
 
+    def block_cell_launches(self):
+        """LINE-2: launches per cell (the hub slots exchanged after each)."""
+        return int(lib.smore_block_cell_launches(self.ctx))
+
     def block_hub_scales(self, samples, c0):
         h = self.block_hubs()[0]
         out = np.zeros(max(1, h), np.float32)

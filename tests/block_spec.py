@@ -63,9 +63,9 @@ def prob_thr(p):
 
 
 def hub_count(V, nb, hubs=-1, c_slots=None):
-    """blocks.cpp hub_count: -1 automatic (4096, at most V / 8nb)."""
+    """blocks.cpp hub_count: -1 automatic (none at 2 parts, else 4096, at most V / 8nb)."""
     c_slots = min(65536, V) if c_slots is None else c_slots
-    h = min(4096, V // (8 * nb)) if hubs < 0 else hubs
+    h = (0 if nb <= 4 else min(4096, V // (8 * nb))) if hubs < 0 else hubs
     return max(0, min(h, c_slots, V // 2))
 
 

@@ -202,17 +202,17 @@ def _hub_scale():
     return torch.tensor([1.0, 0.75, 0.5])
 
 
-def _cell_hubs(W, C, wb, cb, r, b, s):
-    """A cell that touches W part r, C block b and the hub slots (the shape of
-    a LINE-2 cell with hub atoms and hub negatives)."""
-    _cell(W, C, wb, cb, r, b, s)
+def _cell_hubs(W, C, wb, cb, r, b, s, q=0):
+    """A launch (part q of a cell) that touches W part r, C block b and the hub
+    slots (the shape of a LINE-2 cell with hub atoms and hub negatives)."""
+    _cell(W, C, wb, cb, r, b, s + 7 * q)
     h = C[V:V + HUBS]
     w = W[wb[r]:wb[r + 1]]
-    h.mul_(0.995).add_(torch.tanh(w.mean(0) + h) * (0.01 * (r + 1)) + 0.0005 * (b + s))
+    h.mul_(0.995).add_(torch.tanh(w.mean(0) + h) * (0.01 * (r + 1)) + 0.0005 * (b + s + q))
     w.add_(h.mean(0) * 0.01)
 
 
-def _reference_hubs(world, subrounds, hub_rows):
+def _reference_hubs(world, subrounds, hub_rows, parts=1):
     """BlockSync with hubs restated in one process: per-rank tables, cells in
     sub-round order, after each sub-round the slots' begin / cycle passes and
     the summed deltas, then the rotation; at the end the last exchange's end,
@@ -229,22 +229,23 @@ def _reference_hubs(world, subrounds, hub_rows):
     sc = _hub_scale().view(-1, 1)
     pending = False
     for s in range(subrounds):
-        for r in range(world):
-            _cell_hubs(Ws[r], Cs[r], wb, cb, r, (2 * r + s) % nb, s)
-        for r in range(world):
-            T = Cs[r][V:]
-            if pending:                       # TorchPasses.cycle: end, then begin
-                R[r].mul_(sc).sub_(Dd[r])
-                T.add_(R[r])
-                S[r].add_(R[r])
-            torch.sub(T, S[r], out=Dd[r])
-            R[r].copy_(Dd[r])
-            S[r].copy_(T)
-        tot = R[0].clone()
-        for r in range(1, world):
-            tot += R[r]
-        R = [tot.clone() for _ in range(world)]
-        pending = True
+        for q in range(parts):
+            for r in range(world):
+                _cell_hubs(Ws[r], Cs[r], wb, cb, r, (2 * r + s) % nb, s, q)
+            for r in range(world):
+                T = Cs[r][V:]
+                if pending:                       # TorchPasses.cycle: end, then begin
+                    R[r].mul_(sc).sub_(Dd[r])
+                    T.add_(R[r])
+                    S[r].add_(R[r])
+                torch.sub(T, S[r], out=Dd[r])
+                R[r].copy_(Dd[r])
+                S[r].copy_(T)
+            tot = R[0].clone()
+            for r in range(1, world):
+                tot += R[r]
+            R = [tot.clone() for _ in range(world)]
+            pending = True
         moved = [Cs[r][cb[(2 * r + s) % nb]:cb[(2 * r + s) % nb + 1]].clone() for r in range(world)]
         for r in range(world):
             b = (2 * r + s) % nb
@@ -262,7 +263,7 @@ def _reference_hubs(world, subrounds, hub_rows):
     return W, C
 
 
-def _worker_hubs(rank, world, port, subrounds, out):
+def _worker_hubs(rank, world, port, subrounds, out, parts=1):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -282,9 +283,12 @@ def _worker_hubs(rank, world, port, subrounds, out):
     bs = BlockSync(W, C[:V], wb, cb, hubs=hubs)
     for _ in range(subrounds):
         s = bs.s
-        bs.sub_round(lambda b: _cell_hubs(W, C, wb, cb, rank, b, s))
+        if parts == 1:
+            bs.sub_round(lambda b: _cell_hubs(W, C, wb, cb, rank, b, s))
+        else:
+            bs.sub_round(lambda b, q: _cell_hubs(W, C, wb, cb, rank, b, s, q), parts)
     bs.finish(gather=True)
-    RW, RC = _reference_hubs(world, subrounds, hub_rows)
+    RW, RC = _reference_hubs(world, subrounds, hub_rows, parts)
     exact = world == 2            # sums of 2 are order-free; gloo's ring may add 3+ in another order
     if exact:
         ok = torch.equal(W, RW) and torch.equal(C[:V], RC)
@@ -295,15 +299,16 @@ def _worker_hubs(rank, world, port, subrounds, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,subrounds", [(2, 4), (2, 9), (3, 7), (4, 8)])
-def test_block_rotation_with_hubs_gloo(world, subrounds):
-    """BlockSync with hub slots over gloo equals its one-process restatement
-    (bit for bit at 2 ranks), and every rank ends with the hub rows equal to
-    the exchanged slots."""
+@pytest.mark.parametrize("world,subrounds,parts", [(2, 4, 1), (2, 9, 4), (3, 7, 1), (4, 8, 4)])
+def test_block_rotation_with_hubs_gloo(world, subrounds, parts):
+    """BlockSync with hub slots over gloo (cells in 1 or 4 launches, the slots
+    exchanged after each) equals its one-process restatement (bit for bit at
+    2 ranks), and every rank ends with the hub rows equal to the exchanged
+    slots."""
     ctx = mp.get_context("spawn")
     out = ctx.Array("i", [0] * world)
     port = _free_port()
-    procs = [ctx.Process(target=_worker_hubs, args=(r, world, port, subrounds, out)) for r in range(world)]
+    procs = [ctx.Process(target=_worker_hubs, args=(r, world, port, subrounds, out, parts)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

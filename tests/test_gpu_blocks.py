@@ -140,6 +140,30 @@ def test_block_cell_serial_equals_oracle(smore, graph):
     pn.close()
 
 
+def _hub_exchange(n, V, Cs, Ss, Ds, Rs, sc, pending):
+    """The hub slots' one-late exchange after a launch of every replica
+    (replica_sync.hip begin / cycle passes in fp32, the all-reduce summing the
+    replicas in order); returns the new pending state."""
+    for r in range(n):
+        T = Cs[r][V:]
+        if pending:
+            X = sc * Rs[r] - Ds[r]
+            tn, sn = T + X, Ss[r] + X
+            Ds[r] = tn - sn
+            T[:] = tn
+            Ss[r] = tn.copy()
+        else:
+            Ds[r] = T - Ss[r]
+            Ss[r] = T.copy()
+        Rs[r] = Ds[r].copy()
+    tot = Rs[0].copy()
+    for r in range(1, n):
+        tot = tot + Rs[r]
+    for r in range(n):
+        Rs[r] = tot.copy()
+    return True
+
+
 def _schedule_edges(smore, graph, n, begin, count, per, total, K, dim, W0, C0, hubs=-1):
     """exchange.cpp group_block_edges restated: rounds of per * n samples
     split over the replicas by their parts' source mass (largest remainder),
@@ -160,7 +184,9 @@ def _schedule_edges(smore, graph, n, begin, count, per, total, K, dim, W0, C0, h
         p.block_setup("line2", n, r, K, "serial")
         ctxs.append(p)
     H, V, hub_rows, _ = ctxs[0].block_hubs()
-    sc = ctxs[0].block_hub_scales(min(per, count // n) / nb, 2048.0)[:, None] if H else None
+    L = ctxs[0].block_cell_launches()          # a cell in L launches, the slots exchanged after each
+    assert L == (4 if H else 1)
+    sc = ctxs[0].block_hub_scales(min(per, count // n) / nb / L, 2048.0)[:, None] if H else None
     Ws = [W0.copy() for _ in range(n)]
     Cs = [np.concatenate([C0, C0[hub_rows]]) for _ in range(n)]
     Ss = [c[V:].copy() for c in Cs]
@@ -176,32 +202,18 @@ def _schedule_edges(smore, graph, n, begin, count, per, total, K, dim, W0, C0, h
         cur = [lo + sum(share[:r]) for r in range(n)]
         cnt = [ctxs[r].block_counts(share[r]) for r in range(n)]
         for s in range(nb):
-            for r in range(n):
-                b = (2 * r + s) % nb
-                x = int(cnt[r][b])
-                if x:
-                    rec = ctxs[r].block_sample_edges(b, SEED, begin + cur[r], x, K)
-                    orc.train_records_f32("line2", Ws[r], Cs[r], rec, K, 0.025, 0.0, total, begin + cur[r],
-                                          ctxs[r].block_neg_scale(b))
-                cur[r] += x
-            if H:          # the hub slots' exchange (replica_sync.hip passes, fp32)
+            for q in range(L):
                 for r in range(n):
-                    T = Cs[r][V:]
-                    if pending:
-                        X = sc * Rs[r] - Ds[r]
-                        tn, sn = T + X, Ss[r] + X
-                        Ds[r] = tn - sn
-                        T[:] = tn
-                        Ss[r] = tn.copy()
-                    else:
-                        Ds[r] = T - Ss[r]
-                        Ss[r] = T.copy()
-                    Rs[r] = Ds[r].copy()
-                tot = Rs[0].copy()
-                for r in range(1, n):
-                    tot = tot + Rs[r]
-                Rs = [tot.copy() for _ in range(n)]
-                pending = True
+                    b = (2 * r + s) % nb
+                    x0, x1 = int(cnt[r][b]) * q // L, int(cnt[r][b]) * (q + 1) // L
+                    if x1 > x0:
+                        rec = ctxs[r].block_sample_edges(b, SEED, begin + cur[r] + x0, x1 - x0, K)
+                        orc.train_records_f32("line2", Ws[r], Cs[r], rec, K, 0.025, 0.0, total,
+                                              begin + cur[r] + x0, ctxs[r].block_neg_scale(b))
+                if H:
+                    pending = _hub_exchange(n, V, Cs, Ss, Ds, Rs, sc, pending)
+            for r in range(n):
+                cur[r] += int(cnt[r][(2 * r + s) % nb])
             moved = [Cs[r][cb[(2 * r + s) % nb]:cb[(2 * r + s) % nb + 1]].copy() for r in range(n)]
             for r in range(n):
                 b = (2 * r + s) % nb
