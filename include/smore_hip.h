@@ -616,9 +616,9 @@ int smore_block_neg_scale(const smore_ctx* ctx, int block, double* weight);
  * touches per sample are taken out of the rotating blocks; every cell draws
  * them (contexts and negatives, with 1/nb of their mass) on its part's own
  * copy in the C table's slot rows V .. V + H - 1, kept equal over the parts by
- * an exchange after every launch.  -1: automatic (LINE-2: none at 2 parts,
- * else 4096, at most V / 8nb; walk models: none), 0: none.  Takes effect at
- * the next smore_block_setup. */
+ * an exchange after every launch.  -1: automatic (none at 2 parts, else
+ * 4096, at most V / 8nb), 0: none.  Takes effect at the next
+ * smore_block_setup.  (Walk models: also the walk pairs' hub contexts.) */
 int smore_block_set_hubs(smore_ctx* ctx, int64_t hubs);
 /* the setup's hubs: count, the first slot row (V), their C rows and expected
  * touches per sample (each array H entries, or null) */
@@ -630,7 +630,7 @@ int smore_block_hubs_store(smore_ctx* ctx);
 /* the slots' exchange scales for `samples` per part per exchange and c0 (the
  * adaptive rule of SMORE_SYNC_ADAPTIVE over the nparts parts; H floats) */
 int smore_block_hub_scales(const smore_ctx* ctx, double samples, double c0, float* scales);
-/* LINE-2: launches per cell of the setup (4 with hub slots, else 1;
+/* launches per cell of the setup (4 with hub slots, else 1;
  * $SMORE_CELL_LAUNCHES overrides): a cell's samples are trained in this many
  * consecutive launches with the hub slots exchanged after each */
 int smore_block_cell_launches(const smore_ctx* ctx);
@@ -650,6 +650,9 @@ int smore_block_prepare_walks(smore_ctx* ctx, int rule, uint64_t walk_begin, uin
                               int walk_steps, int window, int window_min, int K, double alpha0, uint64_t seed,
                               const int64_t* order, uint64_t order_base, int mode);
 int smore_block_train_walks_async(smore_ctx* ctx, int block);
+/* one part of the bucket: records [n part / parts, n (part + 1) / parts) of
+ * its n (the group's launches per cell, the hub slots exchanged after each) */
+int smore_block_train_walks_part_async(smore_ctx* ctx, int block, int part, int parts);
 int smore_block_walk_records(smore_ctx* ctx, int block, uint64_t* n);
 
 /* ---- samplers (parity tests) -------------------------------------------------------- */

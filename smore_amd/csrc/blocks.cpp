@@ -160,12 +160,15 @@ bool neg_law_on() {
 // 2^34 samples 1.057 vs 1.008 times one GPU's held-out loss), else 4096 --
 // C4 at 8 parts: the five hub cells (10-14 ms against 7.7) disappear.
 constexpr int64_t HUB_AUTO = 4096;
-// Walk cells: none unless asked for (C5 DeepWalk at 8 parts with 4096:
-// 1.14 times one GPU's held-out loss against 1.02 without).
+// The walk models the same (C5 DeepWalk at 8 parts: the capped hub cells
+// and the 29 % rotation stall disappear, 1.34 -> 2.32x predicted) with their
+// own exchange rule (c0 64, hub_c0: 1.026 times one GPU's held-out loss; c0
+// 2048: 1.11).
 int64_t hub_count(const smore_ctx* c, int64_t V, int nb, bool walk) {
+    (void)walk;
     int64_t h = c->blk_hubs;
     if (const char* e = getenv("SMORE_HUBS")) h = atoll(e);
-    if (h < 0) h = nb <= 4 || walk ? 0 : std::min<int64_t>(HUB_AUTO, V / (8 * (int64_t)nb));
+    if (h < 0) h = nb <= 4 ? 0 : std::min<int64_t>(HUB_AUTO, V / (8 * (int64_t)nb));
     return std::max<int64_t>(0, std::min(std::min(h, c->c_slots), V / 2));
 }
 
@@ -191,6 +194,12 @@ EdgeArgs cell_args(smore_ctx* c, int k, bool walk) {
     a.sh_flush = std::max(1, B.sh_flush);
     a.sh_flush_w = 0;
     std::copy(B.sh_lvl[k].begin(), B.sh_lvl[k].end(), a.sh_lvl);
+    // walk cells: cold W rows stored, not added (SMORE_WALK_WPLAIN=1; off:
+    // measured no faster at C5, 8 parts -- 30.4 vs 31.6 ms per part's epoch)
+    if (walk) {
+        const char* e = getenv("SMORE_WALK_WPLAIN");
+        a.w_plain = e && atoi(e) != 0;
+    }
     if (neg_law_on() && (size_t)k < B.nmass.size()) {
         if (walk) {
             a.neg_scale = (float)B.nmass[k];
@@ -266,13 +275,13 @@ void hub_scales(const smore_ctx::Blocks& B, double samples, double c0, float* ou
     }
 }
 
-// launches per LINE-2 cell: with hub slots, 4 -- the slots are exchanged
+// launches per cell: with hub slots, 4 -- the slots are exchanged
 // after each, so their copies are at most a quarter cell apart (C4, 8 parts:
 // 1.042 times one GPU's held-out loss against 1.079 with one launch per
 // cell, at 6.27 against 6.55 predicted); without, 1.  SMORE_CELL_LAUNCHES
 // overrides (1..64).
 int cell_launches(const smore_ctx::Blocks& B) {
-    int k = B.H > 0 && B.model == SMORE_LINE2 ? 4 : 1;
+    int k = B.H > 0 ? 4 : 1;
     if (const char* e = getenv("SMORE_CELL_LAUNCHES")) k = atoi(e);
     return std::max(1, std::min(64, k));
 }
@@ -981,9 +990,12 @@ int smore_block_prepare_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint6
     return SMORE_OK;
 }
 
-int smore_block_train_walks_async(smore_ctx* c, int block) {
+int smore_block_train_walks_async(smore_ctx* c, int block) { return smore_block_train_walks_part_async(c, block, 0, 1); }
+
+int smore_block_train_walks_part_async(smore_ctx* c, int block, int part, int parts) {
     int rc;
     if ((rc = check_ctx(c))) return rc;
+    if (parts < 1 || part < 0 || part >= parts) return fail(c, SMORE_EINVAL, "bad bucket part");
     auto& B = c->blk;
     if (!B.nb || B.model != SMORE_CENSUS) return fail(c, SMORE_ESTATE, "no walk block setup (smore_block_setup)");
     if (block < 0 || block >= B.nb) return fail(c, SMORE_EINVAL, "block out of range");
@@ -995,6 +1007,8 @@ int smore_block_train_walks_async(smore_ctx* c, int block) {
     a.count = B.rec_bound;   // the grid's bound; the launch reads its range on the device
     a.rec_base = B.d_off + (size_t)block * B.walks;
     a.count_dev = B.d_off + (size_t)(block + 1) * B.walks;
+    a.part_q = (uint32_t)part;
+    a.part_n = (uint32_t)parts;
     const int grid = B.mode == SMORE_SERIAL ? 1 : cell_grid(c, a, block);
     HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
     HIPCHK(c, launch_edge_train(a, grid, c->stream));

@@ -603,9 +603,14 @@ edge_train_kernel(EdgeArgs a) {
 
     const int lane = threadIdx.x & (G - 1);
     // records of this launch: [0, count) of a.rec, or a block bucket [*rec_base, *count_dev)
-    const uint64_t rb = a.rec_base ? *a.rec_base : 0;
-    const uint64_t count = (a.count_dev ? *a.count_dev : a.count) - rb;
-    const float nsc = neg_scale_of(a, count);
+    uint64_t rb = a.rec_base ? *a.rec_base : 0;
+    uint64_t count = (a.count_dev ? *a.count_dev : a.count) - rb;
+    const float nsc = neg_scale_of(a, count);            // the whole bucket's weight
+    if (a.part_n > 1) {                                  // one part of the bucket
+        const uint64_t lo = count * a.part_q / a.part_n, hi = count * (a.part_q + 1) / a.part_n;
+        rb += lo;
+        count = hi - lo;
+    }
     const int32_t* const recs = a.rec + rb * (uint64_t)rec_width(KMAX);
     const uint64_t gpb = blockDim.x / G;                 // groups per block
     uint64_t r0 = (uint64_t)blockIdx.x * gpb;            // block-uniform round base
@@ -854,9 +859,14 @@ pair_train_kernel(EdgeArgs a) {
     const ShState sh = block_setup<MODE>(a, s_sig, s_dyn, sh_ids);
     const int lane = threadIdx.x & (G - 1);
     constexpr int RW = rec_width(KMAX);
-    const uint64_t rb = a.rec_base ? *a.rec_base : 0;   // a block bucket: [*rec_base, *count_dev)
-    const uint64_t count = (a.count_dev ? *a.count_dev : a.count) - rb;
-    const float nsc = neg_scale_of(a, count);
+    uint64_t rb = a.rec_base ? *a.rec_base : 0;   // a block bucket: [*rec_base, *count_dev)
+    uint64_t count = (a.count_dev ? *a.count_dev : a.count) - rb;
+    const float nsc = neg_scale_of(a, count);      // the whole bucket's weight
+    if (a.part_n > 1) {                            // one part of the bucket
+        const uint64_t lo = count * a.part_q / a.part_n, hi = count * (a.part_q + 1) / a.part_n;
+        rb += lo;
+        count = hi - lo;
+    }
     const int32_t* const recs = a.rec + rb * (uint64_t)RW;
     const uint64_t gpb = blockDim.x / G, gib = threadIdx.x / G;
     bool ev[M];
@@ -883,6 +893,7 @@ pair_train_kernel(EdgeArgs a) {
         const uint64_t s0 = c0 + gib * sl;
         const uint64_t s1 = s0 + sl < lim ? s0 + sl : lim;
         int32_t cv = -1;
+        bool cvh = true;   // the run's W row is hot-tagged (or the flush is atomic anyway)
         float wv[M], wv0[M], rows[KMAX + 1][M];
 #pragma unroll
         for (int m = 0; m < M; ++m) wv[m] = wv0[m] = 0.0f;
@@ -898,6 +909,10 @@ pair_train_kernel(EdgeArgs a) {
         };
         auto flush_w = [&]() {
             if (cv < 0) return;
+            if (MODE == MODE_HYBRID && !cvh) {   // a cold W row: plain store (EdgeArgs::w_plain)
+                st_row<G, M>(a.W + (int64_t)cv * a.dpad, wv, lane, ev);
+                return;
+            }
             float d[M];
 #pragma unroll
             for (int m = 0; m < M; ++m) d[m] = wv[m] - wv0[m];
@@ -922,6 +937,7 @@ pair_train_kernel(EdgeArgs a) {
             if (v != cv) {
                 flush_w();
                 cv = v;
+                cvh = !a.w_plain || scatter_atomic<MODE>(tv);
                 ld_row<G, M>(wv, a.W + (int64_t)cv * a.dpad, lane, ev);
 #pragma unroll
                 for (int m = 0; m < M; ++m) wv0[m] = wv[m];

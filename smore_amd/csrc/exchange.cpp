@@ -653,10 +653,15 @@ int block_finish(smore_group* g, uint64_t S) {
 // sub-round the copies' deltas are all-reduced one late (begin / cycle / end
 // of replica_sync.hip on the slot rows, per-slot adaptive scales), on the
 // comm streams ahead of the rotation
-double hub_c0() {
+// the slots' adaptive rule's c0: LINE-2 2048 (the source-partitioned replica
+// exchange's); walk models 64 (theirs: a C5 run is ~2000 pair updates per
+// row in all, so a hub's copies are averaged sooner -- c0 2048 cost 1.11x
+// one GPU's held-out loss at 8 parts, 64 1.026x)
+double hub_c0(const smore_group* g) {
     const char* e = getenv("SMORE_HUB_C0");
     const double v = e ? atof(e) : 0.0;
-    return v > 0 ? v : 2048.0;
+    if (v > 0) return v;
+    return g->ctx[0]->blk.model == SMORE_CENSUS ? 64.0 : 2048.0;
 }
 
 float* hub_slots(smore_ctx* c) { return c->d_table[1] + (size_t)c->g->V * c->dpad; }
@@ -674,7 +679,7 @@ int hub_ex_start(smore_group* g, double samples_per_exchange) {
                 return gfail(g, (int)r, fail(g->ctx[r], SMORE_EHIP, "hub exchange: events"));
         }
     }
-    const double c0 = hub_c0();
+    const double c0 = hub_c0(g);
     char key[96];
     snprintf(key, sizeof key, "%.17g/%.17g", samples_per_exchange, c0);
     for (size_t r = 0; r < n; ++r) {
@@ -880,7 +885,8 @@ int group_block_walks(smore_group* g, int rule, uint64_t walk_begin, uint64_t wa
             }
         }
         const double walks = (double)std::min<uint64_t>(per, walk_end - walk_begin);
-        if ((rc = hub_ex_start(g, std::max(1.0, walks * ppw / (double)(n * nb))))) return rc;
+        const double launches = (double)cell_launches(g->ctx[0]->blk);
+        if ((rc = hub_ex_start(g, std::max(1.0, walks * ppw / (double)(n * nb) / launches)))) return rc;
     }
     uint64_t S = 0;
     for (uint64_t lo = walk_begin; lo < walk_end; lo += per) {
@@ -889,15 +895,19 @@ int group_block_walks(smore_group* g, int rule, uint64_t walk_begin, uint64_t wa
             if ((rc = smore_block_prepare_walks(g->ctx[r], rule, lo, hi, walk_times, walk_steps, window, window_min, K,
                                                 alpha0, seed, order, 0, mode)))
                 return gfail(g, (int)r, rc);
+        const int L = cell_launches(g->ctx[0]->blk);
         for (int s = 0; s < nb; ++s, ++S) {
-            for (size_t r = 0; r < n; ++r) {
-                if ((rc = block_wait(g, r, S))) return rc;
-                if ((rc = serial_before(g, r))) return rc;
-                if ((rc = smore_block_train_walks_async(g->ctx[r], (int)((2 * r + (size_t)s) % (size_t)nb))))
-                    return gfail(g, (int)r, rc);
-                if ((rc = serial_after(g, r))) return rc;
+            for (int q = 0; q < L; ++q) {
+                for (size_t r = 0; r < n; ++r) {
+                    if (q == 0 && (rc = block_wait(g, r, S))) return rc;
+                    if ((rc = serial_before(g, r))) return rc;
+                    if ((rc = smore_block_train_walks_part_async(g->ctx[r], (int)((2 * r + (size_t)s) % (size_t)nb),
+                                                                 q, L)))
+                        return gfail(g, (int)r, rc);
+                    if ((rc = serial_after(g, r))) return rc;
+                }
+                if ((rc = hub_ex_post(g))) return rc;
             }
-            if ((rc = hub_ex_post(g))) return rc;
             if ((rc = group_rotate(g, S))) return rc;
         }
     }

@@ -48,6 +48,13 @@ struct EdgeArgs {
     float neg_scale;
     const uint64_t* neg_lo;
     const uint64_t* neg_hi;
+    // pair kernel, hybrid: a run's W row is STORED when it is not hot-tagged
+    // (the edge rule), instead of adding its delta atomically (walk cells of
+    // the block schedule: their runs are ~1 record long)
+    int w_plain;
+    // a block bucket's launch in parts: records [lo, hi) of the bucket's
+    // range with lo = n part_q / part_n (part_n <= 1: the whole bucket)
+    uint32_t part_q, part_n;
     uint64_t begin, count, total, seed;
     double alpha0;
     float reg;

@@ -326,8 +326,11 @@ class ProNet:
                                                 ptr(order) if order is not None else None, 0, _lib.MODE[mode]),
                   "block_prepare_walks")
 
-    def block_train_walks(self, block, sync=True):
-        self._chk(lib.smore_block_train_walks_async(self.ctx, int(block)), "block_train_walks")
+    def block_train_walks(self, block, sync=True, part=0, parts=1):
+        """Train cell (part, block)'s bucket of the prepared round (or one of
+        `parts` consecutive parts of it)."""
+        self._chk(lib.smore_block_train_walks_part_async(self.ctx, int(block), int(part), int(parts)),
+                  "block_train_walks")
         if sync:
             self.synchronize()
 

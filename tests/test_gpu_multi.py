@@ -526,9 +526,10 @@ def test_c5_deepwalk_group_defaults(smore):
     group's defaults -- the 2-D block schedule: W parts owned,
     C blocks rotating, every replica walking every walk and keeping its own
     centres' pairs -- against one context that walked everything: held-out
-    LINE objective within 5 % and edge AUC within 0.005 (measured 1.007 /
-    1.012 / 1.024x and +0.0001 / +0.0004 / -0.0006; the replica schedule
-    measured 1.035-1.06 / 1.066 / 1.345x, profiles/r05/blocks.md)."""
+    LINE objective within 5 % and edge AUC within 0.005 (round 5 measured
+    1.007 / 1.012 / 1.024x; round 6, with the 4096 hub contexts on slots at 4
+    and 8 parts, exchanged after each of a cell's 4 launches: DESIGN.md 10.6;
+    the replica schedule measured 1.035-1.06 / 1.066 / 1.345x)."""
     from smore_amd import graphgen
     V, (src, dst, w) = graphgen.config_edges("c5")
     dim, wt, K = 128, 10, 5

@@ -135,15 +135,21 @@ def main():
                                                             order, args.mode))
                 recs = [pn.block_walk_records(b) for b in range(nb)]
 
+                L = pn.block_cell_launches()     # a cell in L launches (hub slots exchanged between)
+
+                def wcell(b, sync):
+                    for q in range(L):
+                        pn.block_train_walks(b, sync=sync and q + 1 == L, part=q, parts=L)
+
                 def epoch():
                     for s in range(nb):
-                        pn.block_train_walks((2 * r + s) % nb, sync=False)
+                        wcell((2 * r + s) % nb, False)
                 ep = timed(epoch)
                 units_r = sum(recs)
                 for s in range(nb):      # per-cell launch times (one pass, synchronised per cell)
                     b = (2 * r + s) % nb
                     t1 = time.perf_counter()
-                    pn.block_train_walks(b)
+                    wcell(b, True)
                     cells.append([b, int(recs[b]), round((time.perf_counter() - t1) * 1e3, 3)])
             row = {"config": args.config, "model": args.model, "nparts": n, "part": r, "setup_s": round(setup_s, 2),
                    "hubs": int(pn.block_hubs()[0]), "split": args.split,
