@@ -2030,26 +2030,31 @@ int smore_train_pairs_rows(smore_ctx* c, const int32_t* v, const int32_t* cc, in
 // 96-120; pkg/pronet/optimizer.go:8-18).  A GPU call per batch costs a
 // synchronisation and two small transfers whatever the batch, so a serialised
 // hook loses to the CPU path once two goroutines run.  Flat combining: every
-// caller queues its request; whichever finds the context idle becomes the
-// leader, takes every request queued so far and runs them as ONE call -- the
-// union of their rows up once (each row from the earliest request that holds
-// it), the batches' pair kernels in queue order on the stream (each batch sees
-// the rows the earlier ones wrote: the serial order of the queue), the union
-// back once, every request's rows copied out of it -- then wakes the others.
-// A caller whose request ran in another's call returns its status.
+// caller copies its batch (pairs, row ids, rows) into a pinned staging slot of
+// its own -- in parallel with the other callers -- and queues it; whichever
+// finds the context idle becomes the leader, takes every request queued so far
+// and runs them as ONE device call: per request in queue order, its rows up
+// (asynchronous from pinned memory; rows an earlier request of the call
+// already brought are NOT uploaded again, so each batch sees the rows the
+// earlier ones wrote -- the serial order of the queue), its pairs, its rows
+// back; one synchronisation; then every caller copies its rows out of its
+// slot, again in parallel.  A request's rows come back as they are after its
+// own batch.
+struct PairSlot {   // pinned staging of one request; capacities in elements
+    float *w_rows = nullptr, *c_rows = nullptr;
+    int32_t *w_ids = nullptr, *c_ids = nullptr, *v = nullptr, *cc = nullptr, *w_sel = nullptr, *c_sel = nullptr;
+    size_t cap[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+};
+
 struct PairReq {
-    const int32_t *v, *cc;
     int64_t n;
     int K;
     double alpha;
     uint64_t seed, unit;
     int mode;
-    const int32_t* w_ids;
-    int64_t nw;
-    float* w_rows;
-    const int32_t* c_ids;
-    int64_t nc;
-    float* c_rows;
+    int64_t nw, nc;
+    PairSlot* slot;
+    int64_t msel_w = 0, msel_c = 0;   // rows this request uploads (not already on the device in this call)
     int rc = SMORE_OK;
     bool done = false;
 };
@@ -2060,51 +2065,152 @@ struct PairCombiner {
     std::vector<PairReq*> q;
     bool busy = false;
     uint64_t calls = 0, requests = 0;   // combined device calls, requests served
+    std::mutex pool_mu;                 // the free slots
+    std::vector<PairSlot*> pool;
+    std::vector<PairSlot*> all;
+    std::vector<uint8_t> seen[2];       // the leader's marks of the rows already brought (cleared after use)
+    bool seen_dirty = false;            // a call failed before clearing its marks
+    // device staging of one combined call
+    float* d_rows = nullptr;
+    int32_t *d_ids = nullptr, *d_sel = nullptr;
+    size_t rows_cap = 0;   // rows
+    ~PairCombiner() {
+        for (PairSlot* p : all) {
+            for (void* x : {(void*)p->w_rows, (void*)p->c_rows, (void*)p->w_ids, (void*)p->c_ids, (void*)p->v,
+                            (void*)p->cc, (void*)p->w_sel, (void*)p->c_sel})
+                if (x) (void)hipHostFree(x);
+            delete p;
+        }
+        if (d_rows) (void)hipFree(d_rows);
+        if (d_ids) (void)hipFree(d_ids);
+        if (d_sel) (void)hipFree(d_sel);
+    }
 };
 
 namespace {
-// the union of the requests' rows of one table: sorted unique ids, and per id
-// its first (request, row) in queue order
-struct RowUnion {
-    std::vector<int32_t> ids;
-    std::vector<float> rows;
-};
-
-void row_union(const std::vector<PairReq*>& reqs, int which, int dim, RowUnion& u) {
-    struct Src {
-        int32_t id;
-        uint32_t req;
-        int64_t pos;
-    };
-    std::vector<Src> all;
-    for (uint32_t r = 0; r < reqs.size(); ++r) {
-        const PairReq* q = reqs[r];
-        const int32_t* ids = which ? q->c_ids : q->w_ids;
-        const int64_t n = which ? q->nc : q->nw;
-        for (int64_t i = 0; i < n; ++i) all.push_back({ids[i], r, i});
-    }
-    std::stable_sort(all.begin(), all.end(), [](const Src& a, const Src& b) { return a.id < b.id; });
-    u.ids.clear();
-    u.rows.clear();
-    for (size_t i = 0; i < all.size(); ++i) {
-        if (i && all[i].id == all[i - 1].id) continue;   // the earliest request's copy
-        u.ids.push_back(all[i].id);
-        const PairReq* q = reqs[all[i].req];
-        const float* src = (which ? q->c_rows : q->w_rows) + all[i].pos * dim;
-        u.rows.insert(u.rows.end(), src, src + dim);
-    }
+// a pinned host buffer of at least `need` elements of `size` bytes
+bool host_grow(void** p, size_t& cap, size_t need, size_t size) {
+    if (need <= cap && *p) return true;
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    cap = 0;
+    const size_t n = std::max<size_t>(need, 1024);
+    if (hipHostMalloc(p, n * size, hipHostMallocDefault) != hipSuccess) return false;
+    cap = n;
+    return true;
 }
 
-void row_scatter(const std::vector<PairReq*>& reqs, int which, int dim, const RowUnion& u) {
-    for (PairReq* q : reqs) {
-        const int32_t* ids = which ? q->c_ids : q->w_ids;
-        const int64_t n = which ? q->nc : q->nw;
-        float* dst = which ? q->c_rows : q->w_rows;
-        for (int64_t i = 0; i < n; ++i) {
-            const size_t k = (size_t)(std::lower_bound(u.ids.begin(), u.ids.end(), ids[i]) - u.ids.begin());
-            std::copy(u.rows.begin() + k * dim, u.rows.begin() + (k + 1) * dim, dst + i * dim);
+PairSlot* slot_acquire(PairCombiner& pc, int64_t n, int64_t nw, int64_t nc, int dim) {
+    PairSlot* s = nullptr;
+    {
+        std::lock_guard<std::mutex> g(pc.pool_mu);
+        if (!pc.pool.empty()) {
+            s = pc.pool.back();
+            pc.pool.pop_back();
+        } else {
+            s = new PairSlot();
+            pc.all.push_back(s);
         }
     }
+    const size_t need[8] = {(size_t)nw * dim, (size_t)nc * dim, (size_t)nw, (size_t)nc, (size_t)n, (size_t)n,
+                            (size_t)nw, (size_t)nc};
+    void** buf[8] = {(void**)&s->w_rows, (void**)&s->c_rows, (void**)&s->w_ids, (void**)&s->c_ids, (void**)&s->v,
+                     (void**)&s->cc, (void**)&s->w_sel, (void**)&s->c_sel};
+    bool ok = true;
+    for (int k = 0; k < 8 && ok; ++k) ok = host_grow(buf[k], s->cap[k], need[k], k < 2 ? sizeof(float) : sizeof(int32_t));
+    if (!ok) {
+        std::lock_guard<std::mutex> g(pc.pool_mu);
+        pc.pool.push_back(s);
+        return nullptr;
+    }
+    return s;
+}
+
+void slot_release(PairCombiner& pc, PairSlot* s) {
+    std::lock_guard<std::mutex> g(pc.pool_mu);
+    pc.pool.push_back(s);
+}
+
+// the leader: every request of the call, in queue order, on the stream
+int combined_call(smore_ctx* c, PairCombiner& pc, const std::vector<PairReq*>& reqs) {
+    const int dim = c->dim;
+    size_t rows = 0;
+    for (const PairReq* q : reqs) rows += (size_t)(q->nw + q->nc);
+    if (pc.rows_cap < rows) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (pc.d_rows) (void)hipFree(pc.d_rows);
+        if (pc.d_ids) (void)hipFree(pc.d_ids);
+        if (pc.d_sel) (void)hipFree(pc.d_sel);
+        pc.d_rows = nullptr;
+        pc.d_ids = pc.d_sel = nullptr;
+        pc.rows_cap = 0;
+        const size_t cap = std::max<size_t>(rows * 2, 1 << 16);
+        HIPCHK(c, hipMalloc((void**)&pc.d_rows, cap * dim * sizeof(float)));
+        HIPCHK(c, hipMalloc((void**)&pc.d_ids, cap * sizeof(int32_t)));
+        HIPCHK(c, hipMalloc((void**)&pc.d_sel, cap * sizeof(int32_t)));
+        pc.rows_cap = cap;
+    }
+    // the rows each request must bring: those no earlier request of the call brought
+    auto& seen = pc.seen;
+    const int64_t V = c->g->V;
+    for (auto& x : seen)
+        if ((int64_t)x.size() != V || pc.seen_dirty) x.assign((size_t)V, 0);
+    pc.seen_dirty = true;
+    for (PairReq* q : reqs) {
+        PairSlot* s = q->slot;
+        q->msel_w = q->msel_c = 0;
+        for (int64_t i = 0; i < q->nw; ++i)
+            if (!seen[0][s->w_ids[i]]) {
+                seen[0][s->w_ids[i]] = 1;
+                s->w_sel[q->msel_w++] = (int32_t)i;
+            }
+        for (int64_t i = 0; i < q->nc; ++i)
+            if (!seen[1][s->c_ids[i]]) {
+                seen[1][s->c_ids[i]] = 1;
+                s->c_sel[q->msel_c++] = (int32_t)i;
+            }
+    }
+    int rc;
+    size_t off = 0;
+    for (PairReq* q : reqs) {
+        PairSlot* s = q->slot;
+        for (int t = 0; t < 2; ++t) {
+            const int64_t n = t ? q->nc : q->nw, m = t ? q->msel_c : q->msel_w;
+            if (n == 0) continue;
+            float* dr = pc.d_rows + (off + (t ? (size_t)q->nw : 0)) * dim;
+            int32_t* di = pc.d_ids + off + (t ? (size_t)q->nw : 0);
+            int32_t* ds = pc.d_sel + off + (t ? (size_t)q->nw : 0);
+            HIPCHK(c, hipMemcpyAsync(di, t ? s->c_ids : s->w_ids, n * sizeof(int32_t), hipMemcpyHostToDevice,
+                                     c->stream));
+            if (m > 0) {
+                HIPCHK(c, hipMemcpyAsync(ds, t ? s->c_sel : s->w_sel, m * sizeof(int32_t), hipMemcpyHostToDevice,
+                                         c->stream));
+                HIPCHK(c, hipMemcpyAsync(dr, t ? s->c_rows : s->w_rows, (size_t)n * dim * sizeof(float),
+                                         hipMemcpyHostToDevice, c->stream));
+                HIPCHK(c, launch_rows_put_sel(c->d_table[t], di, ds, (uint64_t)m, c->dpad, dim, dr, c->stream));
+            }
+        }
+        q->rc = train_pairs_core(c, s->v, s->cc, q->n, q->K, q->alpha, q->seed, q->unit, q->mode);
+        if (q->rc) return q->rc;
+        for (int t = 0; t < 2; ++t) {
+            const int64_t n = t ? q->nc : q->nw;
+            if (n == 0) continue;
+            float* dr = pc.d_rows + (off + (t ? (size_t)q->nw : 0)) * dim;
+            int32_t* di = pc.d_ids + off + (t ? (size_t)q->nw : 0);
+            HIPCHK(c, launch_rows_io(c->d_table[t], di, (uint64_t)n, c->dpad, dim, dr, 0, c->stream));
+            HIPCHK(c, hipMemcpyAsync(t ? s->c_rows : s->w_rows, dr, (size_t)n * dim * sizeof(float),
+                                     hipMemcpyDeviceToHost, c->stream));
+        }
+        off += (size_t)(q->nw + q->nc);
+    }
+    for (PairReq* q : reqs) {   // clear the marks this call set
+        for (int64_t i = 0; i < q->msel_w; ++i) seen[0][q->slot->w_ids[q->slot->w_sel[i]]] = 0;
+        for (int64_t i = 0; i < q->msel_c; ++i) seen[1][q->slot->c_ids[q->slot->c_sel[i]]] = 0;
+    }
+    pc.seen_dirty = false;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    (void)rc;
+    return SMORE_OK;
 }
 }  // namespace
 
@@ -2115,6 +2221,12 @@ int smore_train_pairs_rows_mt(smore_ctx* c, const int32_t* v, const int32_t* cc,
     if (n < 0 || nw < 0 || nc < 0 || (n > 0 && (!v || !cc)) || (nw > 0 && (!w_ids || !w_rows)) ||
         (nc > 0 && (!c_ids || !c_rows)))
         return SMORE_EINVAL;
+    if (!c->has_graph || c->ntables < 2 || c->dim <= 0) return fail(c, SMORE_ESTATE, "pairs: no graph or tables");
+    const int64_t V = c->g->V;
+    for (int64_t i = 0; i < nw; ++i)
+        if (w_ids[i] < 0 || w_ids[i] >= V) return fail(c, SMORE_EINVAL, "row id out of range");
+    for (int64_t i = 0; i < nc; ++i)
+        if (c_ids[i] < 0 || c_ids[i] >= V) return fail(c, SMORE_EINVAL, "row id out of range");
     std::shared_ptr<PairCombiner> pc;
     {
         static std::mutex create_mu;   // the context's combiner, made once
@@ -2122,46 +2234,45 @@ int smore_train_pairs_rows_mt(smore_ctx* c, const int32_t* v, const int32_t* cc,
         if (!c->pair_comb) c->pair_comb = std::make_shared<PairCombiner>();
         pc = c->pair_comb;
     }
-    PairReq me{v, cc, n, K, alpha, seed, unit, mode, w_ids, nw, w_rows, c_ids, nc, c_rows};
+    const int dim = c->dim;
+    PairSlot* slot = slot_acquire(*pc, n, nw, nc, dim);
+    if (!slot) return fail(c, SMORE_EHIP, "pairs: pinned staging");
+    // this caller's copies into its slot (in parallel with the other callers)
+    std::copy(v, v + n, slot->v);
+    std::copy(cc, cc + n, slot->cc);
+    std::copy(w_ids, w_ids + nw, slot->w_ids);
+    std::copy(c_ids, c_ids + nc, slot->c_ids);
+    std::copy(w_rows, w_rows + (size_t)nw * dim, slot->w_rows);
+    std::copy(c_rows, c_rows + (size_t)nc * dim, slot->c_rows);
+    PairReq me{n, K, alpha, seed, unit, mode, nw, nc, slot};
     std::unique_lock<std::mutex> lk(pc->mu);
     pc->q.push_back(&me);
     pc->cv.wait(lk, [&] { return me.done || !pc->busy; });
-    if (me.done) return me.rc;
-    // leader: every queued request (its own among them) in one device call
-    pc->busy = true;
-    std::vector<PairReq*> reqs;
-    reqs.swap(pc->q);
-    lk.unlock();
-    int rc = SMORE_OK;
-    const int dim = c->dim;
-    RowUnion uw, uc;
-    if (dim <= 0) rc = fail(c, SMORE_ESTATE, "tables not allocated");
-    if (!rc) {
-        row_union(reqs, 0, dim, uw);
-        row_union(reqs, 1, dim, uc);
-        rc = rows_io_async(c, 0, uw.ids.data(), (int64_t)uw.ids.size(), uw.rows.data(), true);
-        if (!rc) rc = rows_io_async(c, 1, uc.ids.data(), (int64_t)uc.ids.size(), uc.rows.data(), true);
+    if (!me.done) {
+        // leader: every queued request (its own among them) in one device call
+        pc->busy = true;
+        std::vector<PairReq*> reqs;
+        reqs.swap(pc->q);
+        lk.unlock();
+        const int rc = set_device(c) ? SMORE_EHIP : combined_call(c, *pc, reqs);
+        lk.lock();
+        for (PairReq* q : reqs) {
+            if (rc && !q->rc) q->rc = rc;
+            q->done = true;
+        }
+        pc->calls++;
+        pc->requests += reqs.size();
+        pc->busy = false;
+        lk.unlock();
+        pc->cv.notify_all();
+    } else {
+        lk.unlock();
     }
-    for (PairReq* q : reqs) {
-        q->rc = rc ? rc : train_pairs_core(c, q->v, q->cc, q->n, q->K, q->alpha, q->seed, q->unit, q->mode);
+    if (me.rc == SMORE_OK) {   // this caller's rows out of its slot (in parallel)
+        std::copy(slot->w_rows, slot->w_rows + (size_t)nw * dim, w_rows);
+        std::copy(slot->c_rows, slot->c_rows + (size_t)nc * dim, c_rows);
     }
-    if (!rc) rc = rows_io_async(c, 0, uw.ids.data(), (int64_t)uw.ids.size(), uw.rows.data(), false);
-    if (!rc) rc = rows_io_async(c, 1, uc.ids.data(), (int64_t)uc.ids.size(), uc.rows.data(), false);
-    if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = fail(c, SMORE_EHIP, "pairs combine: sync");
-    if (!rc) {
-        row_scatter(reqs, 0, dim, uw);
-        row_scatter(reqs, 1, dim, uc);
-    }
-    lk.lock();
-    for (PairReq* q : reqs) {
-        if (rc) q->rc = rc;
-        q->done = true;
-    }
-    pc->calls++;
-    pc->requests += reqs.size();
-    pc->busy = false;
-    lk.unlock();
-    pc->cv.notify_all();
+    slot_release(*pc, slot);
     return me.rc;
 }
 

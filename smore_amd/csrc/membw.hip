@@ -70,4 +70,24 @@ hipError_t launch_rows_io(float* T, const int32_t* ids, uint64_t n, int dpad, in
     return hipGetLastError();
 }
 
+// rows ids[pos[j]] <- buf[pos[j]] for j < m (the combining pairs call's
+// upload of the rows an earlier request in the call did not already bring)
+__global__ void __launch_bounds__(256) rows_put_sel_kernel(float* T, const int32_t* ids, const int32_t* pos,
+                                                           uint64_t m, int dpad, int dim, const float* buf) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m * (uint64_t)dim) return;
+    const uint64_t j = i / (uint64_t)dim, e = i - j * (uint64_t)dim;
+    const uint64_t r = (uint64_t)pos[j];
+    T[(uint64_t)ids[r] * (uint64_t)dpad + e] = buf[r * (uint64_t)dim + e];
+}
+
+hipError_t launch_rows_put_sel(float* T, const int32_t* ids, const int32_t* pos, uint64_t m, int dpad, int dim,
+                               const float* buf, hipStream_t st) {
+    const uint64_t n = m * (uint64_t)dim;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(rows_put_sel_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, T, ids, pos, m, dpad,
+                       dim, buf);
+    return hipGetLastError();
+}
+
 }  // namespace smore

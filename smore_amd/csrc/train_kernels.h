@@ -256,6 +256,8 @@ hipError_t launch_block_pair_emit(const WalkArgs& w, const BlockArgs& b, uint64_
 // rows `ids` of T [*][dpad] from (to_table 1) / to (0) buf [n][dim] (membw.hip)
 hipError_t launch_rows_io(float* T, const int32_t* ids, uint64_t n, int dpad, int dim, float* buf, int to_table,
                           hipStream_t st);
+hipError_t launch_rows_put_sel(float* T, const int32_t* ids, const int32_t* pos, uint64_t m, int dpad, int dim,
+                               const float* buf, hipStream_t st);
 // streaming copy of n16 16-B words (membw.hip); variant 1 = non-temporal
 hipError_t launch_copy(const void* src, void* dst, uint64_t n16, int blocks, int variant, hipStream_t st);
 hipError_t launch_init_uniform(float* T, int64_t rows, int dim, int dpad, uint64_t seed,
