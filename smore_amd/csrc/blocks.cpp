@@ -429,7 +429,15 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
     if (hyb) {
         M = resident_groups(c, walk, K, mode);
         small = c->hot_tau < 0 && 16.0 * (double)M >= (double)V;
-        tau = c->hot_tau >= 0 ? c->hot_tau : small ? 0.0 : hot_tau_cell_default(walk);
+        // LINE-2 cells at 3-4 parts of a large graph: tau 0.6 (their rows are
+        // 6-8x hotter than one GPU's, not 16x: C4 at 4 parts 1.037-1.040x one
+        // GPU's held-out loss at 3.68x predicted, against 1.034x at 3.39x with
+        // 0.3; at 8 parts 0.6 costs 1.054x; C2 -- 1M vertices, 125k rows per
+        // block at 4 parts -- 1.048x, so graphs under 4M vertices keep 0.3;
+        // DESIGN.md 10.6)
+        const bool t06 = !walk && nparts >= 3 && nparts <= 4 && V >= ((int64_t)1 << 22);
+        const double tcell = t06 ? 0.6 : hot_tau_cell_default(walk);
+        tau = c->hot_tau >= 0 ? c->hot_tau : small ? 0.0 : tcell;
         if (walk && (rc = hot_maps(c, SMORE_LINE2, K, M, true, (double)nparts, (double)nb))) return rc;
     }
     const int T = (int)std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), (unsigned)nb);
