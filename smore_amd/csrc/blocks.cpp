@@ -431,7 +431,7 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
         small = c->hot_tau < 0 && 16.0 * (double)M >= (double)V;
         // LINE-2 cells at 3-4 parts of a large graph: tau 0.6 (their rows are
         // 6-8x hotter than one GPU's, not 16x: C4 at 4 parts 1.037-1.040x one
-        // GPU's held-out loss at 3.68x predicted, against 1.034x at 3.39x with
+        // GPU's held-out loss at 3.60x predicted, against 1.034x at 3.39x with
         // 0.3; at 8 parts 0.6 costs 1.054x; C2 -- 1M vertices, 125k rows per
         // block at 4 parts -- 1.048x, so graphs under 4M vertices keep 0.3;
         // DESIGN.md 10.6)

@@ -39,7 +39,8 @@ def main():
     ap.add_argument("--combine-rows", type=int, default=None, help="hybrid: LDS write-combined rows (0: off)")
     ap.add_argument("--skip-one", action="store_true", help="no one-GPU reference (profiling the cells alone)")
     ap.add_argument("--hubs", type=int, default=-1, help="line2: hub C rows (-1 the library's default, 0 none)")
-    ap.add_argument("--split", type=int, default=1, help="line2: launches per cell (the hub slots' exchanges)")
+    ap.add_argument("--split", type=int, default=0,
+                    help="line2: launches per cell (the hub slots' exchanges; 0: the library's default)")
     args = ap.parse_args()
 
     import torch  # noqa: F401  (one HIP runtime with torch, as bench.py)
@@ -105,13 +106,14 @@ def main():
             if line:
                 cnt = pn.block_counts(S)      # weak scaling: S samples per GPU per epoch, as bench.py
                 mine = S
+                split = args.split or pn.block_cell_launches()
 
                 def cell(b, b0, x, sync):
-                    for q in range(args.split):      # the cell in --split launches
-                        lo, hi = x * q // args.split, x * (q + 1) // args.split
+                    for q in range(split):      # the cell in `split` launches
+                        lo, hi = x * q // split, x * (q + 1) // split
                         if hi > lo:
                             pn.block_train_edges(b, b0 + lo, hi - lo, total, K, 0.025, args.seed, args.mode,
-                                                 sync=sync and q + 1 == args.split)
+                                                 sync=sync and q + 1 == split)
 
                 def epoch():
                     b0 = 0
@@ -152,7 +154,7 @@ def main():
                     wcell(b, True)
                     cells.append([b, int(recs[b]), round((time.perf_counter() - t1) * 1e3, 3)])
             row = {"config": args.config, "model": args.model, "nparts": n, "part": r, "setup_s": round(setup_s, 2),
-                   "hubs": int(pn.block_hubs()[0]), "split": args.split,
+                   "hubs": int(pn.block_hubs()[0]), "split": split if line else pn.block_cell_launches(),
                    "epoch_ms": round(ep * 1e3, 3), "units": units_r,
                    "rate_M_per_s": round(units_r / ep / 1e6, 2),
                    "per_gpu_factor": round((units_r / ep) / (units / one), 4) if one else None,
