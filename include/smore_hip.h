@@ -649,6 +649,18 @@ int smore_block_sample_edges(smore_ctx* ctx, int block, uint64_t seed, uint64_t 
 int smore_block_prepare_walks(smore_ctx* ctx, int rule, uint64_t walk_begin, uint64_t walk_end, int walk_times,
                               int walk_steps, int window, int window_min, int K, double alpha0, uint64_t seed,
                               const int64_t* order, uint64_t order_base, int mode);
+/* the same round in two steps, for walk-partitioned generation (the group
+ * driver's default): smore_block_walks_generate walks only [gen_lo, gen_hi)
+ * of the round [walk_begin, walk_end) into the context's round buffer
+ * (smore_block_walks_buffer: device pointers of the walks, int32 [walks][stride],
+ * and their lengths, int32 [walks]); the host fills in the other parts' walks
+ * (each part walks 1/N, then every slice is broadcast from its walker), then
+ * smore_block_walks_emit buckets every walk's owned pairs */
+int smore_block_walks_generate(smore_ctx* ctx, int rule, uint64_t walk_begin, uint64_t walk_end, uint64_t gen_lo,
+                               uint64_t gen_hi, int walk_times, int walk_steps, int window, int window_min, int K,
+                               double alpha0, uint64_t seed, const int64_t* order, uint64_t order_base, int mode);
+int smore_block_walks_buffer(smore_ctx* ctx, void** walks, void** lens, int64_t* stride);
+int smore_block_walks_emit(smore_ctx* ctx);
 int smore_block_train_walks_async(smore_ctx* ctx, int block);
 /* one part of the bucket: records [n part / parts, n (part + 1) / parts) of
  * its n (the group's launches per cell, the hub slots exchanged after each) */

@@ -164,6 +164,10 @@ def _load():
         "smore_block_hubs_store": (i32, [P]),
         "smore_block_hub_scales": (i32, [P, dbl, dbl, P]),
         "smore_block_cell_launches": (i32, [P]),
+        "smore_block_walks_generate": (i32, [P, i32, u64, u64, u64, u64, i32, i32, i32, i32, i32, dbl, u64, P, u64,
+                                             i32]),
+        "smore_block_walks_emit": (i32, [P]),
+        "smore_block_walks_buffer": (i32, [P, P, P, P]),
         "smore_block_train_walks_part_async": (i32, [P, i32, i32, i32]),
         "smore_block_counts": (i32, [P, u64, P]),
         "smore_block_train_edges_async": (i32, [P, i32, u64, u64, u64, i32, dbl, u64, i32]),

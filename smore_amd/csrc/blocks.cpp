@@ -199,6 +199,8 @@ EdgeArgs cell_args(smore_ctx* c, int k, bool walk) {
     if (walk) {
         const char* e = getenv("SMORE_WALK_WPLAIN");
         a.w_plain = e && atoi(e) != 0;
+        const char* x = getenv("SMORE_WALK_EDGE");   // walk cells through the edge kernel (study)
+        a.rec_edge = x && atoi(x) != 0;
     }
     if (neg_law_on() && (size_t)k < B.nmass.size()) {
         if (walk) {
@@ -300,6 +302,133 @@ void largest_remainder(uint64_t n, const double* mass, int parts, uint64_t* coun
     for (size_t i = 0; used < n && i < rem.size(); ++i, ++used) counts[rem[i].second]++;
     for (int k = 0; used < n; k = (k + 1) % parts, ++used) counts[k]++;   // rounding slack (never in practice)
 }
+
+int block_walks_gen(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t walk_end, uint64_t gen_lo, uint64_t gen_hi,
+                    int walk_times, int walk_steps, int window, int window_min, int K, double alpha0, uint64_t seed,
+                    const int64_t* order, uint64_t order_base, int mode) {
+    int rc;
+    if ((rc = check_ctx(c))) return rc;
+    auto& B = c->blk;
+    if (!B.nb || B.model != SMORE_CENSUS) return fail(c, SMORE_ESTATE, "no walk block setup (smore_block_setup)");
+    if (K != B.K || mode != B.mode) return fail(c, SMORE_EINVAL, "K / mode differ from smore_block_setup's");
+    if (rule != 0 && rule != 1) return fail(c, SMORE_EINVAL, "block rounds: DeepWalk (0) or Walklets (1)");
+    if ((rule == 0 && !order) || walk_times <= 0 || walk_steps < 0 || window <= 0)
+        return fail(c, SMORE_EINVAL, "bad walk arguments");
+    if (rule == 1 && (window_min < 0 || window_min > window)) return fail(c, SMORE_EINVAL, "Walklets: bad window");
+    const uint64_t total = (uint64_t)walk_times * (uint64_t)c->g->V;
+    if (walk_end > total) walk_end = total;
+    B.walks = 0;
+    if (walk_begin >= walk_end) return SMORE_OK;
+    const uint64_t nw = walk_end - walk_begin;
+    if (nw > WALK_ROUND_MAX) return fail(c, SMORE_EINVAL, "a block round holds at most 2^20 walks");
+    if (order) {
+        if (walk_begin < order_base) return fail(c, SMORE_EINVAL, "walk order slice does not cover the range");
+        order -= order_base;
+        for (uint64_t i = walk_begin; i < walk_end; ++i)
+            if (order[i] < 0 || order[i] >= c->g->V) return fail(c, SMORE_EINVAL, "walk start out of range");
+    }
+    if ((rc = set_device(c))) return rc;
+    // the walk ids' tags: the scaled hot maps (a no-op when current)
+    if (mode == SMORE_HYBRID) {
+        const int64_t M = resident_groups(c, true, K, mode);
+        if ((rc = hot_maps(c, SMORE_LINE2, K, M, true, (double)B.n, (double)B.nb))) return rc;
+    }
+    if (order) {
+        if (c->order_cap < nw) {
+            dfree(c->d_order);
+            c->order_cap = 0;
+            HIPCHK(c, hipMalloc((void**)&c->d_order, nw * sizeof(int64_t)));
+            c->order_cap = nw;
+        }
+        HIPCHK(c, hipMemcpyAsync(c->d_order, order + walk_begin, nw * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+    }
+    const int RW = rec_width(kmax_of(K));
+    const uint64_t pb = std::max<uint64_t>(1, pair_bound(walk_steps, window, rule, window_min));
+    const size_t need = nw * (size_t)(walk_steps + 1);
+    if (c->walk_buf_n < need) {
+        dfree(c->d_walks);
+        c->walk_buf_n = 0;
+        HIPCHK(c, hipMalloc((void**)&c->d_walks, need * sizeof(int32_t)));
+        c->walk_buf_n = need;
+    }
+    if (c->walk_lens_n < nw) {
+        dfree(c->d_lens);
+        c->walk_lens_n = 0;
+        HIPCHK(c, hipMalloc((void**)&c->d_lens, nw * sizeof(int32_t)));
+        c->walk_lens_n = nw;
+    }
+    const size_t ncount = (size_t)B.nb * nw + 1;
+    if (B.count_cap < ncount) {
+        dfree(B.d_count);
+        dfree(B.d_off);
+        B.count_cap = 0;
+        HIPCHK(c, hipMalloc((void**)&B.d_count, ncount * sizeof(uint32_t)));
+        HIPCHK(c, hipMalloc((void**)&B.d_off, ncount * sizeof(uint64_t)));
+        B.count_cap = ncount;
+    }
+    if (c->rec_cap < nw * pb * RW) {
+        dfree(c->d_rec);
+        c->rec_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_rec, nw * pb * RW * sizeof(int32_t)));
+        c->rec_cap = nw * pb * RW;
+    }
+    WalkArgs w;
+    w.order = order ? c->d_order : nullptr;
+    w.order_base = walk_begin;
+    w.walks = c->d_walks;
+    w.lens = c->d_lens;
+    w.walk_begin = walk_begin;
+    w.nwalks = nw;
+    w.total_walks = total;
+    w.steps = walk_steps;
+    w.window = window;
+    w.rule = rule;
+    w.window_min = window_min;
+    w.inv_p = w.inv_q = 1.0;
+    w.wts = nullptr;
+    w.nbr_sorted = nullptr;
+    w.ntype = nullptr;
+    w.ttargets = nullptr;
+    w.toff = nullptr;
+    w.paths = nullptr;
+    w.path_off = nullptr;
+    w.ntypes = w.npaths = 0;
+    w.slot_extra = 0;
+    w.own_lo = (int32_t)B.wb[B.r];
+    w.own_hi = (int32_t)B.wb[B.r + 1];
+    B.wargs = w;
+    B.wseed = seed;
+    B.walpha0 = alpha0;
+    B.wpairs = pb;
+    B.walks = nw;
+    B.rec_bound = nw * pb;
+    if (gen_lo < walk_begin || gen_hi > walk_end || gen_lo > gen_hi)
+        return fail(c, SMORE_EINVAL, "walk generation range outside the round");
+    if (gen_hi > gen_lo) {   // this context's share of the round's walks
+        WalkArgs wg = w;
+        const uint64_t o = gen_lo - walk_begin;
+        wg.walk_begin = gen_lo;
+        wg.nwalks = gen_hi - gen_lo;
+        wg.walks = w.walks + o * (uint64_t)(walk_steps + 1);
+        wg.lens = w.lens + o;
+        HIPCHK(c, launch_walk_gen(dev_graph(c), wg, seed, c->stream));
+    }
+    return SMORE_OK;
+}
+
+int block_walks_emit(smore_ctx* c) {
+    auto& B = c->blk;
+    if (!B.walks) return SMORE_OK;
+    const WalkArgs& w = B.wargs;
+    const size_t ncount = (size_t)B.nb * B.walks + 1;
+    const BlockArgs ba = block_args(c);
+    HIPCHK(c, hipMemsetAsync(B.d_count + (ncount - 1), 0, sizeof(uint32_t), c->stream));
+    HIPCHK(c, launch_block_pair_count(w, ba, B.wseed, B.d_count, c->stream));
+    HIPCHK(c, scan_pair_counts(B.d_count, B.d_off, ncount, &c->d_scan_tmp, &c->scan_tmp_bytes, c->stream));
+    HIPCHK(c, launch_block_pair_emit(w, ba, B.wseed, B.K, B.walpha0, B.d_off, c->d_rec, c->stream));
+    return SMORE_OK;
+}
+
 
 void blocks_release(smore_ctx* c) {
     auto& B = c->blk;
@@ -894,108 +1023,35 @@ int smore_block_sample_edges(smore_ctx* c, int block, uint64_t seed, uint64_t be
     return SMORE_OK;
 }
 
+int smore_block_walks_generate(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t walk_end, uint64_t gen_lo,
+                               uint64_t gen_hi, int walk_times, int walk_steps, int window, int window_min, int K,
+                               double alpha0, uint64_t seed, const int64_t* order, uint64_t order_base, int mode) {
+    return block_walks_gen(c, rule, walk_begin, walk_end, gen_lo, gen_hi, walk_times, walk_steps, window, window_min,
+                           K, alpha0, seed, order, order_base, mode);
+}
+
+int smore_block_walks_emit(smore_ctx* c) {
+    int rc;
+    if ((rc = check_ctx(c))) return rc;
+    if ((rc = set_device(c))) return rc;
+    return block_walks_emit(c);
+}
+
+int smore_block_walks_buffer(smore_ctx* c, void** walks, void** lens, int64_t* stride) {
+    if (!c) return SMORE_EINVAL;
+    if (walks) *walks = c->d_walks;
+    if (lens) *lens = c->d_lens;
+    if (stride) *stride = (int64_t)c->blk.wargs.steps + 1;
+    return SMORE_OK;
+}
+
 int smore_block_prepare_walks(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t walk_end, int walk_times,
                               int walk_steps, int window, int window_min, int K, double alpha0, uint64_t seed,
                               const int64_t* order, uint64_t order_base, int mode) {
-    int rc;
-    if ((rc = check_ctx(c))) return rc;
-    auto& B = c->blk;
-    if (!B.nb || B.model != SMORE_CENSUS) return fail(c, SMORE_ESTATE, "no walk block setup (smore_block_setup)");
-    if (K != B.K || mode != B.mode) return fail(c, SMORE_EINVAL, "K / mode differ from smore_block_setup's");
-    if (rule != 0 && rule != 1) return fail(c, SMORE_EINVAL, "block rounds: DeepWalk (0) or Walklets (1)");
-    if ((rule == 0 && !order) || walk_times <= 0 || walk_steps < 0 || window <= 0)
-        return fail(c, SMORE_EINVAL, "bad walk arguments");
-    if (rule == 1 && (window_min < 0 || window_min > window)) return fail(c, SMORE_EINVAL, "Walklets: bad window");
-    const uint64_t total = (uint64_t)walk_times * (uint64_t)c->g->V;
-    if (walk_end > total) walk_end = total;
-    B.walks = 0;
-    if (walk_begin >= walk_end) return SMORE_OK;
-    const uint64_t nw = walk_end - walk_begin;
-    if (nw > WALK_ROUND_MAX) return fail(c, SMORE_EINVAL, "a block round holds at most 2^20 walks");
-    if (order) {
-        if (walk_begin < order_base) return fail(c, SMORE_EINVAL, "walk order slice does not cover the range");
-        order -= order_base;
-        for (uint64_t i = walk_begin; i < walk_end; ++i)
-            if (order[i] < 0 || order[i] >= c->g->V) return fail(c, SMORE_EINVAL, "walk start out of range");
-    }
-    if ((rc = set_device(c))) return rc;
-    // the walk ids' tags: the scaled hot maps (a no-op when current)
-    if (mode == SMORE_HYBRID) {
-        const int64_t M = resident_groups(c, true, K, mode);
-        if ((rc = hot_maps(c, SMORE_LINE2, K, M, true, (double)B.n, (double)B.nb))) return rc;
-    }
-    if (order) {
-        if (c->order_cap < nw) {
-            dfree(c->d_order);
-            c->order_cap = 0;
-            HIPCHK(c, hipMalloc((void**)&c->d_order, nw * sizeof(int64_t)));
-            c->order_cap = nw;
-        }
-        HIPCHK(c, hipMemcpyAsync(c->d_order, order + walk_begin, nw * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
-    }
-    const int RW = rec_width(kmax_of(K));
-    const uint64_t pb = std::max<uint64_t>(1, pair_bound(walk_steps, window, rule, window_min));
-    const size_t need = nw * (size_t)(walk_steps + 1);
-    if (c->walk_buf_n < need) {
-        dfree(c->d_walks);
-        c->walk_buf_n = 0;
-        HIPCHK(c, hipMalloc((void**)&c->d_walks, need * sizeof(int32_t)));
-        c->walk_buf_n = need;
-    }
-    if (c->walk_lens_n < nw) {
-        dfree(c->d_lens);
-        c->walk_lens_n = 0;
-        HIPCHK(c, hipMalloc((void**)&c->d_lens, nw * sizeof(int32_t)));
-        c->walk_lens_n = nw;
-    }
-    const size_t ncount = (size_t)B.nb * nw + 1;
-    if (B.count_cap < ncount) {
-        dfree(B.d_count);
-        dfree(B.d_off);
-        B.count_cap = 0;
-        HIPCHK(c, hipMalloc((void**)&B.d_count, ncount * sizeof(uint32_t)));
-        HIPCHK(c, hipMalloc((void**)&B.d_off, ncount * sizeof(uint64_t)));
-        B.count_cap = ncount;
-    }
-    if (c->rec_cap < nw * pb * RW) {
-        dfree(c->d_rec);
-        c->rec_cap = 0;
-        HIPCHK(c, hipMalloc(&c->d_rec, nw * pb * RW * sizeof(int32_t)));
-        c->rec_cap = nw * pb * RW;
-    }
-    WalkArgs w;
-    w.order = order ? c->d_order : nullptr;
-    w.order_base = walk_begin;
-    w.walks = c->d_walks;
-    w.lens = c->d_lens;
-    w.walk_begin = walk_begin;
-    w.nwalks = nw;
-    w.total_walks = total;
-    w.steps = walk_steps;
-    w.window = window;
-    w.rule = rule;
-    w.window_min = window_min;
-    w.inv_p = w.inv_q = 1.0;
-    w.wts = nullptr;
-    w.nbr_sorted = nullptr;
-    w.ntype = nullptr;
-    w.ttargets = nullptr;
-    w.toff = nullptr;
-    w.paths = nullptr;
-    w.path_off = nullptr;
-    w.ntypes = w.npaths = 0;
-    w.slot_extra = 0;
-    w.own_lo = (int32_t)B.wb[B.r];
-    w.own_hi = (int32_t)B.wb[B.r + 1];
-    const BlockArgs ba = block_args(c);
-    HIPCHK(c, launch_walk_gen(dev_graph(c), w, seed, c->stream));
-    HIPCHK(c, hipMemsetAsync(B.d_count + (ncount - 1), 0, sizeof(uint32_t), c->stream));
-    HIPCHK(c, launch_block_pair_count(w, ba, seed, B.d_count, c->stream));
-    HIPCHK(c, scan_pair_counts(B.d_count, B.d_off, ncount, &c->d_scan_tmp, &c->scan_tmp_bytes, c->stream));
-    HIPCHK(c, launch_block_pair_emit(w, ba, seed, K, alpha0, B.d_off, c->d_rec, c->stream));
-    B.walks = nw;
-    B.rec_bound = nw * pb;
-    return SMORE_OK;
+    int rc = block_walks_gen(c, rule, walk_begin, walk_end, walk_begin, walk_end, walk_times, walk_steps, window,
+                             window_min, K, alpha0, seed, order, order_base, mode);
+    if (rc) return rc;
+    return block_walks_emit(c);
 }
 
 int smore_block_train_walks_async(smore_ctx* c, int block) { return smore_block_train_walks_part_async(c, block, 0, 1); }

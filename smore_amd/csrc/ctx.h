@@ -215,6 +215,12 @@ struct smore_ctx {
         size_t count_cap = 0;
         uint64_t walks = 0;             // walks of the prepared round (0: none)
         uint64_t rec_bound = 0;         // records the prepared round may hold
+        // the round being prepared (block_walks_gen -> block_walks_emit):
+        // its walk arguments over all the round's walks, and the pair draws'
+        WalkArgs wargs{};
+        uint64_t wseed = 0;
+        double walpha0 = 0.0;
+        uint64_t wpairs = 0;            // pair bound per walk
     } blk;
 };
 
@@ -228,7 +234,16 @@ constexpr int64_t HUB_SLOTS_MAX = 65536;
 
 // blocks.cpp: frees the block tables (a new graph, smore_destroy)
 void blocks_release(smore_ctx* c);
-// blocks.cpp: launches per LINE-2 cell (the hub slots are exchanged after each)
+// blocks.cpp: a walk round in two steps -- the walks [gen_lo, gen_hi) of the
+// round [walk_begin, walk_end) generated into this context's round buffer
+// (the rest may come from the other parts: walk-partitioned generation), then
+// every walk's owned pairs bucketed into records (smore_block_prepare_walks =
+// both over the whole round)
+int block_walks_gen(smore_ctx* c, int rule, uint64_t walk_begin, uint64_t walk_end, uint64_t gen_lo, uint64_t gen_hi,
+                    int walk_times, int walk_steps, int window, int window_min, int K, double alpha0, uint64_t seed,
+                    const int64_t* order, uint64_t order_base, int mode);
+int block_walks_emit(smore_ctx* c);
+// blocks.cpp: launches per cell (the hub slots are exchanged after each)
 int cell_launches(const smore_ctx::Blocks& B);
 // blocks.cpp: the hub slots' exchange scales for `samples` per part per exchange
 void hub_scales(const smore_ctx::Blocks& B, double samples, double c0, float* out);

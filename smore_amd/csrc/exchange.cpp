@@ -889,12 +889,37 @@ int group_block_walks(smore_group* g, int rule, uint64_t walk_begin, uint64_t wa
         if ((rc = hub_ex_start(g, std::max(1.0, walks * ppw / (double)(n * nb) / launches)))) return rc;
     }
     uint64_t S = 0;
+    const char* ga = getenv("SMORE_WALK_GEN_ALL");
+    const bool split_gen = !(ga && atoi(ga) != 0);
     for (uint64_t lo = walk_begin; lo < walk_end; lo += per) {
-        const uint64_t hi = std::min(walk_end, lo + per);
-        for (size_t r = 0; r < n; ++r)
-            if ((rc = smore_block_prepare_walks(g->ctx[r], rule, lo, hi, walk_times, walk_steps, window, window_min, K,
-                                                alpha0, seed, order, 0, mode)))
+        const uint64_t hi = std::min(walk_end, lo + per), nw = hi - lo;
+        // walk-partitioned generation: replica r walks its 1/N of the round,
+        // every replica gets every walk (one broadcast of each slice from its
+        // walker), then each buckets its own centres' pairs.  SMORE_WALK_GEN_ALL=1:
+        // every replica walks every walk (round 5)
+        for (size_t r = 0; r < n; ++r) {
+            const uint64_t glo = split_gen ? lo + nw * r / n : lo, ghi = split_gen ? lo + nw * (r + 1) / n : hi;
+            if ((rc = block_walks_gen(g->ctx[r], rule, lo, hi, glo, ghi, walk_times, walk_steps, window, window_min, K,
+                                      alpha0, seed, order, 0, mode)))
                 return gfail(g, (int)r, rc);
+        }
+        if (split_gen && n > 1) {
+            const std::vector<hipStream_t> st = compute_streams(g);
+            const size_t L = (size_t)walk_steps + 1;
+            for (size_t q = 0; q < n; ++q) {
+                const uint64_t o = nw * q / n, m = nw * (q + 1) / n - o;
+                if (!m) continue;
+                std::vector<float*> wb, lb;
+                for (smore_ctx* c : g->ctx) {
+                    wb.push_back(reinterpret_cast<float*>(c->d_walks + o * L));
+                    lb.push_back(reinterpret_cast<float*>(c->d_lens + o));
+                }
+                if ((rc = coll_broadcast(g, wb, m * L, (int)q, st, "walks ncclBroadcast"))) return rc;
+                if ((rc = coll_broadcast(g, lb, m, (int)q, st, "walk lengths ncclBroadcast"))) return rc;
+            }
+        }
+        for (size_t r = 0; r < n; ++r)
+            if ((rc = block_walks_emit(g->ctx[r]))) return gfail(g, (int)r, rc);
         const int L = cell_launches(g->ctx[0]->blk);
         for (int s = 0; s < nb; ++s, ++S) {
             for (int q = 0; q < L; ++q) {

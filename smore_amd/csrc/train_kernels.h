@@ -55,6 +55,9 @@ struct EdgeArgs {
     // a block bucket's launch in parts: records [lo, hi) of the bucket's
     // range with lo = n part_q / part_n (part_n <= 1: the whole bucket)
     uint32_t part_q, part_n;
+    // walk records through the (row-prefetching) edge kernel instead of the
+    // pair kernel (block walk cells: their W runs are ~1 record long)
+    int rec_edge;
     uint64_t begin, count, total, seed;
     double alpha0;
     float reg;

@@ -76,7 +76,7 @@ int lanes_of(int dpad) {
         return k5 ? fn##s5(__VA_ARGS__) : fn##s10(__VA_ARGS__);                \
     }
 
-static bool pair_path(const EdgeArgs& a) { return a.alpha_rec == 1 && a.mode != 2 && a.K <= 10; }
+static bool pair_path(const EdgeArgs& a) { return a.alpha_rec == 1 && a.mode != 2 && a.K <= 10 && !a.rec_edge; }
 
 hipError_t launch_edge_train(const EdgeArgs& a, int grid, hipStream_t st) {
     if (pair_path(a)) SMORE_PAIR_DISPATCH(launch_pair_, a, grid, st)

@@ -326,6 +326,21 @@ class ProNet:
                                                 ptr(order) if order is not None else None, 0, _lib.MODE[mode]),
                   "block_prepare_walks")
 
+    def block_walks_generate(self, walk_begin, walk_end, gen_lo, gen_hi, walk_times, walk_steps, window, K, alpha0,
+                             seed, order=None, mode="hybrid", rule="deepwalk", window_min=0):
+        """Walk only [gen_lo, gen_hi) of the round [walk_begin, walk_end)
+        (walk-partitioned generation); smore_block_walks_emit buckets the pairs."""
+        if order is not None:
+            order = np.ascontiguousarray(order, np.int64)
+        self._chk(lib.smore_block_walks_generate(self.ctx, 0 if rule == "deepwalk" else 1, int(walk_begin),
+                                                 int(walk_end), int(gen_lo), int(gen_hi), int(walk_times),
+                                                 int(walk_steps), int(window), int(window_min), int(K), float(alpha0),
+                                                 int(seed), ptr(order) if order is not None else None, 0,
+                                                 _lib.MODE[mode]), "block_walks_generate")
+
+    def block_walks_emit(self):
+        self._chk(lib.smore_block_walks_emit(self.ctx), "block_walks_emit")
+
     def block_train_walks(self, block, sync=True, part=0, parts=1):
         """Train cell (part, block)'s bucket of the prepared round (or one of
         `parts` consecutive parts of it)."""

@@ -349,3 +349,29 @@ def test_block_walks_parallel_modes_train(smore, graph, mode):
         ln = _heldout_loss(W, C, held)
         print("pl1k DeepWalk blocks", mode, n, ln, "one", l1, flush=True)
         assert np.isfinite(W).all() and np.isfinite(C).all() and ln <= 1.10 * l1, (n, ln, l1)
+
+
+def test_block_group_walks_partitioned_generation(smore, graph, monkeypatch):
+    """Walk-partitioned generation: each replica walks
+    1/N of a round and the slices are broadcast from their walkers before the
+    pairs are bucketed.  Walks are deterministic per walk index, so a serial
+    group of 3 and of 4 ends bit-identical to every replica walking every walk
+    (SMORE_WALK_GEN_ALL=1, round 5)."""
+    K, dim = 5, 32
+    order = orc.deepwalk_order(graph.V, 2, 0)
+    for n in (3, 4):
+        out = []
+        for gen_all in ("1", "0"):
+            monkeypatch.setenv("SMORE_WALK_GEN_ALL", gen_all)
+            g = smore.Group([0] * n)
+            g.LoadEdgeList(PL1K, 1)
+            g.alloc_tables(dim, 2)
+            g.primary.init_table_glibc(0, 0)
+            g.primary.zero_table(1)
+            g.broadcast_tables()
+            g.set_schedule("blocks")
+            g.train_deepwalk(0, 2 * graph.V, 2, 20, 4, K, 0.025, SEED, order, "serial", per=500)
+            out.append((g.primary.get_table(0), g.primary.get_table(1)))
+            g.close()
+        np.testing.assert_array_equal(out[0][0], out[1][0])
+        np.testing.assert_array_equal(out[0][1], out[1][1])

@@ -133,8 +133,16 @@ def main():
                                      ([round(ph[0], 3), round(ph[1], 3)] if ph else []))
                 units_r = mine
             else:
-                prep = timed(lambda: pn.block_prepare_walks(0, args.walks, wt, steps, window, K, 0.025, args.seed,
-                                                            order, args.mode))
+                # walk-partitioned generation (the group default): this part walks
+                # its 1/N of the round and buckets every walk's pairs; the other
+                # slices' broadcast is block_sim's (walk_bytes over the link)
+                def prep_split():
+                    pn.block_walks_generate(0, args.walks, args.walks * r // n, args.walks * (r + 1) // n, wt, steps,
+                                            window, K, 0.025, args.seed, order, args.mode)
+                    pn.block_walks_emit()
+                prep = timed(prep_split)
+                prep_all = timed(lambda: pn.block_prepare_walks(0, args.walks, wt, steps, window, K, 0.025, args.seed,
+                                                                order, args.mode))
                 recs = [pn.block_walk_records(b) for b in range(nb)]
 
                 L = pn.block_cell_launches()     # a cell in L launches (hub slots exchanged between)
@@ -161,6 +169,8 @@ def main():
                    "cells": cells}
             if not line:
                 row["prepare_ms"] = round(prep * 1e3, 3)
+                row["prepare_all_ms"] = round(prep_all * 1e3, 3)
+                row["walk_bytes"] = args.walks * (steps + 2) * 4
                 row["per_gpu_factor_with_prepare"] = round((units_r / (ep + prep)) / (units / one), 4) if one else None
             # the C block a rotation moves: its bytes (xGMI time is estimated in DESIGN.md 10)
             _, cb = pn.block_bounds()

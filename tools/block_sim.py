@@ -73,8 +73,11 @@ def main():
                     dt[r][b] = sum(v) / len(v)
         any_row = next(iter(meas.values()))
         xfer = any_row["block_bytes_max"] / (args.link_gbs * 1e9) * 1e3
-        # walks: every replica generates the round's walks before its cells
+        # walks: every replica generates its slice of the round's walks and
+        # receives the others' (walk_bytes (N-1)/N over the link) before its cells
         prep = sum(d.get("prepare_ms", 0.0) for d in meas.values()) / len(meas)
+        wbytes = max(d.get("walk_bytes", 0) for d in meas.values())
+        prep += wbytes * (n - 1) / n / (args.link_gbs * 1e9) * 1e3
         ep = simulate(n, dt, xfer) + prep
         bound = max(sum(dt[r]) for r in range(n)) + prep
         units = sum(d["units"] for d in meas.values()) / len(meas)
