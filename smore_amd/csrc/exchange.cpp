@@ -613,6 +613,8 @@ int block_wait(smore_group* g, size_t r, uint64_t s) {
     return SMORE_OK;
 }
 
+int hub_ex_finish(smore_group* g);
+
 // after the last rotation: every transfer done before the tables are read;
 // then every replica gets the W parts from their owners and the C blocks from
 // their holders (after S sub-rounds block b sits on replica ((b - S) mod nb) / 2)
@@ -630,6 +632,10 @@ int block_finish(smore_group* g, uint64_t S) {
                 return gfail(g, (int)r, fail(c, SMORE_EHIP, "block schedule: drain"));
         }
     }
+    // the hub slots back into their rows only now: the last rotation's
+    // transfer carries the block's stale copy of those rows and would
+    // overwrite a store queued ahead of the drain
+    if ((rc = hub_ex_finish(g))) return rc;
     const std::vector<hipStream_t> st = compute_streams(g);
     smore_ctx* c0 = g->ctx[0];
     for (size_t p = 0; p < n; ++p) {
@@ -855,8 +861,7 @@ int group_block_edges(smore_group* g, uint64_t begin, uint64_t count, uint64_t p
             if ((rc = group_rotate(g, S))) return rc;
         }
     }
-    if ((rc = hub_ex_finish(g))) return rc;
-    return block_finish(g, S);
+    return block_finish(g, S);   // hub_ex_finish after the drain
 }
 
 int group_block_walks(smore_group* g, int rule, uint64_t walk_begin, uint64_t walk_end, int walk_times,
@@ -936,8 +941,7 @@ int group_block_walks(smore_group* g, int rule, uint64_t walk_begin, uint64_t wa
             if ((rc = group_rotate(g, S))) return rc;
         }
     }
-    if ((rc = hub_ex_finish(g))) return rc;
-    return block_finish(g, S);
+    return block_finish(g, S);   // hub_ex_finish after the drain
 }
 
 }  // namespace

@@ -524,8 +524,9 @@ def test_c5_deepwalk_group_defaults(smore):
     """Config 5's DeepWalk (the Youtube-sized stand-in, d=128, 10 walks per
     vertex, 40 steps, window 5, K 5, hybrid) on 2, 4 and 8 replicas with the
     group's defaults -- the 2-D block schedule: W parts owned,
-    C blocks rotating, every replica walking every walk and keeping its own
-    centres' pairs -- against one context that walked everything: held-out
+    C blocks rotating, each replica walking 1/N of a round and every replica
+    keeping its own centres' pairs of all the walks (the slices broadcast) --
+    against one context that walked everything: held-out
     LINE objective within 5 % and edge AUC within 0.005 (round 5 measured
     1.007 / 1.012 / 1.024x; round 6, with the 4096 hub contexts on slots at 4
     and 8 parts, exchanged after each of a cell's 4 launches: DESIGN.md 10.6;
