@@ -666,6 +666,10 @@ int smore_block_train_walks_async(smore_ctx* ctx, int block);
  * its n (the group's launches per cell, the hub slots exchanged after each) */
 int smore_block_train_walks_part_async(smore_ctx* ctx, int block, int part, int parts);
 int smore_block_walk_records(smore_ctx* ctx, int block, uint64_t* n);
+/* a bucket's records to the host (parity tests): *n records of *width int32
+ * each -- W id | tag, C id | tag, the K negatives (-1 padded), alpha's bits;
+ * out may be NULL (count and width only), else it holds cap records */
+int smore_block_walk_records_copy(smore_ctx* ctx, int block, int32_t* out, uint64_t cap, uint64_t* n, int* width);
 
 /* ---- samplers (parity tests) -------------------------------------------------------- */
 /* replaces: SourceSample/TargetSample/NegativeSample (src/proNet.cpp:623-683):

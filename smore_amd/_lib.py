@@ -175,6 +175,7 @@ def _load():
         "smore_block_prepare_walks": (i32, [P, i32, u64, u64, i32, i32, i32, i32, i32, dbl, u64, P, u64, i32]),
         "smore_block_train_walks_async": (i32, [P, i32]),
         "smore_block_walk_records": (i32, [P, i32, C.POINTER(u64)]),
+        "smore_block_walk_records_copy": (i32, [P, i32, P, u64, C.POINTER(u64), C.POINTER(i32)]),
         "smore_save_weights": (i32, [P, i32, C.c_char_p, i32]),
         "smore_load_pretrain": (i32, [P, i32, C.c_char_p]),
     }

@@ -1093,4 +1093,25 @@ int smore_block_walk_records(smore_ctx* c, int block, uint64_t* n) {
     return SMORE_OK;
 }
 
+int smore_block_walk_records_copy(smore_ctx* c, int block, int32_t* out, uint64_t cap, uint64_t* n, int* width) {
+    if (!c || !n || !width) return SMORE_EINVAL;
+    auto& B = c->blk;
+    if (!B.nb || B.model != SMORE_CENSUS || block < 0 || block >= B.nb) return SMORE_EINVAL;
+    const int RW = rec_width(kmax_of(B.K));
+    *width = RW;
+    *n = 0;
+    if (!B.walks) return SMORE_OK;
+    uint64_t lo = 0, hi = 0;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(&lo, B.d_off + (size_t)block * B.walks, sizeof lo, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(&hi, B.d_off + (size_t)(block + 1) * B.walks, sizeof hi, hipMemcpyDeviceToHost));
+    *n = hi - lo;
+    if (!out) return SMORE_OK;
+    if (cap < hi - lo) return fail(c, SMORE_EINVAL, "walk records: buffer too small");
+    if (hi > lo)
+        HIPCHK(c, hipMemcpy(out, static_cast<const int32_t*>(c->d_rec) + lo * RW, (hi - lo) * RW * sizeof(int32_t),
+                            hipMemcpyDeviceToHost));
+    return SMORE_OK;
+}
+
 }  // extern "C"

@@ -23,7 +23,9 @@
 // in its part, bucketed by the context's block; a pair's negatives come from
 // its block's restricted law (same slots as pair_emit_kernel, the index drawn
 // over the block).  Buckets keep walk order, so a bucket's records are the
-// one-GPU records restricted to the cell, in order.
+// one-GPU records restricted to the cell, in order.  The group driver walks
+// 1/N of a round per GPU and broadcasts the slices (exchange.cpp); the count
+// and emit run one wave per walk (block_pairs_wave_kernel).
 #include "train_kernels.h"
 
 namespace smore {
@@ -261,9 +263,163 @@ __global__ void __launch_bounds__(256) block_pair_emit_kernel(WalkArgs w, BlockA
     }
 }
 
+// ---- the same count and emit with one wave per walk.  The kernels above give
+// a thread a whole walk: 2^18 threads per round, each looping over ~40
+// positions with its 2N block cursors in scratch (C5, 8 parts: emit 3.0 ms,
+// count 0.8 ms of a 20-30 ms part epoch).  Here lane i takes position i (64
+// at a time): its pair count is scanned across the wave -- its negatives'
+// Philox words start after every earlier pair's, own or not -- and its pairs
+// per block go into the wave's LDS column, scanned per block (lane k scans
+// row k), so its records in block k follow every earlier position's.  Same
+// words, same records, same order as the per-walk kernels (bit-exact; the
+// host keeps those for windows too wide for the 16-bit columns).
+constexpr int WALKS_PER_BLOCK = 4;
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    return x;
+}
+
+// LDS written by one lane and read by another of the same wave: the writes
+// complete (s_waitcnt) and the compiler keeps the order
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// position i's context ranges (as the per-walk kernels) and its pair count
+__device__ __forceinline__ uint32_t position_ranges(const WalkArgs& w, WalkWordsB& wd, uint32_t win_base, int i,
+                                                    int L, int (&rg)[2][2], int& nr) {
+    if (w.rule == 1) {
+        scale_ranges(i, L, w.window_min, w.window, rg);
+        nr = 2;
+    } else {
+        const int r = (int)draw_index(wd(win_base + (uint32_t)i), (uint32_t)w.window) + 1;
+        rg[0][0] = i - r < 0 ? 0 : i - r;
+        rg[0][1] = i + r >= L ? L - 1 : i + r;
+        nr = 1;
+    }
+    uint32_t n = 0;
+    for (int q = 0; q < nr; ++q)
+        if (rg[q][1] >= rg[q][0]) n += (uint32_t)(rg[q][1] - rg[q][0] + 1) - (i >= rg[q][0] && i <= rg[q][1] ? 1u : 0u);
+    return n;
+}
+
+template <int KMAX, bool EMIT>
+__global__ void __launch_bounds__(256) block_pairs_wave_kernel(WalkArgs w, BlockArgs b, uint64_t seed, int K,
+                                                               double alpha0, const uint64_t* off, uint32_t* count,
+                                                               int32_t* rec) {
+    constexpr int RW = rec_width(KMAX);
+    __shared__ uint16_t col[WALKS_PER_BLOCK][BLOCK_MAX][65];   // [walk][block][lane], padded row
+    __shared__ uint64_t base[WALKS_PER_BLOCK][BLOCK_MAX];       // block k's next record of the walk
+    const int wv = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+    const uint64_t t = (uint64_t)blockIdx.x * WALKS_PER_BLOCK + (uint64_t)wv;
+    if (t >= w.nwalks) return;   // whole waves: nothing below syncs the block
+    const int nb = b.nb;
+    const int L = w.lens[t];
+    const int32_t* walk = w.walks + t * (uint64_t)(w.steps + 1);
+    const uint64_t unit = w.walk_begin + t;
+    const float alpha = alpha_walk(unit, alpha0, w.total_walks);
+    WalkWordsB win{seed, unit}, neg{seed, unit};
+    const uint32_t win_base = 2u * (uint32_t)(L - 1);
+    uint32_t slot_run = win_base + (w.rule == 1 ? 0u : (uint32_t)L);   // the chunk's first negative word
+    uint64_t total = 0;                                               // count: lane k's block-k pairs
+    if (EMIT && lane < nb) base[wv][lane] = off[(uint64_t)lane * w.nwalks + t];
+    for (int p0 = 0; p0 < L; p0 += 64) {
+        const int i = p0 + lane;
+        int rg[2][2] = {{0, -1}, {0, -1}};
+        int nr = 0;
+        uint32_t np = 0;
+        int32_t vi = 0;
+        bool own = false;
+        if (i < L) {
+            np = position_ranges(w, win, win_base, i, L, rg, nr);
+            vi = walk[i];
+            const int32_t v = vi & ID_MASK;
+            own = v >= w.own_lo && v < w.own_hi;
+        }
+        const uint32_t incl = wave_incl_scan(np, lane);
+        const uint32_t slot0 = slot_run + 2u * (uint32_t)K * (incl - np);
+        slot_run += 2u * (uint32_t)K * (uint32_t)__shfl((int)incl, 63, 64);
+        for (int k = 0; k < nb; ++k) col[wv][k][lane] = 0;
+        if (own)
+            for (int q = 0; q < nr; ++q)
+                for (int j = rg[q][0]; j <= rg[q][1]; ++j)
+                    if (j != i) {
+                        int32_t cw;
+                        col[wv][pair_block(b, walk[j], unit, i, cw)][lane]++;
+                    }
+        wave_lds_sync();
+        uint32_t run = 0;   // lane k: block k's pairs of the chunk
+        if (lane < nb)
+            for (int m = 0; m < 64; ++m) {
+                const uint32_t x = col[wv][lane][m];
+                col[wv][lane][m] = (uint16_t)run;
+                run += x;
+            }
+        if (!EMIT) {
+            total += run;
+            wave_lds_sync();
+            continue;
+        }
+        wave_lds_sync();
+        if (own) {
+            uint32_t slot = slot0;
+            const int32_t v = vi & ID_MASK;
+            for (int q = 0; q < nr; ++q)
+                for (int j = rg[q][0]; j <= rg[q][1]; ++j) {
+                    if (j == i) continue;
+                    int32_t cw;
+                    const int k = pair_block(b, walk[j], unit, i, cw);
+                    int32_t x[RW];
+                    x[0] = v | (int32_t)((((uint32_t)vi >> 31) & 1u) << 30);
+                    x[1] = cw;
+#pragma unroll
+                    for (int n = 0; n < RW - 2; ++n) x[2 + n] = -1;
+#pragma unroll
+                    for (int n = 0; n < KMAX; ++n)
+                        if (n < K)
+                            x[2 + n] = block_negative(b, k, neg(slot + 2u * (uint32_t)n), neg(slot + 2u * (uint32_t)n + 1u));
+                    x[2 + KMAX] = __float_as_int(alpha);
+                    slot += 2u * (uint32_t)K;
+                    const uint32_t at = col[wv][k][lane];
+                    col[wv][k][lane] = (uint16_t)(at + 1u);
+                    i32x4* o = reinterpret_cast<i32x4*>(rec + (base[wv][k] + at) * RW);
+#pragma unroll
+                    for (int qq = 0; qq < RW / 4; ++qq) {
+                        const i32x4 y = {x[4 * qq], x[4 * qq + 1], x[4 * qq + 2], x[4 * qq + 3]};
+                        __builtin_nontemporal_store(y, o + qq);
+                    }
+                }
+        }
+        wave_lds_sync();
+        if (lane < nb) base[wv][lane] += run;
+        wave_lds_sync();
+    }
+    if (!EMIT && lane < nb) count[(uint64_t)lane * w.nwalks + t] = (uint32_t)total;
+}
+
+// the wave kernels' 16-bit columns hold a chunk's pairs of one block: at most
+// 64 positions x (2 window) contexts
+bool wave_pairs_ok(const WalkArgs& w) {
+    const char* e = getenv("SMORE_WALK_EMIT_LEGACY");
+    if (e && atoi(e) != 0) return false;
+    return w.window > 0 && 64 * 2 * (int64_t)w.window < 65535;
+}
+
 hipError_t launch_block_pair_count(const WalkArgs& w, const BlockArgs& b, uint64_t seed, uint32_t* count,
                                    hipStream_t st) {
     const int block = 256;
+    if (wave_pairs_ok(w)) {
+        const dim3 grid((unsigned)((w.nwalks + WALKS_PER_BLOCK - 1) / WALKS_PER_BLOCK));
+        hipLaunchKernelGGL((block_pairs_wave_kernel<5, false>), grid, dim3(block), 0, st, w, b, seed, 0, 0.0, nullptr,
+                           count, nullptr);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(block_pair_count_kernel, dim3((unsigned)((w.nwalks + block - 1) / block)), dim3(block), 0, st,
                        w, b, seed, count);
     return hipGetLastError();
@@ -272,6 +428,16 @@ hipError_t launch_block_pair_count(const WalkArgs& w, const BlockArgs& b, uint64
 hipError_t launch_block_pair_emit(const WalkArgs& w, const BlockArgs& b, uint64_t seed, int K, double alpha0,
                                   const uint64_t* off, int32_t* rec, hipStream_t st) {
     const int block = 256;
+    if (wave_pairs_ok(w)) {
+        const dim3 grid((unsigned)((w.nwalks + WALKS_PER_BLOCK - 1) / WALKS_PER_BLOCK));
+        if (kmax_of(K) == 5)
+            hipLaunchKernelGGL((block_pairs_wave_kernel<5, true>), grid, dim3(block), 0, st, w, b, seed, K, alpha0, off,
+                               nullptr, rec);
+        else
+            hipLaunchKernelGGL((block_pairs_wave_kernel<10, true>), grid, dim3(block), 0, st, w, b, seed, K, alpha0,
+                               off, nullptr, rec);
+        return hipGetLastError();
+    }
     const dim3 grid((unsigned)((w.nwalks + block - 1) / block));
     if (kmax_of(K) == 5)
         hipLaunchKernelGGL(block_pair_emit_kernel<5>, grid, dim3(block), 0, st, w, b, seed, K, alpha0, off, rec);

@@ -354,6 +354,16 @@ class ProNet:
         self._chk(lib.smore_block_walk_records(self.ctx, int(block), C.byref(n)), "block_walk_records")
         return n.value
 
+    def block_walk_records_copy(self, block):
+        """A bucket's records, int32 [n, width] (parity tests)."""
+        n, w = C.c_uint64(), C.c_int32()
+        self._chk(lib.smore_block_walk_records_copy(self.ctx, int(block), None, 0, C.byref(n), C.byref(w)),
+                  "block_walk_records_copy")
+        out = np.zeros((n.value, w.value), np.int32)
+        self._chk(lib.smore_block_walk_records_copy(self.ctx, int(block), out.ctypes.data_as(C.c_void_p), n.value,
+                                                    C.byref(n), C.byref(w)), "block_walk_records_copy")
+        return out
+
     def pairs_rows(self, v, c, K, seed, unit=0):
         """(W row ids, C row ids) a train_pairs batch touches: its vertices, and
         its contexts plus the K negatives it will draw (smore_pairs_rows)."""

@@ -280,6 +280,33 @@ def test_block_walk_rounds_cover_the_pairs(smore, graph):
         assert got == total_pairs, (n, got, total_pairs)
 
 
+@pytest.mark.parametrize("n,rule,steps,window,K", [(2, "deepwalk", 20, 4, 5), (3, "deepwalk", 100, 10, 5),
+                                                   (4, "walklets", 90, 6, 10), (8, "deepwalk", 40, 5, 5)])
+def test_block_walk_records_wave_kernels(smore, graph, monkeypatch, n, rule, steps, window, K):
+    """The wave-per-walk count / emit kernels (train_blocks.hip
+    block_pairs_wave_kernel: lane = position, the pair counts scanned across
+    the wave for the negatives' Philox words and per block for the records'
+    places) write the per-walk kernels' records bit for bit: every bucket of
+    every part, hybrid tags, hub slots (3 and 8 parts), walks longer than a
+    wave (101 and 91 positions), Walklets' two ranges and K = 10."""
+    order = orc.deepwalk_order(graph.V, 2, 0)
+    total = 0
+    for r in range(n):
+        recs = []
+        for legacy in ("1", "0"):
+            monkeypatch.setenv("SMORE_WALK_EMIT_LEGACY", legacy)
+            pn = _ctx(smore)
+            pn.block_setup("census", n, r, K, "hybrid")
+            pn.block_prepare_walks(0, 900, 2, steps, window, K, 0.025, SEED, order, "hybrid", rule=rule,
+                                   window_min=2 if rule == "walklets" else 0)
+            recs.append([pn.block_walk_records_copy(b) for b in range(2 * n)])
+            pn.close()
+        for b, (x, y) in enumerate(zip(*recs)):
+            np.testing.assert_array_equal(x, y, err_msg=f"part {r} block {b}")
+            total += len(x)
+    assert total > 0
+
+
 def test_block_group_walks_serial_replicas_agree(smore, graph):
     """A serial DeepWalk block group of 3: every replica ends with the same
     tables (gathered), they moved, and two identical runs agree bit for bit
