@@ -80,13 +80,22 @@ int64_t resident_groups(smore_ctx* c, bool walk, int K, int mode) {
 // its cell's C-row law (pcb, flags hcb; entry i of block k is row cb[k] + i,
 // or hub slot V + i - rows past the block's rows), with the edge rule's
 // staleness bound and a two-tier drain (capi build_hot_maps)
+// Walk cells add their part's hottest W rows (key v | SH_WKEY, rate ps(v) N
+// per record: wcand): the pair kernel keeps a run's W row in registers and
+// flushed it atomically at the run's end, so C5's hub centre -- ~1 record
+// runs, 16 % of its part's records at 8 parts -- queued every group's flush
+// on one 512-B row (its part's cells 1.4x slower than the others'); combined,
+// the block adds its groups' deltas in LDS and drains them on the row's
+// interval (SMORE_WALK_WCOMB=1; off by default)
 void block_sh_sets(smore_ctx* c, bool walk, bool on, int64_t Mg, const std::vector<std::vector<double>>& pcb,
-                   const std::vector<std::vector<uint8_t>>& hcb, std::vector<int2>& hash, std::vector<int32_t>& ids) {
+                   const std::vector<std::vector<uint8_t>>& hcb, std::vector<int2>& hash, std::vector<int32_t>& ids,
+                   const std::vector<std::pair<double, int32_t>>& wcand) {
     const int64_t V = c->g->V;
     auto& B = c->blk;
     const int cap = on ? std::max(0, std::min(c->sh_max, sh_rows_max(c->dpad))) : 0;
     B.sh_cap = std::max(cap, 1);
     B.sh_n.assign((size_t)B.nb, 0);
+    B.sh_wn.assign((size_t)B.nb, 0);
     B.sh_lvl.assign((size_t)B.nb, std::array<int, 8>{});
     hash.assign((size_t)B.nb * SH_HASH, make_int2(-1, -1));
     ids.assign((size_t)B.nb * B.sh_cap, -1);
@@ -112,12 +121,17 @@ void block_sh_sets(smore_ctx* c, bool walk, bool on, int64_t Mg, const std::vect
             const int64_t id = (int64_t)i < rows ? B.cb[k] + (int64_t)i : V + ((int64_t)i - rows);
             if (M * p * f <= stale) r.push_back({p, (int32_t)id});
         }
+        for (const auto& x : wcand) {
+            const double f = two_tier ? (double)sh_slot_interval(M * x.first, flush_cap, walk) : (double)flush_cap;
+            if (M * x.first * f <= stale) r.push_back(x);
+        }
         const int64_t n = std::min<int64_t>(cap, (int64_t)r.size());
         std::partial_sort(r.begin(), r.begin() + n, r.end(), [](const auto& x, const auto& y) {
             return x.first > y.first || (x.first == y.first && x.second < y.second);
         });
         int2* h = hash.data() + (size_t)k * SH_HASH;
         for (int64_t i = 0; i < n; ++i) {
+            B.sh_wn[k] += (r[i].second & SH_WKEY) ? 1 : 0;
             ids[(size_t)k * B.sh_cap + i] = r[i].second;
             uint32_t p = sh_hash_of(r[i].second);
             while (h[p & (SH_HASH - 1)].x >= 0) ++p;
@@ -148,6 +162,11 @@ void block_sh_sets(smore_ctx* c, bool walk, bool on, int64_t Mg, const std::vect
 // updates per row exactly the one-GPU ones (tests/test_blocks_cpu.py computes
 // the epoch marginal).  LINE-2 cells take m(r, b) from the atoms' mass; walk
 // cells from the round's record counts, on the device (neg_scale_of).
+bool wcomb_on() {
+    const char* e = getenv("SMORE_WALK_WCOMB");
+    return e && atoi(e) != 0;
+}
+
 bool neg_law_on() {
     const char* e = getenv("SMORE_NEG_LAW");
     return !e || atoi(e) != 0;
@@ -201,6 +220,7 @@ EdgeArgs cell_args(smore_ctx* c, int k, bool walk) {
         a.w_plain = e && atoi(e) != 0;
         const char* x = getenv("SMORE_WALK_EDGE");   // walk cells through the edge kernel (study)
         a.rec_edge = x && atoi(x) != 0;
+        a.w_comb = on && (size_t)k < B.sh_wn.size() && B.sh_wn[k] > 0;
     }
     if (neg_law_on() && (size_t)k < B.nmass.size()) {
         if (walk) {
@@ -827,7 +847,18 @@ int smore_block_setup(smore_ctx* c, int model, int nparts, int part, int K, int 
     c->hot_M = M;
     std::vector<int2> hash;
     std::vector<int32_t> ids;
-    block_sh_sets(c, walk, hyb && !small, M, pcb, hcb, hash, ids);
+    std::vector<std::pair<double, int32_t>> wcand;   // walk cells: the part's hot W rows (block_sh_sets)
+    if (walk && hyb && wcomb_on()) {
+        // a W row's rate counts each record's 1 + K gradient terms against the
+        // pair budget (SMORE_WALK_WCOMB_X overrides the factor)
+        const char* xe = getenv("SMORE_WALK_WCOMB_X");
+        const double wx = xe ? atof(xe) : (double)(1 + K);
+        for (int64_t v = wlo; v < whi; ++v) {
+            const double p = ps[v] * nparts * wx;
+            if ((double)M * p > tau) wcand.push_back({p, (int32_t)(v | SH_WKEY)});
+        }
+    }
+    block_sh_sets(c, walk, hyb && !small, M, pcb, hcb, hash, ids, wcand);
     if (getenv("SMORE_SH_DEBUG"))
         for (int k = 0; k < nb; ++k)
             fprintf(stderr, "[cell] part %d/%d block %d M %lld M*pmax_w %.4g M*pmax_c %.4g hubs %lld hub_p %.4g\n", part,

@@ -204,6 +204,7 @@ struct smore_ctx {
         int32_t* d_sh_ids = nullptr;    // nb x sh_cap
         int sh_cap = 0;
         std::vector<int> sh_n;
+        std::vector<int> sh_wn;                   // per block: W-row slots (walk cells: EdgeArgs::w_comb)
         std::vector<std::array<int, 8>> sh_lvl;   // per block: EdgeArgs::sh_lvl
         int sh_flush = 32;              // every slot's drain interval
         std::vector<double> pmax_w, pmax_c;   // per block: the cell's largest per-sample W / C row probability

@@ -893,6 +893,7 @@ pair_train_kernel(EdgeArgs a) {
         const uint64_t s0 = c0 + gib * sl;
         const uint64_t s1 = s0 + sl < lim ? s0 + sl : lim;
         int32_t cv = -1;
+        int slotw = -1;    // the run's W row's write-combined slot (EdgeArgs::w_comb)
         bool cvh = true;   // the run's W row is hot-tagged (or the flush is atomic anyway)
         float wv[M], wv0[M], rows[KMAX + 1][M];
 #pragma unroll
@@ -909,6 +910,15 @@ pair_train_kernel(EdgeArgs a) {
         };
         auto flush_w = [&]() {
             if (cv < 0) return;
+            if constexpr (MODE == MODE_HYBRID) {
+                if (slotw >= 0) {   // a combined W row: the run's delta into the block's pending row
+                    float* pp = sh.pend + slotw * a.dpad;
+#pragma unroll
+                    for (int m = 0; m < M; ++m)
+                        if (ev[m]) atomicAdd(pp + elem_off<G>(lane, m), wv[m] - wv0[m]);
+                    return;
+                }
+            }
             if (MODE == MODE_HYBRID && !cvh) {   // a cold W row: plain store (EdgeArgs::w_plain)
                 st_row<G, M>(a.W + (int64_t)cv * a.dpad, wv, lane, ev);
                 return;
@@ -939,6 +949,15 @@ pair_train_kernel(EdgeArgs a) {
                 cv = v;
                 cvh = !a.w_plain || scatter_atomic<MODE>(tv);
                 ld_row<G, M>(wv, a.W + (int64_t)cv * a.dpad, lane, ev);
+                if constexpr (MODE == MODE_HYBRID) {
+                    slotw = a.w_comb && sh.n > 0 ? sh_lookup(sh.hash, cv | SH_WKEY) : -1;
+                    if (slotw >= 0) {   // HBM value + the block's pending delta
+                        const float* pp = sh.pend + slotw * a.dpad;
+#pragma unroll
+                        for (int m = 0; m < M; ++m)
+                            if (ev[m]) wv[m] += pp[elem_off<G>(lane, m)];
+                    }
+                }
 #pragma unroll
                 for (int m = 0; m < M; ++m) wv0[m] = wv[m];
             }

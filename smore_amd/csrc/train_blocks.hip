@@ -25,8 +25,10 @@
 // over the block).  Buckets keep walk order, so a bucket's records are the
 // one-GPU records restricted to the cell, in order.  The group driver walks
 // 1/N of a round per GPU and broadcasts the slices (exchange.cpp); the count
-// and emit run one wave per walk (block_pairs_wave_kernel).
+// runs one wave per walk (block_pairs_wave_kernel), the emit one thread.
 #include "train_kernels.h"
+
+#include <string>
 
 namespace smore {
 
@@ -403,18 +405,23 @@ __global__ void __launch_bounds__(256) block_pairs_wave_kernel(WalkArgs w, Block
     if (!EMIT && lane < nb) count[(uint64_t)lane * w.nwalks + t] = (uint32_t)total;
 }
 
-// the wave kernels' 16-bit columns hold a chunk's pairs of one block: at most
-// 64 positions x (2 window) contexts
-bool wave_pairs_ok(const WalkArgs& w) {
-    const char* e = getenv("SMORE_WALK_EMIT_LEGACY");
-    if (e && atoi(e) != 0) return false;
+// which kernels (SMORE_WALK_PAIR_KERNELS): "auto" (default) the wave count and
+// the per-walk emit -- at 8 parts only ~1/8 of a wave's lanes own their
+// position, so the wave emit idles the rest through the K negative draws (C5:
+// 3.5 ms against the per-walk emit's 3.05; the wave count 0.65 against 0.83);
+// "wave" both wave kernels, "walk" both per-walk ones.  The wave kernels'
+// 16-bit columns hold a chunk's pairs of one block: 64 positions x 2 window
+bool wave_pairs_ok(const WalkArgs& w, bool emit) {
+    const char* e = getenv("SMORE_WALK_PAIR_KERNELS");
+    const std::string k = e ? e : "auto";
+    if (k == "walk" || (emit && k != "wave")) return false;
     return w.window > 0 && 64 * 2 * (int64_t)w.window < 65535;
 }
 
 hipError_t launch_block_pair_count(const WalkArgs& w, const BlockArgs& b, uint64_t seed, uint32_t* count,
                                    hipStream_t st) {
     const int block = 256;
-    if (wave_pairs_ok(w)) {
+    if (wave_pairs_ok(w, false)) {
         const dim3 grid((unsigned)((w.nwalks + WALKS_PER_BLOCK - 1) / WALKS_PER_BLOCK));
         hipLaunchKernelGGL((block_pairs_wave_kernel<5, false>), grid, dim3(block), 0, st, w, b, seed, 0, 0.0, nullptr,
                            count, nullptr);
@@ -428,7 +435,7 @@ hipError_t launch_block_pair_count(const WalkArgs& w, const BlockArgs& b, uint64
 hipError_t launch_block_pair_emit(const WalkArgs& w, const BlockArgs& b, uint64_t seed, int K, double alpha0,
                                   const uint64_t* off, int32_t* rec, hipStream_t st) {
     const int block = 256;
-    if (wave_pairs_ok(w)) {
+    if (wave_pairs_ok(w, true)) {
         const dim3 grid((unsigned)((w.nwalks + WALKS_PER_BLOCK - 1) / WALKS_PER_BLOCK));
         if (kmax_of(K) == 5)
             hipLaunchKernelGGL((block_pairs_wave_kernel<5, true>), grid, dim3(block), 0, st, w, b, seed, K, alpha0, off,

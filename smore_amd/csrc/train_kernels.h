@@ -58,6 +58,7 @@ struct EdgeArgs {
     // walk records through the (row-prefetching) edge kernel instead of the
     // pair kernel (block walk cells: their W runs are ~1 record long)
     int rec_edge;
+    int w_comb;          // pair kernel (walk cells): the runs' W rows looked up in the write-combined set
     uint64_t begin, count, total, seed;
     double alpha0;
     float reg;

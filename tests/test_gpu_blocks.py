@@ -293,8 +293,8 @@ def test_block_walk_records_wave_kernels(smore, graph, monkeypatch, n, rule, ste
     total = 0
     for r in range(n):
         recs = []
-        for legacy in ("1", "0"):
-            monkeypatch.setenv("SMORE_WALK_EMIT_LEGACY", legacy)
+        for kernels in ("walk", "wave"):
+            monkeypatch.setenv("SMORE_WALK_PAIR_KERNELS", kernels)
             pn = _ctx(smore)
             pn.block_setup("census", n, r, K, "hybrid")
             pn.block_prepare_walks(0, 900, 2, steps, window, K, 0.025, SEED, order, "hybrid", rule=rule,

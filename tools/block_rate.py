@@ -136,13 +136,15 @@ def main():
                 # walk-partitioned generation (the group default): this part walks
                 # its 1/N of the round and buckets every walk's pairs; the other
                 # slices' broadcast is block_sim's (walk_bytes over the link)
+                # (the round buffer first holds every walk, as after the broadcast:
+                # the emit then buckets the whole round, as in the group)
                 def prep_split():
                     pn.block_walks_generate(0, args.walks, args.walks * r // n, args.walks * (r + 1) // n, wt, steps,
                                             window, K, 0.025, args.seed, order, args.mode)
                     pn.block_walks_emit()
-                prep = timed(prep_split)
                 prep_all = timed(lambda: pn.block_prepare_walks(0, args.walks, wt, steps, window, K, 0.025, args.seed,
                                                                 order, args.mode))
+                prep = timed(prep_split)
                 recs = [pn.block_walk_records(b) for b in range(nb)]
 
                 L = pn.block_cell_launches()     # a cell in L launches (hub slots exchanged between)
