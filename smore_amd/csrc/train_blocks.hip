@@ -25,7 +25,7 @@
 // over the block).  Buckets keep walk order, so a bucket's records are the
 // one-GPU records restricted to the cell, in order.  The group driver walks
 // 1/N of a round per GPU and broadcasts the slices (exchange.cpp); the count
-// runs one wave per walk (block_pairs_wave_kernel), the emit one thread.
+// and the emit run one wave per walk (block_pairs_wave_kernel).
 #include "train_kernels.h"
 
 #include <string>
@@ -269,12 +269,14 @@ __global__ void __launch_bounds__(256) block_pair_emit_kernel(WalkArgs w, BlockA
 // a thread a whole walk: 2^18 threads per round, each looping over ~40
 // positions with its 2N block cursors in scratch (C5, 8 parts: emit 3.0 ms,
 // count 0.8 ms of a 20-30 ms part epoch).  Here lane i takes position i (64
-// at a time): its pair count is scanned across the wave -- its negatives'
-// Philox words start after every earlier pair's, own or not -- and its pairs
-// per block go into the wave's LDS column, scanned per block (lane k scans
-// row k), so its records in block k follow every earlier position's.  Same
-// words, same records, same order as the per-walk kernels (bit-exact; the
-// host keeps those for windows too wide for the 16-bit columns).
+// at a time) and its pair counts are scanned across the wave: all pairs for
+// the negatives' Philox words (a position's start after every earlier pair's,
+// own or not), the owned ones for the records.  The records are then spread
+// over the lanes (lane r: record r of the chunk, looked up in the wave's LDS
+// tables), so a part's 1/N of the positions does not idle the other lanes
+// through the K negative draws; a record's place in block k is the walk's
+// base for k plus its rank among the lanes' block-k records (ballots).  Same
+// words, same records, same order as the per-walk kernels (bit-exact).
 constexpr int WALKS_PER_BLOCK = 4;
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
@@ -311,13 +313,21 @@ __device__ __forceinline__ uint32_t position_ranges(const WalkArgs& w, WalkWords
     return n;
 }
 
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t x, int src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)x, src, 64), hi = (uint32_t)__shfl((int)(uint32_t)(x >> 32), src, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 template <int KMAX, bool EMIT>
 __global__ void __launch_bounds__(256) block_pairs_wave_kernel(WalkArgs w, BlockArgs b, uint64_t seed, int K,
                                                                double alpha0, const uint64_t* off, uint32_t* count,
                                                                int32_t* rec) {
     constexpr int RW = rec_width(KMAX);
-    __shared__ uint16_t col[WALKS_PER_BLOCK][BLOCK_MAX][65];   // [walk][block][lane], padded row
-    __shared__ uint64_t base[WALKS_PER_BLOCK][BLOCK_MAX];       // block k's next record of the walk
+    // per wave: the chunk's owned-pair prefix (e), negative-word start (s0)
+    // and context ranges of each position, for the record lanes to look up
+    __shared__ uint32_t s_e[WALKS_PER_BLOCK][65];
+    __shared__ uint32_t s_s0[WALKS_PER_BLOCK][64];
+    __shared__ int4 s_rg[WALKS_PER_BLOCK][64];
     const int wv = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
     const uint64_t t = (uint64_t)blockIdx.x * WALKS_PER_BLOCK + (uint64_t)wv;
     if (t >= w.nwalks) return;   // whole waves: nothing below syncs the block
@@ -329,93 +339,108 @@ __global__ void __launch_bounds__(256) block_pairs_wave_kernel(WalkArgs w, Block
     WalkWordsB win{seed, unit}, neg{seed, unit};
     const uint32_t win_base = 2u * (uint32_t)(L - 1);
     uint32_t slot_run = win_base + (w.rule == 1 ? 0u : (uint32_t)L);   // the chunk's first negative word
-    uint64_t total = 0;                                               // count: lane k's block-k pairs
-    if (EMIT && lane < nb) base[wv][lane] = off[(uint64_t)lane * w.nwalks + t];
+    // lane k < nb: block k's next record of this walk (emit) / its pairs (count)
+    uint64_t kb = (EMIT && lane < nb) ? off[(uint64_t)lane * w.nwalks + t] : 0;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;   // lanes below this one
     for (int p0 = 0; p0 < L; p0 += 64) {
         const int i = p0 + lane;
         int rg[2][2] = {{0, -1}, {0, -1}};
         int nr = 0;
         uint32_t np = 0;
-        int32_t vi = 0;
         bool own = false;
         if (i < L) {
             np = position_ranges(w, win, win_base, i, L, rg, nr);
-            vi = walk[i];
-            const int32_t v = vi & ID_MASK;
+            const int32_t v = walk[i] & ID_MASK;
             own = v >= w.own_lo && v < w.own_hi;
         }
+        // every pair draws 2K negative words, own or not; owned pairs become records
         const uint32_t incl = wave_incl_scan(np, lane);
-        const uint32_t slot0 = slot_run + 2u * (uint32_t)K * (incl - np);
+        const uint32_t no = own ? np : 0u, oincl = wave_incl_scan(no, lane);
+        const uint32_t T = (uint32_t)__shfl((int)oincl, 63, 64);
+        s_e[wv][lane] = oincl - no;
+        if (lane == 63) s_e[wv][64] = oincl;
+        s_s0[wv][lane] = slot_run + 2u * (uint32_t)K * (incl - np);
+        s_rg[wv][lane] = make_int4(rg[0][0], rg[0][1], nr == 2 ? rg[1][0] : 0, nr == 2 ? rg[1][1] : -1);
         slot_run += 2u * (uint32_t)K * (uint32_t)__shfl((int)incl, 63, 64);
-        for (int k = 0; k < nb; ++k) col[wv][k][lane] = 0;
-        if (own)
-            for (int q = 0; q < nr; ++q)
-                for (int j = rg[q][0]; j <= rg[q][1]; ++j)
-                    if (j != i) {
-                        int32_t cw;
-                        col[wv][pair_block(b, walk[j], unit, i, cw)][lane]++;
-                    }
         wave_lds_sync();
-        uint32_t run = 0;   // lane k: block k's pairs of the chunk
-        if (lane < nb)
-            for (int m = 0; m < 64; ++m) {
-                const uint32_t x = col[wv][lane][m];
-                col[wv][lane][m] = (uint16_t)run;
-                run += x;
-            }
-        if (!EMIT) {
-            total += run;
-            wave_lds_sync();
-            continue;
-        }
-        wave_lds_sync();
-        if (own) {
-            uint32_t slot = slot0;
-            const int32_t v = vi & ID_MASK;
-            for (int q = 0; q < nr; ++q)
-                for (int j = rg[q][0]; j <= rg[q][1]; ++j) {
-                    if (j == i) continue;
-                    int32_t cw;
-                    const int k = pair_block(b, walk[j], unit, i, cw);
-                    int32_t x[RW];
-                    x[0] = v | (int32_t)((((uint32_t)vi >> 31) & 1u) << 30);
-                    x[1] = cw;
-#pragma unroll
-                    for (int n = 0; n < RW - 2; ++n) x[2 + n] = -1;
-#pragma unroll
-                    for (int n = 0; n < KMAX; ++n)
-                        if (n < K)
-                            x[2 + n] = block_negative(b, k, neg(slot + 2u * (uint32_t)n), neg(slot + 2u * (uint32_t)n + 1u));
-                    x[2 + KMAX] = __float_as_int(alpha);
-                    slot += 2u * (uint32_t)K;
-                    const uint32_t at = col[wv][k][lane];
-                    col[wv][k][lane] = (uint16_t)(at + 1u);
-                    i32x4* o = reinterpret_cast<i32x4*>(rec + (base[wv][k] + at) * RW);
-#pragma unroll
-                    for (int qq = 0; qq < RW / 4; ++qq) {
-                        const i32x4 y = {x[4 * qq], x[4 * qq + 1], x[4 * qq + 2], x[4 * qq + 3]};
-                        __builtin_nontemporal_store(y, o + qq);
-                    }
+        // the chunk's T records, 64 at a time: record r is pair m of position
+        // li, the last lane whose prefix is <= r
+        for (uint32_t r0 = 0; r0 < T; r0 += 64) {
+            const uint32_t r = r0 + (uint32_t)lane;
+            const bool act = r < T;
+            int k = -1, li = 0, j = 0;
+            uint32_t m = 0;
+            int32_t cw = 0;
+            if (act) {
+                int lo = 0, hi = 64;   // s_e[lo] <= r < s_e[hi]
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (s_e[wv][mid] <= r) lo = mid;
+                    else hi = mid;
                 }
+                li = lo;
+                m = r - s_e[wv][li];
+                const int ip = p0 + li;
+                const int4 g = s_rg[wv][li];
+                // the m-th context of position ip: its ranges in order, ip skipped
+                uint32_t x = m;
+                int a0 = g.x, a1 = g.y;
+                uint32_t n0 = a1 >= a0 ? (uint32_t)(a1 - a0 + 1) - (ip >= a0 && ip <= a1 ? 1u : 0u) : 0u;
+                if (x >= n0) {
+                    x -= n0;
+                    a0 = g.z;
+                    a1 = g.w;
+                }
+                j = a0 + (int)x;
+                if (ip >= a0 && ip <= a1 && j >= ip) ++j;
+                k = pair_block(b, walk[j], unit, ip, cw);
+            }
+            // the record's place in block k: after every earlier record of k
+            // (this walk's base for k from lane k, its rank among the lanes)
+            uint32_t rank = 0;
+            uint64_t base = 0;
+            for (int kk = 0; kk < nb; ++kk) {
+                const uint64_t mask = __ballot(k == kk);
+                const uint64_t bk = shfl_u64(kb, kk);
+                if (k == kk) {
+                    rank = (uint32_t)__popcll(mask & lt);
+                    base = bk;
+                }
+                if (lane == kk) kb += (uint64_t)__popcll(mask);
+            }
+            if (EMIT && act) {
+                const int ip = p0 + li;
+                const int32_t vi = walk[ip];
+                const uint32_t slot = s_s0[wv][li] + 2u * (uint32_t)K * m;
+                int32_t xr[RW];
+                xr[0] = (vi & ID_MASK) | (int32_t)((((uint32_t)vi >> 31) & 1u) << 30);
+                xr[1] = cw;
+#pragma unroll
+                for (int n = 0; n < RW - 2; ++n) xr[2 + n] = -1;
+#pragma unroll
+                for (int n = 0; n < KMAX; ++n)
+                    if (n < K)
+                        xr[2 + n] = block_negative(b, k, neg(slot + 2u * (uint32_t)n), neg(slot + 2u * (uint32_t)n + 1u));
+                xr[2 + KMAX] = __float_as_int(alpha);
+                i32x4* o = reinterpret_cast<i32x4*>(rec + (base + rank) * RW);
+#pragma unroll
+                for (int qq = 0; qq < RW / 4; ++qq) {
+                    const i32x4 y = {xr[4 * qq], xr[4 * qq + 1], xr[4 * qq + 2], xr[4 * qq + 3]};
+                    __builtin_nontemporal_store(y, o + qq);
+                }
+            }
         }
-        wave_lds_sync();
-        if (lane < nb) base[wv][lane] += run;
-        wave_lds_sync();
+        wave_lds_sync();   // the next chunk rewrites the wave's tables
     }
-    if (!EMIT && lane < nb) count[(uint64_t)lane * w.nwalks + t] = (uint32_t)total;
+    if (!EMIT && lane < nb) count[(uint64_t)lane * w.nwalks + t] = (uint32_t)kb;
 }
 
-// which kernels (SMORE_WALK_PAIR_KERNELS): "auto" (default) the wave count and
-// the per-walk emit -- at 8 parts only ~1/8 of a wave's lanes own their
-// position, so the wave emit idles the rest through the K negative draws (C5:
-// 3.5 ms against the per-walk emit's 3.05; the wave count 0.65 against 0.83);
-// "wave" both wave kernels, "walk" both per-walk ones.  The wave kernels'
-// 16-bit columns hold a chunk's pairs of one block: 64 positions x 2 window
-bool wave_pairs_ok(const WalkArgs& w, bool emit) {
+// which kernels (SMORE_WALK_PAIR_KERNELS): "wave" (default) or "walk" (the
+// per-walk ones); windows wider than a wave's chunk can hold take the per-walk
+bool wave_pairs_ok(const WalkArgs& w, bool) {
     const char* e = getenv("SMORE_WALK_PAIR_KERNELS");
-    const std::string k = e ? e : "auto";
-    if (k == "walk" || (emit && k != "wave")) return false;
-    return w.window > 0 && 64 * 2 * (int64_t)w.window < 65535;
+    if (e && std::string(e) == "walk") return false;
+    return w.window > 0 && w.window < 1024;
 }
 
 hipError_t launch_block_pair_count(const WalkArgs& w, const BlockArgs& b, uint64_t seed, uint32_t* count,
